@@ -1,0 +1,204 @@
+"""ctypes wrapper for the CPU restatement in oracle/arrow_oracle.cpp -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and only
+as the checker.  The product (pbccs_amd) never imports it.  Parity pin: see arrow_oracle.cpp's header.
+"""
+import ctypes
+import math
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+INSERTION, DELETION, SUBSTITUTION = 0, 1, 2
+FORWARD, REVERSE = 0, 1
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        c_d, c_i, c_p, c_s = ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p
+        D = ctypes.POINTER(ctypes.c_double)
+        I = ctypes.POINTER(ctypes.c_int)
+        Lg = ctypes.POINTER(ctypes.c_long)
+        L.orc_scorer_new.restype = c_p
+        L.orc_scorer_new.argtypes = [c_s, D, c_d, c_d, c_d]
+        L.orc_scorer_free.argtypes = [c_p]
+        L.orc_scorer_add_read.argtypes = [c_p, c_s, c_i, c_i, c_i, c_d]
+        L.orc_scorer_num_reads.argtypes = [c_p]
+        L.orc_scorer_read_info.argtypes = [c_p, c_i, I, I, I, D, I]
+        L.orc_scorer_score.restype = c_d
+        L.orc_scorer_score.argtypes = [c_p, c_i, c_i, c_i, c_s, c_d]
+        L.orc_scorer_scores.argtypes = [c_p, c_i, c_i, c_i, c_s, c_d, D]
+        L.orc_scorer_baseline.restype = c_d
+        L.orc_scorer_baseline.argtypes = [c_p]
+        L.orc_scorer_template.argtypes = [c_p, c_i, ctypes.c_char_p, c_i]
+        L.orc_scorer_apply.argtypes = [c_p, c_i, I, I, I, c_s]
+        L.orc_scorer_zscores.argtypes = [c_p, D, D, D]
+        L.orc_refine.argtypes = [c_p, c_i, c_i, c_i, Lg, Lg, I, c_i, I]
+        L.orc_qvs.argtypes = [c_p, I, c_i]
+        L.orc_enum_unique.argtypes = [c_s, c_i, c_i, I, I, c_s, c_i]
+        L.orc_enum_nearby.argtypes = [c_s, c_i, I, c_i, I, I, c_s, c_i]
+        L.orc_apply_mutations.argtypes = [c_s, c_i, I, I, I, c_s, c_s, c_i, I, c_i]
+        L.orc_context_params.argtypes = [D, D]
+        _lib = L
+    return _lib
+
+
+def _darr(vals):
+    return (ctypes.c_double * len(vals))(*vals)
+
+
+def _iarr(vals):
+    return (ctypes.c_int * len(vals))(*vals)
+
+
+def mutation_end(mtype, start):
+    return start if mtype == INSERTION else start + 1
+
+
+class Scorer:
+    """Mirror of ConsensusCore::Arrow::MultiReadMutationScorer (CPU restatement)."""
+
+    def __init__(self, tpl, snr, score_diff=12.5, fast_threshold=-12.5, add_threshold=float("nan")):
+        self._h = lib().orc_scorer_new(tpl.encode(), _darr(snr), score_diff, fast_threshold, add_threshold)
+        if not self._h:
+            raise ValueError("invalid template")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_scorer_free(self._h)
+            self._h = None
+
+    def add_read(self, seq, strand=FORWARD, ts=0, te=None, threshold=float("nan")):
+        if te is None:
+            te = len(self.template())
+        return lib().orc_scorer_add_read(self._h, seq.encode(), strand, ts, te, threshold)
+
+    def num_reads(self):
+        return lib().orc_scorer_num_reads(self._h)
+
+    def read_info(self, r):
+        a, ts, te, fl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        ll = ctypes.c_double()
+        lib().orc_scorer_read_info(self._h, r, ctypes.byref(a), ctypes.byref(ts), ctypes.byref(te),
+                                   ctypes.byref(ll), ctypes.byref(fl))
+        return {"active": bool(a.value), "ts": ts.value, "te": te.value, "ll": ll.value, "flipflops": fl.value}
+
+    def score(self, mtype, start, base="-", fast_threshold=-1.7976931348623157e308):
+        nb = b"" if mtype == DELETION else base.encode()
+        return lib().orc_scorer_score(self._h, mtype, start, mutation_end(mtype, start), nb, fast_threshold)
+
+    def scores(self, mtype, start, base="-", unscored=0.0):
+        out = (ctypes.c_double * max(1, self.num_reads()))()
+        nb = b"" if mtype == DELETION else base.encode()
+        n = lib().orc_scorer_scores(self._h, mtype, start, mutation_end(mtype, start), nb, unscored, out)
+        return list(out[:n])
+
+    def baseline(self):
+        return lib().orc_scorer_baseline(self._h)
+
+    def template(self, strand=FORWARD):
+        buf = ctypes.create_string_buffer(1 << 20)
+        n = lib().orc_scorer_template(self._h, strand, buf, len(buf))
+        return buf.value.decode()
+
+    def apply(self, muts):
+        types = _iarr([m[0] for m in muts])
+        starts = _iarr([m[1] for m in muts])
+        ends = _iarr([mutation_end(m[0], m[1]) for m in muts])
+        bases = "".join(m[2] if m[0] != DELETION else "-" for m in muts).encode()
+        return lib().orc_scorer_apply(self._h, len(muts), types, starts, ends, bases)
+
+    def zscores(self):
+        zg, za = ctypes.c_double(), ctypes.c_double()
+        zs = (ctypes.c_double * max(1, self.num_reads()))()
+        lib().orc_scorer_zscores(self._h, ctypes.byref(zg), ctypes.byref(za), zs)
+        return zg.value, za.value, list(zs[: self.num_reads()])
+
+    def refine(self, max_iter=40, separation=10, neighborhood=20):
+        nt, na = ctypes.c_long(), ctypes.c_long()
+        cap = 100000
+        log = (ctypes.c_int * (4 * cap))()
+        nlog = ctypes.c_int()
+        conv = lib().orc_refine(self._h, max_iter, separation, neighborhood, ctypes.byref(nt), ctypes.byref(na),
+                                log, cap, ctypes.byref(nlog))
+        applied = [(log[4 * k], log[4 * k + 1], log[4 * k + 2], chr(log[4 * k + 3])) for k in range(min(cap, nlog.value))]
+        return {"converged": conv == 1, "error": conv < 0, "n_tested": nt.value, "n_applied": na.value,
+                "applied": applied}
+
+    def qvs(self):
+        L = len(self.template())
+        out = (ctypes.c_int * max(1, L))()
+        n = lib().orc_qvs(self._h, out, L)
+        if n < 0:
+            raise RuntimeError("qv failure")
+        return list(out[:n])
+
+
+def unique_mutations(tpl, b=0, e=None):
+    if e is None:
+        e = len(tpl)
+    cap = 8 * len(tpl) + 8
+    t, s = (ctypes.c_int * cap)(), (ctypes.c_int * cap)()
+    bs = ctypes.create_string_buffer(cap)
+    n = lib().orc_enum_unique(tpl.encode(), b, e, t, s, bs, cap)
+    return [(t[k], s[k], bs.raw[k:k + 1].decode()) for k in range(n)]
+
+
+def nearby_mutations(tpl, centers, nbhd):
+    cap = 8 * len(tpl) + 8
+    t, s = (ctypes.c_int * cap)(), (ctypes.c_int * cap)()
+    bs = ctypes.create_string_buffer(cap)
+    n = lib().orc_enum_nearby(tpl.encode(), len(centers), _iarr(centers), nbhd, t, s, bs, cap)
+    return [(t[k], s[k], bs.raw[k:k + 1].decode()) for k in range(n)]
+
+
+def apply_mutations(tpl, muts):
+    types = _iarr([m[0] for m in muts])
+    starts = _iarr([m[1] for m in muts])
+    ends = _iarr([mutation_end(m[0], m[1]) for m in muts])
+    bases = "".join(m[2] if m[0] != DELETION else "-" for m in muts).encode()
+    cap = len(tpl) + len(muts) + 2
+    out = ctypes.create_string_buffer(cap)
+    mtp = (ctypes.c_int * (len(tpl) + 1))()
+    n = lib().orc_apply_mutations(tpl.encode(), len(muts), types, starts, ends, bases, out, cap, mtp, len(tpl) + 1)
+    if n < 0:
+        raise RuntimeError("apply failed")
+    return out.value.decode(), list(mtp)
+
+
+def context_params(snr):
+    out = (ctypes.c_double * 32)()
+    lib().orc_context_params(_darr(snr), out)
+    return [list(out[4 * c: 4 * c + 4]) for c in range(8)]
+
+
+def polish_zmw(draft, reads, snr, min_zscore=-5.0, max_iter=40, separation=10, neighborhood=20, qvs=True):
+    """The ccs per-ZMW polish step after the POA (include/pacbio/ccs/Consensus.h:436-512), restated.
+
+    reads: list of dicts {seq, strand, ts, te}.  Returns the same fields the reference result carries.
+    """
+    s = Scorer(draft, snr)
+    status = [s.add_read(r["seq"], r["strand"], r["ts"], r["te"], min_zscore) for r in reads]
+    zg, za, zs = s.zscores()
+    ref = s.refine(max_iter, separation, neighborhood)
+    out = {"add_read_results": status, "zg": zg, "za": za, "zscores": zs, "baseline_lls": [],
+           "converged": ref["converged"], "n_tested": ref["n_tested"], "n_applied": ref["n_applied"],
+           "applied": ref["applied"], "template": s.template()}
+    out["baseline_lls"] = [s.read_info(r)["ll"] for r in range(s.num_reads())]
+    if qvs and ref["converged"]:
+        q = s.qvs()
+        out["qvs"] = q
+        out["pred_acc"] = 1.0 - sum(10.0 ** (v / -10.0) for v in q) / max(1, len(q))
+    return out

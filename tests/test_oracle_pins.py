@@ -1,0 +1,89 @@
+"""Pin the CPU restatement (oracle/) against the reference's own known answers.
+
+* ConsensusCore/src/Demos/MatrixTester.cpp:74-204 -- 12 Arrow KATs, 1e-5 relative (the demo's ASSERT_EQ).
+* src/Tests/TestMutations.cpp, TestMutationEnumerator.cpp -- ApplyMutations / transcripts / enumerators.
+* SURVEY.md §0 item 4 -- the reference's recorded polish of tests/data ZMW 6251.
+"""
+import json
+import os
+
+import pytest
+
+from oracle import oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _kats():
+    return json.load(open(os.path.join(GOLD, "arrow_kats.json")))
+
+
+def test_matrixtester_baselines():
+    k = _kats()
+    for b in k["baseline"]:
+        s = O.Scorer(b["tpl"], k["snr"])
+        for r in b["reads"]:
+            s.add_read(r)
+        v = s.baseline()
+        assert abs(1 - v / b["expected"]) < k["tolerance_rel"], (b, v)
+
+
+@pytest.mark.parametrize("idx", range(8))
+def test_matrixtester_mutation_scores(idx):
+    k = _kats()
+    m = k["mutations"][idx]
+    s = O.Scorer(m["tpl"], k["snr"])
+    for r in m["reads"] * m.get("copies", 1):
+        s.add_read(r)
+    v = s.score(m["type"], m["start"], m["base"]) / m.get("divide_by", 1)
+    assert abs(1 - v / m["expected"]) < k["tolerance_rel"], (m["line"], v)
+
+
+def test_matrixtester_short_equalities():
+    k = _kats()
+    se = k["short_equalities"]
+    a = O.Scorer(se["tpl_short"], k["snr"])
+    a.add_read(se["read"])
+    b = O.Scorer(se["tpl_long"], k["snr"])
+    b.add_read(se["read"])
+    assert abs(1 - a.baseline() / (b.baseline() + b.score(se["type"], se["start"]))) < 1e-5
+    b.apply([(se["type"], se["start"], "-")])
+    assert b.template() == se["tpl_short"]
+    assert abs(1 - a.baseline() / b.baseline()) < 1e-5
+
+
+def test_enumerators_match_gtests():
+    # TestMutationEnumerator.cpp:73-104
+    assert len(O.unique_mutations("GAATC")) == 7 * 5 + 1 - 1
+    assert len(O.nearby_mutations("GAATC", [1], 1)) == 8 + 7
+    assert len(O.nearby_mutations("GAATC", [1], 2)) == 8 + 7 + 6
+    assert sorted(O.nearby_mutations("GAATC", [1, 3], 2)) == sorted(O.unique_mutations("GAATC"))
+
+
+def test_apply_mutations_match_gtests():
+    # TestMutations.cpp:64-181
+    I, D, S = O.INSERTION, O.DELETION, O.SUBSTITUTION
+    assert O.apply_mutations("ACGTACGTACGT", [(S, 0, "C")])[0] == "CCGTACGTACGT"
+    assert O.apply_mutations("ACGTACGTACGT", [(D, 4, "-")])[0] == "ACGTCGTACGT"
+    assert O.apply_mutations("ACGTACGTACGT", [(I, 0, "C")])[0] == "CACGTACGTACGT"
+    muts = [(I, 3, "C"), (I, 2, "T"), (I, 0, "G"), (S, 6, "T"), (D, 4, "-")]
+    assert O.apply_mutations("GATTACA", muts)[0] == "GGATTCTCT"
+    assert O.apply_mutations("GATTACA", [(S, 2, "A"), (I, 2, "T")])[0] == "GATATACA"
+    assert O.apply_mutations("GATTACA", [(D, 2, "-"), (I, 5, "C"), (S, 4, "G")])[1] == [0, 1, 2, 2, 3, 5, 6, 7]
+    assert O.apply_mutations("GG", [(I, 0, "A")])[1] == [1, 2, 3]
+    assert O.apply_mutations("AGG", [(D, 0, "-")])[1] == [0, 0, 1, 2]
+
+
+def test_zmw6251_polish_matches_reference_record():
+    z = json.load(open(os.path.join(GOLD, "zmw6251.json")))
+    r = O.polish_zmw(z["draft"], z["reads"], z["snr"], z["min_zscore"])
+    e = z["expected"]
+    tol = e["tolerance_abs"]
+    assert r["add_read_results"] == e["add_read_results"]
+    assert abs(r["zg"] - e["zg"]) < tol["zg"]
+    assert abs(r["za"] - e["za"]) < tol["za"]
+    assert r["converged"] == e["converged"]
+    assert r["n_tested"] == e["n_tested"]
+    assert r["n_applied"] == e["n_applied"]
+    assert len(r["template"]) == e["final_length"]
+    assert abs(r["pred_acc"] - e["pred_acc"]) < tol["pred_acc"]
