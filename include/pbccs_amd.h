@@ -1,0 +1,183 @@
+/*
+ * pbccs_amd.h -- C ABI of the MI355X consensus-polishing engine (drop-in for pbccs' polish path).
+ *
+ * The reference's hot path is a C++ template API, not an FFI: pbccs' per-ZMW driver
+ * (include/pacbio/ccs/Consensus.h:436-512) drives ConsensusCore's
+ *   Arrow::MultiReadMutationScorer  (ConsensusCore/include/ConsensusCore/Arrow/MultiReadMutationScorer.hpp:82-284)
+ *   RefineConsensus / ConsensusQVs  (ConsensusCore/include/ConsensusCore/Consensus.hpp:63-79, Consensus-inl.hpp:159-295)
+ * Every entry point below replaces one of those calls (cited per function); include/pbccs_amd/ConsensusCore.hpp
+ * wraps them back into the reference's C++ class names so a Consensus.h-equivalent compiles unchanged
+ * (INTEGRATION.md).  Plain pointers and sizes only; nothing throws across this boundary.
+ */
+#ifndef PBCCS_AMD_H
+#define PBCCS_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------------------------- */
+#define PBCCS_OK 0
+#define PBCCS_EINVAL (-1)   /* bad argument (InvalidInputError, std::out_of_range in the reference) */
+#define PBCCS_EOOM (-2)     /* device allocation failed */
+#define PBCCS_EDEVICE (-3)  /* HIP runtime / kernel failure */
+#define PBCCS_ESTATE (-4)   /* call out of order (e.g. BadExecutionOrderException) */
+#define PBCCS_ERANGE (-5)   /* caller buffer too small; the required size is returned through *len */
+
+/* Mutation types (ConsensusCore/include/ConsensusCore/Mutation.hpp:50-53) */
+#define PBCCS_INSERTION 0
+#define PBCCS_DELETION 1
+#define PBCCS_SUBSTITUTION 2
+/* Strands (ConsensusCore/include/ConsensusCore/Read.hpp:66-70) */
+#define PBCCS_FORWARD_STRAND 0
+#define PBCCS_REVERSE_STRAND 1
+/* AddReadResult (ConsensusCore/include/ConsensusCore/Arrow/MultiReadMutationScorer.hpp:60) */
+#define PBCCS_ADD_SUCCESS 0
+#define PBCCS_ADD_ALPHABETAMISMATCH 1
+#define PBCCS_ADD_MEM_FAIL 2
+#define PBCCS_ADD_POOR_ZSCORE 3
+#define PBCCS_ADD_OTHER 4
+/* Per-ZMW outcome (pbccs ResultType counters, include/pacbio/ccs/Consensus.h:150-210) */
+#define PBCCS_ZMW_SUCCESS 0
+#define PBCCS_ZMW_NO_SUBREADS 1
+#define PBCCS_ZMW_TOO_SHORT 2
+#define PBCCS_ZMW_TOO_MANY_UNUSABLE 3
+#define PBCCS_ZMW_TOO_FEW_PASSES 4
+#define PBCCS_ZMW_NON_CONVERGENT 5
+#define PBCCS_ZMW_POOR_QUALITY 6
+#define PBCCS_ZMW_OTHER 7
+
+typedef struct pbccs_engine pbccs_engine; /* one per GPU; externally synchronised */
+typedef struct pbccs_scorer pbccs_scorer; /* one ArrowMultiReadMutationScorer */
+
+/* A single-base mutation: start/end as in ConsensusCore::Mutation (insertion: end == start). */
+typedef struct {
+    int type;
+    int start;
+    int end;
+    char new_base; /* 'A','C','G','T'; ignored for deletions */
+} pbccs_mutation;
+
+/* ArrowConfig + BandingOptions (ConsensusCore/include/ConsensusCore/Arrow/ArrowConfig.hpp:104-128) */
+typedef struct {
+    double snr[4];               /* SNR(A, C, G, T) -> ContextParameters */
+    double score_diff;           /* BandingOptions::ScoreDiff (ccs: 12.5) */
+    double fast_score_threshold; /* ArrowConfig::FastScoreThreshold (default -12.5) */
+    double add_threshold;        /* ArrowConfig::AddThreshold (default NaN = no z-score gate) */
+} pbccs_arrow_config;
+
+/* RefineOptions (ConsensusCore/include/ConsensusCore/Consensus.hpp:48-60), defaults 40/10/20 */
+typedef struct {
+    int max_iterations;
+    int mutation_separation;
+    int mutation_neighborhood;
+} pbccs_refine_options;
+
+/* ---- engine --------------------------------------------------------------------------------- */
+int pbccs_engine_create(int device, pbccs_engine** out);
+void pbccs_engine_destroy(pbccs_engine* eng);
+const char* pbccs_last_error(void); /* thread-local message of the last failed call */
+int pbccs_device_count(void);
+
+/* ---- ArrowMultiReadMutationScorer (Arrow/MultiReadMutationScorer.cpp) ---------------------- */
+/* MultiReadMutationScorer(const ArrowConfig&, std::string tpl)                       (.cpp:143-154) */
+int pbccs_scorer_create(pbccs_engine* eng, const pbccs_arrow_config* cfg, const char* tpl, int tpl_len,
+                        pbccs_scorer** out);
+void pbccs_scorer_destroy(pbccs_scorer* s);
+/* AddReadResult AddRead(const MappedArrowRead&, double threshold)                    (.cpp:275-325)
+ * threshold NaN = no z-score gate; pass cfg->add_threshold for the one-argument overload (.cpp:334). */
+int pbccs_scorer_add_read(pbccs_scorer* s, const char* seq, int len, int strand, int tstart, int tend,
+                          double threshold, int* result);
+/* double Score(const Mutation&, double fastScoreThreshold = -DBL_MAX)                (.cpp:338-368)
+ * FastScore(m) == Score(m, cfg->fast_score_threshold)                                (.cpp:380-383) */
+int pbccs_scorer_score(pbccs_scorer* s, const pbccs_mutation* m, double fast_threshold, double* score);
+/* Batched Score over n mutations (same semantics per element). */
+int pbccs_scorer_score_many(pbccs_scorer* s, const pbccs_mutation* m, int n, double fast_threshold, double* scores);
+/* std::vector<double> Scores(const Mutation&, double unscoredValue)                  (.cpp:384-417)
+ * per_read must hold NumReads() entries. */
+int pbccs_scorer_scores(pbccs_scorer* s, const pbccs_mutation* m, double unscored, double* per_read);
+/* IsFavorable / FastIsFavorable (score > 0.04)                                       (.cpp:428-440) */
+int pbccs_scorer_is_favorable(pbccs_scorer* s, const pbccs_mutation* m, int fast, int* favorable);
+/* void ApplyMutations(const std::vector<Mutation>&)                                  (.cpp:235-267) */
+int pbccs_scorer_apply_mutations(pbccs_scorer* s, const pbccs_mutation* m, int n);
+/* std::string Template(StrandEnum)                                                   (.cpp:183-188)
+ * writes at most cap bytes (NUL-terminated); *len = template length. */
+int pbccs_scorer_template(pbccs_scorer* s, int strand, char* out, int cap, int* len);
+int pbccs_scorer_template_length(pbccs_scorer* s);                                 /* (.cpp:169-173) */
+int pbccs_scorer_num_reads(pbccs_scorer* s);                                       /* (.cpp:176-180) */
+/* Read(i): active flag and current mapping (MappedArrowRead*, NULL when inactive)    (.cpp:192-196) */
+int pbccs_scorer_read_info(pbccs_scorer* s, int i, int* active, int* strand, int* tstart, int* tend);
+/* double BaselineScore() / std::vector<double> BaselineScores()                      (.cpp:495-520) */
+int pbccs_scorer_baseline_score(pbccs_scorer* s, double* score);
+int pbccs_scorer_baseline_scores(pbccs_scorer* s, double* out, int cap, int* n);
+/* ZScores(): ((zg, za), per-read z)  per_read must hold NumReads() entries      (.hpp:208-263) */
+int pbccs_scorer_zscores(pbccs_scorer* s, double* zg, double* za, double* per_read);
+/* NumFlipFlops() per read                                                            (.cpp:480-488) */
+int pbccs_scorer_num_flipflops(pbccs_scorer* s, int* out);
+
+/* bool RefineConsensus(MRMS&, size_t* nTested, size_t* nApplied, const RefineOptions&)
+ *                                                       (Consensus.hpp:63-67, Consensus-inl.hpp:159-262) */
+int pbccs_refine_consensus(pbccs_scorer* s, const pbccs_refine_options* opts, long long* n_tested,
+                           long long* n_applied, int* converged);
+/* std::vector<int> ConsensusQVs(MRMS&)                  (Consensus.hpp:77-78, Consensus-inl.hpp:274-295) */
+int pbccs_consensus_qvs(pbccs_scorer* s, int* qvs, int cap, int* n);
+
+/* ---- batched ccs polish: Consensus<>() after the POA, for many ZMWs per call ------------------
+ * Mirrors include/pacbio/ccs/Consensus.h:436-552 from `ArrowConfig config(...)` on: AddRead(mr,
+ * MinZScore) per read with status counts, the MinPasses / MaxDropFraction gates, ZScores(),
+ * RefineConsensus(), ConsensusQVs(), predicted accuracy and the MinPredictedAccuracy gate.
+ * Results are written in input order (WorkQueue.h:128-167 ordering). */
+typedef struct {
+    const char* draft;         /* POA consensus (ACGT) */
+    int draft_len;
+    double snr[4];
+    int n_reads;
+    const char* const* seqs;   /* read bases as passed to MappedArrowRead (already extent-clipped) */
+    const int* lens;
+    const int* strands;
+    const int* tstarts;        /* mapped window on the draft [tstart, tend) */
+    const int* tends;
+    const unsigned char* full_pass; /* ADAPTER_BEFORE && ADAPTER_AFTER per read (NULL: all full passes) */
+} pbccs_zmw_input;
+
+typedef struct {
+    int min_passes;               /* ConsensusSettings::MinPasses (3) */
+    int min_length;               /* ConsensusSettings::MinLength (10): draft shorter -> TOO_SHORT */
+    double min_zscore;            /* ConsensusSettings::MinZScore (-5; NaN disables) */
+    double max_drop_fraction;     /* ConsensusSettings::MaxDropFraction (0.34) */
+    double min_predicted_accuracy;/* ConsensusSettings::MinPredictedAccuracy (0.90) */
+    double score_diff;            /* BandingOptions(12.5) */
+    pbccs_refine_options refine;  /* {40, 10, 20} */
+    int zmws_per_batch;           /* device batch size (0 = auto from the memory budget) */
+} pbccs_polish_options;
+
+typedef struct {
+    int status;          /* PBCCS_ZMW_* */
+    char* consensus;     /* caller buffer, consensus_cap bytes; NUL-terminated */
+    int consensus_cap;
+    int consensus_len;   /* -required length when the buffer was too small */
+    int* qvs;            /* caller buffer, consensus_cap entries (raw, unclipped QVs) */
+    int* add_read_results; /* caller buffer, n_reads entries (-1: read not added) */
+    double* zscores;     /* caller buffer, n_reads entries */
+    double zg, za;
+    double predicted_accuracy;
+    long long n_tested, n_applied;
+    int n_passes;
+    int status_counts[5]; /* AddReadResult histogram */
+} pbccs_zmw_output;
+
+void pbccs_polish_options_default(pbccs_polish_options* o);
+int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
+                       pbccs_zmw_output* out);
+
+/* Work counters of the engine since the last reset (for roofline accounting). */
+typedef struct {
+    long long fill_launches, score_launches, score_tasks, mutations;
+} pbccs_counters;
+int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PBCCS_AMD_H */

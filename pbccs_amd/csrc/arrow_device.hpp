@@ -1,0 +1,408 @@
+// pbccs_amd/csrc/arrow_device.hpp
+//
+// Device-side core of the MI355X Arrow polishing engine: the data layout of a ZMW batch in HBM and
+// the per-lane recursions (band fill, extend, link) that the kernels in arrow_kernels.hip run.
+//
+// Execution model: one lane owns one alignment task -- a (read, template-window)
+// fill, or a (mutation, read) score.  Within a task the work is column-serial exactly as in
+// ConsensusCore's Arrow::SimpleRecursor, because per-column rescaling makes every cell of column j
+// depend on the *scaled* column j-1; parallelism comes from the tens of
+// thousands of tasks in a batch.  All arithmetic is IEEE FP64 in the reference's operation order and
+// the library is built with -ffp-contract=off, so band shapes and cell values are bit-identical to the
+// reference; only libm `log` (device OCML vs glibc) may differ in the last ulp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pbccs {
+
+// ---------------------------------------------------------------------------------------------
+// Constants (reference citations in DESIGN.md and at each use)
+// ---------------------------------------------------------------------------------------------
+constexpr int kCtxZero = 8;           // index of the all-zero TransitionParameters slot
+constexpr int kCtxStride = 5;         // {Match, Stick, Branch, Deletion, Stick/3.0}
+constexpr int kNoMutation = -100;     // TemplateParameterPair::NO_MUTATION_SET_FLAG (.hpp:33)
+constexpr int kMaxExtCols = 4;        // max extension columns any single-base mutation needs
+constexpr int kMaxFlipFlops = 5;      // SimpleRecursor.cpp:52
+constexpr double kAlphaBetaTol = 0.001;   // SimpleRecursor.cpp:53
+constexpr double kRebandFrac = 0.04;      // SimpleRecursor.cpp:54
+
+enum MutType : int { kIns = 0, kDel = 1, kSub = 2 };   // Mutation.hpp:50-53
+enum Strand : int { kFwd = 0, kRev = 1 };
+
+enum FillStatus : int { kFillOk = 0, kFillMismatch = 1, kFillOverflow = 2, kFillBadInput = 3 };
+
+// Mutation code: pos << 4 | type << 2 | base(0..3).  Single-base mutations only (what ccs enumerates).
+__host__ __device__ inline int mut_code(int pos, int type, int base) { return (pos << 4) | (type << 2) | base; }
+__host__ __device__ inline int mut_pos(int c) { return c >> 4; }
+__host__ __device__ inline int mut_type(int c) { return (c >> 2) & 3; }
+__host__ __device__ inline int mut_base(int c) { return c & 3; }
+
+__host__ __device__ inline char base_char(int b) { return "ACGT"[b & 3]; }
+__host__ __device__ inline int base_index(char b)
+{
+    return b == 'A' ? 0 : b == 'C' ? 1 : b == 'G' ? 2 : b == 'T' ? 3 : -1;
+}
+__host__ __device__ inline int complement_index(int b) { return 3 - b; }
+
+// ContextParameters::GetParametersForContext (ContextParameters.cpp:35-47): "XX" for a homopolymer
+// pair, "N" + second base otherwise.  Slots 0..3 = AA CC GG TT, 4..7 = NA NC NG NT.
+__host__ __device__ inline int context_index(char b1, char b2)
+{
+    const int i2 = base_index(b2);
+    return (b1 == b2) ? i2 : 4 + i2;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Batch layout in HBM (struct of arrays).  Every array is indexed by zmw id z, read id r, or a
+// column slot (read's column base + j).  Band values live in one FP64 pool; each read owns two
+// regions (alpha, beta) addressed by offsets, with a capacity that the host grows on overflow.
+// ---------------------------------------------------------------------------------------------
+struct DevBatch {
+    // per ZMW
+    const int* zFwdOff;       // offset of the forward template in tplPool
+    const int* zRevOff;       // offset of the reverse-complement template in tplPool
+    const int* zLen;          // template length L
+    const double* zCtx;       // [Z][9][kCtxStride] transition parameters (slot 8 = zeros)
+    const int* zReadBegin;    // reads of zmw z are [zReadBegin, zReadBegin + zNReads)
+    const int* zNReads;
+    const char* tplPool;
+    // per read
+    const long long* rSeqOff; // read bases in seqPool
+    const int* rLen;          // I
+    const int* rStrand;
+    const int* rTs;           // mapped window [ts, te) in forward coordinates
+    const int* rTe;
+    const int* rActive;
+    const int* rZmw;
+    const long long* rColBase;   // column slot base
+    const long long* rValA;      // alpha value region offset in valPool
+    const long long* rValB;      // beta value region offset in valPool
+    const long long* rValCap;    // capacity (values) of each region
+    const char* seqPool;
+    // column slots
+    int2* aRange;
+    int* aOff;
+    double* aLs;
+    double* aPre;             // exclusive prefix of alpha log-scales (GetLogProdScales(0, k))
+    int2* bRange;
+    int* bOff;
+    double* bLs;
+    double* bSuf;             // GetLogProdScales(k, J+1) accumulated left to right (exact order)
+    double* valPool;
+    // per read results of the last fill
+    double* rBaseline;        // MutationScorer::Score() = log(beta(0,0)) + sum(beta log-scales)
+    int* rFlips;
+    int* rStatus;
+    // model constants
+    double prNot;             // ModelParams::PrNotMiscall
+    double prThird;           // ModelParams::PrThirdOfMiscall
+    double sdn;               // exp(BandingOptions::ScoreDiff)
+};
+
+// ---------------------------------------------------------------------------------------------
+// Template views: WrappedTemplateParameterPair over a TemplateParameterPair with an optional
+// virtual mutation (TemplateParameterPair.hpp:88-147, TemplateParameterPair.cpp:61-140).
+// Transition parameters are never stored per position: ctx(T[g], T[g+1]) is recomputed from the
+// bases, which is exactly what the reference keeps in trans_probs after any sequence of real edits.
+// ---------------------------------------------------------------------------------------------
+struct VirtualMut {
+    int mpos = kNoMutation;
+    int moff = 0;
+    char mb0 = '0', mb1 = '0';
+    int mc0 = kCtxZero, mc1 = kCtxZero;
+};
+
+struct TplView {
+    const char* T;   // strand template bases
+    int L;           // strand template length
+    int start;       // window start on this strand
+    int len;         // window length (unmutated)
+    VirtualMut vm;
+
+    __device__ __forceinline__ int Length() const
+    {
+        return (vm.mpos >= start && vm.mpos < start + len) ? len - vm.moff : len;
+    }
+    __device__ __forceinline__ void Plain(int g, char& b, int& c) const
+    {
+        b = T[g];
+        c = (g + 1 < L) ? context_index(T[g], T[g + 1]) : kCtxZero;
+    }
+    __device__ __forceinline__ void At(int idx, char& b, int& c) const
+    {
+        const int g = idx + start;
+        if (g < vm.mpos - 1) Plain(g, b, c);
+        else if (g > vm.mpos) Plain(g + vm.moff, b, c);   // also the no-mutation case (mpos = -100)
+        else if (g == vm.mpos) { b = vm.mb1; c = vm.mc1; }
+        else { b = vm.mb0; c = vm.mc0; }
+    }
+    __device__ __forceinline__ char Base(int idx) const
+    {
+        char b; int c;
+        At(idx, b, c);
+        return b;
+    }
+    __device__ __forceinline__ int Ctx(int idx) const
+    {
+        char b; int c;
+        At(idx, b, c);
+        return c;
+    }
+};
+
+// TemplateParameterPair::ApplyVirtualMutation (TemplateParameterPair.cpp:70-140) on strand template T.
+__device__ inline VirtualMut make_virtual(const char* T, int L, int type, int s, char nb)
+{
+    VirtualMut v;
+    v.mpos = s;
+    if (type == kSub) {
+        v.moff = 0;
+        v.mb1 = nb;
+        if (s > 0) { v.mb0 = T[s - 1]; v.mc0 = context_index(T[s - 1], nb); }
+        if (s + 1 < L) v.mc1 = context_index(nb, T[s + 1]);
+    } else if (type == kDel) {
+        v.moff = 1;
+        const int last = L - 1;
+        if (s > 0 && s < last) {
+            v.mb0 = T[s - 1];
+            v.mb1 = T[s + 1];
+            v.mc0 = context_index(T[s - 1], T[s + 1]);
+            v.mc1 = (s + 2 < L) ? context_index(T[s + 1], T[s + 2]) : kCtxZero;   // trans_probs[s + 1]
+        } else if (s == 0) {
+            v.mb1 = T[1];
+            v.mc1 = (2 < L) ? context_index(T[1], T[2]) : kCtxZero;
+        } else if (s == last) {
+            v.mb0 = T[s - 1];
+        }
+    } else {
+        v.moff = -1;
+        v.mb1 = nb;
+        if (s > 0) { v.mb0 = T[s - 1]; v.mc0 = context_index(T[s - 1], nb); }
+        if (s < L) v.mc1 = context_index(nb, T[s]);
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Band matrix storage for one read (ScaledSparseMatrixD semantics: cells outside a column's used
+// row range read as 0.0).  Alpha columns are stored top-down, beta columns bottom-up, so that each
+// fill appends its cells in the order it computes them.
+// ---------------------------------------------------------------------------------------------
+struct Band {
+    int2* range;
+    int* off;
+    double* ls;
+    double* val;
+    long long cap;
+};
+
+__device__ __forceinline__ double alpha_at(const Band& m, int i, int j)
+{
+    const int2 r = m.range[j];
+    return (i >= r.x && i < r.y) ? m.val[m.off[j] + (i - r.x)] : 0.0;
+}
+
+__device__ __forceinline__ double beta_at(const Band& m, int i, int j)
+{
+    const int2 r = m.range[j];
+    return (i >= r.x && i < r.y) ? m.val[m.off[j] + (r.y - 1 - i)] : 0.0;
+}
+
+struct Params {
+    const double* ctx;   // 9 x kCtxStride
+    double prNot, prThird, sdn;
+    __device__ __forceinline__ const double* P(int c) const { return ctx + c * kCtxStride; }
+};
+// field offsets inside a context slot
+constexpr int kM = 0, kS = 1, kB = 2, kD = 3, kS3 = 4;
+
+// ---------------------------------------------------------------------------------------------
+// FillAlpha (SimpleRecursor.cpp:60-181).  `guide` (nullable) is the other matrix's used ranges;
+// when `selfValid` the matrix's previous used ranges also widen the band (RangeGuide :728-757;
+// RowRange :693-726 never trims scaled columns, so only ranges are consulted).  Ranges are updated
+// in place column by column, after their old value has been read.  Returns the used-entry count,
+// or -1 on value-capacity overflow.
+// ---------------------------------------------------------------------------------------------
+template <class View>
+__device__ long long fill_alpha(const View& tv, const char* rd, int I, const Band& a, const int2* guide,
+                                bool selfValid, const Params& P)
+{
+    const int J = tv.Length();
+    if (a.cap < 1) return -1;
+    a.val[0] = 1.0;
+    a.range[0] = make_int2(0, 1);
+    a.off[0] = 0;
+    a.ls[0] = 0.0;
+    long long used = 1;
+    int hb = 1, he = 1;
+    int prevCtx = kCtxZero;
+    for (int j = 1; j < J; ++j) {
+        char curBase; int curCtx;
+        tv.At(j - 1, curBase, curCtx);
+        if (guide) {
+            const int2 g = guide[j];
+            if (g.x < g.y) { hb = min(g.x, hb); he = max(g.y, he); }
+        }
+        if (selfValid) {
+            const int2 o = a.range[j];
+            if (o.x < o.y) { hb = min(o.x, hb); he = max(o.y, he); }
+        }
+        const int reqEnd = min(I, he);
+        const char nextBase = tv.Base(j);
+        const double* cp = P.P(curCtx);
+        const double* pp = P.P(prevCtx);
+        const double pMatch = pp[kM], pDel = pp[kD];
+        const double cBranch = cp[kB], cStick3 = cp[kS3];
+        const int2 pr = a.range[j - 1];
+        const double* pv = a.val + a.off[j - 1] - pr.x;   // prev column: pv[i], i in [pr.x, pr.y)
+        double* cv = a.val + used - hb;                      // this column: cv[i], i in [hb, end)
+        const int b = hb;
+        double thr = 0.0, mx = 0.0, score = 0.0;
+        int i = b;
+        for (; i < I && (score >= thr || i < reqEnd); ++i) {
+            if (used + (i - b) >= a.cap) return -1;
+            const char rb = rd[i - 1];
+            const double diag = (i - 1 >= pr.x && i - 1 < pr.y) ? pv[i - 1] : 0.0;
+            const double mpe = diag * (rb == curBase ? P.prNot : P.prThird);
+            double move = 0.0;
+            if (i == 1 && j == 1) move = mpe;
+            else if (i != 1 && j != 1) move = mpe * pMatch;
+            score = 0.0 + move;
+            if (i > 1) {
+                const double up = (i - 1 >= b) ? cv[i - 1] : 0.0;
+                score = score + up * (rb == nextBase ? cBranch : cStick3);
+            }
+            if (j > 1) {
+                const double left = (i >= pr.x && i < pr.y) ? pv[i] : 0.0;
+                score = score + left * pDel;
+            }
+            cv[i] = score;
+            if (score > mx) { mx = score; thr = mx / P.sdn; }
+        }
+        const int e = i;
+        // ScaledMatrix::FinishEditingColumn (ScaledMatrix-inl.hpp:35-60); mx == max(0, cells).
+        if (mx != 0.0 && mx != 1.0) {
+            for (int k = b; k < e; ++k) cv[k] = cv[k] / mx;
+            a.ls[j] = log(mx);
+        } else {
+            a.ls[j] = 0.0;
+        }
+        a.range[j] = make_int2(b, e);
+        a.off[j] = (int)used;
+        used += e - b;
+        prevCtx = curCtx;
+        he = e;
+        int k = b;
+        while (k < e && cv[k] < thr) ++k;
+        hb = k;
+    }
+    // last column: pinned final match (:169-179)
+    if (used + 1 > a.cap) return -1;
+    const char lastBase = tv.Base(J - 1);
+    const double em = (rd[I - 1] == lastBase) ? P.prNot : P.prThird;
+    const double lik = alpha_at(a, I - 1, J - 1) * em;
+    const double c = (0.0 < lik) ? lik : 0.0;
+    double v = lik;
+    double ls = 0.0;
+    if (c != 0.0 && c != 1.0) { v = lik / c; ls = log(c); }
+    a.val[used] = v;
+    a.range[J] = make_int2(I, I + 1);
+    a.off[J] = (int)used;
+    a.ls[J] = ls;
+    used += 1;
+    return used;
+}
+
+// FillBeta (SimpleRecursor.cpp:183-296).  Same conventions as fill_alpha; values stored bottom-up.
+template <class View>
+__device__ long long fill_beta(const View& tv, const char* rd, int I, const Band& bm, const int2* guide,
+                               bool selfValid, const Params& P)
+{
+    const int J = tv.Length();
+    if (bm.cap < 1) return -1;
+    bm.val[0] = 1.0;
+    bm.range[J] = make_int2(I, I + 1);
+    bm.off[J] = 0;
+    bm.ls[J] = 0.0;
+    long long used = 1;
+    int hb = I, he = I;
+    for (int j = J - 1; j > 0; --j) {
+        const char nextBase = tv.Base(j);
+        const int curCtx = tv.Ctx(j - 1);
+        if (guide) {
+            const int2 g = guide[j];
+            if (g.x < g.y) { hb = min(g.x, hb); he = max(g.y, he); }
+        }
+        if (selfValid) {
+            const int2 o = bm.range[j];
+            if (o.x < o.y) { hb = min(o.x, hb); he = max(o.y, he); }
+        }
+        const int reqBegin = max(0, hb);
+        const double* cp = P.P(curCtx);
+        const double cMatch = cp[kM], cDel = cp[kD], cBranch = cp[kB], cStick3 = cp[kS3];
+        const int2 nr = bm.range[j + 1];
+        const double* nv = bm.val + bm.off[j + 1] + (nr.y - 1);   // next column: nv[-i], i in [nr.x, nr.y)
+        const int e = he;
+        double* cv = bm.val + used + (e - 1);                     // this column: cv[-i], i in (begin, e)
+        double thr = 0.0, mx = 0.0, score = 0.0;
+        int i = e - 1;
+        for (; i > 0 && (score >= thr || i >= reqBegin); --i) {
+            if (used + (e - 1 - i) >= bm.cap) return -1;
+            const char nb = rd[i];
+            const bool same = nb == nextBase;
+            const double diag = (i + 1 >= nr.x && i + 1 < nr.y) ? nv[-(i + 1)] : 0.0;
+            const double mpe = diag * (same ? P.prNot : P.prThird);
+            score = 0.0;
+            if (i < I - 1) score = 0.0 + mpe * cMatch;
+            else if (i == I - 1 && j == J - 1) score = 0.0 + mpe;
+            if (i < I - 1 && i > 0) {
+                const double up = (i + 1 <= e - 1) ? cv[-(i + 1)] : 0.0;
+                score = score + up * (same ? cBranch : cStick3);
+            }
+            if (j < J - 1 && j > 0) {
+                const double left = (i >= nr.x && i < nr.y) ? nv[-i] : 0.0;
+                score = score + left * cDel;
+            }
+            cv[-i] = score;
+            if (score > mx) { mx = score; thr = mx / P.sdn; }
+        }
+        const int b = i + 1;
+        if (mx != 0.0 && mx != 1.0) {
+            for (int k = b; k < e; ++k) cv[-k] = cv[-k] / mx;
+            bm.ls[j] = log(mx);
+        } else {
+            bm.ls[j] = 0.0;
+        }
+        bm.range[j] = make_int2(b, e);
+        bm.off[j] = (int)used;
+        used += e - b;
+        hb = b;
+        int k = e;
+        while (k > b && cv[-(k - 1)] < thr) --k;
+        he = k;
+    }
+    if (used + 1 > bm.cap) return -1;
+    const double em = (tv.Base(0) == rd[0]) ? P.prNot : P.prThird;
+    const double raw = em * beta_at(bm, 1, 1);
+    const double c = (0.0 < raw) ? raw : 0.0;
+    double v = raw;
+    double ls = 0.0;
+    if (c != 0.0 && c != 1.0) { v = raw / c; ls = log(c); }
+    bm.val[used] = v;
+    bm.range[0] = make_int2(0, 1);
+    bm.off[0] = (int)used;
+    bm.ls[0] = ls;
+    used += 1;
+    return used;
+}
+
+__device__ __forceinline__ double sum_ls(const double* ls, int n)
+{
+    double s = 0.0;   // std::accumulate from 0.0, left to right
+    for (int k = 0; k < n; ++k) s = s + ls[k];
+    return s;
+}
+
+}  // namespace pbccs

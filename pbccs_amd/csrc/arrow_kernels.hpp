@@ -1,0 +1,42 @@
+// pbccs_amd/csrc/arrow_kernels.hpp -- host-visible launch interface of arrow_kernels.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "arrow_device.hpp"
+
+namespace pbccs {
+
+// A scoring round: a list of work items, each = one ZMW with a contiguous list of mutation codes.
+struct ScoreWork {
+    int nWork = 0;
+    const int* zmw = nullptr;              // [nWork]
+    const int* nMut = nullptr;             // [nWork]
+    const long long* mutBase = nullptr;    // [nWork] offset of the item's codes / scores
+    const long long* deltaBase = nullptr;  // [nWork] offset of the item's (read x mutation) deltas
+    const long long* waveStart = nullptr;  // [nWork + 1] cumulative waves (reads x ceil(M / 64))
+    const long long* mutStart = nullptr;   // [nWork + 1] cumulative mutations
+    const long long* posStart = nullptr;   // [nWork + 1] cumulative template positions (QV rounds)
+    const int* codes = nullptr;
+    double* delta = nullptr;
+};
+
+// Bump-allocated scratch for the rare whole-window refill case (tiny windows).
+struct ScoreScratch {
+    double* pool = nullptr;
+    unsigned long long* top = nullptr;
+    unsigned long long cap = 0;
+    int* overflow = nullptr;
+};
+
+void launch_fill(const DevBatch& B, const int* reads, int n, hipStream_t s);
+void launch_suffix(const DevBatch& B, const int* reads, int n, hipStream_t s);
+void launch_enumerate(const DevBatch& B, const int* zmws, int n, const long long* mutBase, const long long* posBase,
+                      int* codes, int* posOff, hipStream_t s);
+void launch_score(const DevBatch& B, const ScoreWork& W, long long nWaves, const ScoreScratch& scratch, hipStream_t s);
+void launch_reduce(const DevBatch& B, const ScoreWork& W, long long nMut, double fastThr, double* score,
+                   unsigned char* fav, hipStream_t s);
+void launch_qv(const DevBatch& B, const ScoreWork& W, long long nPos, const long long* posBase, const int* posOff,
+               const double* score, const long long* qvBase, int* qv, hipStream_t s);
+
+}  // namespace pbccs

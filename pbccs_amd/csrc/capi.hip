@@ -1,0 +1,486 @@
+// pbccs_amd/csrc/capi.hip -- the C ABI (include/pbccs_amd.h) over ArrowBatch.
+#include "../../include/pbccs_amd.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "engine.hpp"
+
+using namespace pbccs;
+
+struct pbccs_engine {
+    int device = 0;
+    Counters counters;
+};
+
+struct pbccs_scorer {
+    pbccs_engine* eng = nullptr;
+    std::unique_ptr<ArrowBatch> batch;
+    pbccs_arrow_config cfg;
+    int z = 0;
+};
+
+namespace {
+
+thread_local std::string g_lastError;
+
+int fail(int code, const char* msg)
+{
+    g_lastError = msg ? msg : "";
+    return code;
+}
+
+template <class F>
+int guarded(F&& f)
+{
+    try {
+        return f();
+    } catch (const DeviceError& e) {
+        return fail(PBCCS_EDEVICE, e.what());
+    } catch (const std::bad_alloc&) {
+        return fail(PBCCS_EOOM, "out of memory");
+    } catch (const std::invalid_argument& e) {
+        return fail(PBCCS_EINVAL, e.what());
+    } catch (const std::out_of_range& e) {
+        return fail(PBCCS_EINVAL, e.what());
+    } catch (const std::exception& e) {
+        return fail(PBCCS_EDEVICE, e.what());
+    } catch (...) {
+        return fail(PBCCS_EDEVICE, "unknown failure");
+    }
+}
+
+ArrowOptions options_from(const pbccs_arrow_config* c)
+{
+    ArrowOptions o;
+    if (c) {
+        o.scoreDiff = c->score_diff;
+        o.fastScoreThreshold = c->fast_score_threshold;
+        o.addThreshold = c->add_threshold;
+    }
+    return o;
+}
+
+bool to_mutation(const pbccs_mutation& in, int L, Mutation* out)
+{
+    if (in.type < 0 || in.type > 2) return false;
+    const int width = in.end - in.start;
+    if (in.type == PBCCS_INSERTION ? width != 0 : width != 1) return false;   // single-base only
+    if (in.start < 0) return false;
+    if (in.type == PBCCS_INSERTION ? in.start > L : in.start >= L) return false;
+    if (in.type != PBCCS_DELETION && !(in.new_base == 'A' || in.new_base == 'C' || in.new_base == 'G' || in.new_base == 'T'))
+        return false;
+    *out = Mutation::Make(in.type, in.start, in.new_base);
+    return true;
+}
+
+bool read_scores(int ts, int te, const Mutation& m)   // MultiReadMutationScorer.cpp:70-80
+{
+    if (m.type == PBCCS_INSERTION) return ts <= m.end && m.start <= te;
+    return ts < m.end && m.start < te;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pbccs_last_error(void) { return g_lastError.c_str(); }
+
+int pbccs_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int pbccs_engine_create(int device, pbccs_engine** out)
+{
+    if (!out) return fail(PBCCS_EINVAL, "null out");
+    return guarded([&] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+            return fail(PBCCS_EDEVICE, "no such HIP device");
+        if (hipSetDevice(device) != hipSuccess) return fail(PBCCS_EDEVICE, "hipSetDevice failed");
+        pbccs_engine* e = new pbccs_engine();
+        e->device = device;
+        *out = e;
+        return PBCCS_OK;
+    });
+}
+
+void pbccs_engine_destroy(pbccs_engine* eng) { delete eng; }
+
+int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset)
+{
+    if (!eng || !out) return fail(PBCCS_EINVAL, "null argument");
+    out->fill_launches = eng->counters.fillLaunches;
+    out->score_launches = eng->counters.scoreLaunches;
+    out->score_tasks = eng->counters.scoreTasks;
+    out->mutations = eng->counters.mutations;
+    if (reset) eng->counters = Counters();
+    return PBCCS_OK;
+}
+
+// ---- scorer ---------------------------------------------------------------------------------------
+int pbccs_scorer_create(pbccs_engine* eng, const pbccs_arrow_config* cfg, const char* tpl, int tpl_len,
+                        pbccs_scorer** out)
+{
+    if (!eng || !cfg || !tpl || tpl_len <= 0 || !out) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::unique_ptr<pbccs_scorer> s(new pbccs_scorer());
+        s->eng = eng;
+        s->cfg = *cfg;
+        s->batch.reset(new ArrowBatch(eng->device));
+        s->z = s->batch->AddZmw(std::string(tpl, tpl_len), cfg->snr, options_from(cfg));
+        *out = s.release();
+        return PBCCS_OK;
+    });
+}
+
+void pbccs_scorer_destroy(pbccs_scorer* s) { delete s; }
+
+int pbccs_scorer_add_read(pbccs_scorer* s, const char* seq, int len, int strand, int tstart, int tend,
+                          double threshold, int* result)
+{
+    if (!s || !seq || len < 0 || !result || (strand != 0 && strand != 1)) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        ArrowBatch& B = *s->batch;
+        const int r = B.AppendRead(s->z, std::string(seq, len), strand, tstart, tend);
+        B.FillReads({r});
+        *result = B.FinishAddRead(r, threshold);
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_scorer_score_many(pbccs_scorer* s, const pbccs_mutation* m, int n, double fast_threshold, double* scores)
+{
+    if (!s || (n > 0 && (!m || !scores)) || n < 0) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        ArrowBatch& B = *s->batch;
+        const int L = (int)B.Template(s->z).size();
+        std::vector<std::vector<int>> codes(1);
+        for (int i = 0; i < n; ++i) {
+            Mutation mu;
+            if (!to_mutation(m[i], L, &mu)) return fail(PBCCS_EINVAL, "invalid single-base mutation");
+            codes[0].push_back(mutation_code(mu));
+        }
+        if (n == 0) return PBCCS_OK;
+        std::vector<std::vector<double>> sc;
+        B.ScoreLists({s->z}, codes, fast_threshold, &sc);
+        for (int i = 0; i < n; ++i) scores[i] = sc[0][i];
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_scorer_score(pbccs_scorer* s, const pbccs_mutation* m, double fast_threshold, double* score)
+{
+    return pbccs_scorer_score_many(s, m, 1, fast_threshold, score);
+}
+
+int pbccs_scorer_scores(pbccs_scorer* s, const pbccs_mutation* m, double unscored, double* per_read)
+{
+    if (!s || !m || !per_read) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        ArrowBatch& B = *s->batch;
+        Mutation mu;
+        if (!to_mutation(*m, (int)B.Template(s->z).size(), &mu)) return fail(PBCCS_EINVAL, "invalid mutation");
+        std::vector<std::vector<double>> sc, pr;
+        B.ScoreLists({s->z}, {{mutation_code(mu)}}, -std::numeric_limits<double>::max(), &sc, &pr);
+        const int nr = B.NumReads(s->z);
+        for (int k = 0; k < nr; ++k) {
+            const int r = B.ReadIndex(s->z, k);
+            const bool scored = B.ReadActive(r) && read_scores(B.ReadTs(r), B.ReadTe(r), mu);
+            per_read[k] = scored ? pr[0][k] : unscored;
+        }
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_scorer_is_favorable(pbccs_scorer* s, const pbccs_mutation* m, int fast, int* favorable)
+{
+    if (!s || !favorable) return fail(PBCCS_EINVAL, "bad argument");
+    double v = 0.0;
+    const double thr = fast ? s->cfg.fast_score_threshold : -std::numeric_limits<double>::max();
+    const int rc = pbccs_scorer_score(s, m, thr, &v);
+    if (rc != PBCCS_OK) return rc;
+    *favorable = v > kMinFavorableScoreDiff ? 1 : 0;
+    return PBCCS_OK;
+}
+
+int pbccs_scorer_apply_mutations(pbccs_scorer* s, const pbccs_mutation* m, int n)
+{
+    if (!s || n < 0 || (n > 0 && !m)) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        ArrowBatch& B = *s->batch;
+        const int L = (int)B.Template(s->z).size();
+        std::vector<Mutation> muts;
+        for (int i = 0; i < n; ++i) {
+            Mutation mu;
+            if (!to_mutation(m[i], L, &mu)) return fail(PBCCS_EINVAL, "invalid mutation");
+            muts.push_back(mu);
+        }
+        if (!B.ApplyMutations(s->z, muts)) return fail(PBCCS_EINVAL, "mutation outside the template");
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_scorer_template(pbccs_scorer* s, int strand, char* out, int cap, int* len)
+{
+    if (!s || !len) return fail(PBCCS_EINVAL, "bad argument");
+    const std::string t = strand == PBCCS_FORWARD_STRAND ? s->batch->Template(s->z) : s->batch->TemplateRev(s->z);
+    *len = (int)t.size();
+    if (!out || cap < (int)t.size() + 1) return fail(PBCCS_ERANGE, "buffer too small");
+    std::memcpy(out, t.c_str(), t.size() + 1);
+    return PBCCS_OK;
+}
+
+int pbccs_scorer_template_length(pbccs_scorer* s) { return s ? (int)s->batch->Template(s->z).size() : -1; }
+
+int pbccs_scorer_num_reads(pbccs_scorer* s) { return s ? s->batch->NumReads(s->z) : -1; }
+
+int pbccs_scorer_read_info(pbccs_scorer* s, int i, int* active, int* strand, int* tstart, int* tend)
+{
+    if (!s || i < 0 || i >= s->batch->NumReads(s->z)) return fail(PBCCS_EINVAL, "bad read index");
+    const int r = s->batch->ReadIndex(s->z, i);
+    if (active) *active = s->batch->ReadActive(r) ? 1 : 0;
+    if (strand) *strand = s->batch->ReadStrand(r);
+    if (tstart) *tstart = s->batch->ReadTs(r);
+    if (tend) *tend = s->batch->ReadTe(r);
+    return PBCCS_OK;
+}
+
+int pbccs_scorer_baseline_score(pbccs_scorer* s, double* score)
+{
+    if (!s || !score) return fail(PBCCS_EINVAL, "bad argument");
+    *score = s->batch->BaselineScore(s->z);
+    return PBCCS_OK;
+}
+
+int pbccs_scorer_baseline_scores(pbccs_scorer* s, double* out, int cap, int* n)
+{
+    if (!s || !n) return fail(PBCCS_EINVAL, "bad argument");
+    std::vector<double> v;
+    for (int k = 0; k < s->batch->NumReads(s->z); ++k) {
+        const int r = s->batch->ReadIndex(s->z, k);
+        if (s->batch->ReadActive(r)) v.push_back(s->batch->ReadScore(r));
+    }
+    *n = (int)v.size();
+    if (!out || cap < (int)v.size()) return fail(PBCCS_ERANGE, "buffer too small");
+    std::copy(v.begin(), v.end(), out);
+    return PBCCS_OK;
+}
+
+int pbccs_scorer_zscores(pbccs_scorer* s, double* zg, double* za, double* per_read)
+{
+    if (!s || !zg || !za) return fail(PBCCS_EINVAL, "bad argument");
+    std::vector<double> zs;
+    s->batch->ZScores(s->z, zg, za, &zs);
+    if (per_read) std::copy(zs.begin(), zs.end(), per_read);
+    return PBCCS_OK;
+}
+
+int pbccs_scorer_num_flipflops(pbccs_scorer* s, int* out)
+{
+    if (!s || !out) return fail(PBCCS_EINVAL, "bad argument");
+    for (int k = 0; k < s->batch->NumReads(s->z); ++k) out[k] = s->batch->ReadFlips(s->batch->ReadIndex(s->z, k));
+    return PBCCS_OK;
+}
+
+int pbccs_refine_consensus(pbccs_scorer* s, const pbccs_refine_options* opts, long long* n_tested,
+                           long long* n_applied, int* converged)
+{
+    if (!s || !n_tested || !n_applied || !converged) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        RefineOptions ro;
+        if (opts) {
+            ro.maxIterations = opts->max_iterations;
+            ro.mutationSeparation = opts->mutation_separation;
+            ro.mutationNeighborhood = opts->mutation_neighborhood;
+        }
+        std::vector<int> conv;
+        std::vector<long long> nt, na;
+        s->batch->Refine({s->z}, ro, &conv, &nt, &na);
+        *n_tested += nt[0];
+        *n_applied += na[0];
+        if (conv[0] < 0) return fail(PBCCS_EINVAL, "mutation could not be applied");
+        *converged = conv[0];
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_consensus_qvs(pbccs_scorer* s, int* qvs, int cap, int* n)
+{
+    if (!s || !n) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::vector<std::vector<int>> q;
+        s->batch->QVs({s->z}, &q);
+        *n = (int)q[0].size();
+        if (!qvs || cap < *n) return fail(PBCCS_ERANGE, "buffer too small");
+        std::copy(q[0].begin(), q[0].end(), qvs);
+        return PBCCS_OK;
+    });
+}
+
+// ---- batched polish -------------------------------------------------------------------------------
+void pbccs_polish_options_default(pbccs_polish_options* o)
+{
+    if (!o) return;
+    o->min_passes = 3;
+    o->min_length = 10;
+    o->min_zscore = -5.0;
+    o->max_drop_fraction = 0.34;
+    o->min_predicted_accuracy = 0.90;
+    o->score_diff = 12.5;
+    o->refine.max_iterations = 40;
+    o->refine.mutation_separation = 10;
+    o->refine.mutation_neighborhood = 20;
+    o->zmws_per_batch = 0;
+}
+
+static int polish_chunk(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options& o,
+                        pbccs_zmw_output* out)
+{
+    ArrowBatch B(eng->device);
+    ArrowOptions ao;
+    ao.scoreDiff = o.score_diff;
+    std::vector<int> zOf(n, -1);
+    std::vector<std::vector<int>> readOf(n);
+    std::vector<int> allReads;
+    for (int i = 0; i < n; ++i) {
+        pbccs_zmw_output& q = out[i];
+        q.status = PBCCS_ZMW_OTHER;
+        q.consensus_len = 0;
+        q.zg = q.za = std::numeric_limits<double>::quiet_NaN();
+        q.predicted_accuracy = 0.0;
+        q.n_tested = q.n_applied = 0;
+        q.n_passes = 0;
+        for (int k = 0; k < 5; ++k) q.status_counts[k] = 0;
+        for (int k = 0; k < in[i].n_reads; ++k) {
+            if (q.add_read_results) q.add_read_results[k] = -1;
+            if (q.zscores) q.zscores[k] = std::numeric_limits<double>::quiet_NaN();
+        }
+        const pbccs_zmw_input& z = in[i];
+        if (z.n_reads <= 0) { q.status = PBCCS_ZMW_NO_SUBREADS; continue; }
+        if (z.draft_len < o.min_length) { q.status = PBCCS_ZMW_TOO_SHORT; continue; }
+        const std::string draft(z.draft, z.draft_len);
+        if (!is_acgt(draft)) { q.status = PBCCS_ZMW_OTHER; continue; }
+        zOf[i] = B.AddZmw(draft, z.snr, ao);
+        for (int k = 0; k < z.n_reads; ++k) {
+            int r = -1;
+            if (z.tstarts[k] >= 0 && z.tends[k] <= z.draft_len && z.tstarts[k] < z.tends[k] && z.lens[k] > 0)
+                r = B.AppendRead(zOf[i], std::string(z.seqs[k], z.lens[k]), z.strands[k] ? 1 : 0, z.tstarts[k],
+                                 z.tends[k]);
+            readOf[i].push_back(r);
+            if (r >= 0) allReads.push_back(r);
+        }
+    }
+    B.FillReads(allReads);
+    std::vector<int> refineZ, refineIdx;
+    for (int i = 0; i < n; ++i) {
+        if (zOf[i] < 0) continue;
+        pbccs_zmw_output& q = out[i];
+        const pbccs_zmw_input& z = in[i];
+        int nPasses = 0, nDropped = 0;
+        for (int k = 0; k < z.n_reads; ++k) {
+            const int r = readOf[i][k];
+            const int st = (r >= 0) ? B.FinishAddRead(r, o.min_zscore) : PBCCS_ADD_OTHER;
+            if (q.add_read_results) q.add_read_results[k] = st;
+            q.status_counts[st] += 1;
+            const bool full = z.full_pass ? z.full_pass[k] != 0 : true;
+            if (st == PBCCS_ADD_SUCCESS && full) ++nPasses;
+            else if (st != PBCCS_ADD_SUCCESS) ++nDropped;
+        }
+        q.n_passes = nPasses;
+        if (nPasses < o.min_passes) { q.status = PBCCS_ZMW_TOO_FEW_PASSES; continue; }
+        const double frac = (double)nDropped / z.n_reads;
+        if (frac > o.max_drop_fraction) { q.status = PBCCS_ZMW_TOO_MANY_UNUSABLE; continue; }
+        std::vector<double> zs;
+        B.ZScores(zOf[i], &q.zg, &q.za, &zs);
+        if (q.zscores) {
+            int j = 0;
+            for (int k = 0; k < z.n_reads; ++k)
+                if (readOf[i][k] >= 0) q.zscores[k] = zs[j++];
+        }
+        refineZ.push_back(zOf[i]);
+        refineIdx.push_back(i);
+    }
+    RefineOptions ro;
+    ro.maxIterations = o.refine.max_iterations;
+    ro.mutationSeparation = o.refine.mutation_separation;
+    ro.mutationNeighborhood = o.refine.mutation_neighborhood;
+    std::vector<int> conv;
+    std::vector<long long> nt, na;
+    B.Refine(refineZ, ro, &conv, &nt, &na);
+    std::vector<int> qvZ, qvIdx;
+    for (size_t k = 0; k < refineZ.size(); ++k) {
+        pbccs_zmw_output& q = out[refineIdx[k]];
+        q.n_tested = nt[k];
+        q.n_applied = na[k];
+        if (conv[k] == 1) { qvZ.push_back(refineZ[k]); qvIdx.push_back(refineIdx[k]); }
+        else q.status = conv[k] < 0 ? PBCCS_ZMW_OTHER : PBCCS_ZMW_NON_CONVERGENT;
+    }
+    std::vector<std::vector<int>> qvs;
+    B.QVs(qvZ, &qvs);
+    for (size_t k = 0; k < qvZ.size(); ++k) {
+        pbccs_zmw_output& q = out[qvIdx[k]];
+        const std::string& t = B.Template(qvZ[k]);
+        double acc = 0.0;   // Consensus.h:506-512
+        for (int v : qvs[k]) acc += std::pow(10.0, static_cast<double>(v) / -10.0);
+        acc = 1.0 - acc / qvs[k].size();
+        q.predicted_accuracy = acc;
+        if ((int)t.size() + 1 > q.consensus_cap || !q.consensus) {
+            q.consensus_len = -(int)t.size();
+            q.status = PBCCS_ZMW_OTHER;
+            continue;
+        }
+        std::memcpy(q.consensus, t.c_str(), t.size() + 1);
+        q.consensus_len = (int)t.size();
+        if (q.qvs) std::copy(qvs[k].begin(), qvs[k].end(), q.qvs);
+        q.status = (acc < o.min_predicted_accuracy) ? PBCCS_ZMW_POOR_QUALITY : PBCCS_ZMW_SUCCESS;
+    }
+    const Counters& c = B.counters();
+    eng->counters.fillLaunches += c.fillLaunches;
+    eng->counters.scoreLaunches += c.scoreLaunches;
+    eng->counters.scoreTasks += c.scoreTasks;
+    eng->counters.mutations += c.mutations;
+    return PBCCS_OK;
+}
+
+int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
+                       pbccs_zmw_output* out)
+{
+    if (!eng || n < 0 || (n > 0 && (!in || !out))) return fail(PBCCS_EINVAL, "bad argument");
+    pbccs_polish_options o;
+    pbccs_polish_options_default(&o);
+    if (opts) o = *opts;
+    return guarded([&] {
+        if (hipSetDevice(eng->device) != hipSuccess) return fail(PBCCS_EDEVICE, "hipSetDevice failed");
+        int per = o.zmws_per_batch;
+        if (per <= 0) {
+            // memory budget: ~2 band regions of 32 rows x window per read + the round's delta buffer
+            const double budget = 96.0 * (1ull << 30);
+            double bytes = 0.0;
+            for (int i = 0; i < n; ++i)
+                for (int k = 0; k < in[i].n_reads; ++k) bytes += (double)in[i].draft_len * (2 * 32 * 8 * 1.25 + 80 + 8 * 8);
+            const double perZmw = n > 0 ? bytes / n : 1.0;
+            per = (int)std::max(1.0, std::min((double)n, budget / std::max(perZmw, 1.0)));
+        }
+        for (int b = 0; b < n; b += per) {
+            const int m = std::min(per, n - b);
+            const int rc = polish_chunk(eng, in + b, m, o, out + b);
+            if (rc != PBCCS_OK) return rc;
+        }
+        return PBCCS_OK;
+    });
+}
+
+}  // extern "C"

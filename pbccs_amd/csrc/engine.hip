@@ -1,0 +1,739 @@
+// pbccs_amd/csrc/engine.hip -- ArrowBatch: HBM residency + orchestration of the polishing rounds.
+#include "engine.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <stdexcept>
+#include <unordered_set>
+
+namespace pbccs {
+
+#define PBCCS_HIP(x)                                                         \
+    do {                                                                     \
+        hipError_t e_ = (x);                                                 \
+        if (e_ != hipSuccess) throw DeviceError(hipGetErrorString(e_));      \
+    } while (0)
+
+template <class T>
+void DevVec<T>::reserve(size_t n, bool keep)
+{
+    if (n <= cap) return;
+    const size_t nc = std::max(n, cap + cap / 2 + 256);
+    T* p = nullptr;
+    PBCCS_HIP(hipMalloc(&p, nc * sizeof(T)));
+    if (keep && ptr && cap) {
+        PBCCS_HIP(hipDeviceSynchronize());
+        PBCCS_HIP(hipMemcpy(p, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice));
+    }
+    if (ptr) {
+        PBCCS_HIP(hipDeviceSynchronize());
+        (void)hipFree(ptr);
+    }
+    ptr = p;
+    cap = nc;
+}
+
+template <class T>
+void DevVec<T>::release()
+{
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+}
+
+namespace {
+
+constexpr int kInitialBandHeight = 32;         // value capacity per column on first allocation
+constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
+
+template <class T>
+void upload(DevVec<T>& d, const std::vector<T>& h, hipStream_t s)
+{
+    d.reserve(std::max<size_t>(h.size(), 1), false);
+    if (!h.empty()) PBCCS_HIP(hipMemcpyAsync(d.ptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
+}
+
+template <class T>
+void download(std::vector<T>& h, const DevVec<T>& d, size_t n, hipStream_t s)
+{
+    h.resize(n);
+    if (n) PBCCS_HIP(hipMemcpyAsync(h.data(), d.ptr, n * sizeof(T), hipMemcpyDeviceToHost, s));
+}
+
+}  // namespace
+
+ArrowBatch::ArrowBatch(int device) : device_(device)
+{
+    PBCCS_HIP(hipSetDevice(device_));
+    PBCCS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    dScratch_.reserve(kInitialScratch, false);
+    dScratchTop_.reserve(1, false);
+    dScratchOverflow_.reserve(1, false);
+}
+
+ArrowBatch::~ArrowBatch()
+{
+    if (stream_) {
+        (void)hipStreamSynchronize(stream_);
+        (void)hipStreamDestroy(stream_);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host description
+// ------------------------------------------------------------------------------------------------
+int ArrowBatch::AddZmw(const std::string& tpl, const double snr[4], const ArrowOptions& opt)
+{
+    if (tpl.empty() || !is_acgt(tpl)) throw std::invalid_argument("template must be a non-empty ACGT string");
+    if (!(opt.scoreDiff >= 0.0)) throw std::invalid_argument("ScoreDiff must be positive!");   // ArrowConfig.hpp:72-77
+    HZmw z;
+    z.tpl = tpl;
+    transition_table(snr, z.trans);
+    device_context_table(z.trans, z.ctx);
+    for (int k = 0; k < 9; ++k) {
+        const std::pair<double, double> mv = expected_context_ll(k < 8 ? z.trans[k] : TransParams(), kMismatchProbability);
+        z.ctxMeanVar[k][0] = mv.first;
+        z.ctxMeanVar[k][1] = mv.second;
+    }
+    z.opt = opt;
+    z.readBegin = (int)reads_.size();
+    z.nReads = 0;
+    const int L = (int)tpl.size();
+    z.tplCap = L + L / 4 + 64;
+    z.tplOff = tplTop_;
+    tplTop_ += 2LL * z.tplCap;
+    zmws_.push_back(z);
+    UploadTemplate((int)zmws_.size() - 1);
+    descDirty_ = true;
+    return (int)zmws_.size() - 1;
+}
+
+int ArrowBatch::AppendRead(int z, const std::string& seq, int strand, int ts, int te)
+{
+    if (z != (int)zmws_.size() - 1) throw std::invalid_argument("reads must be appended to the latest ZMW");
+    const int L = (int)zmws_[z].tpl.size();
+    if (ts < 0 || te > L || ts > te) throw std::invalid_argument("read window outside the template");
+    HRead r;
+    r.seq = seq;
+    r.strand = strand;
+    r.ts = ts;
+    r.te = te;
+    r.zmw = z;
+    r.seqOff = seqTop_;
+    seqTop_ += (long long)seq.size() + 1;
+    hSeq_.insert(hSeq_.end(), seq.begin(), seq.end());
+    hSeq_.push_back('\0');
+    const int J = te - ts;
+    r.colCap = J + J / 4 + 66;
+    r.colBase = colTop_;
+    colTop_ += r.colCap;
+    r.valCap = (long long)r.colCap * kInitialBandHeight;
+    r.valA = valTop_;
+    r.valB = valTop_ + r.valCap;
+    valTop_ += 2 * r.valCap;
+    reads_.push_back(r);
+    zmws_[z].nReads += 1;
+    descDirty_ = true;
+    return (int)reads_.size() - 1;
+}
+
+void ArrowBatch::UploadTemplate(int zi)
+{
+    HZmw& z = zmws_[zi];
+    const int L = (int)z.tpl.size();
+    if (L > z.tplCap) {
+        z.tplCap = L + L / 4 + 64;
+        z.tplOff = tplTop_;
+        tplTop_ += 2LL * z.tplCap;
+        descDirty_ = true;
+    }
+    if ((long long)hTpl_.size() < tplTop_) hTpl_.resize(tplTop_);
+    std::memcpy(&hTpl_[z.tplOff], z.tpl.data(), L);
+    const std::string rc = reverse_complement(z.tpl);
+    std::memcpy(&hTpl_[z.tplOff + z.tplCap], rc.data(), L);
+    descDirty_ = true;
+}
+
+void ArrowBatch::EnsureCapacity(int ri)
+{
+    HRead& r = reads_[ri];
+    const int J = r.te - r.ts;
+    if (J + 2 > r.colCap) {
+        r.colCap = J + J / 4 + 66;
+        r.colBase = colTop_;
+        colTop_ += r.colCap;
+        if ((long long)r.colCap * kInitialBandHeight > r.valCap) {
+            r.valCap = (long long)r.colCap * kInitialBandHeight;
+            r.valA = valTop_;
+            r.valB = valTop_ + r.valCap;
+            valTop_ += 2 * r.valCap;
+        }
+        descDirty_ = true;
+    }
+}
+
+void ArrowBatch::UploadDescriptors()
+{
+    if (!descDirty_) return;
+    const int Z = (int)zmws_.size(), R = (int)reads_.size();
+    std::vector<int> zf(Z), zr(Z), zl(Z), zb(Z), zn(Z);
+    std::vector<double> zc((size_t)Z * 45);
+    for (int i = 0; i < Z; ++i) {
+        const HZmw& z = zmws_[i];
+        zf[i] = (int)z.tplOff;
+        zr[i] = (int)(z.tplOff + z.tplCap);
+        zl[i] = (int)z.tpl.size();
+        zb[i] = z.readBegin;
+        zn[i] = z.nReads;
+        std::memcpy(&zc[(size_t)i * 45], z.ctx, sizeof(z.ctx));
+    }
+    std::vector<long long> so(R), cb(R), va(R), vb(R), vc(R);
+    std::vector<int> rl(R), rs(R), rts(R), rte(R), ra(R), rz(R);
+    for (int i = 0; i < R; ++i) {
+        const HRead& r = reads_[i];
+        so[i] = r.seqOff;
+        cb[i] = r.colBase;
+        va[i] = r.valA;
+        vb[i] = r.valB;
+        vc[i] = r.valCap;
+        rl[i] = (int)r.seq.size();
+        rs[i] = r.strand;
+        rts[i] = r.ts;
+        rte[i] = r.te;
+        ra[i] = r.active ? 1 : 0;
+        rz[i] = r.zmw;
+    }
+    upload(dZFwd_, zf, stream_);
+    upload(dZRev_, zr, stream_);
+    upload(dZLen_, zl, stream_);
+    upload(dZReadBegin_, zb, stream_);
+    upload(dZNReads_, zn, stream_);
+    upload(dZCtx_, zc, stream_);
+    upload(dRSeqOff_, so, stream_);
+    upload(dRColBase_, cb, stream_);
+    upload(dRValA_, va, stream_);
+    upload(dRValB_, vb, stream_);
+    upload(dRValCap_, vc, stream_);
+    upload(dRLen_, rl, stream_);
+    upload(dRStrand_, rs, stream_);
+    upload(dRTs_, rts, stream_);
+    upload(dRTe_, rte, stream_);
+    upload(dRActive_, ra, stream_);
+    upload(dRZmw_, rz, stream_);
+    // pools (templates re-uploaded whole: they change every refine round)
+    upload(dTpl_, hTpl_, stream_);
+    dSeq_.reserve(std::max<size_t>(hSeq_.size(), 1), true);
+    if (hSeq_.size() > seqUploaded_) {
+        PBCCS_HIP(hipMemcpyAsync(dSeq_.ptr + seqUploaded_, hSeq_.data() + seqUploaded_, hSeq_.size() - seqUploaded_,
+                                 hipMemcpyHostToDevice, stream_));
+        seqUploaded_ = hSeq_.size();
+    }
+    const size_t cols = std::max<long long>(colTop_, 1);
+    dARange_.reserve(cols, true);
+    dBRange_.reserve(cols, true);
+    dAOff_.reserve(cols, true);
+    dBOff_.reserve(cols, true);
+    dALs_.reserve(cols, true);
+    dBLs_.reserve(cols, true);
+    dAPre_.reserve(cols, true);
+    dBSuf_.reserve(cols, true);
+    dVal_.reserve(std::max<long long>(valTop_, 1), true);
+    dRBaseline_.reserve(std::max(R, 1), true);
+    dRFlips_.reserve(std::max(R, 1), true);
+    dRStatus_.reserve(std::max(R, 1), true);
+    PBCCS_HIP(hipStreamSynchronize(stream_));   // host vectors above are temporaries
+    descDirty_ = false;
+}
+
+DevBatch ArrowBatch::View() const
+{
+    DevBatch b;
+    b.zFwdOff = dZFwd_.ptr;
+    b.zRevOff = dZRev_.ptr;
+    b.zLen = dZLen_.ptr;
+    b.zCtx = dZCtx_.ptr;
+    b.zReadBegin = dZReadBegin_.ptr;
+    b.zNReads = dZNReads_.ptr;
+    b.tplPool = dTpl_.ptr;
+    b.rSeqOff = dRSeqOff_.ptr;
+    b.rLen = dRLen_.ptr;
+    b.rStrand = dRStrand_.ptr;
+    b.rTs = dRTs_.ptr;
+    b.rTe = dRTe_.ptr;
+    b.rActive = dRActive_.ptr;
+    b.rZmw = dRZmw_.ptr;
+    b.rColBase = dRColBase_.ptr;
+    b.rValA = dRValA_.ptr;
+    b.rValB = dRValB_.ptr;
+    b.rValCap = dRValCap_.ptr;
+    b.seqPool = dSeq_.ptr;
+    b.aRange = dARange_.ptr;
+    b.aOff = dAOff_.ptr;
+    b.aLs = dALs_.ptr;
+    b.aPre = dAPre_.ptr;
+    b.bRange = dBRange_.ptr;
+    b.bOff = dBOff_.ptr;
+    b.bLs = dBLs_.ptr;
+    b.bSuf = dBSuf_.ptr;
+    b.valPool = dVal_.ptr;
+    b.rBaseline = dRBaseline_.ptr;
+    b.rFlips = dRFlips_.ptr;
+    b.rStatus = dRStatus_.ptr;
+    b.prNot = 1.0 - kMismatchProbability;
+    b.prThird = kMismatchProbability / 3.0;
+    b.sdn = zmws_.empty() ? std::exp(12.5) : std::exp(zmws_[0].opt.scoreDiff);
+    return b;
+}
+
+// ------------------------------------------------------------------------------------------------
+// fills
+// ------------------------------------------------------------------------------------------------
+void ArrowBatch::FillReads(const std::vector<int>& readsIn)
+{
+    std::vector<int> todo(readsIn);
+    for (int r : todo) EnsureCapacity(r);
+    for (int attempt = 0; !todo.empty(); ++attempt) {
+        if (attempt > 12) throw DeviceError("band storage keeps overflowing");
+        UploadDescriptors();
+        upload(dList_, todo, stream_);
+        const DevBatch B = View();
+        launch_fill(B, dList_.ptr, (int)todo.size(), stream_);
+        launch_suffix(B, dList_.ptr, (int)todo.size(), stream_);
+        PBCCS_HIP(hipGetLastError());
+        counters_.fillLaunches += 1;
+        const size_t R = reads_.size();
+        std::vector<int> st, fl;
+        std::vector<double> bl;
+        download(st, dRStatus_, R, stream_);
+        download(fl, dRFlips_, R, stream_);
+        download(bl, dRBaseline_, R, stream_);
+        PBCCS_HIP(hipStreamSynchronize(stream_));
+        std::vector<int> again;
+        for (int r : todo) {
+            HRead& h = reads_[r];
+            if (st[r] == kFillOverflow) {
+                h.valCap *= 2;   // move to fresh, larger regions and refill
+                h.valA = valTop_;
+                h.valB = valTop_ + h.valCap;
+                valTop_ += 2 * h.valCap;
+                descDirty_ = true;
+                again.push_back(r);
+                continue;
+            }
+            h.status = st[r];
+            h.flips = fl[r];
+            h.baseline = bl[r];
+            h.filled = true;
+        }
+        todo.swap(again);
+    }
+}
+
+void ArrowBatch::MeanVar(const HZmw& z, int strand, int ts, int te, double* mean, double* var) const
+{
+    const std::string t = strand == kFwd ? z.tpl : reverse_complement(z.tpl);
+    const int L = (int)t.size();
+    double m = 0.0, v = 0.0;
+    for (int i = ts; i < te - 1; ++i) {
+        const int c = (i + 1 < L) ? context_index(t[i], t[i + 1]) : kCtxZero;
+        m += z.ctxMeanVar[c][0];
+        v += z.ctxMeanVar[c][1];
+    }
+    *mean = m;
+    *var = v;
+}
+
+int ArrowBatch::FinishAddRead(int ri, double threshold)
+{
+    // MultiReadMutationScorer::AddRead (MultiReadMutationScorer.cpp:275-325)
+    HRead& r = reads_[ri];
+    int res = kSuccess;
+    if (r.status == kFillBadInput) res = kOther;
+    else if (r.status == kFillMismatch || std::isinf(r.baseline)) res = kAlphaBetaMismatch;   // MutationScorer.cpp:68-69
+    if (res == kSuccess && !std::isnan(threshold)) {
+        double mean = 0.0, var = 0.0;
+        MeanVar(zmws_[r.zmw], r.strand, r.ts, r.te, &mean, &var);
+        const double ll = r.baseline;
+        const double z = (ll - mean) / std::sqrt(var);
+        if (!std::isfinite(ll) || !std::isfinite(z) || z < threshold) res = kPoorZScore;
+    }
+    r.active = res == kSuccess;
+    descDirty_ = true;
+    return res;
+}
+
+double ArrowBatch::BaselineScore(int zi) const
+{
+    const HZmw& z = zmws_[zi];
+    double s = 0.0;
+    for (int k = 0; k < z.nReads; ++k) {
+        const HRead& r = reads_[z.readBegin + k];
+        if (r.active) s += r.baseline;
+    }
+    return s;
+}
+
+void ArrowBatch::ZScores(int zi, double* zg, double* za, std::vector<double>* zs) const
+{
+    // MultiReadMutationScorer::ZScores (MultiReadMutationScorer.hpp:208-263)
+    const HZmw& z = zmws_[zi];
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    zs->clear();
+    double gmean = 0.0, gvar = 0.0;
+    size_t n = 0;
+    for (int k = 0; k < z.nReads; ++k) {
+        const HRead& r = reads_[z.readBegin + k];
+        if (!r.active) { zs->push_back(nan); continue; }
+        n += 1;
+        const int s = r.ts, e = r.te - 1;
+        if (e - s < 1) { zs->push_back(nan); continue; }
+        double mu = 0.0, var = 0.0;
+        MeanVar(z, r.strand, r.ts, r.te, &mu, &var);
+        gmean += mu;
+        gvar += var;
+        zs->push_back((r.baseline - mu) / std::sqrt(var));
+    }
+    const double gs = BaselineScore(zi);
+    *zg = (gvar == 0.0) ? nan : (gs - gmean) / std::sqrt(gvar);
+    *za = (n == 0 || gvar == 0.0) ? nan : (gs / n - gmean / n) / std::sqrt(gvar / n);
+}
+
+// ------------------------------------------------------------------------------------------------
+// scoring rounds
+// ------------------------------------------------------------------------------------------------
+void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vector<int>>* codes, double fastThr,
+                          bool needPositions)
+{
+    UploadDescriptors();
+    const int n = (int)zl.size();
+    rNMut_.assign(n, 0);
+    rMutStart_.assign(n + 1, 0);
+    rPosStart_.assign(n + 1, 0);
+    rDeltaBase_.assign(n, 0);
+    std::vector<long long> waveStart(n + 1, 0), posBase(n, 0);
+    long long delta = 0, posOffTotal = 0;
+    for (int k = 0; k < n; ++k) {
+        const HZmw& z = zmws_[zl[k]];
+        const long long M = codes ? (long long)(*codes)[k].size() : unique_mutation_count(z.tpl);
+        rNMut_[k] = (int)M;
+        rMutStart_[k + 1] = rMutStart_[k] + M;
+        rDeltaBase_[k] = delta;
+        delta += M * z.nReads;
+        waveStart[k + 1] = waveStart[k] + (long long)z.nReads * ((M + 63) / 64);
+        rPosStart_[k + 1] = rPosStart_[k] + (long long)z.tpl.size();
+        posBase[k] = posOffTotal;
+        posOffTotal += (long long)z.tpl.size() + 1;
+    }
+    rTotalMut_ = rMutStart_[n];
+    rTotalPos_ = rPosStart_[n];
+    rTotalDelta_ = delta;
+    std::vector<long long> mutBase(rMutStart_.begin(), rMutStart_.begin() + n);
+    upload(dWZmw_, zl, stream_);
+    upload(dWNMut_, rNMut_, stream_);
+    upload(dWMutBase_, mutBase, stream_);
+    upload(dWDeltaBase_, rDeltaBase_, stream_);
+    upload(dWWaveStart_, waveStart, stream_);
+    upload(dWMutStart_, rMutStart_, stream_);
+    upload(dWPosStart_, rPosStart_, stream_);
+    upload(dWPosBase_, posBase, stream_);
+    dCodes_.reserve(std::max<long long>(rTotalMut_, 1), false);
+    dScore_.reserve(std::max<long long>(rTotalMut_, 1), false);
+    dFav_.reserve(std::max<long long>(rTotalMut_, 1), false);
+    dDelta_.reserve(std::max<long long>(rTotalDelta_, 1), false);
+    const DevBatch B = View();
+    if (codes) {
+        std::vector<int> flat;
+        flat.reserve(rTotalMut_);
+        for (const std::vector<int>& c : *codes) flat.insert(flat.end(), c.begin(), c.end());
+        upload(dCodes_, flat, stream_);
+        PBCCS_HIP(hipStreamSynchronize(stream_));
+    } else {
+        dPosOff_.reserve(std::max<long long>(posOffTotal, 1), false);
+        launch_enumerate(B, dWZmw_.ptr, n, dWMutBase_.ptr, dWPosBase_.ptr, dCodes_.ptr, dPosOff_.ptr, stream_);
+    }
+    (void)needPositions;
+    ScoreWork W;
+    W.nWork = n;
+    W.zmw = dWZmw_.ptr;
+    W.nMut = dWNMut_.ptr;
+    W.mutBase = dWMutBase_.ptr;
+    W.deltaBase = dWDeltaBase_.ptr;
+    W.waveStart = dWWaveStart_.ptr;
+    W.mutStart = dWMutStart_.ptr;
+    W.posStart = dWPosStart_.ptr;
+    W.codes = dCodes_.ptr;
+    W.delta = dDelta_.ptr;
+    for (int attempt = 0;; ++attempt) {
+        PBCCS_HIP(hipMemsetAsync(dScratchTop_.ptr, 0, sizeof(unsigned long long), stream_));
+        PBCCS_HIP(hipMemsetAsync(dScratchOverflow_.ptr, 0, sizeof(int), stream_));
+        ScoreScratch sc;
+        sc.pool = dScratch_.ptr;
+        sc.top = dScratchTop_.ptr;
+        sc.cap = dScratch_.cap;
+        sc.overflow = dScratchOverflow_.ptr;
+        launch_score(B, W, waveStart[n], sc, stream_);
+        PBCCS_HIP(hipGetLastError());
+        int ovf = 0;
+        PBCCS_HIP(hipMemcpyAsync(&ovf, dScratchOverflow_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
+        PBCCS_HIP(hipStreamSynchronize(stream_));
+        if (!ovf) break;
+        if (attempt > 8) throw DeviceError("scratch overflow");
+        dScratch_.reserve(dScratch_.cap * 4, false);
+    }
+    launch_reduce(B, W, rTotalMut_, fastThr, dScore_.ptr, dFav_.ptr, stream_);
+    PBCCS_HIP(hipGetLastError());
+    counters_.scoreLaunches += 1;
+    counters_.scoreTasks += rTotalDelta_;
+    counters_.mutations += rTotalMut_;
+}
+
+void ArrowBatch::ScoreLists(const std::vector<int>& zl, const std::vector<std::vector<int>>& codes, double fastThr,
+                            std::vector<std::vector<double>>* scores, std::vector<std::vector<double>>* perRead)
+{
+    RunRound(zl, &codes, fastThr, false);
+    std::vector<double> s, d;
+    download(s, dScore_, rTotalMut_, stream_);
+    if (perRead) download(d, dDelta_, rTotalDelta_, stream_);
+    PBCCS_HIP(hipStreamSynchronize(stream_));
+    scores->assign(zl.size(), {});
+    if (perRead) perRead->assign(zl.size(), {});
+    for (size_t k = 0; k < zl.size(); ++k) {
+        (*scores)[k].assign(s.begin() + rMutStart_[k], s.begin() + rMutStart_[k + 1]);
+        if (perRead) {
+            const int nr = zmws_[zl[k]].nReads;
+            (*perRead)[k].assign(d.begin() + rDeltaBase_[k], d.begin() + rDeltaBase_[k] + (long long)nr * rNMut_[k]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// ApplyMutations (MultiReadMutationScorer.cpp:235-267): template edit + window remap; refill is
+// done by the caller (batched across ZMWs).
+// ------------------------------------------------------------------------------------------------
+static bool apply_host(std::string* tpl, const std::vector<Mutation>& muts, std::vector<int>* mtp)
+{
+    std::string next;
+    if (!apply_mutations(*tpl, muts, &next, mtp)) return false;
+    *tpl = next;
+    return true;
+}
+
+bool ArrowBatch::ApplyMutations(int zi, const std::vector<Mutation>& muts)
+{
+    HZmw& z = zmws_[zi];
+    std::vector<int> mtp;
+    if (!apply_host(&z.tpl, muts, &mtp)) return false;
+    UploadTemplate(zi);
+    std::vector<int> refill;
+    for (int k = 0; k < z.nReads; ++k) {
+        HRead& r = reads_[z.readBegin + k];
+        r.ts = mtp[r.ts];
+        r.te = mtp[r.te];
+        if (r.active) refill.push_back(z.readBegin + k);
+    }
+    descDirty_ = true;
+    FillReads(refill);
+    for (int r : refill)
+        if (reads_[r].status != kFillOk) reads_[r].active = false;   // AlphaBetaMismatchException -> inactive
+    descDirty_ = true;
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// RefineConsensus (Consensus-inl.hpp:159-251), all listed ZMWs in lock-step rounds
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+struct Scored {
+    int code;
+    float score;
+};
+
+std::vector<Scored> best_subset(std::vector<Scored> in, int sep)   // Consensus-inl.hpp:98-118
+{
+    if (sep == 0) return in;
+    std::vector<Scored> out;
+    while (!in.empty()) {
+        size_t best = 0;
+        for (size_t k = 1; k < in.size(); ++k)
+            if (in[best].score < in[k].score) best = k;
+        const Scored b = in[best];
+        out.push_back(b);
+        const int lo = mut_pos(b.code) - sep, hi = mut_pos(b.code) + sep;
+        std::vector<Scored> keep;
+        keep.reserve(in.size());
+        for (const Scored& s : in)
+            if (!(lo <= mut_pos(s.code) && mut_pos(s.code) <= hi)) keep.push_back(s);
+        in.swap(keep);
+    }
+    return out;
+}
+
+}  // namespace
+
+void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std::vector<int>* converged,
+                        std::vector<long long>* nTested, std::vector<long long>* nApplied)
+{
+    const int n = (int)zl.size();
+    converged->assign(n, 0);
+    nTested->assign(n, 0);
+    nApplied->assign(n, 0);
+    std::vector<char> done(n, 0);
+    std::vector<std::unordered_set<std::string>> history(n);
+    std::vector<std::vector<int>> centers(n);
+    const double fastThr = zl.empty() ? -12.5 : zmws_[zl[0]].opt.fastScoreThreshold;
+    for (int iter = 0; iter < ro.maxIterations; ++iter) {
+        std::vector<int> act, idx;
+        for (int k = 0; k < n; ++k)
+            if (!done[k]) { act.push_back(zl[k]); idx.push_back(k); }
+        if (act.empty()) break;
+        std::vector<std::vector<int>> lists;
+        if (iter == 0) {
+            RunRound(act, nullptr, fastThr, false);
+        } else {
+            lists.resize(act.size());
+            for (size_t a = 0; a < act.size(); ++a)
+                nearby_mutations(zmws_[act[a]].tpl, centers[idx[a]], ro.mutationNeighborhood, &lists[a]);
+            RunRound(act, &lists, fastThr, false);
+        }
+        for (size_t a = 0; a < act.size(); ++a) (*nTested)[idx[a]] += rNMut_[a];
+
+        // favourable mutations, compacted on the device in list order
+        DevVec<long long> dSel;
+        DevVec<double> dSelScore;
+        DevVec<long long> dCount;
+        dSel.reserve(std::max<long long>(rTotalMut_, 1), false);
+        dSelScore.reserve(std::max<long long>(rTotalMut_, 1), false);
+        dCount.reserve(2, false);
+        size_t tmpBytes = 0, tmpBytes2 = 0;
+        hipcub::CountingInputIterator<long long> it(0);
+        PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmpBytes, it, dFav_.ptr, dSel.ptr, dCount.ptr,
+                                                (int)rTotalMut_, stream_));
+        PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmpBytes2, dScore_.ptr, dFav_.ptr, dSelScore.ptr,
+                                                dCount.ptr + 1, (int)rTotalMut_, stream_));
+        DevVec<unsigned char> tmp;
+        tmp.reserve(std::max<size_t>(std::max(tmpBytes, tmpBytes2), 1), false);
+        PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tmpBytes, it, dFav_.ptr, dSel.ptr, dCount.ptr,
+                                                (int)rTotalMut_, stream_));
+        PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tmpBytes2, dScore_.ptr, dFav_.ptr, dSelScore.ptr,
+                                                dCount.ptr + 1, (int)rTotalMut_, stream_));
+        long long cnt[2] = {0, 0};
+        PBCCS_HIP(hipMemcpyAsync(cnt, dCount.ptr, 2 * sizeof(long long), hipMemcpyDeviceToHost, stream_));
+        PBCCS_HIP(hipStreamSynchronize(stream_));
+        std::vector<long long> sel;
+        std::vector<double> selScore;
+        std::vector<int> selCode;
+        download(sel, dSel, cnt[0], stream_);
+        download(selScore, dSelScore, cnt[0], stream_);
+        if (iter == 0) {
+            // the enumerated codes live only on the device: select them too
+            DevVec<int> dSelCode;
+            dSelCode.reserve(std::max<long long>(cnt[0], 1), false);
+            size_t tb = 0;
+            PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,
+                                                    (int)rTotalMut_, stream_));
+            tmp.reserve(std::max<size_t>(tb, 1), false);
+            PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,
+                                                    (int)rTotalMut_, stream_));
+            download(selCode, dSelCode, cnt[0], stream_);
+            PBCCS_HIP(hipStreamSynchronize(stream_));
+        }
+        PBCCS_HIP(hipStreamSynchronize(stream_));
+
+        std::vector<std::vector<Scored>> fav(act.size());
+        for (size_t q = 0; q < sel.size(); ++q) {
+            const long long g = sel[q];
+            const size_t a = std::upper_bound(rMutStart_.begin(), rMutStart_.end(), g) - rMutStart_.begin() - 1;
+            const long long m = g - rMutStart_[a];
+            const int code = (iter == 0) ? selCode[q] : lists[a][m];
+            fav[a].push_back({code, (float)selScore[q]});
+        }
+        std::vector<int> changed;
+        for (size_t a = 0; a < act.size(); ++a) {
+            const int k = idx[a];
+            const int zi = act[a];
+            if (fav[a].empty()) {
+                converged->at(k) = 1;
+                done[k] = 1;
+                continue;
+            }
+            std::vector<Scored> best = best_subset(fav[a], ro.mutationSeparation);
+            std::vector<Mutation> muts;
+            for (const Scored& s : best) muts.push_back(mutation_from_code(s.code));
+            if (best.size() > 1) {
+                std::string next;
+                std::vector<int> mtp;
+                if (apply_mutations(zmws_[zi].tpl, muts, &next, &mtp) && history[k].count(next)) {
+                    best.resize(1);
+                    muts.resize(1);
+                }
+            }
+            (*nApplied)[k] += (long long)best.size();
+            history[k].insert(zmws_[zi].tpl);
+            centers[k].clear();
+            for (const Scored& s : fav[a]) centers[k].push_back(mut_pos(s.code));
+            // apply on the host; refills are batched below
+            HZmw& z = zmws_[zi];
+            std::vector<int> mtp;
+            if (!apply_host(&z.tpl, muts, &mtp)) {
+                done[k] = 1;   // the reference throws out of RefineConsensus here (ZMW -> Other)
+                converged->at(k) = -1;
+                continue;
+            }
+            UploadTemplate(zi);
+            for (int q = 0; q < z.nReads; ++q) {
+                HRead& r = reads_[z.readBegin + q];
+                r.ts = mtp[r.ts];
+                r.te = mtp[r.te];
+                if (r.active) {
+                    EnsureCapacity(z.readBegin + q);
+                    changed.push_back(z.readBegin + q);
+                }
+            }
+            if (iter + 1 >= ro.maxIterations) done[k] = 1;   // NonConvergent
+        }
+        descDirty_ = true;
+        if (!changed.empty()) {
+            FillReads(changed);
+            for (int r : changed)
+                if (reads_[r].status != kFillOk) reads_[r].active = false;
+            descDirty_ = true;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// ConsensusQVs
+// ------------------------------------------------------------------------------------------------
+void ArrowBatch::QVs(const std::vector<int>& zl, std::vector<std::vector<int>>* qvs)
+{
+    RunRound(zl, nullptr, -std::numeric_limits<double>::max(), true);
+    std::vector<long long> qvBase(zl.size());
+    for (size_t k = 0; k < zl.size(); ++k) qvBase[k] = rPosStart_[k];
+    upload(dWQvBase_, qvBase, stream_);
+    dQv_.reserve(std::max<long long>(rTotalPos_, 1), false);
+    ScoreWork W;
+    W.nWork = (int)zl.size();
+    W.zmw = dWZmw_.ptr;
+    W.nMut = dWNMut_.ptr;
+    W.mutBase = dWMutBase_.ptr;
+    W.deltaBase = dWDeltaBase_.ptr;
+    W.waveStart = dWWaveStart_.ptr;
+    W.mutStart = dWMutStart_.ptr;
+    W.posStart = dWPosStart_.ptr;
+    W.codes = dCodes_.ptr;
+    W.delta = dDelta_.ptr;
+    launch_qv(View(), W, rTotalPos_, dWPosBase_.ptr, dPosOff_.ptr, dScore_.ptr, dWQvBase_.ptr, dQv_.ptr, stream_);
+    PBCCS_HIP(hipGetLastError());
+    std::vector<int> q;
+    download(q, dQv_, rTotalPos_, stream_);
+    PBCCS_HIP(hipStreamSynchronize(stream_));
+    qvs->assign(zl.size(), {});
+    for (size_t k = 0; k < zl.size(); ++k) (*qvs)[k].assign(q.begin() + rPosStart_[k], q.begin() + rPosStart_[k + 1]);
+}
+
+}  // namespace pbccs

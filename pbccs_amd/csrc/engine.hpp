@@ -1,0 +1,181 @@
+// pbccs_amd/csrc/engine.hpp -- the batch engine behind the C ABI.
+//
+// ArrowBatch keeps any number of ZMWs (template + mapped reads) resident in HBM and runs the
+// polishing hot path on them: read fills (AddRead / template refills), mutation-scoring rounds,
+// the refine loop and QVs.  The fine-grained ConsensusCore-shaped scorer API is a batch of one ZMW;
+// the ccs-style batch entry point polishes thousands of ZMWs per round trip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "arrow_device.hpp"
+#include "arrow_kernels.hpp"
+#include "arrow_model.hpp"
+
+namespace pbccs {
+
+struct ArrowOptions {   // ArrowConfig (ArrowConfig.hpp:104-128) + BandingOptions
+    double scoreDiff = 12.5;
+    double fastScoreThreshold = -12.5;
+    double addThreshold = std::numeric_limits<double>::quiet_NaN();
+};
+
+struct RefineOptions {   // Consensus.hpp:48-60
+    int maxIterations = 40;
+    int mutationSeparation = 10;
+    int mutationNeighborhood = 20;
+};
+
+enum AddReadResult { kSuccess = 0, kAlphaBetaMismatch = 1, kMemFail = 2, kPoorZScore = 3, kOther = 4 };
+
+class DeviceError : public std::exception {
+public:
+    explicit DeviceError(const char* what) : what_(what) {}
+    const char* what() const noexcept override { return what_; }
+private:
+    const char* what_;
+};
+
+// Device buffer with geometric growth (contents optionally preserved).
+template <class T>
+struct DevVec {
+    T* ptr = nullptr;
+    size_t cap = 0;
+    void reserve(size_t n, bool keep);
+    void release();
+    ~DevVec() { release(); }
+};
+
+struct Counters {   // work counters for the roofline report (bench.py)
+    long long fillCells = 0, fillLaunches = 0;
+    long long scoreTasks = 0, scoreLaunches = 0;
+    long long mutations = 0;
+};
+
+class ArrowBatch {
+public:
+    explicit ArrowBatch(int device);
+    ~ArrowBatch();
+    ArrowBatch(const ArrowBatch&) = delete;
+    ArrowBatch& operator=(const ArrowBatch&) = delete;
+
+    // ---- host description -------------------------------------------------------------
+    int AddZmw(const std::string& tpl, const double snr[4], const ArrowOptions& opt);
+    // Reads are appended to the most recently added ZMW (reads of a ZMW are contiguous).
+    int AppendRead(int z, const std::string& seq, int strand, int ts, int te);
+
+    // ---- device operations ------------------------------------------------------------
+    // Fill the given reads (AddRead / Template() semantics); refreshes baseline, flips, status.
+    void FillReads(const std::vector<int>& reads);
+    // AddRead bookkeeping after FillReads (z-score gate, active flag).  Returns AddReadResult.
+    int FinishAddRead(int r, double threshold);
+    // Score explicit mutation lists (one list per ZMW); returns the summed score per mutation.
+    void ScoreLists(const std::vector<int>& zmws, const std::vector<std::vector<int>>& codes, double fastThr,
+                    std::vector<std::vector<double>>* scores, std::vector<std::vector<double>>* perRead = nullptr);
+    // RefineConsensus for the listed ZMWs (all in lock-step rounds).
+    void Refine(const std::vector<int>& zmws, const RefineOptions& ro, std::vector<int>* converged,
+                std::vector<long long>* nTested, std::vector<long long>* nApplied);
+    // ConsensusQVs for the listed ZMWs.
+    void QVs(const std::vector<int>& zmws, std::vector<std::vector<int>>* qvs);
+    // ApplyMutations (MultiReadMutationScorer.cpp:235-267).  Returns false on an invalid edit.
+    bool ApplyMutations(int z, const std::vector<Mutation>& muts);
+
+    // ---- host queries (MultiReadMutationScorer surface) -------------------------------
+    int NumZmws() const { return (int)zmws_.size(); }
+    int NumReads(int z) const { return zmws_[z].nReads; }
+    int ReadIndex(int z, int k) const { return zmws_[z].readBegin + k; }
+    const std::string& Template(int z) const { return zmws_[z].tpl; }
+    std::string TemplateRev(int z) const { return reverse_complement(zmws_[z].tpl); }
+    double ReadScore(int r) const { return reads_[r].baseline; }
+    bool ReadActive(int r) const { return reads_[r].active; }
+    int ReadTs(int r) const { return reads_[r].ts; }
+    int ReadTe(int r) const { return reads_[r].te; }
+    int ReadStrand(int r) const { return reads_[r].strand; }
+    int ReadFlips(int r) const { return reads_[r].flips; }
+    double BaselineScore(int z) const;
+    void ZScores(int z, double* zg, double* za, std::vector<double>* zs) const;
+    const ArrowOptions& Options(int z) const { return zmws_[z].opt; }
+    const Counters& counters() const { return counters_; }
+    void ResetCounters() { counters_ = Counters(); }
+    hipStream_t stream() const { return stream_; }
+
+private:
+    struct HZmw {
+        std::string tpl;
+        double ctx[45];
+        TransParams trans[8];
+        double ctxMeanVar[9][2];
+        ArrowOptions opt;
+        int readBegin = 0, nReads = 0;
+        long long tplOff = 0;   // fwd at tplOff, rev at tplOff + tplCap
+        int tplCap = 0;
+    };
+    struct HRead {
+        std::string seq;
+        int strand = 0, ts = 0, te = 0;
+        int zmw = 0;
+        bool active = false;
+        bool filled = false;
+        double baseline = 0.0;
+        int flips = 0;
+        int status = 0;
+        long long seqOff = 0;
+        long long colBase = 0;
+        int colCap = 0;
+        long long valA = 0, valB = 0, valCap = 0;
+    };
+
+    void EnsureZmwUploaded();
+    void UploadDescriptors();
+    void UploadTemplate(int z);
+    void EnsureCapacity(int r);
+    DevBatch View() const;
+    void MeanVar(const HZmw& z, int strand, int ts, int te, double* mean, double* var) const;
+    // one scoring round on the device; codes==nullptr => device enumeration of all mutations
+    void RunRound(const std::vector<int>& zmws, const std::vector<std::vector<int>>* codes, double fastThr,
+                  bool needPositions);
+
+    int device_ = 0;
+    hipStream_t stream_ = nullptr;
+    std::vector<HZmw> zmws_;
+    std::vector<HRead> reads_;
+    long long tplTop_ = 0, seqTop_ = 0, colTop_ = 0, valTop_ = 0;
+    bool descDirty_ = true;
+    size_t seqUploaded_ = 0;
+
+    // host mirrors of pools
+    std::vector<char> hTpl_, hSeq_;
+    // device state
+    DevVec<int> dZFwd_, dZRev_, dZLen_, dZReadBegin_, dZNReads_;
+    DevVec<double> dZCtx_;
+    DevVec<char> dTpl_, dSeq_;
+    DevVec<long long> dRSeqOff_, dRColBase_, dRValA_, dRValB_, dRValCap_;
+    DevVec<int> dRLen_, dRStrand_, dRTs_, dRTe_, dRActive_, dRZmw_;
+    DevVec<int2> dARange_, dBRange_;
+    DevVec<int> dAOff_, dBOff_;
+    DevVec<double> dALs_, dBLs_, dAPre_, dBSuf_;
+    DevVec<double> dVal_;
+    DevVec<double> dRBaseline_;
+    DevVec<int> dRFlips_, dRStatus_;
+    // scoring round scratch
+    DevVec<int> dWZmw_, dWNMut_;
+    DevVec<long long> dWMutBase_, dWDeltaBase_, dWWaveStart_, dWMutStart_, dWPosStart_, dWPosBase_, dWQvBase_;
+    DevVec<int> dCodes_, dPosOff_, dQv_, dList_;
+    DevVec<double> dDelta_, dScore_;
+    DevVec<unsigned char> dFav_;
+    DevVec<double> dScratch_;
+    DevVec<unsigned long long> dScratchTop_;
+    DevVec<int> dScratchOverflow_;
+    // last round bookkeeping (host)
+    std::vector<long long> rMutStart_, rPosStart_, rDeltaBase_;
+    std::vector<int> rNMut_;
+    long long rTotalMut_ = 0, rTotalPos_ = 0, rTotalDelta_ = 0;
+    Counters counters_;
+};
+
+}  // namespace pbccs

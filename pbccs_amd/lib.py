@@ -1,0 +1,119 @@
+"""ctypes declarations of include/pbccs_amd.h and the loader of the in-tree libpbccs_amd.so."""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libpbccs_amd.so")
+
+PBCCS_OK = 0
+ERRORS = {-1: "EINVAL", -2: "EOOM", -3: "EDEVICE", -4: "ESTATE", -5: "ERANGE"}
+
+_lib = None
+
+
+class PbccsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"pbccs {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class CMutation(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int), ("start", ctypes.c_int), ("end", ctypes.c_int), ("new_base", ctypes.c_char)]
+
+
+class CArrowConfig(ctypes.Structure):
+    _fields_ = [("snr", ctypes.c_double * 4), ("score_diff", ctypes.c_double),
+                ("fast_score_threshold", ctypes.c_double), ("add_threshold", ctypes.c_double)]
+
+
+class CRefineOptions(ctypes.Structure):
+    _fields_ = [("max_iterations", ctypes.c_int), ("mutation_separation", ctypes.c_int),
+                ("mutation_neighborhood", ctypes.c_int)]
+
+
+class CZmwInput(ctypes.Structure):
+    _fields_ = [("draft", ctypes.c_char_p), ("draft_len", ctypes.c_int), ("snr", ctypes.c_double * 4),
+                ("n_reads", ctypes.c_int), ("seqs", ctypes.POINTER(ctypes.c_char_p)),
+                ("lens", ctypes.POINTER(ctypes.c_int)), ("strands", ctypes.POINTER(ctypes.c_int)),
+                ("tstarts", ctypes.POINTER(ctypes.c_int)), ("tends", ctypes.POINTER(ctypes.c_int)),
+                ("full_pass", ctypes.POINTER(ctypes.c_ubyte))]
+
+
+class CPolishOptions(ctypes.Structure):
+    _fields_ = [("min_passes", ctypes.c_int), ("min_length", ctypes.c_int), ("min_zscore", ctypes.c_double),
+                ("max_drop_fraction", ctypes.c_double), ("min_predicted_accuracy", ctypes.c_double),
+                ("score_diff", ctypes.c_double), ("refine", CRefineOptions), ("zmws_per_batch", ctypes.c_int)]
+
+
+class CZmwOutput(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int), ("consensus", ctypes.c_char_p), ("consensus_cap", ctypes.c_int),
+                ("consensus_len", ctypes.c_int), ("qvs", ctypes.POINTER(ctypes.c_int)),
+                ("add_read_results", ctypes.POINTER(ctypes.c_int)), ("zscores", ctypes.POINTER(ctypes.c_double)),
+                ("zg", ctypes.c_double), ("za", ctypes.c_double), ("predicted_accuracy", ctypes.c_double),
+                ("n_tested", ctypes.c_longlong), ("n_applied", ctypes.c_longlong), ("n_passes", ctypes.c_int),
+                ("status_counts", ctypes.c_int * 5)]
+
+
+class CCounters(ctypes.Structure):
+    _fields_ = [("fill_launches", ctypes.c_longlong), ("score_launches", ctypes.c_longlong),
+                ("score_tasks", ctypes.c_longlong), ("mutations", ctypes.c_longlong)]
+
+
+# exported symbol -> (restype, argtypes); tests check that every symbol of include/pbccs_amd.h is exported
+P = ctypes.c_void_p
+I = ctypes.c_int
+D = ctypes.c_double
+PI = ctypes.POINTER(ctypes.c_int)
+PD = ctypes.POINTER(ctypes.c_double)
+PLL = ctypes.POINTER(ctypes.c_longlong)
+PM = ctypes.POINTER(CMutation)
+SIGNATURES = {
+    "pbccs_engine_create": (I, [I, ctypes.POINTER(P)]),
+    "pbccs_engine_destroy": (None, [P]),
+    "pbccs_last_error": (ctypes.c_char_p, []),
+    "pbccs_device_count": (I, []),
+    "pbccs_engine_counters": (I, [P, ctypes.POINTER(CCounters), I]),
+    "pbccs_scorer_create": (I, [P, ctypes.POINTER(CArrowConfig), ctypes.c_char_p, I, ctypes.POINTER(P)]),
+    "pbccs_scorer_destroy": (None, [P]),
+    "pbccs_scorer_add_read": (I, [P, ctypes.c_char_p, I, I, I, I, D, PI]),
+    "pbccs_scorer_score": (I, [P, PM, D, PD]),
+    "pbccs_scorer_score_many": (I, [P, PM, I, D, PD]),
+    "pbccs_scorer_scores": (I, [P, PM, D, PD]),
+    "pbccs_scorer_is_favorable": (I, [P, PM, I, PI]),
+    "pbccs_scorer_apply_mutations": (I, [P, PM, I]),
+    "pbccs_scorer_template": (I, [P, I, ctypes.c_char_p, I, PI]),
+    "pbccs_scorer_template_length": (I, [P]),
+    "pbccs_scorer_num_reads": (I, [P]),
+    "pbccs_scorer_read_info": (I, [P, I, PI, PI, PI, PI]),
+    "pbccs_scorer_baseline_score": (I, [P, PD]),
+    "pbccs_scorer_baseline_scores": (I, [P, PD, I, PI]),
+    "pbccs_scorer_zscores": (I, [P, PD, PD, PD]),
+    "pbccs_scorer_num_flipflops": (I, [P, PI]),
+    "pbccs_refine_consensus": (I, [P, ctypes.POINTER(CRefineOptions), PLL, PLL, PI]),
+    "pbccs_consensus_qvs": (I, [P, PI, I, PI]),
+    "pbccs_polish_options_default": (None, [ctypes.POINTER(CPolishOptions)]),
+    "pbccs_polish_batch": (I, [P, ctypes.POINTER(CZmwInput), I, ctypes.POINTER(CPolishOptions),
+                               ctypes.POINTER(CZmwOutput)]),
+}
+
+
+def load():
+    """Load the HIP engine.  Raises (never falls back) when the library has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PbccsError(-3, f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != PBCCS_OK:
+        msg = load().pbccs_last_error()
+        raise PbccsError(rc, msg.decode() if msg else "")
+    return rc

@@ -1,0 +1,104 @@
+"""Batched ccs polish driver: pbccs' Consensus<>() from the scorer setup on (Consensus.h:436-552).
+
+The POA draft, FilterReads and ExtractMappedRead (Consensus.h:223-325, 352-390) stay with the caller: the
+boundary takes a draft plus mapped, extent-clipped reads per ZMW, exactly what Consensus.h hands to
+ArrowMultiReadMutationScorer.  Thousands of ZMWs go to the GPU per call; results come back in input order.
+"""
+import ctypes
+import math
+
+from . import lib as L
+
+
+class ConsensusSettings:
+    """ConsensusSettings (include/pacbio/ccs/Consensus.h:86-111, defaults src/Consensus.cpp:46-54)."""
+
+    def __init__(self, min_passes=3, min_length=10, min_zscore=-5.0, max_drop_fraction=0.34,
+                 min_predicted_accuracy=0.90, score_diff=12.5, max_iterations=40, mutation_separation=10,
+                 mutation_neighborhood=20, zmws_per_batch=0):
+        self.min_passes = min_passes
+        self.min_length = min_length
+        self.min_zscore = min_zscore
+        self.max_drop_fraction = max_drop_fraction
+        self.min_predicted_accuracy = min_predicted_accuracy
+        self.score_diff = score_diff
+        self.max_iterations = max_iterations
+        self.mutation_separation = mutation_separation
+        self.mutation_neighborhood = mutation_neighborhood
+        self.zmws_per_batch = zmws_per_batch
+
+    def _c(self):
+        o = L.CPolishOptions()
+        o.min_passes = self.min_passes
+        o.min_length = self.min_length
+        o.min_zscore = self.min_zscore
+        o.max_drop_fraction = self.max_drop_fraction
+        o.min_predicted_accuracy = self.min_predicted_accuracy
+        o.score_diff = self.score_diff
+        o.refine = L.CRefineOptions(self.max_iterations, self.mutation_separation, self.mutation_neighborhood)
+        o.zmws_per_batch = self.zmws_per_batch
+        return o
+
+
+def polish_zmws(zmws, settings=None, engine=None):
+    """Polish ZMWs on the GPU.
+
+    zmws: list of dicts {draft, snr (4), reads: [{seq, strand, ts, te, full_pass?}]}.
+    Returns one dict per ZMW: status, consensus, qvs, add_read_results, zscores, zg, za, predicted_accuracy,
+    n_tested, n_applied, n_passes, status_counts.
+    """
+    from . import default_engine, ZMW_STATUS
+    eng = engine or default_engine()
+    settings = settings or ConsensusSettings()
+    n = len(zmws)
+    ins = (L.CZmwInput * max(1, n))()
+    outs = (L.CZmwOutput * max(1, n))()
+    keep = []
+    for i, z in enumerate(zmws):
+        reads = z["reads"]
+        nr = len(reads)
+        draft = z["draft"].encode()
+        seqs = (ctypes.c_char_p * max(1, nr))(*[r["seq"].encode() for r in reads])
+        lens = (ctypes.c_int * max(1, nr))(*[len(r["seq"]) for r in reads])
+        strands = (ctypes.c_int * max(1, nr))(*[int(r.get("strand", 0)) for r in reads])
+        ts = (ctypes.c_int * max(1, nr))(*[int(r.get("ts", 0)) for r in reads])
+        te = (ctypes.c_int * max(1, nr))(*[int(r.get("te", len(z["draft"]))) for r in reads])
+        fp = (ctypes.c_ubyte * max(1, nr))(*[1 if r.get("full_pass", True) else 0 for r in reads])
+        cap = 2 * len(draft) + 64
+        cons = ctypes.create_string_buffer(cap)
+        qv = (ctypes.c_int * cap)()
+        arr = (ctypes.c_int * max(1, nr))()
+        zs = (ctypes.c_double * max(1, nr))()
+        keep.append((draft, seqs, lens, strands, ts, te, fp, cons, qv, arr, zs))
+        ins[i].draft = draft
+        ins[i].draft_len = len(draft)
+        for k in range(4):
+            ins[i].snr[k] = float(z["snr"][k])
+        ins[i].n_reads = nr
+        ins[i].seqs = seqs
+        ins[i].lens = lens
+        ins[i].strands = strands
+        ins[i].tstarts = ts
+        ins[i].tends = te
+        ins[i].full_pass = fp
+        outs[i].consensus = ctypes.cast(cons, ctypes.c_char_p)
+        outs[i].consensus_cap = cap
+        outs[i].qvs = qv
+        outs[i].add_read_results = arr
+        outs[i].zscores = zs
+    L.check(L.load().pbccs_polish_batch(eng._h, ins, n, ctypes.byref(settings._c()), outs))
+    res = []
+    for i, z in enumerate(zmws):
+        o = outs[i]
+        nr = len(z["reads"])
+        cons = keep[i][7]
+        ln = max(0, o.consensus_len)
+        res.append({
+            "status": ZMW_STATUS[o.status], "status_code": o.status,
+            "consensus": cons.raw[:ln].decode() if o.status in (0, 6) else "",
+            "qvs": list(keep[i][8][:ln]) if o.status in (0, 6) else [],
+            "add_read_results": list(keep[i][9][:nr]), "zscores": list(keep[i][10][:nr]),
+            "zg": o.zg, "za": o.za, "predicted_accuracy": o.predicted_accuracy, "n_tested": o.n_tested,
+            "n_applied": o.n_applied, "n_passes": o.n_passes, "status_counts": list(o.status_counts),
+        })
+    return res

@@ -1,0 +1,71 @@
+"""Deterministic synthetic ZMWs for the benchmark configs (BASELINE.md "Inputs").
+
+Per ZMW: truth = iid ACGT of length J; draft (POA stand-in) = truth with 0.5% insertions, 0.5% deletions,
+0.2% substitutions; subreads = truth with 7% insertions (geometric, before each base), 4% deletions, 1%
+substitutions, odd passes reverse-complemented (REVERSE strand), each mapped over the whole draft.
+There is no BAM input in the reference tree (tests/data holds one FASTA ZMW), so configs #2-#5 use this.
+"""
+import numpy as np
+
+BASES = np.frombuffer(b"ACGT", dtype=np.uint8)
+COMP = np.zeros(256, dtype=np.uint8)
+for a, b in zip(b"ACGT", b"TGCA"):
+    COMP[a] = b
+
+
+def _mutate(rng, seq, p_ins, p_del, p_sub):
+    n = seq.shape[0]
+    keep = rng.random(n) >= p_del
+    sub = rng.random(n) < p_sub
+    out = seq.copy()
+    if sub.any():
+        # a different base: shift by 1..3 in base-index space
+        idx = np.searchsorted(BASES, out[sub])
+        out[sub] = BASES[(idx + rng.integers(1, 4, size=int(sub.sum()))) % 4]
+    ins_counts = rng.geometric(1.0 - p_ins, size=n) - 1 if p_ins > 0 else np.zeros(n, dtype=np.int64)
+    total_ins = int(ins_counts.sum())
+    ins_bases = BASES[rng.integers(0, 4, size=total_ins)]
+    kept = keep.astype(np.int64)
+    lens = ins_counts + kept
+    res = np.empty(int(lens.sum()), dtype=np.uint8)
+    ends = np.cumsum(lens)
+    starts = ends - lens
+    # insertions first (before the base), then the kept base
+    pos_ins = np.repeat(starts, ins_counts) + (np.arange(total_ins) - np.repeat(np.cumsum(ins_counts) - ins_counts, ins_counts))
+    res[pos_ins] = ins_bases
+    res[ends[keep] - 1] = out[keep]
+    return res
+
+
+def make_zmw(rng, length, passes, snr=(10.0, 7.0, 5.0, 11.0)):
+    truth = BASES[rng.integers(0, 4, size=length)]
+    draft = _mutate(rng, truth, 0.005, 0.005, 0.002)
+    reads = []
+    for k in range(passes):
+        r = _mutate(rng, truth, 0.07, 0.04, 0.01)
+        strand = k % 2
+        if strand == 1:
+            r = COMP[r[::-1]]
+        reads.append({"seq": r.tobytes().decode(), "strand": strand, "ts": 0, "te": int(draft.shape[0])})
+    return {"truth": truth.tobytes().decode(), "draft": draft.tobytes().decode(), "snr": list(snr), "reads": reads}
+
+
+def make_zmws(n, length, passes, seed, snr=(10.0, 7.0, 5.0, 11.0), length_range=None, passes_range=None,
+              random_snr=False):
+    """n ZMWs.  length_range/passes_range (inclusive) draw per-ZMW sizes (config #4)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = []
+    for _ in range(n):
+        L = int(rng.integers(length_range[0], length_range[1] + 1)) if length_range else length
+        P = int(rng.integers(passes_range[0], passes_range[1] + 1)) if passes_range else passes
+        s = tuple(float(x) for x in rng.uniform(4.0, 20.0, size=4)) if random_snr else snr
+        out.append(make_zmw(rng, L, P, s))
+    return out
+
+
+CONFIGS = {
+    # name: (n_zmws, insert length, passes, seed) -- BASELINE.json configs[1..3]
+    "2kb_10pass": dict(length=2000, passes=10, seed=1),
+    "10kb_8pass": dict(length=10000, passes=8, seed=2),
+    "mixed": dict(length=None, passes=None, seed=3, length_range=(500, 20000), passes_range=(3, 30), random_snr=True),
+}

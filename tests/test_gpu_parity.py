@@ -1,0 +1,174 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU restatement (oracle/) and the
+reference's own known answers.
+
+Tolerances (north_star): consensus / applied mutations / nTested / nApplied / AddReadResult bit-exact;
+per-mutation and per-read log-likelihoods within 1e-9 relative here (the engine repeats the reference's
+FP64 operation order; only device `log` may differ by an ulp); QVs within +-1.
+"""
+import json
+import math
+import os
+
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+SNR = [10.0, 7.0, 5.0, 11.0]
+
+
+def _close(a, b, rel=1e-9, abs_=1e-9):
+    if math.isinf(a) or math.isinf(b) or math.isnan(a) or math.isnan(b):
+        return (math.isnan(a) and math.isnan(b)) or a == b
+    return abs(a - b) <= abs_ + rel * max(abs(a), abs(b))
+
+
+@pytest.fixture(scope="module")
+def P():
+    import pbccs_amd
+    return pbccs_amd
+
+
+def _scorers(P, tpl, reads, snr=SNR, threshold=float("nan")):
+    g = P.ArrowMultiReadMutationScorer(P.ArrowConfig(snr), tpl)
+    o = O.Scorer(tpl, snr)
+    rg, ro = [], []
+    for r in reads:
+        seq, strand, ts, te = r["seq"], r.get("strand", 0), r.get("ts", 0), r.get("te", len(tpl))
+        rg.append(g.AddRead(seq, strand, ts, te, threshold))
+        ro.append(o.add_read(seq, strand, ts, te, threshold))
+    return g, o, rg, ro
+
+
+def test_matrixtester_kats_on_gpu(P):
+    k = json.load(open(os.path.join(GOLD, "arrow_kats.json")))
+    for b in k["baseline"]:
+        g = P.ArrowMultiReadMutationScorer(P.ArrowConfig(k["snr"]), b["tpl"])
+        for r in b["reads"]:
+            g.AddRead(r)
+        assert abs(1 - g.BaselineScore() / b["expected"]) < k["tolerance_rel"]
+    for m in k["mutations"]:
+        g = P.ArrowMultiReadMutationScorer(P.ArrowConfig(k["snr"]), m["tpl"])
+        for r in m["reads"] * m.get("copies", 1):
+            g.AddRead(r)
+        v = g.Score(P.Mutation(m["type"], m["start"], m["base"])) / m.get("divide_by", 1)
+        assert abs(1 - v / m["expected"]) < k["tolerance_rel"], (m["line"], v)
+    se = k["short_equalities"]
+    a = P.ArrowMultiReadMutationScorer(P.ArrowConfig(k["snr"]), se["tpl_short"])
+    a.AddRead(se["read"])
+    b = P.ArrowMultiReadMutationScorer(P.ArrowConfig(k["snr"]), se["tpl_long"])
+    b.AddRead(se["read"])
+    mL = P.Mutation(se["type"], se["start"])
+    assert abs(1 - a.BaselineScore() / (b.BaselineScore() + b.Score(mL))) < 1e-5
+    b.ApplyMutations([mL])
+    assert b.Template() == se["tpl_short"]
+    assert abs(1 - a.BaselineScore() / b.BaselineScore()) < 1e-5
+
+
+@pytest.mark.parametrize("seed,length,passes", [(11, 60, 3), (12, 150, 4), (13, 400, 6)])
+def test_every_mutation_score_matches_oracle(P, seed, length, passes):
+    from pbccs_amd import synth
+    z = synth.make_zmws(1, length, passes, seed=seed)[0]
+    g, o, rg, ro = _scorers(P, z["draft"], z["reads"])
+    assert rg == ro
+    for r in range(len(z["reads"])):
+        ll_o = o.read_info(r)["ll"]
+    assert _close(g.BaselineScore(), o.baseline())
+    muts = O.unique_mutations(z["draft"])
+    gm = [P.Mutation(t, s, b) for (t, s, b) in muts]
+    full = g.ScoreMany(gm)
+    fast = g.ScoreMany(gm, -12.5)
+    for (t, s, b), vf, vq in zip(muts, full, fast):
+        assert _close(vf, o.score(t, s, b)), (t, s, b)
+        assert _close(vq, o.score(t, s, b, -12.5)), (t, s, b)
+
+
+def test_partial_windows_and_strands(P):
+    from pbccs_amd import synth
+    import numpy as np
+    z = synth.make_zmws(1, 300, 4, seed=21)[0]
+    L = len(z["draft"])
+    reads = []
+    rng = np.random.default_rng(5)
+    for k, r in enumerate(z["reads"]):
+        ts, te = int(rng.integers(0, 40)), L - int(rng.integers(0, 40))
+        # clip the read sequence roughly to the window (non-spanning reads, MultiReadMutationScorer.hpp:112-114)
+        frac0, frac1 = ts / L, te / L
+        s = r["seq"][int(frac0 * len(r["seq"])):int(frac1 * len(r["seq"]))]
+        reads.append({"seq": s, "strand": r["strand"], "ts": ts, "te": te})
+    g, o, rg, ro = _scorers(P, z["draft"], reads)
+    assert rg == ro
+    muts = O.unique_mutations(z["draft"])
+    for (t, s, b) in muts[::3]:
+        m = P.Mutation(t, s, b)
+        assert _close(g.Score(m), o.score(t, s, b)), (t, s, b)
+        sg = g.Scores(m, -1e300)
+        so = o.scores(t, s, b, -1e300)
+        assert len(sg) == len(so)
+        for x, y in zip(sg, so):
+            assert _close(x, y)
+
+
+def test_zscore_gate_and_zscores(P):
+    from pbccs_amd import synth
+    z = synth.make_zmws(1, 300, 5, seed=31)[0]
+    reads = list(z["reads"])
+    reads.append({"seq": "ACGT" * 75, "strand": 0, "ts": 0, "te": len(z["draft"])})   # junk read -> POOR_ZSCORE
+    g, o, rg, ro = _scorers(P, z["draft"], reads, threshold=-5.0)
+    assert rg == ro
+    (zg, za), zs = g.ZScores()
+    ozg, oza, ozs = o.zscores()
+    assert _close(zg, ozg, 1e-9) and _close(za, oza, 1e-9)
+    for a, b in zip(zs, ozs):
+        assert _close(a, b, 1e-9)
+
+
+@pytest.mark.parametrize("seed,length,passes", [(41, 200, 5), (42, 500, 8), (43, 800, 10)])
+def test_refine_and_qvs_match_oracle(P, seed, length, passes):
+    from pbccs_amd import synth
+    z = synth.make_zmws(1, length, passes, seed=seed)[0]
+    g, o, rg, ro = _scorers(P, z["draft"], z["reads"], threshold=-5.0)
+    assert rg == ro
+    conv, nt, na = P.RefineConsensus(g)
+    ref = o.refine()
+    assert conv == ref["converged"]
+    assert (nt, na) == (ref["n_tested"], ref["n_applied"])
+    assert g.Template() == o.template()
+    assert _close(g.BaselineScore(), o.baseline(), 1e-9)
+    qg = P.ConsensusQVs(g)
+    qo = o.qvs()
+    assert len(qg) == len(qo)
+    assert max(abs(a - b) for a, b in zip(qg, qo)) <= 1
+    assert sum(a != b for a, b in zip(qg, qo)) <= max(1, len(qo) // 1000)
+
+
+def test_polish_batch_matches_oracle(P):
+    from pbccs_amd import synth
+    zs = synth.make_zmws(6, 400, 7, seed=51)
+    res = P.polish_zmws(zs)
+    for z, r in zip(zs, res):
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+        assert r["add_read_results"] == e["add_read_results"]
+        assert r["n_tested"] == e["n_tested"] and r["n_applied"] == e["n_applied"]
+        if e["converged"]:
+            assert r["consensus"] == e["template"]
+            assert abs(r["predicted_accuracy"] - e["pred_acc"]) < 1e-3
+            assert max(abs(a - b) for a, b in zip(r["qvs"], e["qvs"])) <= 1
+        assert _close(r["zg"], e["zg"], 1e-9) and _close(r["za"], e["za"], 1e-9)
+
+
+def test_zmw6251_reference_record_on_gpu(P):
+    z = json.load(open(os.path.join(GOLD, "zmw6251.json")))
+    r = P.polish_zmws([{"draft": z["draft"], "snr": z["snr"], "reads": z["reads"]}])[0]
+    e = z["expected"]
+    tol = e["tolerance_abs"]
+    assert r["status"] == "Success"
+    assert r["add_read_results"] == e["add_read_results"]
+    assert abs(r["zg"] - e["zg"]) < tol["zg"] and abs(r["za"] - e["za"]) < tol["za"]
+    assert r["n_tested"] == e["n_tested"] and r["n_applied"] == e["n_applied"]
+    assert len(r["consensus"]) == e["final_length"]
+    assert abs(r["predicted_accuracy"] - e["pred_acc"]) < tol["pred_acc"]
+    o = O.polish_zmw(z["draft"], z["reads"], z["snr"], z["min_zscore"])
+    assert r["consensus"] == o["template"]
