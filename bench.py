@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""CCS polish throughput on MI355X (BASELINE.json metric: CCS ZMWs/sec and GCUPS).
+
+A step polishes one batch of synthetic ZMWs (2 kb insert, 10 full passes)
+end to end on the GPU: AddRead fills + z-score gates, RefineConsensus, ConsensusQVs -- the per-ZMW
+polish that pbccs' Consensus.h runs after the POA.  Inputs are copied to HBM before the timed region
+(pbccs_batch_create); the timed region is exactly K steps (pbccs_batch_polish), bracketed by a barrier
+and torch.cuda.synchronize() on both sides; the job time is the max over ranks.  Default: 5 steps x 2000
+ZMWs = the 10k-ZMW workload of configs[1].  Multi-GPU: each rank polishes its own shard (weak scaling,
+no data-path collective).  rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--zmws-per-step", type=int, default=2000)
+    ap.add_argument("--warmup-zmws", type=int, default=200)
+    ap.add_argument("--length", type=int, default=2000)
+    ap.add_argument("--passes", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-sample", type=int, default=16, help="ZMWs polished by the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(args, rank):
+    """The oracle (bit-faithful CPU restatement, test infrastructure) on host cores, one ZMW per task on a
+    thread pool like `ccs --numThreads` (src/main/ccs.cpp:222-230)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    from pbccs_amd import synth
+
+    n = args.cpu_sample
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, n))
+    zmws = synth.make_zmws(n, args.length, args.passes, seed=args.seed + 99991)
+    O.lib()
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(lambda z: O.polish_zmw(z["draft"], z["reads"], z["snr"]), zmws))
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "ZMWs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} synthetic ZMWs of the same config ({args.length} bp, {args.passes} passes), "
+                      f"oracle/arrow_oracle.cpp polish (AddRead, RefineConsensus, ConsensusQVs) on {threads} "
+                      f"host threads, {dt:.1f} s wall"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # torch first: the engine then binds to the same HIP runtime instance (both carry soname libamdhip64.so.7)
+    import torch
+    import torch.distributed as dist
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group(backend="gloo")   # barrier + max-time only: the polish path has no collective
+
+    import pbccs_amd
+    from pbccs_amd import synth
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    eng = pbccs_amd.Engine(local)
+    settings = pbccs_amd.ConsensusSettings()
+    seed0 = args.seed + 7919 * rank
+
+    # ---- warmup (untimed) -------------------------------------------------------------------
+    for w in range(args.warmup):
+        zs = synth.make_zmws(args.warmup_zmws, args.length, args.passes, seed=seed0 + 1000 + w)
+        b = pbccs_amd.PreparedBatch(zs, settings, eng)
+        b.polish()
+        b.close()
+    log(rank, f"[bench] warmup done ({args.warmup} x {args.warmup_zmws} ZMWs)")
+
+    # ---- inputs resident in HBM before the timed region ------------------------------------------
+    t_prep = time.perf_counter()
+    batches = []
+    for k in range(args.steps):
+        zs = synth.make_zmws(args.zmws_per_step, args.length, args.passes, seed=seed0 + k)
+        batches.append(pbccs_amd.PreparedBatch(zs, settings, eng))
+        log(rank, f"[bench] prepared step {k} ({args.zmws_per_step} ZMWs) t={time.perf_counter() - t_prep:.1f}s")
+    if not args.no_profile:
+        eng.set_profiling(True)
+    eng.kernel_stats(reset=True)
+    eng.counters(reset=True)
+
+    # ---- timed region: exactly K steps --------------------------------------------------------
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k, b in enumerate(batches):
+        b.polish()
+        log(rank, f"[bench] step {k} done t={time.perf_counter() - t0:.2f}s")
+    sync()
+    barrier()
+    t1 = time.perf_counter()
+    local_time = t1 - t0
+    if world > 1:
+        t = torch.tensor([local_time], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        job_time = float(t.item())
+    else:
+        job_time = local_time
+
+    stats = eng.kernel_stats(reset=True)
+    counters = eng.counters(reset=True)
+    res = [r for b in batches for r in b.results()]
+    n_local = len(res)
+    statuses = {}
+    for r in res:
+        statuses[r["status"]] = statuses.get(r["status"], 0) + 1
+    for b in batches:
+        b.close()
+
+    total_zmws = n_local * world
+    value = total_zmws / job_time
+    cells = sum(s["cells"] for s in stats.values())
+    gcups_local = cells / local_time / 1e9 if local_time > 0 else 0.0
+
+    # dominant kernel (by device time) -> roofline: algorithmic band bytes / its device time
+    dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["device_ms"])
+    launches = max(1, dom["launches"])
+    avg_ms = dom["device_ms"] / launches
+    bytes_per_launch = dom["bytes"] / launches
+    achieved = (bytes_per_launch / (avg_ms / 1e3)) / 1e9 if avg_ms > 0 else 0.0
+    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                "kernel": dom_name, "avg_launch_ms": round(avg_ms, 4), "launches": dom["launches"],
+                "bytes_per_launch": bytes_per_launch, "cells_per_launch": dom["cells"] / launches}
+
+    out = {
+        "metric": "CCS ZMWs/sec (and GCUPS) at 1/2/4/8 MI355X vs host-CPU ccs",
+        "value": round(value, 3),
+        "unit": "ZMWs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(job_time / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY.md §8(d): truth iid ACGT; subreads 7%/4%/1% ins/del/sub; draft 0.5/0.5/0.2%)",
+        "config": {"workload": f"configs[1]: synthetic {args.length} bp insert, {args.passes} full passes, "
+                               f"{args.zmws_per_step * args.steps} ZMWs per GPU "
+                               f"({args.steps} steps x {args.zmws_per_step})",
+                   "zmws_per_step": args.zmws_per_step, "insert_bp": args.length, "passes": args.passes,
+                   "parallelism": f"zmw-shard x{world}"},
+        "gcups": round(gcups_local * world, 3),
+        "zmw_status": statuses,
+        "roofline": roofline,
+        "kernels": {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
+                        "gcells": round(v["cells"] / 1e9, 4), "gbytes": round(v["bytes"] / 1e9, 4)}
+                    for k, v in stats.items()},
+        "score_tasks": counters["score_tasks"],
+        "mutations_scored": counters["mutations"],
+    }
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline(args, rank)
+        out["vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -167,14 +167,37 @@ typedef struct {
 } pbccs_zmw_output;
 
 void pbccs_polish_options_default(pbccs_polish_options* o);
+/* One call: upload, polish and download n ZMWs (chunked by opts->zmws_per_batch / memory budget). */
 int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
                        pbccs_zmw_output* out);
+
+/* The same in two phases, so that inputs can be made resident in HBM ahead of time:
+ * pbccs_batch_create copies the ZMWs to the device; pbccs_batch_polish runs the hot path (AddRead fills,
+ * gates, ZScores, RefineConsensus, ConsensusQVs) and writes the outputs.  A batch polishes once. */
+typedef struct pbccs_batch pbccs_batch;
+int pbccs_batch_create(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
+                       pbccs_batch** out);
+int pbccs_batch_polish(pbccs_batch* b, pbccs_zmw_output* out);
+void pbccs_batch_destroy(pbccs_batch* b);
 
 /* Work counters of the engine since the last reset (for roofline accounting). */
 typedef struct {
     long long fill_launches, score_launches, score_tasks, mutations;
 } pbccs_counters;
 int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset);
+
+/* Per-kernel profile (enabled by pbccs_engine_set_profiling): launches, summed device time from HIP
+ * events on the engine's stream, and algorithmic work counted in-kernel: `cells` DP cell-updates,
+ * `bytes` algorithmic band bytes (8 B per stored/read band cell + 16 B per column). */
+typedef struct {
+    char name[32];
+    long long launches;
+    double device_ms;
+    double cells;
+    double bytes;
+} pbccs_kernel_stat;
+int pbccs_engine_set_profiling(pbccs_engine* eng, int on);
+int pbccs_engine_kernel_stats(pbccs_engine* eng, pbccs_kernel_stat* out, int cap, int* n, int reset);
 
 #ifdef __cplusplus
 }

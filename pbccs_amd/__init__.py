@@ -80,6 +80,16 @@ class Engine:
             load().pbccs_engine_destroy(self._h)
             self._h = None
 
+    def set_profiling(self, on=True):
+        _lib_mod.check(load().pbccs_engine_set_profiling(self._h, 1 if on else 0))
+
+    def kernel_stats(self, reset=False):
+        arr = (_lib_mod.CKernelStat * 16)()
+        n = ctypes.c_int()
+        _lib_mod.check(load().pbccs_engine_kernel_stats(self._h, arr, 16, ctypes.byref(n), 1 if reset else 0))
+        return {arr[i].name.decode(): {"launches": arr[i].launches, "device_ms": arr[i].device_ms,
+                                       "cells": arr[i].cells, "bytes": arr[i].bytes} for i in range(n.value)}
+
     def counters(self, reset=False):
         c = _lib_mod.CCounters()
         _lib_mod.check(load().pbccs_engine_counters(self._h, ctypes.byref(c), 1 if reset else 0))
@@ -221,7 +231,7 @@ def QVsToASCII(qvs):
     return "".join(chr(min(max(0, q), 93) + 33) for q in qvs)
 
 
-from .polish import ConsensusSettings, polish_zmws  # noqa: E402  (batched ccs driver)
+from .polish import ConsensusSettings, PreparedBatch, polish_zmws  # noqa: E402  (batched ccs driver)
 
 __all__ = [
     "ArrowConfig", "ArrowMultiReadMutationScorer", "ConsensusQVs", "ConsensusSettings", "Engine", "Mutation",

@@ -99,6 +99,15 @@ struct DevBatch {
     double prNot;             // ModelParams::PrNotMiscall
     double prThird;           // ModelParams::PrThirdOfMiscall
     double sdn;               // exp(BandingOptions::ScoreDiff)
+    // optional algorithmic-work counters (profiling): [2k] cells, [2k+1] bytes for kernel kind k
+    unsigned long long* stats;
+};
+
+enum StatKind : int { kStatFill = 0, kStatSuffix = 1, kStatScore = 2 };
+
+struct TaskStat {
+    unsigned long long cells = 0;
+    unsigned long long bytes = 0;
 };
 
 // ---------------------------------------------------------------------------------------------

@@ -92,10 +92,13 @@ __global__ void __launch_bounds__(64) k_fill(DevBatch B, const int* __restrict__
     const Band a = band_alpha(B, r);
     const Band b = band_beta(B, r);
 
+    unsigned long long cells = 0, passes = 0;
     long long ua = fill_alpha(tv, rd, I, a, nullptr, false, P);
     if (ua < 0) { B.rStatus[r] = kFillOverflow; return; }
     long long ub = fill_beta(tv, rd, I, b, a.range, false, P);
     if (ub < 0) { B.rStatus[r] = kFillOverflow; return; }
+    cells += ua + ub;
+    passes += 2;
     int flips = 0;
     const int maxSize = (int)(0.5 + kRebandFrac * (I + 1) * (J + 1));
     if (ua >= maxSize || ub >= maxSize) {
@@ -103,8 +106,11 @@ __global__ void __launch_bounds__(64) k_fill(DevBatch B, const int* __restrict__
         if (ua < 0) { B.rStatus[r] = kFillOverflow; return; }
         ub = fill_beta(tv, rd, I, b, a.range, true, P);
         if (ub < 0) { B.rStatus[r] = kFillOverflow; return; }
-        ua = fill_alpha(tv, rd, I, a, b.range, true, P);
-        if (ua < 0) { B.rStatus[r] = kFillOverflow; return; }
+        const long long ua2 = fill_alpha(tv, rd, I, a, b.range, true, P);
+        if (ua2 < 0) { B.rStatus[r] = kFillOverflow; return; }
+        cells += ua + ub + ua2;
+        passes += 3;
+        ua = ua2;
         flips += 3;
     }
     double av = log(alpha_at(a, I, J)) + sum_ls(a.ls, J + 1);
@@ -112,11 +118,11 @@ __global__ void __launch_bounds__(64) k_fill(DevBatch B, const int* __restrict__
     // NB: the reference does not re-evaluate alphaV/betaV inside this loop (SimpleRecursor.cpp:667-679).
     const bool mismatched = fabs(av - bv) > kAlphaBetaTol;
     while (mismatched && flips <= kMaxFlipFlops) {
-        if (flips % 2 == 0) {
-            if (fill_alpha(tv, rd, I, a, b.range, true, P) < 0) { B.rStatus[r] = kFillOverflow; return; }
-        } else {
-            if (fill_beta(tv, rd, I, b, a.range, true, P) < 0) { B.rStatus[r] = kFillOverflow; return; }
-        }
+        const long long u = (flips % 2 == 0) ? fill_alpha(tv, rd, I, a, b.range, true, P)
+                                             : fill_beta(tv, rd, I, b, a.range, true, P);
+        if (u < 0) { B.rStatus[r] = kFillOverflow; return; }
+        cells += u;
+        passes += 1;
         ++flips;
     }
     // alpha prefix sums (exactly GetLogProdScales(0, k) for every k) and its total
@@ -133,6 +139,10 @@ __global__ void __launch_bounds__(64) k_fill(DevBatch B, const int* __restrict__
     B.rFlips[r] = flips;
     B.rBaseline[r] = bv;
     B.rStatus[r] = (mism > kAlphaBetaTol) ? kFillMismatch : kFillOk;
+    if (B.stats) {   // algorithmic: 8 B per stored cell + 16 B per column per fill pass
+        atomicAdd(&B.stats[2 * kStatFill], cells);
+        atomicAdd(&B.stats[2 * kStatFill + 1], 8ull * cells + 16ull * passes * (unsigned long long)(J + 1));
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -246,7 +256,7 @@ struct ScoreCtx {
 // ext columns are never stored: sweep t recomputes columns 0..t-1 (scales known) and column t (its
 // max = the FinishEditingColumn constant); a final sweep produces the link sum.  Every recomputation
 // performs the same operations in the same order, so the values are bit-identical to a stored matrix.
-__device__ double extend_alpha_score(const ScoreCtx& S, int sc, int n, bool link, int bc, int absc)
+__device__ double extend_alpha_score(const ScoreCtx& S, int sc, int n, bool link, int bc, int absc, TaskStat& st)
 {
     const int I = S.I;
     const int Jv = S.tv.Length();
@@ -392,8 +402,16 @@ __device__ double extend_alpha_score(const ScoreCtx& S, int sc, int n, bool link
     double E = 0.0;
 #pragma unroll
     for (int c = 0; c < kMaxExtCols; ++c)
-        if (c < n) E = E + ls[c];
-    if (link) return ((log(v) + E) + S.bSuf[bc]) + S.aPre[sc];
+        if (c < n) {
+            E = E + ls[c];
+            st.cells += (unsigned long long)max(0, ce[c] - cb[c]);
+        }
+    st.bytes += 8ull * (unsigned long long)max(0, ar.y - ar.x) + 16ull * (unsigned long long)(n + 2);
+    if (link) {
+        st.cells += (unsigned long long)max(0, le - lb);
+        st.bytes += 8ull * (unsigned long long)max(0, br.y - br.x) + 32ull;
+        return ((log(v) + E) + S.bSuf[bc]) + S.aPre[sc];
+    }
     // at-end read-out: ext(I, n-1)
     double lastC = 0.0, lastRange = 0.0;
     bool lastScl = false;
@@ -409,7 +427,7 @@ __device__ double extend_alpha_score(const ScoreCtx& S, int sc, int n, bool link
 
 // ExtendBeta (SimpleRecursor.cpp:509-628) back to column 0 for mutations near the template start,
 // read out as in MutationScorer.cpp:233-245.  Columns are filled high to low, rows bottom-up.
-__device__ double extend_beta_score(const ScoreCtx& S, int lastCol, int ld)
+__device__ double extend_beta_score(const ScoreCtx& S, int lastCol, int ld, TaskStat& st)
 {
     const int I = S.I;
     const int Jv = S.tv.Length();
@@ -514,7 +532,11 @@ __device__ double extend_beta_score(const ScoreCtx& S, int lastCol, int ld)
     double E = 0.0;
 #pragma unroll
     for (int c = 0; c < kMaxExtCols; ++c)
-        if (c < nExt) E = E + ls[c];
+        if (c < nExt) {
+            E = E + ls[c];
+            st.cells += (unsigned long long)max(0, ce[c] - cb[c]);
+        }
+    st.bytes += 8ull * (unsigned long long)max(0, br.y - br.x) + 16ull * (unsigned long long)(nExt + 2);
     const double ext00 = (0 >= cb[0] && 0 < ce[0]) ? (scl[0] ? rawAt0 / C[0] : rawAt0) : 0.0;
     return (log(ext00) + S.bSuf[lastCol + 1]) + E;
 }
@@ -526,7 +548,7 @@ __device__ __forceinline__ bool read_scores(int ts, int te, int type, int ms, in
 }
 
 // MutationScorer::ScoreMutation(OrientedMutation(read, m)) - MutationScorer::Score() for one read.
-__device__ double score_mutation(const DevBatch& B, int r, int code, const ScoreScratch& scratch)
+__device__ double score_mutation(const DevBatch& B, int r, int code, const ScoreScratch& scratch, TaskStat& st)
 {
     const int z = B.rZmw[r];
     const int L = B.zLen[z];
@@ -568,13 +590,13 @@ __device__ double score_mutation(const DevBatch& B, int r, int code, const Score
     double score;
     if (!atBegin && !atEnd) {
         const int sc = (type == kDel) ? os - 1 : os;
-        score = extend_alpha_score(S, sc, 2, true, betaLinkCol, absLinkCol);
+        score = extend_alpha_score(S, sc, 2, true, betaLinkCol, absLinkCol, st);
     } else if (!atBegin && atEnd) {
         const int sc = os - 1;
         const int n = S.tv.Length() - sc + 1;
-        score = extend_alpha_score(S, sc, n, false, 0, 0);
+        score = extend_alpha_score(S, sc, n, false, 0, 0, st);
     } else if (atBegin && !atEnd) {
-        score = extend_beta_score(S, oe, ld);
+        score = extend_beta_score(S, oe, ld, st);
     } else {
         // whole fill of the virtually mutated window (MutationScorer.cpp:246-266); tiny windows only
         const int Jv = S.tv.Length();
@@ -592,7 +614,9 @@ __device__ double score_mutation(const DevBatch& B, int r, int code, const Score
         m.off = reinterpret_cast<int*>(base0 + 2 * ncol);
         m.val = base0 + 4 * ncol;
         m.cap = ncol * (long long)(S.I + 1);
-        fill_alpha(S.tv, S.rd, S.I, m, nullptr, false, S.P);
+        const long long u = fill_alpha(S.tv, S.rd, S.I, m, nullptr, false, S.P);
+        st.cells += (unsigned long long)max(0LL, u);
+        st.bytes += 8ull * (unsigned long long)max(0LL, u) + 16ull * (unsigned long long)ncol;
         score = log(alpha_at(m, S.I, Jv)) + sum_ls(m.ls, Jv + 1);
     }
     return score - B.rBaseline[r];
@@ -618,14 +642,27 @@ __global__ void __launch_bounds__(256) k_score(DevBatch B, ScoreWork W, ScoreScr
     const long long local = wave - W.waveStart[k];
     const int rr = (int)(local / chunks);
     const int m = (int)(local % chunks) * 64 + lane;
-    if (m >= M) return;
-    const int r = B.zReadBegin[z] + rr;
-    const int code = W.codes[W.mutBase[k] + m];
-    double d = 0.0;
-    const int type = mut_type(code), pos = mut_pos(code);
-    const int me = (type == kIns) ? pos : pos + 1;
-    if (B.rActive[r] && read_scores(B.rTs[r], B.rTe[r], type, pos, me)) d = score_mutation(B, r, code, scratch);
-    W.delta[W.deltaBase[k] + (long long)rr * M + m] = d;
+    TaskStat st;
+    if (m < M) {
+        const int r = B.zReadBegin[z] + rr;
+        const int code = W.codes[W.mutBase[k] + m];
+        double d = 0.0;
+        const int type = mut_type(code), pos = mut_pos(code);
+        const int me = (type == kIns) ? pos : pos + 1;
+        if (B.rActive[r] && read_scores(B.rTs[r], B.rTe[r], type, pos, me)) d = score_mutation(B, r, code, scratch, st);
+        W.delta[W.deltaBase[k] + (long long)rr * M + m] = d;
+    }
+    if (B.stats) {   // wave-reduce, one atomic per wave
+        unsigned long long c = st.cells, b = st.bytes;
+        for (int o = 32; o > 0; o >>= 1) {
+            c += __shfl_xor(c, o, 64);
+            b += __shfl_xor(b, o, 64);
+        }
+        if (lane == 0) {
+            atomicAdd(&B.stats[2 * kStatScore], c);
+            atomicAdd(&B.stats[2 * kStatScore + 1], b);
+        }
+    }
 }
 
 // Ordered reduction over reads with the fast-score break (MultiReadMutationScorer.cpp:352-362).

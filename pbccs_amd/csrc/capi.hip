@@ -20,6 +20,22 @@ using namespace pbccs;
 struct pbccs_engine {
     int device = 0;
     Counters counters;
+    bool profiling = false;
+    KernelStat stats[kKernelKinds];
+};
+
+struct pbccs_batch {
+    pbccs_engine* eng = nullptr;
+    std::unique_ptr<ArrowBatch> B;
+    pbccs_polish_options o;
+    int n = 0;
+    std::vector<int> zOf;                       // -1: rejected before the device (status in preStatus)
+    std::vector<int> preStatus;
+    std::vector<int> nReads;
+    std::vector<std::vector<int>> readOf;       // -1: read not added (invalid window)
+    std::vector<std::vector<unsigned char>> fullPass;
+    std::vector<int> allReads;
+    bool polished = false;
 };
 
 struct pbccs_scorer {
@@ -346,113 +362,151 @@ void pbccs_polish_options_default(pbccs_polish_options* o)
     o->zmws_per_batch = 0;
 }
 
-static int polish_chunk(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options& o,
-                        pbccs_zmw_output* out)
+static void merge_engine_stats(pbccs_engine* eng, ArrowBatch& B)
 {
-    ArrowBatch B(eng->device);
-    ArrowOptions ao;
-    ao.scoreDiff = o.score_diff;
-    std::vector<int> zOf(n, -1);
-    std::vector<std::vector<int>> readOf(n);
-    std::vector<int> allReads;
-    for (int i = 0; i < n; ++i) {
-        pbccs_zmw_output& q = out[i];
-        q.status = PBCCS_ZMW_OTHER;
-        q.consensus_len = 0;
-        q.zg = q.za = std::numeric_limits<double>::quiet_NaN();
-        q.predicted_accuracy = 0.0;
-        q.n_tested = q.n_applied = 0;
-        q.n_passes = 0;
-        for (int k = 0; k < 5; ++k) q.status_counts[k] = 0;
-        for (int k = 0; k < in[i].n_reads; ++k) {
-            if (q.add_read_results) q.add_read_results[k] = -1;
-            if (q.zscores) q.zscores[k] = std::numeric_limits<double>::quiet_NaN();
-        }
-        const pbccs_zmw_input& z = in[i];
-        if (z.n_reads <= 0) { q.status = PBCCS_ZMW_NO_SUBREADS; continue; }
-        if (z.draft_len < o.min_length) { q.status = PBCCS_ZMW_TOO_SHORT; continue; }
-        const std::string draft(z.draft, z.draft_len);
-        if (!is_acgt(draft)) { q.status = PBCCS_ZMW_OTHER; continue; }
-        zOf[i] = B.AddZmw(draft, z.snr, ao);
-        for (int k = 0; k < z.n_reads; ++k) {
-            int r = -1;
-            if (z.tstarts[k] >= 0 && z.tends[k] <= z.draft_len && z.tstarts[k] < z.tends[k] && z.lens[k] > 0)
-                r = B.AppendRead(zOf[i], std::string(z.seqs[k], z.lens[k]), z.strands[k] ? 1 : 0, z.tstarts[k],
-                                 z.tends[k]);
-            readOf[i].push_back(r);
-            if (r >= 0) allReads.push_back(r);
-        }
-    }
-    B.FillReads(allReads);
-    std::vector<int> refineZ, refineIdx;
-    for (int i = 0; i < n; ++i) {
-        if (zOf[i] < 0) continue;
-        pbccs_zmw_output& q = out[i];
-        const pbccs_zmw_input& z = in[i];
-        int nPasses = 0, nDropped = 0;
-        for (int k = 0; k < z.n_reads; ++k) {
-            const int r = readOf[i][k];
-            const int st = (r >= 0) ? B.FinishAddRead(r, o.min_zscore) : PBCCS_ADD_OTHER;
-            if (q.add_read_results) q.add_read_results[k] = st;
-            q.status_counts[st] += 1;
-            const bool full = z.full_pass ? z.full_pass[k] != 0 : true;
-            if (st == PBCCS_ADD_SUCCESS && full) ++nPasses;
-            else if (st != PBCCS_ADD_SUCCESS) ++nDropped;
-        }
-        q.n_passes = nPasses;
-        if (nPasses < o.min_passes) { q.status = PBCCS_ZMW_TOO_FEW_PASSES; continue; }
-        const double frac = (double)nDropped / z.n_reads;
-        if (frac > o.max_drop_fraction) { q.status = PBCCS_ZMW_TOO_MANY_UNUSABLE; continue; }
-        std::vector<double> zs;
-        B.ZScores(zOf[i], &q.zg, &q.za, &zs);
-        if (q.zscores) {
-            int j = 0;
-            for (int k = 0; k < z.n_reads; ++k)
-                if (readOf[i][k] >= 0) q.zscores[k] = zs[j++];
-        }
-        refineZ.push_back(zOf[i]);
-        refineIdx.push_back(i);
-    }
-    RefineOptions ro;
-    ro.maxIterations = o.refine.max_iterations;
-    ro.mutationSeparation = o.refine.mutation_separation;
-    ro.mutationNeighborhood = o.refine.mutation_neighborhood;
-    std::vector<int> conv;
-    std::vector<long long> nt, na;
-    B.Refine(refineZ, ro, &conv, &nt, &na);
-    std::vector<int> qvZ, qvIdx;
-    for (size_t k = 0; k < refineZ.size(); ++k) {
-        pbccs_zmw_output& q = out[refineIdx[k]];
-        q.n_tested = nt[k];
-        q.n_applied = na[k];
-        if (conv[k] == 1) { qvZ.push_back(refineZ[k]); qvIdx.push_back(refineIdx[k]); }
-        else q.status = conv[k] < 0 ? PBCCS_ZMW_OTHER : PBCCS_ZMW_NON_CONVERGENT;
-    }
-    std::vector<std::vector<int>> qvs;
-    B.QVs(qvZ, &qvs);
-    for (size_t k = 0; k < qvZ.size(); ++k) {
-        pbccs_zmw_output& q = out[qvIdx[k]];
-        const std::string& t = B.Template(qvZ[k]);
-        double acc = 0.0;   // Consensus.h:506-512
-        for (int v : qvs[k]) acc += std::pow(10.0, static_cast<double>(v) / -10.0);
-        acc = 1.0 - acc / qvs[k].size();
-        q.predicted_accuracy = acc;
-        if ((int)t.size() + 1 > q.consensus_cap || !q.consensus) {
-            q.consensus_len = -(int)t.size();
-            q.status = PBCCS_ZMW_OTHER;
-            continue;
-        }
-        std::memcpy(q.consensus, t.c_str(), t.size() + 1);
-        q.consensus_len = (int)t.size();
-        if (q.qvs) std::copy(qvs[k].begin(), qvs[k].end(), q.qvs);
-        q.status = (acc < o.min_predicted_accuracy) ? PBCCS_ZMW_POOR_QUALITY : PBCCS_ZMW_SUCCESS;
-    }
     const Counters& c = B.counters();
     eng->counters.fillLaunches += c.fillLaunches;
     eng->counters.scoreLaunches += c.scoreLaunches;
     eng->counters.scoreTasks += c.scoreTasks;
     eng->counters.mutations += c.mutations;
-    return PBCCS_OK;
+    B.ResetCounters();
+    B.CollectProfile(eng->stats);
+}
+
+int pbccs_batch_create(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
+                       pbccs_batch** out)
+{
+    if (!eng || n < 0 || (n > 0 && !in) || !out) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        if (hipSetDevice(eng->device) != hipSuccess) return fail(PBCCS_EDEVICE, "hipSetDevice failed");
+        std::unique_ptr<pbccs_batch> b(new pbccs_batch());
+        b->eng = eng;
+        pbccs_polish_options_default(&b->o);
+        if (opts) b->o = *opts;
+        b->n = n;
+        b->B.reset(new ArrowBatch(eng->device));
+        b->B->SetProfiling(eng->profiling);
+        ArrowOptions ao;
+        ao.scoreDiff = b->o.score_diff;
+        b->zOf.assign(n, -1);
+        b->preStatus.assign(n, PBCCS_ZMW_OTHER);
+        b->nReads.assign(n, 0);
+        b->readOf.assign(n, {});
+        b->fullPass.assign(n, {});
+        for (int i = 0; i < n; ++i) {
+            const pbccs_zmw_input& z = in[i];
+            b->nReads[i] = z.n_reads;
+            if (z.n_reads <= 0) { b->preStatus[i] = PBCCS_ZMW_NO_SUBREADS; continue; }
+            if (z.draft_len < b->o.min_length) { b->preStatus[i] = PBCCS_ZMW_TOO_SHORT; continue; }
+            const std::string draft(z.draft, z.draft_len);
+            if (!is_acgt(draft)) { b->preStatus[i] = PBCCS_ZMW_OTHER; continue; }
+            b->zOf[i] = b->B->AddZmw(draft, z.snr, ao);
+            for (int k = 0; k < z.n_reads; ++k) {
+                int r = -1;
+                if (z.tstarts[k] >= 0 && z.tends[k] <= z.draft_len && z.tstarts[k] < z.tends[k] && z.lens[k] > 0)
+                    r = b->B->AppendRead(b->zOf[i], std::string(z.seqs[k], z.lens[k]), z.strands[k] ? 1 : 0,
+                                         z.tstarts[k], z.tends[k]);
+                b->readOf[i].push_back(r);
+                b->fullPass[i].push_back(z.full_pass ? z.full_pass[k] : 1);
+                if (r >= 0) b->allReads.push_back(r);
+            }
+        }
+        b->B->Prepare();
+        *out = b.release();
+        return PBCCS_OK;
+    });
+}
+
+void pbccs_batch_destroy(pbccs_batch* b) { delete b; }
+
+int pbccs_batch_polish(pbccs_batch* b, pbccs_zmw_output* out)
+{
+    if (!b || (b->n > 0 && !out)) return fail(PBCCS_EINVAL, "bad argument");
+    if (b->polished) return fail(PBCCS_ESTATE, "a batch polishes once");
+    return guarded([&] {
+        b->polished = true;
+        ArrowBatch& B = *b->B;
+        const pbccs_polish_options& o = b->o;
+        const int n = b->n;
+        for (int i = 0; i < n; ++i) {
+            pbccs_zmw_output& q = out[i];
+            q.status = b->preStatus[i];
+            q.consensus_len = 0;
+            q.zg = q.za = std::numeric_limits<double>::quiet_NaN();
+            q.predicted_accuracy = 0.0;
+            q.n_tested = q.n_applied = 0;
+            q.n_passes = 0;
+            for (int k = 0; k < 5; ++k) q.status_counts[k] = 0;
+            for (int k = 0; k < b->nReads[i]; ++k) {
+                if (q.add_read_results) q.add_read_results[k] = -1;
+                if (q.zscores) q.zscores[k] = std::numeric_limits<double>::quiet_NaN();
+            }
+        }
+        B.FillReads(b->allReads);
+        std::vector<int> refineZ, refineIdx;
+        for (int i = 0; i < n; ++i) {
+            if (b->zOf[i] < 0) continue;
+            pbccs_zmw_output& q = out[i];
+            int nPasses = 0, nDropped = 0;
+            for (int k = 0; k < b->nReads[i]; ++k) {
+                const int r = b->readOf[i][k];
+                const int st = (r >= 0) ? B.FinishAddRead(r, o.min_zscore) : PBCCS_ADD_OTHER;
+                if (q.add_read_results) q.add_read_results[k] = st;
+                q.status_counts[st] += 1;
+                if (st == PBCCS_ADD_SUCCESS && b->fullPass[i][k]) ++nPasses;
+                else if (st != PBCCS_ADD_SUCCESS) ++nDropped;
+            }
+            q.n_passes = nPasses;
+            if (nPasses < o.min_passes) { q.status = PBCCS_ZMW_TOO_FEW_PASSES; continue; }
+            const double frac = (double)nDropped / b->nReads[i];
+            if (frac > o.max_drop_fraction) { q.status = PBCCS_ZMW_TOO_MANY_UNUSABLE; continue; }
+            std::vector<double> zs;
+            B.ZScores(b->zOf[i], &q.zg, &q.za, &zs);
+            if (q.zscores) {
+                int j = 0;
+                for (int k = 0; k < b->nReads[i]; ++k)
+                    if (b->readOf[i][k] >= 0) q.zscores[k] = zs[j++];
+            }
+            refineZ.push_back(b->zOf[i]);
+            refineIdx.push_back(i);
+        }
+        RefineOptions ro;
+        ro.maxIterations = o.refine.max_iterations;
+        ro.mutationSeparation = o.refine.mutation_separation;
+        ro.mutationNeighborhood = o.refine.mutation_neighborhood;
+        std::vector<int> conv;
+        std::vector<long long> nt, na;
+        B.Refine(refineZ, ro, &conv, &nt, &na);
+        std::vector<int> qvZ, qvIdx;
+        for (size_t k = 0; k < refineZ.size(); ++k) {
+            pbccs_zmw_output& q = out[refineIdx[k]];
+            q.n_tested = nt[k];
+            q.n_applied = na[k];
+            if (conv[k] == 1) { qvZ.push_back(refineZ[k]); qvIdx.push_back(refineIdx[k]); }
+            else q.status = conv[k] < 0 ? PBCCS_ZMW_OTHER : PBCCS_ZMW_NON_CONVERGENT;
+        }
+        std::vector<std::vector<int>> qvs;
+        B.QVs(qvZ, &qvs);
+        for (size_t k = 0; k < qvZ.size(); ++k) {
+            pbccs_zmw_output& q = out[qvIdx[k]];
+            const std::string& t = B.Template(qvZ[k]);
+            double acc = 0.0;   // Consensus.h:506-512
+            for (int v : qvs[k]) acc += std::pow(10.0, static_cast<double>(v) / -10.0);
+            acc = 1.0 - acc / qvs[k].size();
+            q.predicted_accuracy = acc;
+            if ((int)t.size() + 1 > q.consensus_cap || !q.consensus) {
+                q.consensus_len = -(int)t.size();
+                q.status = PBCCS_ZMW_OTHER;
+                continue;
+            }
+            std::memcpy(q.consensus, t.c_str(), t.size() + 1);
+            q.consensus_len = (int)t.size();
+            if (q.qvs) std::copy(qvs[k].begin(), qvs[k].end(), q.qvs);
+            q.status = (acc < o.min_predicted_accuracy) ? PBCCS_ZMW_POOR_QUALITY : PBCCS_ZMW_SUCCESS;
+        }
+        merge_engine_stats(b->eng, B);
+        return PBCCS_OK;
+    });
 }
 
 int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
@@ -462,25 +516,51 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
     pbccs_polish_options o;
     pbccs_polish_options_default(&o);
     if (opts) o = *opts;
-    return guarded([&] {
-        if (hipSetDevice(eng->device) != hipSuccess) return fail(PBCCS_EDEVICE, "hipSetDevice failed");
-        int per = o.zmws_per_batch;
-        if (per <= 0) {
-            // memory budget: ~2 band regions of 32 rows x window per read + the round's delta buffer
-            const double budget = 96.0 * (1ull << 30);
-            double bytes = 0.0;
-            for (int i = 0; i < n; ++i)
-                for (int k = 0; k < in[i].n_reads; ++k) bytes += (double)in[i].draft_len * (2 * 32 * 8 * 1.25 + 80 + 8 * 8);
-            const double perZmw = n > 0 ? bytes / n : 1.0;
-            per = (int)std::max(1.0, std::min((double)n, budget / std::max(perZmw, 1.0)));
-        }
-        for (int b = 0; b < n; b += per) {
-            const int m = std::min(per, n - b);
-            const int rc = polish_chunk(eng, in + b, m, o, out + b);
-            if (rc != PBCCS_OK) return rc;
-        }
-        return PBCCS_OK;
-    });
+    int per = o.zmws_per_batch;
+    if (per <= 0) {
+        // memory budget: two band regions of 32 rows x window per read, column metadata and the largest
+        // round's (read x mutation) deltas
+        const double budget = 96.0 * (1ull << 30);
+        double bytes = 0.0;
+        for (int i = 0; i < n; ++i)
+            for (int k = 0; k < in[i].n_reads; ++k) bytes += (double)in[i].draft_len * (2 * 32 * 8 * 1.25 + 80 + 8 * 8);
+        const double perZmw = n > 0 ? bytes / n : 1.0;
+        per = (int)std::max(1.0, std::min((double)n, budget / std::max(perZmw, 1.0)));
+    }
+    for (int b = 0; b < n; b += per) {
+        const int m = std::min(per, n - b);
+        pbccs_batch* h = nullptr;
+        int rc = pbccs_batch_create(eng, in + b, m, &o, &h);
+        if (rc != PBCCS_OK) return rc;
+        rc = pbccs_batch_polish(h, out + b);
+        pbccs_batch_destroy(h);
+        if (rc != PBCCS_OK) return rc;
+    }
+    return PBCCS_OK;
+}
+
+int pbccs_engine_set_profiling(pbccs_engine* eng, int on)
+{
+    if (!eng) return fail(PBCCS_EINVAL, "null engine");
+    eng->profiling = on != 0;
+    return PBCCS_OK;
+}
+
+int pbccs_engine_kernel_stats(pbccs_engine* eng, pbccs_kernel_stat* out, int cap, int* n, int reset)
+{
+    if (!eng || !n) return fail(PBCCS_EINVAL, "bad argument");
+    *n = kKernelKinds;
+    if (!out || cap < kKernelKinds) return fail(PBCCS_ERANGE, "buffer too small");
+    for (int k = 0; k < kKernelKinds; ++k) {
+        std::memset(out[k].name, 0, sizeof(out[k].name));
+        std::strncpy(out[k].name, kKernelNames[k], sizeof(out[k].name) - 1);
+        out[k].launches = eng->stats[k].launches;
+        out[k].device_ms = eng->stats[k].ms;
+        out[k].cells = eng->stats[k].cells;
+        out[k].bytes = eng->stats[k].bytes;
+        if (reset) eng->stats[k] = KernelStat();
+    }
+    return PBCCS_OK;
 }
 
 }  // extern "C"

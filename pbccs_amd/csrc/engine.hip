@@ -45,6 +45,9 @@ void DevVec<T>::release()
     cap = 0;
 }
 
+const char* const kKernelNames[kKernelKinds] = {"k_fill", "k_suffix", "k_enumerate", "k_score",
+                                                 "k_reduce", "k_qv", "select"};
+
 namespace {
 
 constexpr int kInitialBandHeight = 32;         // value capacity per column on first allocation
@@ -79,8 +82,103 @@ ArrowBatch::~ArrowBatch()
 {
     if (stream_) {
         (void)hipStreamSynchronize(stream_);
+        for (const Pending& p : pending_) {
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+        for (hipEvent_t e : eventPool_) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(stream_);
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// profiling: HIP events around every launch on the engine stream + in-kernel algorithmic counters
+// ------------------------------------------------------------------------------------------------
+void ArrowBatch::SetProfiling(bool on)
+{
+    profiling_ = on;
+    if (on) {
+        dStats_.reserve(16, false);
+        PBCCS_HIP(hipMemsetAsync(dStats_.ptr, 0, 16 * sizeof(unsigned long long), stream_));
+    }
+}
+
+template <class F>
+void ArrowBatch::Timed(KernelKind k, F&& launch)
+{
+    if (!profiling_) {
+        launch();
+        return;
+    }
+    hipEvent_t ev[2];
+    for (int i = 0; i < 2; ++i) {
+        if (!eventPool_.empty()) {
+            ev[i] = eventPool_.back();
+            eventPool_.pop_back();
+        } else {
+            PBCCS_HIP(hipEventCreate(&ev[i]));
+        }
+    }
+    PBCCS_HIP(hipEventRecord(ev[0], stream_));
+    launch();
+    PBCCS_HIP(hipEventRecord(ev[1], stream_));
+    pending_.push_back({(int)k, ev[0], ev[1]});
+    stats_[k].launches += 1;
+}
+
+void ArrowBatch::ResolveEvents()
+{
+    if (pending_.empty()) return;
+    PBCCS_HIP(hipStreamSynchronize(stream_));
+    for (const Pending& p : pending_) {
+        float ms = 0.0f;
+        PBCCS_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+        stats_[p.kind].ms += ms;
+        eventPool_.push_back(p.a);
+        eventPool_.push_back(p.b);
+    }
+    pending_.clear();
+}
+
+void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
+{
+    ResolveEvents();
+    if (profiling_) {
+        unsigned long long h[16];
+        PBCCS_HIP(hipMemcpyAsync(h, dStats_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
+        PBCCS_HIP(hipStreamSynchronize(stream_));
+        stats_[kKFill].cells += (double)h[2 * kStatFill];
+        stats_[kKFill].bytes += (double)h[2 * kStatFill + 1];
+        stats_[kKScore].cells += (double)h[2 * kStatScore];
+        stats_[kKScore].bytes += (double)h[2 * kStatScore + 1];
+        PBCCS_HIP(hipMemsetAsync(dStats_.ptr, 0, sizeof(h), stream_));
+    }
+    for (int k = 0; k < kKernelKinds; ++k) {
+        out[k].launches += stats_[k].launches;
+        out[k].ms += stats_[k].ms;
+        out[k].cells += stats_[k].cells;
+        out[k].bytes += stats_[k].bytes;
+        stats_[k] = KernelStat();
+    }
+}
+
+void ArrowBatch::Prepare()
+{
+    UploadDescriptors();
+    long long mut = 0, delta = 0, pos = 0;
+    for (const HZmw& z : zmws_) {
+        const long long M = unique_mutation_count(z.tpl) + 64;
+        mut += M;
+        delta += M * z.nReads;
+        pos += (long long)z.tpl.size() + 65;
+    }
+    dCodes_.reserve(std::max<long long>(mut, 1), false);
+    dScore_.reserve(std::max<long long>(mut, 1), false);
+    dFav_.reserve(std::max<long long>(mut, 1), false);
+    dDelta_.reserve(std::max<long long>(delta, 1), false);
+    dPosOff_.reserve(std::max<long long>(pos, 1), false);
+    dQv_.reserve(std::max<long long>(pos, 1), false);
+    PBCCS_HIP(hipStreamSynchronize(stream_));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -286,6 +384,7 @@ DevBatch ArrowBatch::View() const
     b.prNot = 1.0 - kMismatchProbability;
     b.prThird = kMismatchProbability / 3.0;
     b.sdn = zmws_.empty() ? std::exp(12.5) : std::exp(zmws_[0].opt.scoreDiff);
+    b.stats = profiling_ ? dStats_.ptr : nullptr;
     return b;
 }
 
@@ -301,8 +400,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         UploadDescriptors();
         upload(dList_, todo, stream_);
         const DevBatch B = View();
-        launch_fill(B, dList_.ptr, (int)todo.size(), stream_);
-        launch_suffix(B, dList_.ptr, (int)todo.size(), stream_);
+        Timed(kKFill, [&] { launch_fill(B, dList_.ptr, (int)todo.size(), stream_); });
+        Timed(kKSuffix, [&] { launch_suffix(B, dList_.ptr, (int)todo.size(), stream_); });
         PBCCS_HIP(hipGetLastError());
         counters_.fillLaunches += 1;
         const size_t R = reads_.size();
@@ -453,7 +552,9 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
         PBCCS_HIP(hipStreamSynchronize(stream_));
     } else {
         dPosOff_.reserve(std::max<long long>(posOffTotal, 1), false);
-        launch_enumerate(B, dWZmw_.ptr, n, dWMutBase_.ptr, dWPosBase_.ptr, dCodes_.ptr, dPosOff_.ptr, stream_);
+        Timed(kKEnumerate, [&] {
+            launch_enumerate(B, dWZmw_.ptr, n, dWMutBase_.ptr, dWPosBase_.ptr, dCodes_.ptr, dPosOff_.ptr, stream_);
+        });
     }
     (void)needPositions;
     ScoreWork W;
@@ -475,7 +576,7 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
         sc.top = dScratchTop_.ptr;
         sc.cap = dScratch_.cap;
         sc.overflow = dScratchOverflow_.ptr;
-        launch_score(B, W, waveStart[n], sc, stream_);
+        Timed(kKScore, [&] { launch_score(B, W, waveStart[n], sc, stream_); });
         PBCCS_HIP(hipGetLastError());
         int ovf = 0;
         PBCCS_HIP(hipMemcpyAsync(&ovf, dScratchOverflow_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
@@ -484,7 +585,7 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
         if (attempt > 8) throw DeviceError("scratch overflow");
         dScratch_.reserve(dScratch_.cap * 4, false);
     }
-    launch_reduce(B, W, rTotalMut_, fastThr, dScore_.ptr, dFav_.ptr, stream_);
+    Timed(kKReduce, [&] { launch_reduce(B, W, rTotalMut_, fastThr, dScore_.ptr, dFav_.ptr, stream_); });
     PBCCS_HIP(hipGetLastError());
     counters_.scoreLaunches += 1;
     counters_.scoreTasks += rTotalDelta_;
@@ -727,7 +828,10 @@ void ArrowBatch::QVs(const std::vector<int>& zl, std::vector<std::vector<int>>* 
     W.posStart = dWPosStart_.ptr;
     W.codes = dCodes_.ptr;
     W.delta = dDelta_.ptr;
-    launch_qv(View(), W, rTotalPos_, dWPosBase_.ptr, dPosOff_.ptr, dScore_.ptr, dWQvBase_.ptr, dQv_.ptr, stream_);
+    const DevBatch B = View();
+    Timed(kKQv, [&] {
+        launch_qv(B, W, rTotalPos_, dWPosBase_.ptr, dPosOff_.ptr, dScore_.ptr, dWQvBase_.ptr, dQv_.ptr, stream_);
+    });
     PBCCS_HIP(hipGetLastError());
     std::vector<int> q;
     download(q, dQv_, rTotalPos_, stream_);

@@ -57,6 +57,16 @@ struct Counters {   // work counters for the roofline report (bench.py)
     long long mutations = 0;
 };
 
+enum KernelKind { kKFill = 0, kKSuffix, kKEnumerate, kKScore, kKReduce, kKQv, kKSelect, kKernelKinds };
+extern const char* const kKernelNames[kKernelKinds];
+
+struct KernelStat {
+    long long launches = 0;
+    double ms = 0.0;      // summed HIP-event time on the engine stream
+    double cells = 0.0;   // algorithmic DP cell-updates (in-kernel counters)
+    double bytes = 0.0;   // algorithmic band bytes
+};
+
 class ArrowBatch {
 public:
     explicit ArrowBatch(int device);
@@ -103,6 +113,11 @@ public:
     const Counters& counters() const { return counters_; }
     void ResetCounters() { counters_ = Counters(); }
     hipStream_t stream() const { return stream_; }
+    // Upload everything and reserve the largest round's buffers (so a timed polish does no H2D of inputs).
+    void Prepare();
+    void SetProfiling(bool on);
+    // Resolve pending events and in-kernel counters into `out` (added), then clear.
+    void CollectProfile(KernelStat out[kKernelKinds]);
 
 private:
     struct HZmw {
@@ -136,6 +151,9 @@ private:
     void EnsureCapacity(int r);
     DevBatch View() const;
     void MeanVar(const HZmw& z, int strand, int ts, int te, double* mean, double* var) const;
+    template <class F>
+    void Timed(KernelKind k, F&& launch);
+    void ResolveEvents();
     // one scoring round on the device; codes==nullptr => device enumeration of all mutations
     void RunRound(const std::vector<int>& zmws, const std::vector<std::vector<int>>* codes, double fastThr,
                   bool needPositions);
@@ -176,6 +194,16 @@ private:
     std::vector<int> rNMut_;
     long long rTotalMut_ = 0, rTotalPos_ = 0, rTotalDelta_ = 0;
     Counters counters_;
+    // profiling
+    bool profiling_ = false;
+    DevVec<unsigned long long> dStats_;
+    struct Pending {
+        int kind;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending_;
+    std::vector<hipEvent_t> eventPool_;
+    KernelStat stats_[kKernelKinds];
 };
 
 }  // namespace pbccs

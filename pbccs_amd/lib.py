@@ -54,6 +54,11 @@ class CZmwOutput(ctypes.Structure):
                 ("status_counts", ctypes.c_int * 5)]
 
 
+class CKernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_longlong), ("device_ms", ctypes.c_double),
+                ("cells", ctypes.c_double), ("bytes", ctypes.c_double)]
+
+
 class CCounters(ctypes.Structure):
     _fields_ = [("fill_launches", ctypes.c_longlong), ("score_launches", ctypes.c_longlong),
                 ("score_tasks", ctypes.c_longlong), ("mutations", ctypes.c_longlong)]
@@ -94,6 +99,11 @@ SIGNATURES = {
     "pbccs_polish_options_default": (None, [ctypes.POINTER(CPolishOptions)]),
     "pbccs_polish_batch": (I, [P, ctypes.POINTER(CZmwInput), I, ctypes.POINTER(CPolishOptions),
                                ctypes.POINTER(CZmwOutput)]),
+    "pbccs_batch_create": (I, [P, ctypes.POINTER(CZmwInput), I, ctypes.POINTER(CPolishOptions), ctypes.POINTER(P)]),
+    "pbccs_batch_polish": (I, [P, ctypes.POINTER(CZmwOutput)]),
+    "pbccs_batch_destroy": (None, [P]),
+    "pbccs_engine_set_profiling": (I, [P, I]),
+    "pbccs_engine_kernel_stats": (I, [P, ctypes.POINTER(CKernelStat), I, PI, I]),
 }
 
 

@@ -40,65 +40,96 @@ class ConsensusSettings:
         return o
 
 
+class PreparedBatch:
+    """ZMWs copied to HBM (pbccs_batch_create); polish() runs the hot path once (pbccs_batch_polish)."""
+
+    def __init__(self, zmws, settings=None, engine=None):
+        from . import default_engine
+        self.engine = engine or default_engine()
+        self.settings = settings or ConsensusSettings()
+        self.zmws = zmws
+        n = len(zmws)
+        self._ins = (L.CZmwInput * max(1, n))()
+        self._outs = (L.CZmwOutput * max(1, n))()
+        self._keep = []
+        for i, z in enumerate(zmws):
+            reads = z["reads"]
+            nr = len(reads)
+            draft = z["draft"].encode()
+            seqs = (ctypes.c_char_p * max(1, nr))(*[r["seq"].encode() for r in reads])
+            lens = (ctypes.c_int * max(1, nr))(*[len(r["seq"]) for r in reads])
+            strands = (ctypes.c_int * max(1, nr))(*[int(r.get("strand", 0)) for r in reads])
+            ts = (ctypes.c_int * max(1, nr))(*[int(r.get("ts", 0)) for r in reads])
+            te = (ctypes.c_int * max(1, nr))(*[int(r.get("te", len(z["draft"]))) for r in reads])
+            fp = (ctypes.c_ubyte * max(1, nr))(*[1 if r.get("full_pass", True) else 0 for r in reads])
+            cap = 2 * len(draft) + 64
+            cons = ctypes.create_string_buffer(cap)
+            qv = (ctypes.c_int * cap)()
+            arr = (ctypes.c_int * max(1, nr))()
+            zs = (ctypes.c_double * max(1, nr))()
+            self._keep.append((draft, seqs, lens, strands, ts, te, fp, cons, qv, arr, zs))
+            self._ins[i].draft = draft
+            self._ins[i].draft_len = len(draft)
+            for k in range(4):
+                self._ins[i].snr[k] = float(z["snr"][k])
+            self._ins[i].n_reads = nr
+            self._ins[i].seqs = seqs
+            self._ins[i].lens = lens
+            self._ins[i].strands = strands
+            self._ins[i].tstarts = ts
+            self._ins[i].tends = te
+            self._ins[i].full_pass = fp
+            self._outs[i].consensus = ctypes.cast(cons, ctypes.c_char_p)
+            self._outs[i].consensus_cap = cap
+            self._outs[i].qvs = qv
+            self._outs[i].add_read_results = arr
+            self._outs[i].zscores = zs
+        self._opts = self.settings._c()
+        h = ctypes.c_void_p()
+        L.check(L.load().pbccs_batch_create(self.engine._h, self._ins, n, ctypes.byref(self._opts), ctypes.byref(h)))
+        self._h = h
+
+    def polish(self):
+        L.check(L.load().pbccs_batch_polish(self._h, self._outs))
+
+    def results(self):
+        from . import ZMW_STATUS
+        res = []
+        for i, z in enumerate(self.zmws):
+            o = self._outs[i]
+            nr = len(z["reads"])
+            keep = self._keep[i]
+            ln = max(0, o.consensus_len)
+            ok = o.status in (0, 6)
+            res.append({
+                "status": ZMW_STATUS[o.status], "status_code": o.status,
+                "consensus": keep[7].raw[:ln].decode() if ok else "",
+                "qvs": list(keep[8][:ln]) if ok else [],
+                "add_read_results": list(keep[9][:nr]), "zscores": list(keep[10][:nr]),
+                "zg": o.zg, "za": o.za, "predicted_accuracy": o.predicted_accuracy, "n_tested": o.n_tested,
+                "n_applied": o.n_applied, "n_passes": o.n_passes, "status_counts": list(o.status_counts),
+            })
+        return res
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.load().pbccs_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
 def polish_zmws(zmws, settings=None, engine=None):
-    """Polish ZMWs on the GPU.
+    """Polish ZMWs on the GPU (upload, hot path, download).
 
     zmws: list of dicts {draft, snr (4), reads: [{seq, strand, ts, te, full_pass?}]}.
     Returns one dict per ZMW: status, consensus, qvs, add_read_results, zscores, zg, za, predicted_accuracy,
     n_tested, n_applied, n_passes, status_counts.
     """
-    from . import default_engine, ZMW_STATUS
-    eng = engine or default_engine()
-    settings = settings or ConsensusSettings()
-    n = len(zmws)
-    ins = (L.CZmwInput * max(1, n))()
-    outs = (L.CZmwOutput * max(1, n))()
-    keep = []
-    for i, z in enumerate(zmws):
-        reads = z["reads"]
-        nr = len(reads)
-        draft = z["draft"].encode()
-        seqs = (ctypes.c_char_p * max(1, nr))(*[r["seq"].encode() for r in reads])
-        lens = (ctypes.c_int * max(1, nr))(*[len(r["seq"]) for r in reads])
-        strands = (ctypes.c_int * max(1, nr))(*[int(r.get("strand", 0)) for r in reads])
-        ts = (ctypes.c_int * max(1, nr))(*[int(r.get("ts", 0)) for r in reads])
-        te = (ctypes.c_int * max(1, nr))(*[int(r.get("te", len(z["draft"]))) for r in reads])
-        fp = (ctypes.c_ubyte * max(1, nr))(*[1 if r.get("full_pass", True) else 0 for r in reads])
-        cap = 2 * len(draft) + 64
-        cons = ctypes.create_string_buffer(cap)
-        qv = (ctypes.c_int * cap)()
-        arr = (ctypes.c_int * max(1, nr))()
-        zs = (ctypes.c_double * max(1, nr))()
-        keep.append((draft, seqs, lens, strands, ts, te, fp, cons, qv, arr, zs))
-        ins[i].draft = draft
-        ins[i].draft_len = len(draft)
-        for k in range(4):
-            ins[i].snr[k] = float(z["snr"][k])
-        ins[i].n_reads = nr
-        ins[i].seqs = seqs
-        ins[i].lens = lens
-        ins[i].strands = strands
-        ins[i].tstarts = ts
-        ins[i].tends = te
-        ins[i].full_pass = fp
-        outs[i].consensus = ctypes.cast(cons, ctypes.c_char_p)
-        outs[i].consensus_cap = cap
-        outs[i].qvs = qv
-        outs[i].add_read_results = arr
-        outs[i].zscores = zs
-    L.check(L.load().pbccs_polish_batch(eng._h, ins, n, ctypes.byref(settings._c()), outs))
-    res = []
-    for i, z in enumerate(zmws):
-        o = outs[i]
-        nr = len(z["reads"])
-        cons = keep[i][7]
-        ln = max(0, o.consensus_len)
-        res.append({
-            "status": ZMW_STATUS[o.status], "status_code": o.status,
-            "consensus": cons.raw[:ln].decode() if o.status in (0, 6) else "",
-            "qvs": list(keep[i][8][:ln]) if o.status in (0, 6) else [],
-            "add_read_results": list(keep[i][9][:nr]), "zscores": list(keep[i][10][:nr]),
-            "zg": o.zg, "za": o.za, "predicted_accuracy": o.predicted_accuracy, "n_tested": o.n_tested,
-            "n_applied": o.n_applied, "n_passes": o.n_passes, "status_counts": list(o.status_counts),
-        })
-    return res
+    b = PreparedBatch(zmws, settings, engine)
+    try:
+        b.polish()
+        return b.results()
+    finally:
+        b.close()
