@@ -92,6 +92,8 @@ def main():
             torch.cuda.synchronize()
 
     eng = pbccs_amd.Engine(local)
+    if not args.no_profile:
+        eng.set_profiling(True)   # HIP events on the engine stream + in-kernel algorithmic counters
     settings = pbccs_amd.ConsensusSettings()
     seed0 = args.seed + 7919 * rank
 
@@ -110,8 +112,6 @@ def main():
         zs = synth.make_zmws(args.zmws_per_step, args.length, args.passes, seed=seed0 + k)
         batches.append(pbccs_amd.PreparedBatch(zs, settings, eng))
         log(rank, f"[bench] prepared step {k} ({args.zmws_per_step} ZMWs) t={time.perf_counter() - t_prep:.1f}s")
-    if not args.no_profile:
-        eng.set_profiling(True)
     eng.kernel_stats(reset=True)
     eng.counters(reset=True)
 

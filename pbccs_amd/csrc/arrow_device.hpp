@@ -195,28 +195,39 @@ __device__ inline VirtualMut make_virtual(const char* T, int L, int type, int s,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Band matrix storage for one read (ScaledSparseMatrixD semantics: cells outside a column's used
-// row range read as 0.0).  Alpha columns are stored top-down, beta columns bottom-up, so that each
-// fill appends its cells in the order it computes them.
+// Band matrix storage (ScaledSparseMatrixD semantics: cells outside a column's used row range read as
+// 0.0).  Alpha columns are stored top-down, beta columns bottom-up, each fill appending its cells in
+// the order it computes them.  S is the element stride: 1 for a read's compact band (what scoring
+// reads), 64 for the lane-interleaved fill scratch (a fill wave's 64 reads share one region, so each
+// wave-wide access stays within a few pages instead of touching 64 separate 2 MB regions).
 // ---------------------------------------------------------------------------------------------
-struct Band {
+template <int S>
+struct StridedBand {
     int2* range;
     int* off;
     double* ls;
     double* val;
-    long long cap;
+    long long cap;   // capacity in values
+    __device__ __forceinline__ int2& R(int j) const { return range[(long long)j * S]; }
+    __device__ __forceinline__ int& O(int j) const { return off[(long long)j * S]; }
+    __device__ __forceinline__ double& L(int j) const { return ls[(long long)j * S]; }
+    __device__ __forceinline__ double& V(long long k) const { return val[k * S]; }
 };
+using Band = StridedBand<1>;
+using LaneBand = StridedBand<64>;
 
-__device__ __forceinline__ double alpha_at(const Band& m, int i, int j)
+template <int S>
+__device__ __forceinline__ double alpha_at(const StridedBand<S>& m, int i, int j)
 {
-    const int2 r = m.range[j];
-    return (i >= r.x && i < r.y) ? m.val[m.off[j] + (i - r.x)] : 0.0;
+    const int2 r = m.R(j);
+    return (i >= r.x && i < r.y) ? m.V(m.O(j) + (i - r.x)) : 0.0;
 }
 
-__device__ __forceinline__ double beta_at(const Band& m, int i, int j)
+template <int S>
+__device__ __forceinline__ double beta_at(const StridedBand<S>& m, int i, int j)
 {
-    const int2 r = m.range[j];
-    return (i >= r.x && i < r.y) ? m.val[m.off[j] + (r.y - 1 - i)] : 0.0;
+    const int2 r = m.R(j);
+    return (i >= r.x && i < r.y) ? m.V(m.O(j) + (r.y - 1 - i)) : 0.0;
 }
 
 struct Params {
@@ -233,79 +244,115 @@ constexpr int kM = 0, kS = 1, kB = 2, kD = 3, kS3 = 4;
 // RowRange :693-726 never trims scaled columns, so only ranges are consulted).  Ranges are updated
 // in place column by column, after their old value has been read.  Returns the used-entry count,
 // or -1 on value-capacity overflow.
+//
+// Latency structure: the in-column insertion chain a_i = (M_i + a_{i-1} k_i) + D_i is carried in
+// registers; the previous column and the read bases are prefetched kFillChunk rows at a time, so
+// a row costs its dependent FP64 chain, not an HBM/L2 round trip.
 // ---------------------------------------------------------------------------------------------
-template <class View>
-__device__ long long fill_alpha(const View& tv, const char* rd, int I, const Band& a, const int2* guide,
-                                bool selfValid, const Params& P)
+constexpr int kFillChunk = 8;
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+template <class View, int S>
+__device__ long long fill_alpha(const View& tv, const char* __restrict__ rd, int I, const StridedBand<S>& a,
+                                const StridedBand<S>* guide, bool selfValid, const Params& P)
 {
     const int J = tv.Length();
     if (a.cap < 1) return -1;
-    a.val[0] = 1.0;
-    a.range[0] = make_int2(0, 1);
-    a.off[0] = 0;
-    a.ls[0] = 0.0;
+    a.V(0) = 1.0;
+    a.R(0) = make_int2(0, 1);
+    a.O(0) = 0;
+    a.L(0) = 0.0;
     long long used = 1;
     int hb = 1, he = 1;
     int prevCtx = kCtxZero;
+    char curBase;
+    int curCtx;
+    tv.At(0, curBase, curCtx);
     for (int j = 1; j < J; ++j) {
-        char curBase; int curCtx;
-        tv.At(j - 1, curBase, curCtx);
         if (guide) {
-            const int2 g = guide[j];
+            const int2 g = guide->R(j);
             if (g.x < g.y) { hb = min(g.x, hb); he = max(g.y, he); }
         }
         if (selfValid) {
-            const int2 o = a.range[j];
+            const int2 o = a.R(j);
             if (o.x < o.y) { hb = min(o.x, hb); he = max(o.y, he); }
         }
         const int reqEnd = min(I, he);
-        const char nextBase = tv.Base(j);
+        char nextBase;
+        int nextCtx;
+        tv.At(j, nextBase, nextCtx);
         const double* cp = P.P(curCtx);
         const double* pp = P.P(prevCtx);
         const double pMatch = pp[kM], pDel = pp[kD];
         const double cBranch = cp[kB], cStick3 = cp[kS3];
-        const int2 pr = a.range[j - 1];
-        const double* pv = a.val + a.off[j - 1] - pr.x;   // prev column: pv[i], i in [pr.x, pr.y)
-        double* cv = a.val + used - hb;                      // this column: cv[i], i in [hb, end)
+        const int2 pr = a.R(j - 1);
+        const bool prNonEmpty = pr.x < pr.y;
+        const long long pbase = (long long)a.O(j - 1) - pr.x;   // prev column: V(pbase + i), i in [pr.x, pr.y)
+        const long long cbase = used - hb;                        // this column:  V(cbase + i), i in [hb, end)
         const int b = hb;
-        double thr = 0.0, mx = 0.0, score = 0.0;
+        const long long room = a.cap - used;
+        double thr = 0.0, mx = 0.0, score = 0.0, up = 0.0;
+        double diag = (prNonEmpty && b - 1 >= pr.x && b - 1 < pr.y) ? a.V(pbase + b - 1) : 0.0;
         int i = b;
-        for (; i < I && (score >= thr || i < reqEnd); ++i) {
-            if (used + (i - b) >= a.cap) return -1;
-            const char rb = rd[i - 1];
-            const double diag = (i - 1 >= pr.x && i - 1 < pr.y) ? pv[i - 1] : 0.0;
-            const double mpe = diag * (rb == curBase ? P.prNot : P.prThird);
-            double move = 0.0;
-            if (i == 1 && j == 1) move = mpe;
-            else if (i != 1 && j != 1) move = mpe * pMatch;
-            score = 0.0 + move;
-            if (i > 1) {
-                const double up = (i - 1 >= b) ? cv[i - 1] : 0.0;
-                score = score + up * (rb == nextBase ? cBranch : cStick3);
+        bool go = i < I;   // (score >= thr) holds for the first row
+        while (go) {
+            double lf[kFillChunk];
+            char rbs[kFillChunk];
+#pragma unroll
+            for (int q = 0; q < kFillChunk; ++q) {
+                const int row = i + q;
+                const bool in = prNonEmpty && row >= pr.x && row < pr.y;
+                const double x = a.V(prNonEmpty ? pbase + clampi(row, pr.x, pr.y - 1) : (long long)a.O(j - 1));
+                lf[q] = in ? x : 0.0;
+                rbs[q] = rd[clampi(row - 1, 0, I - 1)];
             }
-            if (j > 1) {
-                const double left = (i >= pr.x && i < pr.y) ? pv[i] : 0.0;
-                score = score + left * pDel;
+#pragma unroll
+            for (int q = 0; q < kFillChunk; ++q) {
+                if (i - b >= room) return -1;
+                const char rb = rbs[q];
+                const double left = lf[q];
+                const double mpe = diag * (rb == curBase ? P.prNot : P.prThird);
+                double move = 0.0;
+                if (i == 1 && j == 1) move = mpe;
+                else if (i != 1 && j != 1) move = mpe * pMatch;
+                score = 0.0 + move;
+                if (i > 1) score = score + up * (rb == nextBase ? cBranch : cStick3);
+                if (j > 1) score = score + left * pDel;
+                a.V(cbase + i) = score;
+                if (score > mx) { mx = score; thr = mx / P.sdn; }
+                up = score;
+                diag = left;
+                ++i;
+                go = i < I && (score >= thr || i < reqEnd);
+                if (!go) break;
             }
-            cv[i] = score;
-            if (score > mx) { mx = score; thr = mx / P.sdn; }
         }
         const int e = i;
-        // ScaledMatrix::FinishEditingColumn (ScaledMatrix-inl.hpp:35-60); mx == max(0, cells).
+        // ScaledMatrix::FinishEditingColumn (ScaledMatrix-inl.hpp:35-60); mx == max(0, cells).  The next
+        // column's begin hint is the first row whose *scaled* value reaches the unscaled threshold (:166).
+        int nhb = e;
         if (mx != 0.0 && mx != 1.0) {
-            for (int k = b; k < e; ++k) cv[k] = cv[k] / mx;
-            a.ls[j] = log(mx);
+#pragma unroll 4
+            for (int k = b; k < e; ++k) {
+                const double v = a.V(cbase + k) / mx;
+                a.V(cbase + k) = v;
+                if (nhb == e && !(v < thr)) nhb = k;
+            }
+            a.L(j) = log(mx);
         } else {
-            a.ls[j] = 0.0;
+            for (int k = b; k < e; ++k)
+                if (!(a.V(cbase + k) < thr)) { nhb = k; break; }
+            a.L(j) = 0.0;
         }
-        a.range[j] = make_int2(b, e);
-        a.off[j] = (int)used;
+        a.R(j) = make_int2(b, e);
+        a.O(j) = (int)used;
         used += e - b;
         prevCtx = curCtx;
+        curBase = nextBase;
+        curCtx = nextCtx;
         he = e;
-        int k = b;
-        while (k < e && cv[k] < thr) ++k;
-        hb = k;
+        hb = nhb;
     }
     // last column: pinned final match (:169-179)
     if (used + 1 > a.cap) return -1;
@@ -316,81 +363,111 @@ __device__ long long fill_alpha(const View& tv, const char* rd, int I, const Ban
     double v = lik;
     double ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = lik / c; ls = log(c); }
-    a.val[used] = v;
-    a.range[J] = make_int2(I, I + 1);
-    a.off[J] = (int)used;
-    a.ls[J] = ls;
+    a.V(used) = v;
+    a.R(J) = make_int2(I, I + 1);
+    a.O(J) = (int)used;
+    a.L(J) = ls;
     used += 1;
     return used;
 }
 
 // FillBeta (SimpleRecursor.cpp:183-296).  Same conventions as fill_alpha; values stored bottom-up.
-template <class View>
-__device__ long long fill_beta(const View& tv, const char* rd, int I, const Band& bm, const int2* guide,
-                               bool selfValid, const Params& P)
+template <class View, int S>
+__device__ long long fill_beta(const View& tv, const char* __restrict__ rd, int I, const StridedBand<S>& bm,
+                               const StridedBand<S>* guide, bool selfValid, const Params& P)
 {
     const int J = tv.Length();
     if (bm.cap < 1) return -1;
-    bm.val[0] = 1.0;
-    bm.range[J] = make_int2(I, I + 1);
-    bm.off[J] = 0;
-    bm.ls[J] = 0.0;
+    bm.V(0) = 1.0;
+    bm.R(J) = make_int2(I, I + 1);
+    bm.O(J) = 0;
+    bm.L(J) = 0.0;
     long long used = 1;
     int hb = I, he = I;
+    char nextBase;
+    int nextCtx;
+    tv.At(J - 1, nextBase, nextCtx);
     for (int j = J - 1; j > 0; --j) {
-        const char nextBase = tv.Base(j);
-        const int curCtx = tv.Ctx(j - 1);
+        char curBase;
+        int curCtx;
+        tv.At(j - 1, curBase, curCtx);
         if (guide) {
-            const int2 g = guide[j];
+            const int2 g = guide->R(j);
             if (g.x < g.y) { hb = min(g.x, hb); he = max(g.y, he); }
         }
         if (selfValid) {
-            const int2 o = bm.range[j];
+            const int2 o = bm.R(j);
             if (o.x < o.y) { hb = min(o.x, hb); he = max(o.y, he); }
         }
         const int reqBegin = max(0, hb);
         const double* cp = P.P(curCtx);
         const double cMatch = cp[kM], cDel = cp[kD], cBranch = cp[kB], cStick3 = cp[kS3];
-        const int2 nr = bm.range[j + 1];
-        const double* nv = bm.val + bm.off[j + 1] + (nr.y - 1);   // next column: nv[-i], i in [nr.x, nr.y)
+        const int2 nr = bm.R(j + 1);
+        const bool nrNonEmpty = nr.x < nr.y;
+        const long long nbase = (long long)bm.O(j + 1) + (nr.y - 1);   // next column: V(nbase - i)
         const int e = he;
-        double* cv = bm.val + used + (e - 1);                     // this column: cv[-i], i in (begin, e)
-        double thr = 0.0, mx = 0.0, score = 0.0;
+        const long long cbase = used + (e - 1);                       // this column: V(cbase - i)
+        const long long room = bm.cap - used;
+        double thr = 0.0, mx = 0.0, score = 0.0, up = 0.0;
         int i = e - 1;
-        for (; i > 0 && (score >= thr || i >= reqBegin); --i) {
-            if (used + (e - 1 - i) >= bm.cap) return -1;
-            const char nb = rd[i];
-            const bool same = nb == nextBase;
-            const double diag = (i + 1 >= nr.x && i + 1 < nr.y) ? nv[-(i + 1)] : 0.0;
-            const double mpe = diag * (same ? P.prNot : P.prThird);
-            score = 0.0;
-            if (i < I - 1) score = 0.0 + mpe * cMatch;
-            else if (i == I - 1 && j == J - 1) score = 0.0 + mpe;
-            if (i < I - 1 && i > 0) {
-                const double up = (i + 1 <= e - 1) ? cv[-(i + 1)] : 0.0;
-                score = score + up * (same ? cBranch : cStick3);
+        double diag = (nrNonEmpty && i + 1 >= nr.x && i + 1 < nr.y) ? bm.V(nbase - (i + 1)) : 0.0;
+        bool go = i > 0;
+        while (go) {
+            double lf[kFillChunk];
+            char nbs[kFillChunk];
+#pragma unroll
+            for (int q = 0; q < kFillChunk; ++q) {
+                const int row = i - q;
+                const bool in = nrNonEmpty && row >= nr.x && row < nr.y;
+                const double x = bm.V(nrNonEmpty ? nbase - clampi(row, nr.x, nr.y - 1) : (long long)bm.O(j + 1));
+                lf[q] = in ? x : 0.0;
+                nbs[q] = rd[clampi(row, 0, I - 1)];
             }
-            if (j < J - 1 && j > 0) {
-                const double left = (i >= nr.x && i < nr.y) ? nv[-i] : 0.0;
-                score = score + left * cDel;
+#pragma unroll
+            for (int q = 0; q < kFillChunk; ++q) {
+                if (e - 1 - i >= room) return -1;
+                const char nb = nbs[q];
+                const double left = lf[q];
+                const bool same = nb == nextBase;
+                const double mpe = diag * (same ? P.prNot : P.prThird);
+                score = 0.0;
+                if (i < I - 1) score = 0.0 + mpe * cMatch;
+                else if (i == I - 1 && j == J - 1) score = 0.0 + mpe;
+                if (i < I - 1 && i > 0) score = score + up * (same ? cBranch : cStick3);
+                if (j < J - 1 && j > 0) score = score + left * cDel;
+                bm.V(cbase - i) = score;
+                if (score > mx) { mx = score; thr = mx / P.sdn; }
+                up = score;
+                diag = left;
+                --i;
+                go = i > 0 && (score >= thr || i >= reqBegin);
+                if (!go) break;
             }
-            cv[-i] = score;
-            if (score > mx) { mx = score; thr = mx / P.sdn; }
         }
         const int b = i + 1;
+        // FinishEditingColumn, then the next column's end hint: scan down from the top while the
+        // scaled value stays below the unscaled threshold (:282-285).
+        int nhe = b;
         if (mx != 0.0 && mx != 1.0) {
-            for (int k = b; k < e; ++k) cv[-k] = cv[-k] / mx;
-            bm.ls[j] = log(mx);
+#pragma unroll 4
+            for (int k = e - 1; k >= b; --k) {
+                const double v = bm.V(cbase - k) / mx;
+                bm.V(cbase - k) = v;
+                if (nhe == b && !(v < thr)) nhe = k + 1;
+            }
+            bm.L(j) = log(mx);
         } else {
-            bm.ls[j] = 0.0;
+            for (int k = e - 1; k >= b; --k)
+                if (!(bm.V(cbase - k) < thr)) { nhe = k + 1; break; }
+            bm.L(j) = 0.0;
         }
-        bm.range[j] = make_int2(b, e);
-        bm.off[j] = (int)used;
+        bm.R(j) = make_int2(b, e);
+        bm.O(j) = (int)used;
         used += e - b;
         hb = b;
-        int k = e;
-        while (k > b && cv[-(k - 1)] < thr) --k;
-        he = k;
+        he = nhe;
+        nextBase = curBase;
+        nextCtx = curCtx;
     }
     if (used + 1 > bm.cap) return -1;
     const double em = (tv.Base(0) == rd[0]) ? P.prNot : P.prThird;
@@ -399,18 +476,19 @@ __device__ long long fill_beta(const View& tv, const char* rd, int I, const Band
     double v = raw;
     double ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = raw / c; ls = log(c); }
-    bm.val[used] = v;
-    bm.range[0] = make_int2(0, 1);
-    bm.off[0] = (int)used;
-    bm.ls[0] = ls;
+    bm.V(used) = v;
+    bm.R(0) = make_int2(0, 1);
+    bm.O(0) = (int)used;
+    bm.L(0) = ls;
     used += 1;
     return used;
 }
 
-__device__ __forceinline__ double sum_ls(const double* ls, int n)
+template <int S>
+__device__ __forceinline__ double sum_ls(const StridedBand<S>& m, int n)
 {
     double s = 0.0;   // std::accumulate from 0.0, left to right
-    for (int k = 0; k < n; ++k) s = s + ls[k];
+    for (int k = 0; k < n; ++k) s = s + m.L(k);
     return s;
 }
 

@@ -14,6 +14,8 @@
 #include "arrow_device.hpp"
 #include "arrow_kernels.hpp"
 
+#include <climits>
+
 namespace pbccs {
 
 // ------------------------------------------------------------------------------------------------
@@ -72,76 +74,207 @@ __device__ __forceinline__ TplView window_view(const DevBatch& B, int r)
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_fill: FillAlphaBeta per read (MutationScorer ctor / Template(), MutationScorer.cpp:53-131)
+// k_fill: FillAlphaBeta per read (MutationScorer ctor / Template(), MutationScorer.cpp:53-131), one
+// lane per read, into the lane-interleaved scratch of its 64-read group; k_compact then moves the
+// final alpha/beta bands into each read's compact layout.
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_fill(DevBatch B, const int* __restrict__ reads, int n)
+__device__ __forceinline__ LaneBand scratch_band(const FillScratch& F, int g, int l, int which)
+{
+    const long long gm = 2LL * g + which;
+    LaneBand m;
+    m.range = F.range + gm * F.capCols * 64 + l;
+    m.off = F.off + gm * F.capCols * 64 + l;
+    m.ls = F.ls + gm * F.capCols * 64 + l;
+    m.val = F.val + gm * F.capSlots * 64 + l;
+    m.cap = F.capSlots;
+    return m;
+}
+
+__global__ void __launch_bounds__(64) k_fill(DevBatch B, FillScratch F, const int* __restrict__ reads, int n)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
+    const int g = t >> 6, l = t & 63;
     const int r = reads[t];
     const int z = B.rZmw[r];
     const int I = B.rLen[r];
     const TplView tv = window_view(B, r);
     const int J = tv.Length();
-    if (I < 1 || J < 1) {
-        B.rStatus[r] = kFillBadInput;
+    if (I < 1 || J < 1 || J + 2 > F.capCols) {
+        B.rStatus[r] = (I < 1 || J < 1) ? kFillBadInput : kFillOverflow;
         return;
     }
     const char* rd = B.seqPool + B.rSeqOff[r];
     const Params P = params_for(B, z);
-    const Band a = band_alpha(B, r);
-    const Band b = band_beta(B, r);
+    const LaneBand a = scratch_band(F, g, l, 0);
+    const LaneBand b = scratch_band(F, g, l, 1);
 
     unsigned long long cells = 0, passes = 0;
-    long long ua = fill_alpha(tv, rd, I, a, nullptr, false, P);
+    long long ua = fill_alpha(tv, rd, I, a, (const LaneBand*)nullptr, false, P);
     if (ua < 0) { B.rStatus[r] = kFillOverflow; return; }
-    long long ub = fill_beta(tv, rd, I, b, a.range, false, P);
+    long long ub = fill_beta(tv, rd, I, b, &a, false, P);
     if (ub < 0) { B.rStatus[r] = kFillOverflow; return; }
     cells += ua + ub;
     passes += 2;
     int flips = 0;
     const int maxSize = (int)(0.5 + kRebandFrac * (I + 1) * (J + 1));
     if (ua >= maxSize || ub >= maxSize) {
-        ua = fill_alpha(tv, rd, I, a, b.range, true, P);
-        if (ua < 0) { B.rStatus[r] = kFillOverflow; return; }
-        ub = fill_beta(tv, rd, I, b, a.range, true, P);
+        const long long a1 = fill_alpha(tv, rd, I, a, &b, true, P);
+        if (a1 < 0) { B.rStatus[r] = kFillOverflow; return; }
+        ub = fill_beta(tv, rd, I, b, &a, true, P);
         if (ub < 0) { B.rStatus[r] = kFillOverflow; return; }
-        const long long ua2 = fill_alpha(tv, rd, I, a, b.range, true, P);
-        if (ua2 < 0) { B.rStatus[r] = kFillOverflow; return; }
-        cells += ua + ub + ua2;
+        ua = fill_alpha(tv, rd, I, a, &b, true, P);
+        if (ua < 0) { B.rStatus[r] = kFillOverflow; return; }
+        cells += a1 + ub + ua;
         passes += 3;
-        ua = ua2;
         flips += 3;
     }
-    double av = log(alpha_at(a, I, J)) + sum_ls(a.ls, J + 1);
-    double bv = log(beta_at(b, 0, 0)) + sum_ls(b.ls, J + 1);
+    double av = log(alpha_at(a, I, J)) + sum_ls(a, J + 1);
+    double bv = log(beta_at(b, 0, 0)) + sum_ls(b, J + 1);
     // NB: the reference does not re-evaluate alphaV/betaV inside this loop (SimpleRecursor.cpp:667-679).
     const bool mismatched = fabs(av - bv) > kAlphaBetaTol;
     while (mismatched && flips <= kMaxFlipFlops) {
-        const long long u = (flips % 2 == 0) ? fill_alpha(tv, rd, I, a, b.range, true, P)
-                                             : fill_beta(tv, rd, I, b, a.range, true, P);
-        if (u < 0) { B.rStatus[r] = kFillOverflow; return; }
-        cells += u;
+        if (flips % 2 == 0) {
+            ua = fill_alpha(tv, rd, I, a, &b, true, P);
+            if (ua < 0) { B.rStatus[r] = kFillOverflow; return; }
+            cells += ua;
+        } else {
+            ub = fill_beta(tv, rd, I, b, &a, true, P);
+            if (ub < 0) { B.rStatus[r] = kFillOverflow; return; }
+            cells += ub;
+        }
         passes += 1;
         ++flips;
     }
     // alpha prefix sums (exactly GetLogProdScales(0, k) for every k) and its total
-    double* pre = B.aPre + B.rColBase[r];
+    double* pre = F.pre + (long long)g * (F.capCols + 1) * 64 + l;
     double s = 0.0;
     pre[0] = 0.0;
     for (int k = 0; k <= J; ++k) {
-        s = s + a.ls[k];
-        pre[k + 1] = s;
+        s = s + a.L(k);
+        pre[(long long)(k + 1) * 64] = s;
     }
     av = log(alpha_at(a, I, J)) + s;
-    bv = log(beta_at(b, 0, 0)) + sum_ls(b.ls, J + 1);
+    bv = log(beta_at(b, 0, 0)) + sum_ls(b, J + 1);
     const double mism = fabs(1.0 - av / bv);
     B.rFlips[r] = flips;
     B.rBaseline[r] = bv;
+    F.usedA[r] = (int)ua;
+    F.usedB[r] = (int)ub;
     B.rStatus[r] = (mism > kAlphaBetaTol) ? kFillMismatch : kFillOk;
     if (B.stats) {   // algorithmic: 8 B per stored cell + 16 B per column per fill pass
         atomicAdd(&B.stats[2 * kStatFill], cells);
         atomicAdd(&B.stats[2 * kStatFill + 1], 8ull * cells + 16ull * passes * (unsigned long long)(J + 1));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_compact: one workgroup per 64-read fill group.  Transposes the group's [slot][lane] scratch through
+// LDS into each read's contiguous band (coalesced 512 B rows in, 512 B per-read runs out), and the
+// [column][lane] metadata into the per-read column slots the scoring kernels index.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_compact(DevBatch B, FillScratch F, const int* __restrict__ reads, int n)
+{
+    __shared__ double tile[64][65];
+    __shared__ int rid[64], uA[64], uB[64], ncol[64], ok[64];
+    __shared__ long long dA[64], dB[64], cb[64];
+    const int g = blockIdx.x;
+    const int t = threadIdx.x;
+    if (t < 64) {
+        const int idx = g * 64 + t;
+        int r = -1, good = 0;
+        if (idx < n) {
+            r = reads[idx];
+            good = (B.rStatus[r] == kFillOk || B.rStatus[r] == kFillMismatch) ? 1 : 0;
+        }
+        rid[t] = r;
+        ok[t] = good;
+        uA[t] = good ? F.usedA[r] : 0;
+        uB[t] = good ? F.usedB[r] : 0;
+        ncol[t] = good ? window_view(B, r).Length() + 1 : 0;
+        dA[t] = good ? B.rValA[r] : 0;
+        dB[t] = good ? B.rValB[r] : 0;
+        cb[t] = good ? B.rColBase[r] : 0;
+    }
+    __syncthreads();
+    int maxA = 0, maxB = 0, maxC = 0;
+    for (int q = 0; q < 64; ++q) {
+        maxA = max(maxA, uA[q]);
+        maxB = max(maxB, uB[q]);
+        maxC = max(maxC, ncol[q]);
+    }
+    const int w = t >> 6, ln = t & 63;
+    // values: alpha then beta
+    for (int which = 0; which < 2; ++which) {
+        const int maxU = which ? maxB : maxA;
+        const double* src = F.val + (2LL * g + which) * F.capSlots * 64;
+        for (int s0 = 0; s0 < maxU; s0 += 64) {
+            for (int q = w; q < 64; q += 4) {
+                const int slot = s0 + q;
+                tile[q][ln] = (slot < maxU) ? src[(long long)slot * 64 + ln] : 0.0;
+            }
+            __syncthreads();
+            for (int q = w; q < 64; q += 4) {   // q = read (lane) of the group, ln = slot within the tile
+                const int used = which ? uB[q] : uA[q];
+                const int slot = s0 + ln;
+                if (ok[q] && slot < used) B.valPool[(which ? dB[q] : dA[q]) + slot] = tile[ln][q];
+            }
+            __syncthreads();
+        }
+    }
+    // column metadata: ranges, offsets, log-scales of both matrices, and the alpha prefix (J+2 entries)
+    for (int c0 = 0; c0 < maxC + 1; c0 += 64) {
+        for (int which = 0; which < 2; ++which) {
+            const long long gm = (2LL * g + which) * F.capCols * 64;
+            // ls (double) through the tile
+            for (int q = w; q < 64; q += 4) {
+                const int c = c0 + q;
+                tile[q][ln] = (c < maxC) ? F.ls[gm + (long long)c * 64 + ln] : 0.0;
+            }
+            __syncthreads();
+            for (int q = w; q < 64; q += 4) {
+                const int c = c0 + ln;
+                if (ok[q] && c < ncol[q]) (which ? B.bLs : B.aLs)[cb[q] + c] = tile[ln][q];
+            }
+            __syncthreads();
+            // ranges and offsets packed into the tile as raw bits
+            for (int q = w; q < 64; q += 4) {
+                const int c = c0 + q;
+                const int2 rg = (c < maxC) ? F.range[gm + (long long)c * 64 + ln] : make_int2(0, 0);
+                tile[q][ln] = __longlong_as_double((long long)(((unsigned long long)(unsigned)rg.y << 32) | (unsigned)rg.x));
+            }
+            __syncthreads();
+            for (int q = w; q < 64; q += 4) {
+                const int c = c0 + ln;
+                if (ok[q] && c < ncol[q]) {
+                    const long long bits = __double_as_longlong(tile[ln][q]);
+                    (which ? B.bRange : B.aRange)[cb[q] + c] = make_int2((int)(bits & 0xffffffff), (int)(bits >> 32));
+                }
+            }
+            __syncthreads();
+            for (int q = w; q < 64; q += 4) {
+                const int c = c0 + q;
+                tile[q][ln] = __longlong_as_double((c < maxC) ? (long long)F.off[gm + (long long)c * 64 + ln] : 0LL);
+            }
+            __syncthreads();
+            for (int q = w; q < 64; q += 4) {
+                const int c = c0 + ln;
+                if (ok[q] && c < ncol[q]) (which ? B.bOff : B.aOff)[cb[q] + c] = (int)__double_as_longlong(tile[ln][q]);
+            }
+            __syncthreads();
+        }
+        // alpha prefix: J+2 entries (columns 0..J+1)
+        const double* pre = F.pre + (long long)g * (F.capCols + 1) * 64;
+        for (int q = w; q < 64; q += 4) {
+            const int c = c0 + q;
+            tile[q][ln] = (c < maxC + 1) ? pre[(long long)c * 64 + ln] : 0.0;
+        }
+        __syncthreads();
+        for (int q = w; q < 64; q += 4) {
+            const int c = c0 + ln;
+            if (ok[q] && c < ncol[q] + 1) B.aPre[cb[q] + c] = tile[ln][q];
+        }
+        __syncthreads();
     }
 }
 
@@ -547,20 +680,165 @@ __device__ __forceinline__ bool read_scores(int ts, int te, int type, int ms, in
     return ts < me && ms < te;
 }
 
-// MutationScorer::ScoreMutation(OrientedMutation(read, m)) - MutationScorer::Score() for one read.
-__device__ double score_mutation(const DevBatch& B, int r, int code, const ScoreScratch& scratch, TaskStat& st)
+// ------------------------------------------------------------------------------------------------
+// Middle-case scoring (the ~99% case: 3 <= start, end <= J-2): ExtendAlpha over 2 columns + LinkAlphaBeta
+// (MutationScorer.cpp:193-218, SimpleRecursor.cpp:306-357 / :373-487), specialised.  In this case
+// absLinkCol == sc + 2 for every mutation type, j0 + 2 < Jv, and every guarded branch of the generic
+// ExtendAlpha resolves statically except the per-row ones kept below.
+//   av: alpha(i, sc-1) = av[i] for i in ar;  bv: beta(i, bc) = bv[-i] for i in br;  rdp[i] = read base i.
+// The pointers address either the wave's LDS stage or HBM (oversized bands).
+// ------------------------------------------------------------------------------------------------
+struct MidGeom {
+    int b0, e0, b1, e1;   // ext column row ranges
+    int lb, le;           // link row range
+};
+
+__device__ __forceinline__ MidGeom middle_geometry(const Band& a, const Band& b, int sc, int bc)
+{
+    MidGeom g;
+    const int2 r0 = a.range[sc - 1], r1 = a.range[sc], r2 = a.range[sc + 1], r3 = a.range[sc + 2];
+    g.b0 = min(min(r1.x, r0.x), r2.x);
+    g.e0 = max(max(r1.y, r0.y), r2.y);
+    g.b1 = min(min(r2.x, r1.x), r3.x);
+    g.e1 = max(max(r2.y, r1.y), r3.y);
+    const int2 q0 = b.range[bc], q1 = b.range[bc + 1];
+    g.lb = min(min(g.b0, g.b1), min(q0.x, q1.x));
+    g.le = max(max(g.e0, g.e1), max(q0.y, q1.y));
+    return g;
+}
+
+__device__ __forceinline__ double score_middle(const ScoreCtx& S, int sc, int bc, const MidGeom& g,
+                                               const double* __restrict__ av, int2 ar,
+                                               const double* __restrict__ bv, int2 br,
+                                               const char* __restrict__ rdp, TaskStat& st)
+{
+    const int I = S.I;
+    // template positions sc-2 .. sc+1 under the virtual mutation
+    char t0, t1, t2, t3;
+    int x0, x1, x2, x3;
+    S.tv.At(sc - 2, t0, x0);
+    S.tv.At(sc - 1, t1, x1);
+    S.tv.At(sc, t2, x2);
+    S.tv.At(sc + 1, t3, x3);
+    (void)t0;
+    const double* P0 = S.P.P(sc > 1 ? x0 : kCtxZero);
+    const double* P1 = S.P.P(x1);
+    const double* P2 = S.P.P(x2);
+    // ext column 0 (j = sc):   cur = pos sc-1, prev = pos sc-2, next base = pos sc
+    const double pM0 = P0[kM], pD0 = P0[kD], cB0 = P1[kB], cS0 = P1[kS3];
+    // ext column 1 (j = sc+1): cur = pos sc, prev = pos sc-1, next base = pos sc+1
+    const double pM1 = P1[kM], pD1 = P1[kD], cB1 = P2[kB], cS1 = P2[kS3];
+    // link (absLinkCol = sc+2): cur base = pos sc+1, prev params = pos sc
+    const double lM = P2[kM], lD = P2[kD];
+    const double pn = S.P.prNot, p3 = S.P.prThird;
+
+#define PB_ALPHA(i) (((i) >= ar.x && (i) < ar.y) ? av[(i)] : 0.0)
+#define PB_BETA(i) (((i) >= br.x && (i) < br.y) ? bv[-(i)] : 0.0)
+    // one ext cell (ExtendAlpha :445-483) with j in (1, Jv): only the row conditions remain
+#define PB_CELL(out, i, rb, curB, nxtB, pM, pD, cB, cS, pd, pl, rawPrev)                    \
+    {                                                                                     \
+        const double em_ = ((rb) == (curB)) ? pn : p3;                                    \
+        double s_ = ((i) > 0) ? (((i) < I) ? (pd) * (pM) * em_ : 0.0) : (rawPrev);        \
+        if ((i) > 1 && (i) < I) s_ = s_ + (rawPrev) * (((nxtB) == (rb)) ? (cB) : (cS));   \
+        if ((i) != I) s_ = s_ + (pl) * (pD);                                              \
+        out = s_;                                                                         \
+    }
+
+    // sweep 1: column 0 raw values -> its FinishEditingColumn constant C0
+    double C0 = 0.0;
+    {
+        double aD = PB_ALPHA(g.b0 - 1), raw = 0.0;
+        for (int i = g.b0; i < g.e0; ++i) {
+            const double aL = PB_ALPHA(i);
+            const char rb = rdp[i - 1];
+            double v;
+            PB_CELL(v, i, rb, t1, t2, pM0, pD0, cB0, cS0, aD, aL, raw);
+            raw = v;
+            if (C0 < v) C0 = v;
+            aD = aL;
+        }
+    }
+    const bool s0 = (C0 != 0.0 && C0 != 1.0);
+    // sweep 2: column 0 scaled, column 1 raw -> C1
+    const int u0 = min(g.b0, g.b1), u1 = max(g.e0, g.e1);
+    double C1 = 0.0;
+    {
+        double aD = PB_ALPHA(u0 - 1), raw0 = 0.0, raw1 = 0.0, sc0p = 0.0;
+        for (int i = u0; i < u1; ++i) {
+            const double aL = PB_ALPHA(i);
+            const char rb = rdp[i - 1];
+            double v0 = 0.0, v1 = 0.0, sc0 = 0.0;
+            if (i >= g.b0 && i < g.e0) {
+                PB_CELL(v0, i, rb, t1, t2, pM0, pD0, cB0, cS0, aD, aL, raw0);
+                sc0 = s0 ? v0 / C0 : v0;
+            }
+            if (i >= g.b1 && i < g.e1) {
+                PB_CELL(v1, i, rb, t2, t3, pM1, pD1, cB1, cS1, sc0p, sc0, raw1);
+                if (C1 < v1) C1 = v1;
+            }
+            raw0 = v0;
+            raw1 = v1;
+            sc0p = sc0;
+            aD = aL;
+        }
+    }
+    const bool s1 = (C1 != 0.0 && C1 != 1.0);
+    // sweep 3: both columns scaled + LinkAlphaBeta over the union of the four used ranges
+    double v = 0.0;
+    {
+        double aD = PB_ALPHA(g.lb - 1), raw0 = 0.0, raw1 = 0.0, sc0p = 0.0;
+        double bH = PB_BETA(g.lb);
+        for (int i = g.lb; i < g.le; ++i) {
+            const double aL = PB_ALPHA(i);
+            const double bN = PB_BETA(i + 1);
+            const char rb = (i >= 1) ? rdp[i - 1] : (char)0;
+            double v0 = 0.0, v1 = 0.0, sc0 = 0.0, sc1 = 0.0;
+            if (i >= g.b0 && i < g.e0) {
+                PB_CELL(v0, i, rb, t1, t2, pM0, pD0, cB0, cS0, aD, aL, raw0);
+                sc0 = s0 ? v0 / C0 : v0;
+            }
+            if (i >= g.b1 && i < g.e1) {
+                PB_CELL(v1, i, rb, t2, t3, pM1, pD1, cB1, cS1, sc0p, sc0, raw1);
+                sc1 = s1 ? v1 / C1 : v1;
+            }
+            if (i < I) {
+                const double mprob = lM * ((rdp[i] == t3) ? pn : p3);
+                v = v + sc1 * mprob * bN;
+            }
+            v = v + sc1 * lD * bH;
+            raw0 = v0;
+            raw1 = v1;
+            sc0p = sc0;
+            aD = aL;
+            bH = bN;
+        }
+    }
+#undef PB_CELL
+#undef PB_BETA
+#undef PB_ALPHA
+    const double E = (0.0 + (s0 ? log(C0) : 0.0)) + (s1 ? log(C1) : 0.0);
+    st.cells += (unsigned long long)(max(0, g.e0 - g.b0) + max(0, g.e1 - g.b1) + max(0, g.le - g.lb));
+    st.bytes += 8ull * (unsigned long long)(max(0, ar.y - ar.x) + max(0, br.y - br.x)) + 16ull * 6ull;
+    return ((log(v) + E) + S.bSuf[bc]) + S.aPre[sc];
+}
+
+// ScoreCtx + oriented mutation for read r (OrientedMutation, MultiReadMutationScorer.cpp:93-139;
+// the virtual mutation of MultiReadMutationScorer::Score, :338-348).
+struct Oriented {
+    int os, oe, ld, type;
+};
+
+__device__ __forceinline__ Oriented setup_score(const DevBatch& B, int r, int code, ScoreCtx& S)
 {
     const int z = B.rZmw[r];
     const int L = B.zLen[z];
     const int ts = B.rTs[r], te = B.rTe[r];
-    const int type = mut_type(code);
+    Oriented o;
+    o.type = mut_type(code);
     const int pos = mut_pos(code);
     const int base = mut_base(code);
-    const int mStart = pos;
-    const int mEnd = (type == kIns) ? pos : pos + 1;
-    const int ld = (type == kIns) ? 1 : (type == kDel ? -1 : 0);
-
-    ScoreCtx S;
+    const int mEnd = (o.type == kIns) ? pos : pos + 1;
+    o.ld = (o.type == kIns) ? 1 : (o.type == kDel ? -1 : 0);
     S.B = &B;
     S.P = params_for(B, z);
     S.rd = B.seqPool + B.rSeqOff[r];
@@ -572,96 +850,231 @@ __device__ double score_mutation(const DevBatch& B, int r, int code, const Score
     S.aPre = B.aPre + cbase;
     S.bSuf = B.bSuf + cbase;
     S.tv = window_view(B, r);
-    int os, oe;
     if (B.rStrand[r] == kFwd) {
-        S.tv.vm = make_virtual(S.tv.T, L, type, mStart, base_char(base));
-        os = mStart - ts;
-        oe = mEnd - ts;
+        S.tv.vm = make_virtual(S.tv.T, L, o.type, pos, base_char(base));
+        o.os = pos - ts;
+        o.oe = mEnd - ts;
     } else {
-        S.tv.vm = make_virtual(S.tv.T, L, type, L - mEnd, base_char(complement_index(base)));
-        os = te - mEnd;
-        oe = te - mStart;
+        S.tv.vm = make_virtual(S.tv.T, L, o.type, L - mEnd, base_char(complement_index(base)));
+        o.os = te - mEnd;
+        o.oe = te - pos;
     }
-    const int J = S.Jorig;
-    const int betaLinkCol = 1 + oe;
-    const int absLinkCol = 1 + oe + ld;
-    const bool atBegin = os < 3;
-    const bool atEnd = oe > (J + 1) - 1 - 2;
-    double score;
-    if (!atBegin && !atEnd) {
-        const int sc = (type == kDel) ? os - 1 : os;
-        score = extend_alpha_score(S, sc, 2, true, betaLinkCol, absLinkCol, st);
-    } else if (!atBegin && atEnd) {
-        const int sc = os - 1;
-        const int n = S.tv.Length() - sc + 1;
-        score = extend_alpha_score(S, sc, n, false, 0, 0, st);
-    } else if (atBegin && !atEnd) {
-        score = extend_beta_score(S, oe, ld, st);
-    } else {
-        // whole fill of the virtually mutated window (MutationScorer.cpp:246-266); tiny windows only
-        const int Jv = S.tv.Length();
-        const long long ncol = Jv + 1;
-        const long long need = ncol * (long long)(S.I + 1) + 4 * ncol + 16;
-        const unsigned long long at = atomicAdd(scratch.top, (unsigned long long)need);
-        if (at + need > scratch.cap) {
-            atomicOr(scratch.overflow, 1);
-            return __longlong_as_double(0x7ff8000000000001LL);
-        }
-        double* base0 = scratch.pool + at;
-        Band m;
-        m.ls = base0;
-        m.range = reinterpret_cast<int2*>(base0 + ncol);
-        m.off = reinterpret_cast<int*>(base0 + 2 * ncol);
-        m.val = base0 + 4 * ncol;
-        m.cap = ncol * (long long)(S.I + 1);
-        const long long u = fill_alpha(S.tv, S.rd, S.I, m, nullptr, false, S.P);
-        st.cells += (unsigned long long)max(0LL, u);
-        st.bytes += 8ull * (unsigned long long)max(0LL, u) + 16ull * (unsigned long long)ncol;
-        score = log(alpha_at(m, S.I, Jv)) + sum_ls(m.ls, Jv + 1);
-    }
-    return score - B.rBaseline[r];
+    return o;
 }
 
-// One wave per (work item, read, 64-mutation chunk); lanes take consecutive mutations of one read so
-// that a wave walks adjacent template positions of a single read's bands (L1/L2 reuse).
+// The non-middle cases of MutationScorer::ScoreMutation (MutationScorer.cpp:219-267), from HBM.
+__device__ double score_edge(const ScoreCtx& S, const Oriented& o, const ScoreScratch& scratch, TaskStat& st)
+{
+    const int J = S.Jorig;
+    const bool atBegin = o.os < 3;
+    const bool atEnd = o.oe > (J + 1) - 1 - 2;
+    if (!atBegin && atEnd) {
+        const int sc = o.os - 1;
+        const int n = S.tv.Length() - sc + 1;
+        return extend_alpha_score(S, sc, n, false, 0, 0, st);
+    }
+    if (atBegin && !atEnd) return extend_beta_score(S, o.oe, o.ld, st);
+    if (!atBegin && !atEnd) {   // not reached from k_score (middle case has its own path)
+        const int sc = (o.type == kDel) ? o.os - 1 : o.os;
+        return extend_alpha_score(S, sc, 2, true, 1 + o.oe, 1 + o.oe + o.ld, st);
+    }
+    // whole fill of the virtually mutated window (MutationScorer.cpp:246-266); tiny windows only
+    const int Jv = S.tv.Length();
+    const long long ncol = Jv + 1;
+    const long long need = ncol * (long long)(S.I + 1) + 4 * ncol + 16;
+    const unsigned long long at = atomicAdd(scratch.top, (unsigned long long)need);
+    if (at + need > scratch.cap) {
+        atomicOr(scratch.overflow, 1);
+        return __longlong_as_double(0x7ff8000000000001LL);
+    }
+    double* base0 = scratch.pool + at;
+    Band m;
+    m.ls = base0;
+    m.range = reinterpret_cast<int2*>(base0 + ncol);
+    m.off = reinterpret_cast<int*>(base0 + 2 * ncol);
+    m.val = base0 + 4 * ncol;
+    m.cap = ncol * (long long)(S.I + 1);
+    const long long u = fill_alpha(S.tv, S.rd, S.I, m, (const Band*)nullptr, false, S.P);
+    st.cells += (unsigned long long)max(0LL, u);
+    st.bytes += 8ull * (unsigned long long)max(0LL, u) + 16ull * (unsigned long long)ncol;
+    return log(alpha_at(m, S.I, Jv)) + sum_ls(m, Jv + 1);
+}
+
+__device__ __forceinline__ int wave_min(int v)
+{
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ int wave_max(int v)
+{
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// LDS stage of one wave: the alpha columns sc-1 and beta columns bc its 64 lanes read (contiguous in
+// HBM because fills append columns in order) and the read bases under their rows.
+constexpr int kScoreWaves = 4;
+constexpr int kStageA = 512;
+constexpr int kStageB = 512;
+constexpr int kStageR = 1024;
+struct WaveStage {
+    double a[kStageA];
+    double b[kStageB];
+    char rd[kStageR];
+};
+
+// One wave per (work item, read, 64-mutation chunk): the lanes take consecutive mutations of one read,
+// i.e. adjacent template positions, so the wave shares a handful of band columns.
 __global__ void __launch_bounds__(256) k_score(DevBatch B, ScoreWork W, ScoreScratch scratch)
 {
-    const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    __shared__ WaveStage stage[kScoreWaves];
+    const int wid = threadIdx.x >> 6;
+    const long long wave = (long long)blockIdx.x * kScoreWaves + wid;
     const int lane = threadIdx.x & 63;
-    if (wave >= W.waveStart[W.nWork]) return;
-    // binary search of the work item (wave-uniform)
-    int lo = 0, hi = W.nWork;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (W.waveStart[mid] <= wave) lo = mid; else hi = mid;
+    const bool waveLive = wave < W.waveStart[W.nWork];
+    int k = 0;
+    if (waveLive) {   // binary search of the work item (wave-uniform)
+        int lo = 0, hi = W.nWork;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (W.waveStart[mid] <= wave) lo = mid; else hi = mid;
+        }
+        k = lo;
     }
-    const int k = lo;
-    const int z = W.zmw[k];
-    const int M = W.nMut[k];
-    const int chunks = (M + 63) >> 6;
-    const long long local = wave - W.waveStart[k];
+    const int z = waveLive ? W.zmw[k] : 0;
+    const int M = waveLive ? W.nMut[k] : 0;
+    const int chunks = max(1, (M + 63) >> 6);
+    const long long local = waveLive ? wave - W.waveStart[k] : 0;
     const int rr = (int)(local / chunks);
     const int m = (int)(local % chunks) * 64 + lane;
-    TaskStat st;
-    if (m < M) {
-        const int r = B.zReadBegin[z] + rr;
-        const int code = W.codes[W.mutBase[k] + m];
-        double d = 0.0;
+    const bool valid = waveLive && m < M;
+    const int r = waveLive ? B.zReadBegin[z] + rr : 0;
+
+    // classify this lane's task
+    int code = 0;
+    bool scored = false;
+    if (valid) {
+        code = W.codes[W.mutBase[k] + m];
         const int type = mut_type(code), pos = mut_pos(code);
         const int me = (type == kIns) ? pos : pos + 1;
-        if (B.rActive[r] && read_scores(B.rTs[r], B.rTe[r], type, pos, me)) d = score_mutation(B, r, code, scratch, st);
-        W.delta[W.deltaBase[k] + (long long)rr * M + m] = d;
+        scored = B.rActive[r] && read_scores(B.rTs[r], B.rTe[r], type, pos, me);
     }
+    ScoreCtx S;
+    Oriented o;
+    o.os = o.oe = o.ld = o.type = 0;
+    bool middle = false;
+    int sc = 0, bc = 0;
+    MidGeom g;
+    g.b0 = g.e0 = g.b1 = g.e1 = g.lb = g.le = 0;
+    if (scored) {
+        o = setup_score(B, r, code, S);
+        const int J = S.Jorig;
+        middle = !(o.os < 3) && !(o.oe > J - 2);
+        if (middle) {
+            sc = (o.type == kDel) ? o.os - 1 : o.os;
+            bc = 1 + o.oe;
+            g = middle_geometry(S.a, S.b, sc, bc);
+        }
+    }
+    // wave-wide stage extents (only over middle lanes)
+    const int aLo = wave_min(middle ? sc - 1 : INT_MAX), aHi = wave_max(middle ? sc - 1 : -1);
+    const int bLo = wave_min(middle ? bc : INT_MAX), bHi = wave_max(middle ? bc : -1);
+    const int rLo = wave_min(middle ? g.lb - 1 : INT_MAX), rHi = wave_max(middle ? g.le + 1 : -1);
+    WaveStage& ws = stage[wid];
+    bool staged = false;
+    long long aBase = 0, bBase = 0;
+    int rBase = 0;
+    if (aHi >= 0) {
+        const long long cb = B.rColBase[r];
+        const int2 rah = B.aRange[cb + aHi];
+        const int offLo = B.aOff[cb + aLo], offHi = B.aOff[cb + aHi];
+        const int spanA = offHi + (rah.y - rah.x) - offLo;
+        const int2 rbl = B.bRange[cb + bLo];
+        const int boLo = B.bOff[cb + bLo], boHi = B.bOff[cb + bHi];
+        const int spanB = boLo + (rbl.y - rbl.x) - boHi;
+        const int I = B.rLen[r];
+        const int r0 = max(0, rLo), r1 = min(I, rHi);
+        const int spanR = r1 - r0;
+        staged = spanA <= kStageA && spanB <= kStageB && spanR <= kStageR;
+        if (staged) {
+            const double* ga = B.valPool + B.rValA[r] + offLo;
+            const double* gb = B.valPool + B.rValB[r] + boHi;
+            const char* gr = B.seqPool + B.rSeqOff[r] + r0;
+            for (int q = lane; q < spanA; q += 64) ws.a[q] = ga[q];
+            for (int q = lane; q < spanB; q += 64) ws.b[q] = gb[q];
+            for (int q = lane; q < spanR; q += 64) ws.rd[q] = gr[q];
+            aBase = offLo;
+            bBase = boHi;
+            rBase = r0;
+        }
+    }
+    __syncthreads();   // every wave of the block reaches this point exactly once
+
+    TaskStat st;
+    double d = 0.0;
+    if (scored) {
+        if (middle) {
+            const int2 ar = S.a.range[sc - 1];
+            const int2 br = S.b.range[bc];
+            const int ao = S.a.off[sc - 1], bo = S.b.off[bc];
+            double score;
+            if (staged) {
+                const double* av = ws.a + (ao - aBase) - ar.x;
+                const double* bv = ws.b + (bo - bBase) + (br.y - 1);
+                const char* rdp = ws.rd - rBase;
+                score = score_middle(S, sc, bc, g, av, ar, bv, br, rdp, st);
+            } else {
+                const double* av = S.a.val + ao - ar.x;
+                const double* bv = S.b.val + bo + (br.y - 1);
+                score = score_middle(S, sc, bc, g, av, ar, bv, br, S.rd, st);
+            }
+            d = score - B.rBaseline[r];
+        } else {
+            // rare: mutations within 3 columns of a read's window ends -> k_score_edge
+            const int slot = atomicAdd(W.edgeCount, 1);
+            if (slot < W.edgeCap) {
+                W.edgeList[3 * slot + 0] = k;
+                W.edgeList[3 * slot + 1] = rr;
+                W.edgeList[3 * slot + 2] = m;
+            } else {
+                atomicOr(scratch.overflow, 2);
+            }
+        }
+    }
+    if (valid && !(scored && !middle)) W.delta[W.deltaBase[k] + (long long)rr * M + m] = d;
     if (B.stats) {   // wave-reduce, one atomic per wave
         unsigned long long c = st.cells, b = st.bytes;
-        for (int o = 32; o > 0; o >>= 1) {
-            c += __shfl_xor(c, o, 64);
-            b += __shfl_xor(b, o, 64);
+        for (int q = 32; q > 0; q >>= 1) {
+            c += __shfl_xor(c, q, 64);
+            b += __shfl_xor(b, q, 64);
         }
-        if (lane == 0) {
+        if (lane == 0 && waveLive) {
             atomicAdd(&B.stats[2 * kStatScore], c);
             atomicAdd(&B.stats[2 * kStatScore + 1], b);
         }
+    }
+}
+
+// Edge cases of ScoreMutation (ExtendAlpha to the end, ExtendBeta to the start, whole refill), listed
+// by k_score.  A separate kernel keeps their 4-column register state out of k_score's budget.
+__global__ void __launch_bounds__(64) k_score_edge(DevBatch B, ScoreWork W, ScoreScratch scratch)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= *W.edgeCount || t >= W.edgeCap) return;
+    const int k = W.edgeList[3 * t + 0], rr = W.edgeList[3 * t + 1], m = W.edgeList[3 * t + 2];
+    const int z = W.zmw[k];
+    const int M = W.nMut[k];
+    const int r = B.zReadBegin[z] + rr;
+    const int code = W.codes[W.mutBase[k] + m];
+    ScoreCtx S;
+    const Oriented o = setup_score(B, r, code, S);
+    TaskStat st;
+    const double d = score_edge(S, o, scratch, st) - B.rBaseline[r];
+    W.delta[W.deltaBase[k] + (long long)rr * M + m] = d;
+    if (B.stats) {
+        atomicAdd(&B.stats[2 * kStatScore], st.cells);
+        atomicAdd(&B.stats[2 * kStatScore + 1], st.bytes);
     }
 }
 
@@ -724,10 +1137,16 @@ __global__ void __launch_bounds__(256) k_qv(DevBatch B, ScoreWork W, const long 
 // ------------------------------------------------------------------------------------------------
 // launch wrappers (host side)
 // ------------------------------------------------------------------------------------------------
-void launch_fill(const DevBatch& B, const int* reads, int n, hipStream_t s)
+void launch_fill(const DevBatch& B, const FillScratch& F, const int* reads, int n, hipStream_t s)
 {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_fill, dim3((n + 63) / 64), dim3(64), 0, s, B, reads, n);
+    hipLaunchKernelGGL(k_fill, dim3((n + 63) / 64), dim3(64), 0, s, B, F, reads, n);
+}
+
+void launch_compact(const DevBatch& B, const FillScratch& F, const int* reads, int n, hipStream_t s)
+{
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_compact, dim3((n + 63) / 64), dim3(256), 0, s, B, F, reads, n);
 }
 
 void launch_suffix(const DevBatch& B, const int* reads, int n, hipStream_t s)
@@ -746,8 +1165,10 @@ void launch_enumerate(const DevBatch& B, const int* zmws, int n, const long long
 void launch_score(const DevBatch& B, const ScoreWork& W, long long nWaves, const ScoreScratch& scratch, hipStream_t s)
 {
     if (nWaves <= 0) return;
-    const long long blocks = (nWaves + 3) / 4;
-    hipLaunchKernelGGL(k_score, dim3((unsigned)blocks), dim3(256), 0, s, B, W, scratch);
+    const long long blocks = (nWaves + kScoreWaves - 1) / kScoreWaves;
+    hipLaunchKernelGGL(k_score, dim3((unsigned)blocks), dim3(64 * kScoreWaves), 0, s, B, W, scratch);
+    if (W.edgeCap > 0)
+        hipLaunchKernelGGL(k_score_edge, dim3((W.edgeCap + 63) / 64), dim3(64), 0, s, B, W, scratch);
 }
 
 void launch_reduce(const DevBatch& B, const ScoreWork& W, long long nMut, double fastThr, double* score,

@@ -19,6 +19,10 @@ struct ScoreWork {
     const long long* posStart = nullptr;   // [nWork + 1] cumulative template positions (QV rounds)
     const int* codes = nullptr;
     double* delta = nullptr;
+    // tasks near a read's window ends, appended by k_score for k_score_edge
+    int* edgeList = nullptr;   // [edgeCap][3] = (work item, read, mutation)
+    int* edgeCount = nullptr;
+    int edgeCap = 0;
 };
 
 // Bump-allocated scratch for the rare whole-window refill case (tiny windows).
@@ -29,7 +33,21 @@ struct ScoreScratch {
     int* overflow = nullptr;
 };
 
-void launch_fill(const DevBatch& B, const int* reads, int n, hipStream_t s);
+// Lane-interleaved fill scratch: group g (64 reads) x matrix (alpha, beta) x slot/column x lane.
+struct FillScratch {
+    double* val = nullptr;    // [2G][capSlots][64]
+    int2* range = nullptr;    // [2G][capCols][64]
+    int* off = nullptr;
+    double* ls = nullptr;
+    double* pre = nullptr;    // [G][capCols + 1][64] alpha log-scale prefix
+    int* usedA = nullptr;     // per read: values used by the final alpha / beta
+    int* usedB = nullptr;
+    long long capSlots = 0;
+    int capCols = 0;
+};
+
+void launch_fill(const DevBatch& B, const FillScratch& F, const int* reads, int n, hipStream_t s);
+void launch_compact(const DevBatch& B, const FillScratch& F, const int* reads, int n, hipStream_t s);
 void launch_suffix(const DevBatch& B, const int* reads, int n, hipStream_t s);
 void launch_enumerate(const DevBatch& B, const int* zmws, int n, const long long* mutBase, const long long* posBase,
                       int* codes, int* posOff, hipStream_t s);

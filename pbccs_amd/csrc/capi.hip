@@ -22,6 +22,7 @@ struct pbccs_engine {
     Counters counters;
     bool profiling = false;
     KernelStat stats[kKernelKinds];
+    Workspace ws;   // resident pools shared by the engine's batches (they polish one at a time)
 };
 
 struct pbccs_batch {
@@ -384,7 +385,7 @@ int pbccs_batch_create(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
         pbccs_polish_options_default(&b->o);
         if (opts) b->o = *opts;
         b->n = n;
-        b->B.reset(new ArrowBatch(eng->device));
+        b->B.reset(new ArrowBatch(eng->device, &eng->ws));
         b->B->SetProfiling(eng->profiling);
         ArrowOptions ao;
         ao.scoreDiff = b->o.score_diff;

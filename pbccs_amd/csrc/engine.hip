@@ -4,6 +4,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -18,39 +19,14 @@ namespace pbccs {
         if (e_ != hipSuccess) throw DeviceError(hipGetErrorString(e_));      \
     } while (0)
 
-template <class T>
-void DevVec<T>::reserve(size_t n, bool keep)
-{
-    if (n <= cap) return;
-    const size_t nc = std::max(n, cap + cap / 2 + 256);
-    T* p = nullptr;
-    PBCCS_HIP(hipMalloc(&p, nc * sizeof(T)));
-    if (keep && ptr && cap) {
-        PBCCS_HIP(hipDeviceSynchronize());
-        PBCCS_HIP(hipMemcpy(p, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice));
-    }
-    if (ptr) {
-        PBCCS_HIP(hipDeviceSynchronize());
-        (void)hipFree(ptr);
-    }
-    ptr = p;
-    cap = nc;
-}
-
-template <class T>
-void DevVec<T>::release()
-{
-    if (ptr) (void)hipFree(ptr);
-    ptr = nullptr;
-    cap = 0;
-}
-
 const char* const kKernelNames[kKernelKinds] = {"k_fill", "k_suffix", "k_enumerate", "k_score",
-                                                 "k_reduce", "k_qv", "select"};
+                                                 "k_reduce", "k_qv", "select", "k_compact"};
 
 namespace {
 
-constexpr int kInitialBandHeight = 32;         // value capacity per column on first allocation
+constexpr int kInitialBandHeight = 20;         // compact band values per column, first estimate
+constexpr int kFillBandHeight = 28;            // fill scratch values per column (doubled on overflow)
+constexpr double kFillScratchBudget = 24.0 * (1ull << 30);
 constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
 
 template <class T>
@@ -69,7 +45,15 @@ void download(std::vector<T>& h, const DevVec<T>& d, size_t n, hipStream_t s)
 
 }  // namespace
 
-ArrowBatch::ArrowBatch(int device) : device_(device)
+ArrowBatch::ArrowBatch(int device, Workspace* shared)
+    : device_(device),
+      ownWs_(shared ? nullptr : new Workspace()),
+      ws_(shared ? shared : ownWs_.get()),
+      dARange_(ws_->aRange), dBRange_(ws_->bRange), dAOff_(ws_->aOff), dBOff_(ws_->bOff), dALs_(ws_->aLs),
+      dBLs_(ws_->bLs), dAPre_(ws_->aPre), dBSuf_(ws_->bSuf), dVal_(ws_->val), dCodes_(ws_->codes),
+      dPosOff_(ws_->posOff), dQv_(ws_->qv), dList_(ws_->list), dEdge_(ws_->edge), dEdgeCount_(ws_->edgeCount),
+      dDelta_(ws_->delta), dScore_(ws_->score), dFav_(ws_->fav), dScratch_(ws_->scratch),
+      dScratchTop_(ws_->scratchTop), dScratchOverflow_(ws_->scratchOverflow)
 {
     PBCCS_HIP(hipSetDevice(device_));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -164,6 +148,17 @@ void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
 
 void ArrowBatch::Prepare()
 {
+    // the workspace may hold another (finished) batch's bands: size it without preserving them
+    const size_t cols = std::max<long long>(colTop_, 1);
+    dARange_.reserve(cols, false);
+    dBRange_.reserve(cols, false);
+    dAOff_.reserve(cols, false);
+    dBOff_.reserve(cols, false);
+    dALs_.reserve(cols, false);
+    dBLs_.reserve(cols, false);
+    dAPre_.reserve(cols, false);
+    dBSuf_.reserve(cols, false);
+    dVal_.reserve(std::max<long long>(valTop_, 1), false);
     UploadDescriptors();
     long long mut = 0, delta = 0, pos = 0;
     for (const HZmw& z : zmws_) {
@@ -395,40 +390,86 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
 {
     std::vector<int> todo(readsIn);
     for (int r : todo) EnsureCapacity(r);
+    int H = kFillBandHeight;
     for (int attempt = 0; !todo.empty(); ++attempt) {
-        if (attempt > 12) throw DeviceError("band storage keeps overflowing");
+        if (attempt > 8) throw DeviceError("band storage keeps overflowing");
+        // a 64-read fill group should hold windows of similar length (lanes run in lock-step)
+        std::stable_sort(todo.begin(), todo.end(), [&](int x, int y) {
+            return reads_[x].te - reads_[x].ts > reads_[y].te - reads_[y].ts;
+        });
         UploadDescriptors();
-        upload(dList_, todo, stream_);
-        const DevBatch B = View();
-        Timed(kKFill, [&] { launch_fill(B, dList_.ptr, (int)todo.size(), stream_); });
-        Timed(kKSuffix, [&] { launch_suffix(B, dList_.ptr, (int)todo.size(), stream_); });
-        PBCCS_HIP(hipGetLastError());
-        counters_.fillLaunches += 1;
         const size_t R = reads_.size();
-        std::vector<int> st, fl;
-        std::vector<double> bl;
-        download(st, dRStatus_, R, stream_);
-        download(fl, dRFlips_, R, stream_);
-        download(bl, dRBaseline_, R, stream_);
-        PBCCS_HIP(hipStreamSynchronize(stream_));
+        dUsedA_.reserve(std::max<size_t>(R, 1), true);
+        dUsedB_.reserve(std::max<size_t>(R, 1), true);
         std::vector<int> again;
-        for (int r : todo) {
-            HRead& h = reads_[r];
-            if (st[r] == kFillOverflow) {
-                h.valCap *= 2;   // move to fresh, larger regions and refill
-                h.valA = valTop_;
-                h.valB = valTop_ + h.valCap;
-                valTop_ += 2 * h.valCap;
-                descDirty_ = true;
-                again.push_back(r);
-                continue;
+        size_t pos = 0;
+        while (pos < todo.size()) {
+            const int capCols = reads_[todo[pos]].te - reads_[todo[pos]].ts + 2;
+            const long long capSlots = (long long)capCols * H + 64;
+            const double perGroup = 2.0 * capSlots * 64 * 8 + 2.0 * capCols * 64 * 20 + (capCols + 1.0) * 64 * 8;
+            const long long maxGroups = std::max<long long>(1, (long long)(kFillScratchBudget / perGroup));
+            const size_t n = std::min<size_t>(todo.size() - pos, (size_t)maxGroups * 64);
+            std::vector<int> chunk(todo.begin() + pos, todo.begin() + pos + n);
+            const long long groups = (long long)(n + 63) / 64;
+            ws_->fVal.reserve((size_t)(2 * groups * capSlots * 64), false);
+            ws_->fRange.reserve((size_t)(2 * groups * capCols * 64), false);
+            ws_->fOff.reserve((size_t)(2 * groups * capCols * 64), false);
+            ws_->fLs.reserve((size_t)(2 * groups * capCols * 64), false);
+            ws_->fPre.reserve((size_t)(groups * (capCols + 1) * 64), false);
+            FillScratch F;
+            F.val = ws_->fVal.ptr;
+            F.range = ws_->fRange.ptr;
+            F.off = ws_->fOff.ptr;
+            F.ls = ws_->fLs.ptr;
+            F.pre = ws_->fPre.ptr;
+            F.usedA = dUsedA_.ptr;
+            F.usedB = dUsedB_.ptr;
+            F.capSlots = capSlots;
+            F.capCols = capCols;
+            upload(dList_, chunk, stream_);
+            const DevBatch B = View();
+            Timed(kKFill, [&] { launch_fill(B, F, dList_.ptr, (int)n, stream_); });
+            PBCCS_HIP(hipGetLastError());
+            counters_.fillLaunches += 1;
+            std::vector<int> st, fl, ua, ub;
+            std::vector<double> bl;
+            download(st, dRStatus_, R, stream_);
+            download(fl, dRFlips_, R, stream_);
+            download(bl, dRBaseline_, R, stream_);
+            download(ua, dUsedA_, R, stream_);
+            download(ub, dUsedB_, R, stream_);
+            PBCCS_HIP(hipStreamSynchronize(stream_));
+            for (int r : chunk) {
+                HRead& h = reads_[r];
+                if (st[r] == kFillOverflow) {
+                    again.push_back(r);
+                    continue;
+                }
+                h.status = st[r];
+                h.flips = fl[r];
+                h.baseline = bl[r];
+                h.filled = true;
+                if (st[r] == kFillOk || st[r] == kFillMismatch) {
+                    const long long need = std::max(ua[r], ub[r]);
+                    if (need > h.valCap) {   // move to a larger compact region
+                        h.valCap = need + need / 4 + 64;
+                        h.valA = valTop_;
+                        h.valB = valTop_ + h.valCap;
+                        valTop_ += 2 * h.valCap;
+                        descDirty_ = true;
+                    }
+                }
             }
-            h.status = st[r];
-            h.flips = fl[r];
-            h.baseline = bl[r];
-            h.filled = true;
+            UploadDescriptors();
+            const DevBatch B2 = View();
+            Timed(kKCompact, [&] { launch_compact(B2, F, dList_.ptr, (int)n, stream_); });
+            Timed(kKSuffix, [&] { launch_suffix(B2, dList_.ptr, (int)n, stream_); });
+            PBCCS_HIP(hipGetLastError());
+            PBCCS_HIP(hipStreamSynchronize(stream_));   // the next chunk reuses the scratch and the list
+            pos += n;
         }
         todo.swap(again);
+        H *= 2;
     }
 }
 
@@ -568,7 +609,17 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
     W.posStart = dWPosStart_.ptr;
     W.codes = dCodes_.ptr;
     W.delta = dDelta_.ptr;
+    // k_score_edge list: tasks within 3 columns of a window end; bound = 80 per (work item, read)
+    long long edgeCap = 0;
+    for (int k = 0; k < n; ++k) edgeCap += 80LL * zmws_[zl[k]].nReads;
+    edgeCap = std::min<long long>(std::max<long long>(edgeCap, 64), rTotalDelta_ + 64);
+    dEdge_.reserve(3 * edgeCap, false);
+    dEdgeCount_.reserve(1, false);
+    W.edgeList = dEdge_.ptr;
+    W.edgeCount = dEdgeCount_.ptr;
+    W.edgeCap = (int)edgeCap;
     for (int attempt = 0;; ++attempt) {
+        PBCCS_HIP(hipMemsetAsync(dEdgeCount_.ptr, 0, sizeof(int), stream_));
         PBCCS_HIP(hipMemsetAsync(dScratchTop_.ptr, 0, sizeof(unsigned long long), stream_));
         PBCCS_HIP(hipMemsetAsync(dScratchOverflow_.ptr, 0, sizeof(int), stream_));
         ScoreScratch sc;
@@ -583,7 +634,13 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
         PBCCS_HIP(hipStreamSynchronize(stream_));
         if (!ovf) break;
         if (attempt > 8) throw DeviceError("scratch overflow");
-        dScratch_.reserve(dScratch_.cap * 4, false);
+        if (ovf & 1) dScratch_.reserve(dScratch_.cap * 4, false);
+        if (ovf & 2) {
+            edgeCap *= 4;
+            dEdge_.reserve(3 * edgeCap, false);
+            W.edgeList = dEdge_.ptr;
+            W.edgeCap = (int)std::min<long long>(edgeCap, INT_MAX / 4);
+        }
     }
     Timed(kKReduce, [&] { launch_reduce(B, W, rTotalMut_, fastThr, dScore_.ptr, dFav_.ptr, stream_); });
     PBCCS_HIP(hipGetLastError());

@@ -8,8 +8,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <limits>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -46,8 +48,33 @@ template <class T>
 struct DevVec {
     T* ptr = nullptr;
     size_t cap = 0;
-    void reserve(size_t n, bool keep);
-    void release();
+    void reserve(size_t n, bool keep)
+    {
+        if (n <= cap) return;
+        const size_t nc = std::max(n, cap + cap / 2 + 256);
+        T* p = nullptr;
+        if (hipMalloc(&p, nc * sizeof(T)) != hipSuccess) throw DeviceError("hipMalloc failed (device memory)");
+        if (keep && ptr && cap) {
+            if (hipDeviceSynchronize() != hipSuccess ||
+                hipMemcpy(p, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice) != hipSuccess)
+                throw DeviceError("device copy failed");
+        }
+        if (ptr) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(ptr);
+        }
+        ptr = p;
+        cap = nc;
+    }
+    void release()
+    {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+    DevVec() = default;
+    DevVec(const DevVec&) = delete;
+    DevVec& operator=(const DevVec&) = delete;
     ~DevVec() { release(); }
 };
 
@@ -57,7 +84,7 @@ struct Counters {   // work counters for the roofline report (bench.py)
     long long mutations = 0;
 };
 
-enum KernelKind { kKFill = 0, kKSuffix, kKEnumerate, kKScore, kKReduce, kKQv, kKSelect, kKernelKinds };
+enum KernelKind { kKFill = 0, kKSuffix, kKEnumerate, kKScore, kKReduce, kKQv, kKSelect, kKCompact, kKernelKinds };
 extern const char* const kKernelNames[kKernelKinds];
 
 struct KernelStat {
@@ -67,9 +94,30 @@ struct KernelStat {
     double bytes = 0.0;   // algorithmic band bytes
 };
 
+// Large device pools.  A batch either owns one (fine-grained scorers) or borrows its engine's (batch
+// polish): batches polish one after another, so they stream through one resident workspace.
+struct Workspace {
+    // per-read compact bands (what scoring reads)
+    DevVec<int2> aRange, bRange;
+    DevVec<int> aOff, bOff;
+    DevVec<double> aLs, bLs, aPre, bSuf;
+    DevVec<double> val;
+    // lane-interleaved fill scratch
+    DevVec<double> fVal, fLs, fPre;
+    DevVec<int2> fRange;
+    DevVec<int> fOff;
+    // scoring rounds
+    DevVec<int> codes, posOff, qv, list, edge, edgeCount;
+    DevVec<double> delta, score;
+    DevVec<unsigned char> fav;
+    DevVec<double> scratch;
+    DevVec<unsigned long long> scratchTop;
+    DevVec<int> scratchOverflow;
+};
+
 class ArrowBatch {
 public:
-    explicit ArrowBatch(int device);
+    explicit ArrowBatch(int device, Workspace* shared = nullptr);
     ~ArrowBatch();
     ArrowBatch(const ArrowBatch&) = delete;
     ArrowBatch& operator=(const ArrowBatch&) = delete;
@@ -160,6 +208,8 @@ private:
 
     int device_ = 0;
     hipStream_t stream_ = nullptr;
+    std::unique_ptr<Workspace> ownWs_;
+    Workspace* ws_;
     std::vector<HZmw> zmws_;
     std::vector<HRead> reads_;
     long long tplTop_ = 0, seqTop_ = 0, colTop_ = 0, valTop_ = 0;
@@ -168,27 +218,38 @@ private:
 
     // host mirrors of pools
     std::vector<char> hTpl_, hSeq_;
-    // device state
+    // device state owned by the batch (inputs + descriptors)
     DevVec<int> dZFwd_, dZRev_, dZLen_, dZReadBegin_, dZNReads_;
     DevVec<double> dZCtx_;
     DevVec<char> dTpl_, dSeq_;
     DevVec<long long> dRSeqOff_, dRColBase_, dRValA_, dRValB_, dRValCap_;
     DevVec<int> dRLen_, dRStrand_, dRTs_, dRTe_, dRActive_, dRZmw_;
-    DevVec<int2> dARange_, dBRange_;
-    DevVec<int> dAOff_, dBOff_;
-    DevVec<double> dALs_, dBLs_, dAPre_, dBSuf_;
-    DevVec<double> dVal_;
     DevVec<double> dRBaseline_;
-    DevVec<int> dRFlips_, dRStatus_;
-    // scoring round scratch
+    DevVec<int> dRFlips_, dRStatus_, dUsedA_, dUsedB_;
     DevVec<int> dWZmw_, dWNMut_;
     DevVec<long long> dWMutBase_, dWDeltaBase_, dWWaveStart_, dWMutStart_, dWPosStart_, dWPosBase_, dWQvBase_;
-    DevVec<int> dCodes_, dPosOff_, dQv_, dList_;
-    DevVec<double> dDelta_, dScore_;
-    DevVec<unsigned char> dFav_;
-    DevVec<double> dScratch_;
-    DevVec<unsigned long long> dScratchTop_;
-    DevVec<int> dScratchOverflow_;
+    // workspace pools (aliases into *ws_)
+    DevVec<int2>& dARange_;
+    DevVec<int2>& dBRange_;
+    DevVec<int>& dAOff_;
+    DevVec<int>& dBOff_;
+    DevVec<double>& dALs_;
+    DevVec<double>& dBLs_;
+    DevVec<double>& dAPre_;
+    DevVec<double>& dBSuf_;
+    DevVec<double>& dVal_;
+    DevVec<int>& dCodes_;
+    DevVec<int>& dPosOff_;
+    DevVec<int>& dQv_;
+    DevVec<int>& dList_;
+    DevVec<int>& dEdge_;
+    DevVec<int>& dEdgeCount_;
+    DevVec<double>& dDelta_;
+    DevVec<double>& dScore_;
+    DevVec<unsigned char>& dFav_;
+    DevVec<double>& dScratch_;
+    DevVec<unsigned long long>& dScratchTop_;
+    DevVec<int>& dScratchOverflow_;
     // last round bookkeeping (host)
     std::vector<long long> rMutStart_, rPosStart_, rDeltaBase_;
     std::vector<int> rNMut_;
