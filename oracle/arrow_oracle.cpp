@@ -1340,3 +1340,23 @@ void orc_context_params(const double* snr, double* out /* 8 x 4: match, stick, b
 }
 
 }  // extern "C"
+
+// Diagnostics (test infrastructure): used-cell count and tallest column of read r's alpha and beta bands.
+extern "C" int orc_scorer_band_stats(void* h, int r, long long* aUsed, long long* bUsed, int* aMaxH, int* bMaxH)
+{
+    MultiReadScorer* s = static_cast<MultiReadScorer*>(h);
+    const ReadState& rs = s->reads.at(r);
+    if (!rs.scorer) return -1;
+    auto stats = [](const BandMatrix& m, long long* used, int* mh) {
+        *used = 0;
+        *mh = 0;
+        for (int j = 0; j < m.cols; ++j) {
+            const int hgt = std::max(0, m.ue[j] - m.ub[j]);
+            *used += hgt;
+            *mh = std::max(*mh, hgt);
+        }
+    };
+    stats(rs.scorer->alpha, aUsed, aMaxH);
+    stats(rs.scorer->beta, bUsed, bMaxH);
+    return 0;
+}

@@ -37,6 +37,8 @@ def lib():
         L.orc_scorer_add_read.argtypes = [c_p, c_s, c_i, c_i, c_i, c_d]
         L.orc_scorer_num_reads.argtypes = [c_p]
         L.orc_scorer_read_info.argtypes = [c_p, c_i, I, I, I, D, I]
+        L.orc_scorer_band_stats.argtypes = [c_p, c_i, ctypes.POINTER(ctypes.c_longlong),
+                                            ctypes.POINTER(ctypes.c_longlong), I, I]
         L.orc_scorer_score.restype = c_d
         L.orc_scorer_score.argtypes = [c_p, c_i, c_i, c_i, c_s, c_d]
         L.orc_scorer_scores.argtypes = [c_p, c_i, c_i, c_i, c_s, c_d, D]
@@ -94,6 +96,12 @@ class Scorer:
         lib().orc_scorer_read_info(self._h, r, ctypes.byref(a), ctypes.byref(ts), ctypes.byref(te),
                                    ctypes.byref(ll), ctypes.byref(fl))
         return {"active": bool(a.value), "ts": ts.value, "te": te.value, "ll": ll.value, "flipflops": fl.value}
+
+    def band_stats(self, r):
+        """Diagnostics: (alpha used cells, beta used cells, tallest alpha column, tallest beta column)."""
+        au, bu, ah, bh = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_int(), ctypes.c_int()
+        lib().orc_scorer_band_stats(self._h, r, ctypes.byref(au), ctypes.byref(bu), ctypes.byref(ah), ctypes.byref(bh))
+        return au.value, bu.value, ah.value, bh.value
 
     def score(self, mtype, start, base="-", fast_threshold=-1.7976931348623157e308):
         nb = b"" if mtype == DELETION else base.encode()

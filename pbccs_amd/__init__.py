@@ -73,11 +73,12 @@ class Engine:
         h = ctypes.c_void_p()
         _lib_mod.check(L.pbccs_engine_create(device, ctypes.byref(h)))
         self._h = h
+        self._lib = L   # kept for interpreter shutdown, when module globals are already cleared
         self.device = device
 
     def __del__(self):
         if getattr(self, "_h", None):
-            load().pbccs_engine_destroy(self._h)
+            self._lib.pbccs_engine_destroy(self._h)
             self._h = None
 
     def set_profiling(self, on=True):

@@ -31,7 +31,8 @@ constexpr double kRebandFrac = 0.04;      // SimpleRecursor.cpp:54
 enum MutType : int { kIns = 0, kDel = 1, kSub = 2 };   // Mutation.hpp:50-53
 enum Strand : int { kFwd = 0, kRev = 1 };
 
-enum FillStatus : int { kFillOk = 0, kFillMismatch = 1, kFillOverflow = 2, kFillBadInput = 3 };
+// kFillTall: a column did not fit the cooperative fill's LDS buffer (re-run on a wider path)
+enum FillStatus : int { kFillOk = 0, kFillMismatch = 1, kFillOverflow = 2, kFillBadInput = 3, kFillTall = 4 };
 
 // Mutation code: pos << 4 | type << 2 | base(0..3).  Single-base mutations only (what ccs enumerates).
 __host__ __device__ inline int mut_code(int pos, int type, int base) { return (pos << 4) | (type << 2) | base; }
@@ -160,6 +161,25 @@ struct TplView {
         return c;
     }
 };
+
+// The mapped window [ts, te) of read r on its strand's template (no virtual mutation).
+__device__ __forceinline__ TplView window_view(const DevBatch& B, int r)
+{
+    const int z = B.rZmw[r];
+    const int L = B.zLen[z];
+    const int ts = B.rTs[r], te = B.rTe[r];
+    TplView v;
+    if (B.rStrand[r] == kFwd) {
+        v.T = B.tplPool + B.zFwdOff[z];
+        v.start = ts;
+    } else {
+        v.T = B.tplPool + B.zRevOff[z];
+        v.start = L - te;
+    }
+    v.L = L;
+    v.len = te - ts;
+    return v;
+}
 
 // TemplateParameterPair::ApplyVirtualMutation (TemplateParameterPair.cpp:70-140) on strand template T.
 __device__ inline VirtualMut make_virtual(const char* T, int L, int type, int s, char nb)

@@ -55,23 +55,6 @@ __device__ __forceinline__ Band band_beta(const DevBatch& B, int r)
     return m;
 }
 
-__device__ __forceinline__ TplView window_view(const DevBatch& B, int r)
-{
-    const int z = B.rZmw[r];
-    const int L = B.zLen[z];
-    const int ts = B.rTs[r], te = B.rTe[r];
-    TplView v;
-    if (B.rStrand[r] == kFwd) {
-        v.T = B.tplPool + B.zFwdOff[z];
-        v.start = ts;
-    } else {
-        v.T = B.tplPool + B.zRevOff[z];
-        v.start = L - te;
-    }
-    v.L = L;
-    v.len = te - ts;
-    return v;
-}
 
 // ------------------------------------------------------------------------------------------------
 // k_fill: FillAlphaBeta per read (MutationScorer ctor / Template(), MutationScorer.cpp:53-131), one
@@ -95,6 +78,7 @@ __global__ void __launch_bounds__(64) k_fill(DevBatch B, FillScratch F, const in
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const int g = t >> 6, l = t & 63;
+    const long long tStart = F.trace ? (long long)wall_clock64() : 0;
     const int r = reads[t];
     const int z = B.rZmw[r];
     const int I = B.rLen[r];
@@ -162,6 +146,17 @@ __global__ void __launch_bounds__(64) k_fill(DevBatch B, FillScratch F, const in
     F.usedA[r] = (int)ua;
     F.usedB[r] = (int)ub;
     B.rStatus[r] = (mism > kAlphaBetaTol) ? kFillMismatch : kFillOk;
+    if (F.trace) {
+        long long* tr = F.trace + 8LL * t;
+        tr[0] = tStart;
+        tr[1] = (long long)wall_clock64();
+        tr[2] = (long long)cells;
+        tr[3] = (long long)passes;
+        tr[4] = J;
+        tr[5] = I;
+        tr[6] = ua;
+        tr[7] = ub;
+    }
     if (B.stats) {   // algorithmic: 8 B per stored cell + 16 B per column per fill pass
         atomicAdd(&B.stats[2 * kStatFill], cells);
         atomicAdd(&B.stats[2 * kStatFill + 1], 8ull * cells + 16ull * passes * (unsigned long long)(J + 1));
@@ -279,13 +274,14 @@ __global__ void __launch_bounds__(256) k_compact(DevBatch B, FillScratch F, cons
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_suffix: bSuf[k] = accumulate(bLs[k..J], 0.0) for k in [0, J+1] (bSuf[J+1] = 0).  Each lane sums
+// k_suffix: bSuf[k] = accumulate(bLs[k..J], 0.0) for k in [0, J+1] (bSuf[J+1] = 0), and with
+// withPrefix the alpha prefixes aPre (the cooperative fill leaves them to this kernel).  Each lane sums
 // its own suffix left to right, reading the shared log-scale column from LDS (broadcast-friendly:
 // lanes k, k+1, ... read consecutive words at every step).
 // ------------------------------------------------------------------------------------------------
 constexpr int kSuffixTile = 2048;
 
-__global__ void __launch_bounds__(256) k_suffix(DevBatch B, const int* __restrict__ reads, int n)
+__global__ void __launch_bounds__(256) k_suffix(DevBatch B, const int* __restrict__ reads, int n, int withPrefix)
 {
     __shared__ double tile[kSuffixTile];
     const int r = reads[blockIdx.x];
@@ -309,6 +305,24 @@ __global__ void __launch_bounds__(256) k_suffix(DevBatch B, const int* __restric
                 for (int q = lo; q < hi; ++q) s = s + tile[q];
         }
         if (k <= ncol) suf[k] = s;
+    }
+    if (!withPrefix) return;
+    // aPre[k] = accumulate(aLs[0..k), 0.0) for k in [0, J+1] (GetLogProdScales(0, k))
+    const double* als = B.aLs + cb;
+    double* pre = B.aPre + cb;
+    for (int k0 = 0; k0 <= ncol; k0 += blockDim.x) {
+        const int k = k0 + threadIdx.x;
+        double s = 0.0;
+        const int cend = min(ncol, k0 + (int)blockDim.x);
+        for (int c0 = 0; c0 < cend; c0 += kSuffixTile) {
+            __syncthreads();
+            for (int q = threadIdx.x; q < kSuffixTile && c0 + q < ncol; q += blockDim.x) tile[q] = als[c0 + q];
+            __syncthreads();
+            const int hi = min(min(k, ncol) - c0, kSuffixTile);
+            if (k <= ncol)
+                for (int q = 0; q < hi; ++q) s = s + tile[q];
+        }
+        if (k <= ncol) pre[k] = s;
     }
 }
 
@@ -1149,10 +1163,10 @@ void launch_compact(const DevBatch& B, const FillScratch& F, const int* reads, i
     hipLaunchKernelGGL(k_compact, dim3((n + 63) / 64), dim3(256), 0, s, B, F, reads, n);
 }
 
-void launch_suffix(const DevBatch& B, const int* reads, int n, hipStream_t s)
+void launch_suffix(const DevBatch& B, const int* reads, int n, hipStream_t s, bool withPrefix)
 {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_suffix, dim3(n), dim3(256), 0, s, B, reads, n);
+    hipLaunchKernelGGL(k_suffix, dim3(n), dim3(256), 0, s, B, reads, n, withPrefix ? 1 : 0);
 }
 
 void launch_enumerate(const DevBatch& B, const int* zmws, int n, const long long* mutBase, const long long* posBase,

@@ -44,11 +44,24 @@ struct FillScratch {
     int* usedB = nullptr;
     long long capSlots = 0;
     int capCols = 0;
+    long long* trace = nullptr;   // optional [n][8] per-lane timing (PBCCS_FILL_TRACE diagnostics)
 };
+
+// Cooperative fill (fill_coop.hip): bands written straight into each read's compact region.
+struct CoopFill {
+    int* usedA = nullptr;    // per read: values used by the final alpha / beta (or needed, on overflow)
+    int* usedB = nullptr;
+    int hcap = 0;            // LDS rows per column buffer
+    int readWords = 0;       // nibble-packed read words per group (>= ceil(I / 8) of every read)
+    int tplWords = 0;        // nibble-packed template words per group (>= ceil((J + 1) / 8))
+    size_t groupBytes = 0;   // coop_group_bytes(hcap, readWords, tplWords)
+};
+size_t coop_group_bytes(int hcap, int readWords, int tplWords);
+void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* reads, int n, hipStream_t s);
 
 void launch_fill(const DevBatch& B, const FillScratch& F, const int* reads, int n, hipStream_t s);
 void launch_compact(const DevBatch& B, const FillScratch& F, const int* reads, int n, hipStream_t s);
-void launch_suffix(const DevBatch& B, const int* reads, int n, hipStream_t s);
+void launch_suffix(const DevBatch& B, const int* reads, int n, hipStream_t s, bool withPrefix = false);
 void launch_enumerate(const DevBatch& B, const int* zmws, int n, const long long* mutBase, const long long* posBase,
                       int* codes, int* posOff, hipStream_t s);
 void launch_score(const DevBatch& B, const ScoreWork& W, long long nWaves, const ScoreScratch& scratch, hipStream_t s);

@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <stdexcept>
@@ -27,6 +29,8 @@ namespace {
 constexpr int kInitialBandHeight = 20;         // compact band values per column, first estimate
 constexpr int kFillBandHeight = 28;            // fill scratch values per column (doubled on overflow)
 constexpr double kFillScratchBudget = 24.0 * (1ull << 30);
+constexpr int kCoopNarrowRows = 64;           // LDS column rows of the 16-lane fill path
+constexpr size_t kCoopLdsBytes = 64 * 1024;    // LDS budget of one 64-lane fill group
 constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
 
 template <class T>
@@ -386,7 +390,128 @@ DevBatch ArrowBatch::View() const
 // ------------------------------------------------------------------------------------------------
 // fills
 // ------------------------------------------------------------------------------------------------
+// Cooperative fills (fill_coop.hip): reads start on the 16-lane path; a read whose band outgrows the
+// LDS column buffer moves to the 64-lane path, then to the lane-serial fallback (the path is
+// remembered for its refills).  Value-capacity overflow moves the read to a region of the exact size
+// the kernel reported.  Bands land directly in the compact layout; k_suffix adds the log-scale sums.
 void ArrowBatch::FillReads(const std::vector<int>& readsIn)
+{
+    for (int r : readsIn) EnsureCapacity(r);
+    std::vector<int> todo[2], serial, done;
+    for (int r : readsIn) {
+        const int p = reads_[r].fillPath;
+        if (p >= 2) serial.push_back(r);
+        else todo[p].push_back(r);
+    }
+    for (int attempt = 0; !todo[0].empty() || !todo[1].empty(); ++attempt) {
+        if (attempt > 8) throw DeviceError("band storage keeps overflowing");
+        for (auto& v : todo)   // similar lengths share a launch (LDS is sized by the longest)
+            std::stable_sort(v.begin(), v.end(), [&](int x, int y) {
+                return reads_[x].te - reads_[x].ts > reads_[y].te - reads_[y].ts;
+            });
+        // LDS fit: four 16-lane groups per block, or one 64-lane group with at least one chunk of rows
+        auto words = [&](int r) {
+            return (int)(reads_[r].seq.size() + 7) / 8 + (reads_[r].te - reads_[r].ts + 8) / 8;
+        };
+        for (int p = 0; p < 2; ++p) {
+            std::vector<int> keep;
+            for (int r : todo[p]) {
+                const size_t need = p == 0 ? 4 * coop_group_bytes(kCoopNarrowRows, words(r), 0)
+                                           : coop_group_bytes(64, words(r), 0);
+                if (need <= kCoopLdsBytes) keep.push_back(r);
+                else if (p == 0) todo[1].push_back(r);
+                else {
+                    reads_[r].fillPath = 2;
+                    serial.push_back(r);
+                }
+            }
+            todo[p].swap(keep);
+        }
+        UploadDescriptors();
+        const size_t R = reads_.size();
+        dUsedA_.reserve(std::max<size_t>(R, 1), true);
+        dUsedB_.reserve(std::max<size_t>(R, 1), true);
+        std::vector<int> list(todo[0]);
+        list.insert(list.end(), todo[1].begin(), todo[1].end());
+        upload(dList_, list, stream_);
+        const DevBatch B = View();
+        size_t off = 0;
+        for (int p = 0; p < 2; ++p) {
+            const int n = (int)todo[p].size();
+            if (n == 0) continue;
+            int maxI = 1, maxJ = 1;
+            for (int r : todo[p]) {
+                maxI = std::max(maxI, (int)reads_[r].seq.size());
+                maxJ = std::max(maxJ, reads_[r].te - reads_[r].ts);
+            }
+            CoopFill F;
+            F.usedA = dUsedA_.ptr;
+            F.usedB = dUsedB_.ptr;
+            F.readWords = (maxI + 7) / 8;
+            F.tplWords = (maxJ + 8) / 8;
+            if (p == 0) {
+                F.hcap = kCoopNarrowRows;
+            } else {   // as tall as 64 KB of LDS allows (columns never exceed I + 1 rows)
+                const size_t rest = coop_group_bytes(0, F.readWords, F.tplWords);
+                const long long room = ((long long)kCoopLdsBytes - (long long)rest) / 16;
+                F.hcap = (int)std::min<long long>(std::max<long long>(64, room / 64 * 64), (maxI + 64) / 64 * 64);
+            }
+            F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);
+            const int* lp = dList_.ptr + off;
+            Timed(kKFill, [&] { launch_fill_coop(p == 0 ? 16 : 64, B, F, lp, n, stream_); });
+            PBCCS_HIP(hipGetLastError());
+            counters_.fillLaunches += 1;
+            off += n;
+        }
+        std::vector<int> st, fl, ua, ub;
+        std::vector<double> bl;
+        download(st, dRStatus_, R, stream_);
+        download(fl, dRFlips_, R, stream_);
+        download(bl, dRBaseline_, R, stream_);
+        download(ua, dUsedA_, R, stream_);
+        download(ub, dUsedB_, R, stream_);
+        PBCCS_HIP(hipStreamSynchronize(stream_));
+        std::vector<int> next[2];
+        for (int p = 0; p < 2; ++p) {
+            for (int r : todo[p]) {
+                HRead& h = reads_[r];
+                if (st[r] == kFillTall) {
+                    h.fillPath = p + 1;
+                    if (h.fillPath >= 2) serial.push_back(r);
+                    else next[1].push_back(r);
+                    continue;
+                }
+                if (st[r] == kFillOverflow) {
+                    const long long need = std::max(ua[r], ub[r]);
+                    h.valCap = std::max(need + need / 4 + 64, h.valCap + 1);
+                    h.valA = valTop_;
+                    h.valB = valTop_ + h.valCap;
+                    valTop_ += 2 * h.valCap;
+                    descDirty_ = true;
+                    next[p].push_back(r);
+                    continue;
+                }
+                h.status = st[r];
+                h.flips = fl[r];
+                h.baseline = bl[r];
+                h.filled = true;
+                if (st[r] == kFillOk || st[r] == kFillMismatch) done.push_back(r);
+            }
+        }
+        todo[0].swap(next[0]);
+        todo[1].swap(next[1]);
+    }
+    if (!done.empty()) {
+        upload(dList_, done, stream_);
+        const DevBatch B = View();
+        Timed(kKSuffix, [&] { launch_suffix(B, dList_.ptr, (int)done.size(), stream_, true); });
+        PBCCS_HIP(hipGetLastError());
+        PBCCS_HIP(hipStreamSynchronize(stream_));   // the list buffer is reused by the next step
+    }
+    if (!serial.empty()) FillReadsSerial(serial);
+}
+
+void ArrowBatch::FillReadsSerial(const std::vector<int>& readsIn)
 {
     std::vector<int> todo(readsIn);
     for (int r : todo) EnsureCapacity(r);
@@ -426,6 +551,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.usedB = dUsedB_.ptr;
             F.capSlots = capSlots;
             F.capCols = capCols;
+            static const bool trace = std::getenv("PBCCS_FILL_TRACE") != nullptr;
+            if (trace) {
+                dTrace_.reserve(8 * n, false);
+                F.trace = dTrace_.ptr;
+            }
             upload(dList_, chunk, stream_);
             const DevBatch B = View();
             Timed(kKFill, [&] { launch_fill(B, F, dList_.ptr, (int)n, stream_); });
@@ -439,6 +569,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             download(ua, dUsedA_, R, stream_);
             download(ub, dUsedB_, R, stream_);
             PBCCS_HIP(hipStreamSynchronize(stream_));
+            if (trace) TraceSummary(n, H, capSlots);
             for (int r : chunk) {
                 HRead& h = reads_[r];
                 if (st[r] == kFillOverflow) {
@@ -471,6 +602,35 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         todo.swap(again);
         H *= 2;
     }
+}
+
+// Per-lane timing of the last fill launch (wall clock, 100 MHz), summarised to stderr.
+void ArrowBatch::TraceSummary(size_t n, int H, long long capSlots)
+{
+    std::vector<long long> tr;
+    download(tr, dTrace_, 8 * n, stream_);
+    PBCCS_HIP(hipStreamSynchronize(stream_));
+    long long t0 = LLONG_MAX, t1 = 0, maxDur = 0, maxCells = 0, sumCells = 0, sumPass = 0, maxPass = 0;
+    double sumDur = 0;
+    long long done = 0;
+    for (size_t t = 0; t < n; ++t) {
+        const long long* e = &tr[8 * t];
+        if (e[1] <= 0) continue;
+        ++done;
+        t0 = std::min(t0, e[0]);
+        t1 = std::max(t1, e[1]);
+        maxDur = std::max(maxDur, e[1] - e[0]);
+        sumDur += double(e[1] - e[0]);
+        maxCells = std::max(maxCells, e[2]);
+        sumCells += e[2];
+        sumPass += e[3];
+        maxPass = std::max(maxPass, e[3]);
+    }
+    std::fprintf(stderr,
+                 "[fill-trace] lanes=%zu done=%lld H=%d capSlots=%lld span_ms=%.3f maxlane_ms=%.3f avglane_ms=%.3f "
+                 "cells avg=%.0f max=%lld passes avg=%.2f max=%lld\n",
+                 n, done, H, capSlots, (t1 - t0) / 1e5, maxDur / 1e5, done ? sumDur / done / 1e5 : 0.0,
+                 done ? double(sumCells) / done : 0.0, maxCells, done ? double(sumPass) / done : 0.0, maxPass);
 }
 
 void ArrowBatch::MeanVar(const HZmw& z, int strand, int ts, int te, double* mean, double* var) const

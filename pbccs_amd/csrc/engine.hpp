@@ -130,6 +130,8 @@ public:
     // ---- device operations ------------------------------------------------------------
     // Fill the given reads (AddRead / Template() semantics); refreshes baseline, flips, status.
     void FillReads(const std::vector<int>& reads);
+    // lane-serial fallback for bands taller than the cooperative paths hold (k_fill + k_compact)
+    void FillReadsSerial(const std::vector<int>& reads);
     // AddRead bookkeeping after FillReads (z-score gate, active flag).  Returns AddReadResult.
     int FinishAddRead(int r, double threshold);
     // Score explicit mutation lists (one list per ZMW); returns the summed score per mutation.
@@ -187,6 +189,7 @@ private:
         double baseline = 0.0;
         int flips = 0;
         int status = 0;
+        int fillPath = 0;   // 0: k_fill_coop G=16, 1: k_fill_coop G=64, 2: lane-serial k_fill
         long long seqOff = 0;
         long long colBase = 0;
         int colCap = 0;
@@ -198,6 +201,7 @@ private:
     void UploadTemplate(int z);
     void EnsureCapacity(int r);
     DevBatch View() const;
+    void TraceSummary(size_t n, int H, long long capSlots);
     void MeanVar(const HZmw& z, int strand, int ts, int te, double* mean, double* var) const;
     template <class F>
     void Timed(KernelKind k, F&& launch);
@@ -258,6 +262,7 @@ private:
     // profiling
     bool profiling_ = false;
     DevVec<unsigned long long> dStats_;
+    DevVec<long long> dTrace_;   // PBCCS_FILL_TRACE diagnostics
     struct Pending {
         int kind;
         hipEvent_t a, b;

@@ -1,0 +1,576 @@
+// pbccs_amd/csrc/fill_coop.hip -- cooperative band fill: G lanes per read.
+//
+// FillAlphaBeta + flip-flop controller (SimpleRecursor.cpp:60-296, 642-691) with the rows of a column
+// spread over the G lanes of a group (G = 16: four reads per wavefront; G = 64: one read per wavefront
+// for tall bands).  Per column:
+//   1. every lane computes, for its row i, the three terms that do not depend on the in-column chain:
+//        m_i = match move (diag * emission * transition), k_i = insertion transition, d_i = deletion move,
+//      reading the previous (already scaled) column from an LDS ping-pong buffer;
+//   2. the insertion chain a_i = (m_i + a_{i-1} k_i) + d_i is resolved with G shift-by-one DPP steps
+//      (lane l holds its final value after step l; each step is the reference's exact operation order,
+//      -ffp-contract=off, so every cell is bit-identical to SimpleRecursor);
+//   3. a group prefix-max gives each row the running column maximum the reference's loop would hold,
+//      hence its threshold maxScore / exp(ScoreDiff) and the loop's continue condition; a ballot finds
+//      the row where the reference loop stops (rows past it are discarded);
+//   4. the column is scaled by its maximum (ScaledMatrix::FinishEditingColumn), stored to the read's
+//      compact band in HBM (coalesced: consecutive rows -> consecutive addresses) and kept in LDS as the
+//      next column's input; a second ballot gives the next column's hint row.
+// Columns taller than the LDS capacity abort the read with kFillTall (the host re-runs it with G = 64
+// and a larger buffer, then on the lane-serial k_fill); value-capacity overflow switches the read to
+// count-only mode and reports the exact size it needs (kFillOverflow).
+#include "arrow_device.hpp"
+#include "arrow_kernels.hpp"
+
+namespace pbccs {
+namespace {
+
+constexpr int kCtxDoubles = 9 * kCtxStride;   // 45
+constexpr int kBaseOther = 4;                 // nibble code of a non-ACGT read base (never matches)
+
+__device__ __forceinline__ int base_code(char c)
+{
+    return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : kBaseOther;
+}
+
+__device__ __forceinline__ int nib(const unsigned* w, int x) { return (w[x >> 3] >> ((x & 7) << 2)) & 15; }
+
+// ContextParameters::GetParametersForContext slot from two template base codes (ACGT only).
+__device__ __forceinline__ int ctx_code(int b1, int b2) { return b1 == b2 ? b2 : 4 + b2; }
+
+// --- cross-lane primitives (gfx9 DPP) -------------------------------------------------------------
+template <int CTRL, int ROWMASK, bool BOUND>
+__device__ __forceinline__ double dpp_d(double old, double x)
+{
+    const int xl = __double2loint(x), xh = __double2hiint(x);
+    const int ol = __double2loint(old), oh = __double2hiint(old);
+    const int rl = __builtin_amdgcn_update_dpp(ol, xl, CTRL, ROWMASK, 0xF, BOUND);
+    const int rh = __builtin_amdgcn_update_dpp(oh, xh, CTRL, ROWMASK, 0xF, BOUND);
+    return __hiloint2double(rh, rl);
+}
+
+// value of lane l-1 of the group; lane 0 receives `first`
+template <int G>
+__device__ __forceinline__ double shift_up(double x, double first)
+{
+    if constexpr (G == 16) return dpp_d<0x111, 0xF, false>(first, x);   // row_shr:1
+    else return dpp_d<0x138, 0xF, false>(first, x);                     // wave_shr:1
+}
+
+// inclusive prefix maximum over the group's lanes (values >= 0)
+template <int G>
+__device__ __forceinline__ double prefix_max(double x)
+{
+    x = fmax(x, dpp_d<0x111, 0xF, true>(0.0, x));
+    x = fmax(x, dpp_d<0x112, 0xF, true>(0.0, x));
+    x = fmax(x, dpp_d<0x114, 0xF, true>(0.0, x));
+    x = fmax(x, dpp_d<0x118, 0xF, true>(0.0, x));
+    if constexpr (G == 64) {
+        x = fmax(x, dpp_d<0x142, 0xA, false>(0.0, x));   // row_bcast:15
+        x = fmax(x, dpp_d<0x143, 0xC, false>(0.0, x));   // row_bcast:31
+    }
+    return x;
+}
+
+template <int G>
+struct Group {
+    int lane;   // lane within the group
+    int base;   // first wavefront lane of the group
+    __device__ __forceinline__ unsigned long long bits(bool p) const
+    {
+        const unsigned long long m = __ballot(p);
+        if constexpr (G == 64) return m;
+        else return (m >> base) & ((1ull << G) - 1);
+    }
+    __device__ __forceinline__ double bcast(double x, int src) const { return __shfl(x, src, G); }
+    __device__ __forceinline__ int bcast(int x, int src) const { return __shfl(x, src, G); }
+};
+
+// Everything a group needs about its read (group-uniform values) + LDS views.
+template <int G>
+struct Task {
+    Group<G> g;
+    int I, J, L, start;
+    const unsigned* rdW;   // read bases, nibble-packed
+    const unsigned* tpW;   // template window bases [0, J], nibble-packed
+    const double* ctx;     // 9 x kCtxStride transition parameters
+    double* col0;
+    double* col1;
+    int hcap;              // rows per LDS column buffer
+    double prNot, prThird, sdn;
+
+    __device__ __forceinline__ int TBase(int idx) const { return nib(tpW, idx); }
+    __device__ __forceinline__ int TCtx(int idx) const
+    {
+        return (start + idx + 1 < L) ? ctx_code(nib(tpW, idx), nib(tpW, idx + 1)) : kCtxZero;
+    }
+};
+
+struct PassOut {
+    long long used;   // values used by the pass (also when they did not fit)
+    double last;      // alpha(I, J) or beta(0, 0)
+    double sumL;      // accumulate(logScales, 0.0) left to right
+    bool tall;        // a column exceeded the LDS buffer
+};
+
+// ---- FillAlpha (SimpleRecursor.cpp:60-181) --------------------------------------------------------
+template <int G>
+__device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide, bool selfValid, bool& ovf)
+{
+    const int I = T.I, J = T.J, lane = T.g.lane;
+    PassOut out{0, 0.0, 0.0, false};
+    if (a.cap < 1) ovf = true;
+    if (lane == 0) {
+        if (!ovf) a.V(0) = 1.0;
+        a.R(0) = make_int2(0, 1);
+        a.O(0) = 0;
+        a.L(0) = 0.0;
+    }
+    double* prev = T.col0;
+    double* cur = T.col1;
+    if (lane == 0) prev[0] = 1.0;
+    int pb = 0, pe = 1;
+    long long used = 1;
+    int hb = 1, he = 1;
+    int prevCtx = kCtxZero;
+    int curBase = T.TBase(0), curCtx = T.TCtx(0);
+    double s = 0.0;   // 0.0 + L(0)
+    int2 gR = make_int2(0, 0), sR = make_int2(0, 0);
+    for (int j = 1; j < J; ++j) {
+        const int jb = (j - 1) & (G - 1);
+        if (jb == 0) {   // ranges of columns [j, j + G): the guide's, and this matrix's previous ones
+            const int jj = j + lane;
+            if (guide) gR = (jj < J) ? guide->R(jj) : make_int2(0, 0);
+            if (selfValid) sR = (jj < J) ? a.R(jj) : make_int2(0, 0);
+        }
+        if (guide) {   // RangeGuide (SimpleRecursor.cpp:728-757)
+            const int gx = T.g.bcast(gR.x, jb), gy = T.g.bcast(gR.y, jb);
+            if (gx < gy) { hb = min(gx, hb); he = max(gy, he); }
+        }
+        if (selfValid) {
+            const int sx = T.g.bcast(sR.x, jb), sy = T.g.bcast(sR.y, jb);
+            if (sx < sy) { hb = min(sx, hb); he = max(sy, he); }
+        }
+        const int reqEnd = min(I, he);
+        const int nextBase = T.TBase(j), nextCtx = T.TCtx(j);
+        const double* cp = T.ctx + curCtx * kCtxStride;
+        const double* pp = T.ctx + prevCtx * kCtxStride;
+        const double pMatch = pp[kM], pDel = pp[kD];
+        const double cBranch = cp[kB], cStick3 = cp[kS3];
+        const int b = hb;
+        double mx = 0.0, aLast = 0.0;
+        int e = b, nc = 0;
+        if (b < I) {
+            double carry = 0.0;
+            for (int i0 = b;; i0 += G) {
+                if ((nc + 1) * G > T.hcap) { out.tall = true; return out; }
+                const int i = i0 + lane;
+                const int rb = (i >= 1 && i <= I) ? nib(T.rdW, i - 1) : 15;
+                const double left = (i >= pb && i < pe) ? prev[i - pb] : 0.0;
+                const double diag = (i - 1 >= pb && i - 1 < pe) ? prev[i - 1 - pb] : 0.0;
+                const double mpe = diag * (rb == curBase ? T.prNot : T.prThird);
+                const double m = (i == 1 && j == 1) ? mpe : ((i != 1 && j != 1) ? mpe * pMatch : 0.0);
+                const double k = (i > 1) ? (rb == nextBase ? cBranch : cStick3) : 0.0;
+                const double d = (j > 1) ? left * pDel : 0.0;
+                double x = 0.0, up = carry;   // lane 0's `up` stays the carry: DPP leaves it untouched
+#pragma unroll
+                for (int q = 0; q < G; ++q) {
+                    up = shift_up<G>(x, up);
+                    x = (m + up * k) + d;
+                }
+                const double pm = fmax(mx, prefix_max<G>(x));
+                const double thr = pm / T.sdn;
+                const bool cont = (i + 1 < I) && (x >= thr || i + 1 < reqEnd);
+                const unsigned long long stop = T.g.bits(!cont);
+                const int lastLane = stop ? (__ffsll((long long)stop) - 1) : (G - 1);
+                mx = T.g.bcast(pm, lastLane);
+                ++nc;
+                if (stop) {
+                    e = i0 + lastLane + 1;
+                    aLast = x;
+                    break;
+                }
+                cur[(nc - 1) * G + lane] = x;
+                carry = T.g.bcast(x, G - 1);
+            }
+        }
+        // ScaledMatrix::FinishEditingColumn (ScaledMatrix-inl.hpp:35-60) + the next begin hint (:166)
+        const double thrF = mx / T.sdn;
+        const bool scale = (mx != 0.0 && mx != 1.0);
+        int nhb = e;
+        bool found = false;
+        for (int c = 0; c < nc; ++c) {
+            const int kk = c * G + lane;
+            const bool ok = b + kk < e;
+            const double x = (c == nc - 1) ? aLast : cur[kk];
+            const double v = scale ? x / mx : x;
+            if (ok) {
+                cur[kk] = v;
+                if (!ovf && used + kk < a.cap) a.V(used + kk) = v;
+            }
+            const unsigned long long hit = T.g.bits(ok && !(v < thrF));
+            if (!found && hit) {
+                nhb = b + c * G + __ffsll((long long)hit) - 1;
+                found = true;
+            }
+        }
+        if (used + (e - b) > a.cap) ovf = true;
+        const double lsj = scale ? log(mx) : 0.0;
+        if (lane == 0) {
+            a.R(j) = make_int2(b, e);
+            a.O(j) = (int)used;
+            a.L(j) = lsj;
+        }
+        s = s + lsj;
+        used += e - b;
+        double* t = prev;
+        prev = cur;
+        cur = t;
+        pb = b;
+        pe = e;
+        prevCtx = curCtx;
+        curBase = nextBase;
+        curCtx = nextCtx;
+        he = e;
+        hb = nhb;
+    }
+    // pinned final match (:169-179)
+    const double em = (nib(T.rdW, I - 1) == T.TBase(J - 1)) ? T.prNot : T.prThird;
+    const double lik = ((I - 1 >= pb && I - 1 < pe) ? prev[I - 1 - pb] : 0.0) * em;
+    const double c = (0.0 < lik) ? lik : 0.0;
+    double v = lik, ls = 0.0;
+    if (c != 0.0 && c != 1.0) { v = lik / c; ls = log(c); }
+    if (used + 1 > a.cap) ovf = true;
+    if (lane == 0) {
+        if (!ovf) a.V(used) = v;
+        a.R(J) = make_int2(I, I + 1);
+        a.O(J) = (int)used;
+        a.L(J) = ls;
+    }
+    out.used = used + 1;
+    out.last = v;
+    out.sumL = s + ls;
+    return out;
+}
+
+// ---- FillBeta (SimpleRecursor.cpp:183-296); rows run bottom-up, stored bottom-up --------------------
+template <int G>
+__device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide, bool selfValid, bool& ovf)
+{
+    const int I = T.I, J = T.J, lane = T.g.lane;
+    PassOut out{0, 0.0, 0.0, false};
+    if (bm.cap < 1) ovf = true;
+    if (lane == 0) {
+        if (!ovf) bm.V(0) = 1.0;
+        bm.R(J) = make_int2(I, I + 1);
+        bm.O(J) = 0;
+        bm.L(J) = 0.0;
+    }
+    // the next column (j + 1) holds rows [pb, pe) at index pe - 1 - row
+    double* nxt = T.col0;
+    double* cur = T.col1;
+    if (lane == 0) nxt[0] = 1.0;
+    int pb = I, pe = I + 1;
+    long long used = 1;
+    int hb = I, he = I;
+    int nextBase = T.TBase(J - 1);
+    int2 gR = make_int2(0, 0), sR = make_int2(0, 0);
+    for (int j = J - 1; j > 0; --j) {
+        const int jb = (J - 1 - j) & (G - 1);
+        if (jb == 0) {   // ranges of columns (j - G, j]
+            const int jj = j - lane;
+            if (guide) gR = (jj > 0) ? guide->R(jj) : make_int2(0, 0);
+            if (selfValid) sR = (jj > 0) ? bm.R(jj) : make_int2(0, 0);
+        }
+        const int curBase = T.TBase(j - 1), curCtx = T.TCtx(j - 1);
+        if (guide) {
+            const int gx = T.g.bcast(gR.x, jb), gy = T.g.bcast(gR.y, jb);
+            if (gx < gy) { hb = min(gx, hb); he = max(gy, he); }
+        }
+        if (selfValid) {
+            const int sx = T.g.bcast(sR.x, jb), sy = T.g.bcast(sR.y, jb);
+            if (sx < sy) { hb = min(sx, hb); he = max(sy, he); }
+        }
+        const int reqBegin = max(0, hb);
+        const double* cp = T.ctx + curCtx * kCtxStride;
+        const double cMatch = cp[kM], cDel = cp[kD], cBranch = cp[kB], cStick3 = cp[kS3];
+        const int e = he;
+        double mx = 0.0, aLast = 0.0;
+        int b = e, nc = 0;
+        if (e - 1 > 0) {
+            double carry = 0.0;
+            for (int c = 0;; ++c) {
+                if ((c + 1) * G > T.hcap) { out.tall = true; return out; }
+                const int off = c * G + lane;
+                const int i = e - 1 - off;
+                const int nb = (i >= 0 && i < I) ? nib(T.rdW, i) : 15;
+                const double left = (i >= pb && i < pe) ? nxt[pe - 1 - i] : 0.0;
+                const double diag = (i + 1 >= pb && i + 1 < pe) ? nxt[pe - 2 - i] : 0.0;
+                const bool same = nb == nextBase;
+                const double mpe = diag * (same ? T.prNot : T.prThird);
+                const double m = (i < I - 1) ? mpe * cMatch : ((i == I - 1 && j == J - 1) ? mpe : 0.0);
+                const double k = (i < I - 1 && i > 0) ? (same ? cBranch : cStick3) : 0.0;
+                const double d = (j < J - 1 && j > 0) ? left * cDel : 0.0;
+                double x = 0.0, up = carry;   // lane 0's `up` stays the carry: DPP leaves it untouched
+#pragma unroll
+                for (int q = 0; q < G; ++q) {
+                    up = shift_up<G>(x, up);
+                    x = (m + up * k) + d;
+                }
+                const double pm = fmax(mx, prefix_max<G>(x));
+                const double thr = pm / T.sdn;
+                const bool cont = (i - 1 > 0) && (x >= thr || i - 1 >= reqBegin);
+                const unsigned long long stop = T.g.bits(!cont);
+                const int lastLane = stop ? (__ffsll((long long)stop) - 1) : (G - 1);
+                mx = T.g.bcast(pm, lastLane);
+                ++nc;
+                if (stop) {
+                    b = e - 1 - (c * G + lastLane);
+                    aLast = x;
+                    break;
+                }
+                cur[off] = x;
+                carry = T.g.bcast(x, G - 1);
+            }
+        }
+        const double thrF = mx / T.sdn;
+        const bool scale = (mx != 0.0 && mx != 1.0);
+        int nhe = b;
+        bool found = false;
+        for (int c = 0; c < nc; ++c) {
+            const int off = c * G + lane;
+            const bool ok = e - 1 - off >= b;
+            const double x = (c == nc - 1) ? aLast : cur[off];
+            const double v = scale ? x / mx : x;
+            if (ok) {
+                cur[off] = v;
+                if (!ovf && used + off < bm.cap) bm.V(used + off) = v;
+            }
+            const unsigned long long hit = T.g.bits(ok && !(v < thrF));
+            if (!found && hit) {
+                nhe = e - (c * G + __ffsll((long long)hit) - 1);
+                found = true;
+            }
+        }
+        if (used + (e - b) > bm.cap) ovf = true;
+        const double lsj = scale ? log(mx) : 0.0;
+        if (lane == 0) {
+            bm.R(j) = make_int2(b, e);
+            bm.O(j) = (int)used;
+            bm.L(j) = lsj;
+        }
+        used += e - b;
+        double* t = nxt;
+        nxt = cur;
+        cur = t;
+        pb = b;
+        pe = e;
+        hb = b;
+        he = nhe;
+        nextBase = curBase;
+    }
+    const double em = (T.TBase(0) == nib(T.rdW, 0)) ? T.prNot : T.prThird;
+    const double raw = em * ((1 >= pb && 1 < pe) ? nxt[pe - 2] : 0.0);
+    const double c = (0.0 < raw) ? raw : 0.0;
+    double v = raw, ls = 0.0;
+    if (c != 0.0 && c != 1.0) { v = raw / c; ls = log(c); }
+    if (used + 1 > bm.cap) ovf = true;
+    double s = 0.0;
+    if (lane == 0) {
+        if (!ovf) bm.V(used) = v;
+        bm.R(0) = make_int2(0, 1);
+        bm.O(0) = (int)used;
+        bm.L(0) = ls;
+        // accumulate(logScales, 0.0) in column order; lane 0 wrote every L(j) of this pass itself
+        s = s + ls;
+        for (int k = 1; k <= J; ++k) s = s + bm.L(k);
+    }
+    out.used = used + 1;
+    out.last = v;
+    out.sumL = T.g.bcast(s, 0);
+    return out;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// k_fill_coop: one G-lane group per read; 64 / G reads per 64-thread block.
+// LDS per group: 2 column buffers (hcap doubles each), the ZMW's transition table, nibble-packed read
+// and template window.
+// ------------------------------------------------------------------------------------------------
+template <int G>
+__global__ void __launch_bounds__(64) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int grp = threadIdx.x / G;
+    const int t = blockIdx.x * (64 / G) + grp;
+    const int lane = threadIdx.x & (G - 1);
+    unsigned char* gbase = smem + (size_t)grp * F.groupBytes;
+    double* col = reinterpret_cast<double*>(gbase);
+    double* ctx = col + 2 * F.hcap;
+    unsigned* rdW = reinterpret_cast<unsigned*>(ctx + kCtxDoubles + 1);
+    unsigned* tpW = rdW + F.readWords;
+
+    const bool valid = t < n;
+    int r = 0, z = 0, I = 0, J = 0;
+    TplView tv{};
+    bool bad = true;
+    if (valid) {
+        r = reads[t];
+        z = B.rZmw[r];
+        I = B.rLen[r];
+        tv = window_view(B, r);
+        J = tv.Length();
+        bad = I < 1 || J < 1 || (I + 7) / 8 > F.readWords || (J + 8) / 8 > F.tplWords;
+        if (!bad) {
+            const double* zc = B.zCtx + (long long)z * kCtxDoubles;
+            for (int k = lane; k < kCtxDoubles; k += G) ctx[k] = zc[k];
+            const char* rd = B.seqPool + B.rSeqOff[r];
+            for (int w = lane; w < (I + 7) / 8; w += G) {
+                unsigned word = 0;
+                for (int q = 0; q < 8; ++q) {
+                    const int x = 8 * w + q;
+                    word |= (unsigned)(x < I ? base_code(rd[x]) : kBaseOther) << (4 * q);
+                }
+                rdW[w] = word;
+            }
+            for (int w = lane; w < (J + 8) / 8; w += G) {
+                unsigned word = 0;
+                for (int q = 0; q < 8; ++q) {
+                    const int x = 8 * w + q;
+                    const int g = tv.start + x;
+                    word |= (unsigned)((x <= J && g < tv.L) ? base_code(tv.T[g]) : kBaseOther) << (4 * q);
+                }
+                tpW[w] = word;
+            }
+        }
+    }
+    __syncthreads();
+    if (!valid) return;
+    if (bad) {
+        if (lane == 0) B.rStatus[r] = (I < 1 || J < 1) ? kFillBadInput : kFillOverflow;
+        return;
+    }
+
+    Task<G> T;
+    T.g.lane = lane;
+    T.g.base = threadIdx.x & ~(G - 1);
+    T.I = I;
+    T.J = J;
+    T.L = tv.L;
+    T.start = tv.start;
+    T.rdW = rdW;
+    T.tpW = tpW;
+    T.ctx = ctx;
+    T.col0 = col;
+    T.col1 = col + F.hcap;
+    T.hcap = F.hcap;
+    T.prNot = B.prNot;
+    T.prThird = B.prThird;
+    T.sdn = B.sdn;
+
+    const long long cb = B.rColBase[r];
+    Band a, bm;
+    a.range = B.aRange + cb;
+    a.off = B.aOff + cb;
+    a.ls = B.aLs + cb;
+    a.val = B.valPool + B.rValA[r];
+    a.cap = B.rValCap[r];
+    bm.range = B.bRange + cb;
+    bm.off = B.bOff + cb;
+    bm.ls = B.bLs + cb;
+    bm.val = B.valPool + B.rValB[r];
+    bm.cap = B.rValCap[r];
+
+    bool ovf = false;
+    long long needA = 0, needB = 0;
+    unsigned long long cells = 0, passes = 0;
+    int flips = 0;
+    auto fail_tall = [&]() {
+        if (lane == 0) B.rStatus[r] = kFillTall;
+    };
+    // MutationScorer ctor -> FillAlphaBeta (SimpleRecursor.cpp:642-691)
+    PassOut pa = coop_alpha<G>(T, a, nullptr, false, ovf);
+    if (pa.tall) return fail_tall();
+    PassOut pb = coop_beta<G>(T, bm, &a, false, ovf);
+    if (pb.tall) return fail_tall();
+    needA = max(needA, pa.used);
+    needB = max(needB, pb.used);
+    cells += pa.used + pb.used;
+    passes += 2;
+    long long ua = pa.used, ub = pb.used;
+    const int maxSize = (int)(0.5 + kRebandFrac * (I + 1) * (J + 1));
+    if (ua >= maxSize || ub >= maxSize) {
+        PassOut a1 = coop_alpha<G>(T, a, &bm, true, ovf);
+        if (a1.tall) return fail_tall();
+        pb = coop_beta<G>(T, bm, &a, true, ovf);
+        if (pb.tall) return fail_tall();
+        pa = coop_alpha<G>(T, a, &bm, true, ovf);
+        if (pa.tall) return fail_tall();
+        needA = max(needA, max(a1.used, pa.used));
+        needB = max(needB, pb.used);
+        cells += a1.used + pb.used + pa.used;
+        passes += 3;
+        flips += 3;
+        ua = pa.used;
+        ub = pb.used;
+    }
+    double av = log(pa.last) + pa.sumL;
+    double bv = log(pb.last) + pb.sumL;
+    // NB: alphaV / betaV are not re-evaluated inside the loop (SimpleRecursor.cpp:667-679)
+    const bool mismatched = fabs(av - bv) > kAlphaBetaTol;
+    while (mismatched && flips <= kMaxFlipFlops) {
+        if (flips % 2 == 0) {
+            pa = coop_alpha<G>(T, a, &bm, true, ovf);
+            if (pa.tall) return fail_tall();
+            needA = max(needA, pa.used);
+            cells += pa.used;
+            ua = pa.used;
+        } else {
+            pb = coop_beta<G>(T, bm, &a, true, ovf);
+            if (pb.tall) return fail_tall();
+            needB = max(needB, pb.used);
+            cells += pb.used;
+            ub = pb.used;
+        }
+        passes += 1;
+        ++flips;
+    }
+    av = log(pa.last) + pa.sumL;
+    bv = log(pb.last) + pb.sumL;
+    const double mism = fabs(1.0 - av / bv);
+    if (lane == 0) {
+        if (ovf) {
+            B.rStatus[r] = kFillOverflow;
+            F.usedA[r] = (int)needA;
+            F.usedB[r] = (int)needB;
+        } else {
+            B.rFlips[r] = flips;
+            B.rBaseline[r] = bv;
+            F.usedA[r] = (int)ua;
+            F.usedB[r] = (int)ub;
+            B.rStatus[r] = (mism > kAlphaBetaTol) ? kFillMismatch : kFillOk;
+            if (B.stats) {   // algorithmic: 8 B per stored cell + 16 B per column per fill pass
+                atomicAdd(&B.stats[2 * kStatFill], cells);
+                atomicAdd(&B.stats[2 * kStatFill + 1], 8ull * cells + 16ull * passes * (unsigned long long)(J + 1));
+            }
+        }
+    }
+}
+
+size_t coop_group_bytes(int hcap, int readWords, int tplWords)
+{
+    size_t b = (size_t)(2 * hcap + kCtxDoubles + 1) * sizeof(double) + (size_t)(readWords + tplWords) * 4;
+    return (b + 15) & ~(size_t)15;
+}
+
+void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* reads, int n, hipStream_t s)
+{
+    if (n <= 0) return;
+    const int per = 64 / G;
+    const size_t lds = (size_t)per * F.groupBytes;
+    const dim3 grid((n + per - 1) / per);
+    if (G == 16) hipLaunchKernelGGL(k_fill_coop<16>, grid, dim3(64), lds, s, B, F, reads, n);
+    else hipLaunchKernelGGL(k_fill_coop<64>, grid, dim3(64), lds, s, B, F, reads, n);
+}
+
+}  // namespace pbccs

@@ -45,6 +45,7 @@ class PreparedBatch:
 
     def __init__(self, zmws, settings=None, engine=None):
         from . import default_engine
+        self._lib = L.load()
         self.engine = engine or default_engine()
         self.settings = settings or ConsensusSettings()
         self.zmws = zmws
@@ -113,7 +114,7 @@ class PreparedBatch:
 
     def close(self):
         if getattr(self, "_h", None):
-            L.load().pbccs_batch_destroy(self._h)
+            self._lib.pbccs_batch_destroy(self._h)
             self._h = None
 
     def __del__(self):
