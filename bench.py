@@ -4,9 +4,11 @@
 A step polishes one batch of synthetic ZMWs (2 kb insert, 10 full passes)
 end to end on the GPU: AddRead fills + z-score gates, RefineConsensus, ConsensusQVs -- the per-ZMW
 polish that pbccs' Consensus.h runs after the POA.  Inputs are copied to HBM before the timed region
-(pbccs_batch_create); the timed region is exactly K steps (pbccs_batch_polish), bracketed by a barrier
-and torch.cuda.synchronize() on both sides; the job time is the max over ranks.  Default: 5 steps x 2000
-ZMWs = the 10k-ZMW workload of configs[1].  Multi-GPU: each rank polishes its own shard (weak scaling,
+(pbccs_batch_create); the timed region is exactly K steps, bracketed by a barrier and
+torch.cuda.synchronize() on both sides; the job time is the max over ranks.  The K steps are pipelined
+(pbccs_batch_polish_many: one host thread + HIP stream per batch in flight), so one batch's convergence
+tail -- the last refine rounds of its few slow ZMWs -- overlaps the others' work, the way ccs's ZMW thread
+pool overlaps ZMWs.  Default: 5 steps x 2000 ZMWs = the 10k-ZMW workload of configs[1].  Multi-GPU: each rank polishes its own shard (weak scaling,
 no data-path collective).  rank 0 prints one JSON line.
 """
 import argparse
@@ -35,6 +37,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-sample", type=int, default=16, help="ZMWs polished by the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--streams", type=int, default=0,
+                    help="batches polished concurrently (0 = min(steps, 4)); each has its own HIP stream")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
@@ -92,6 +96,8 @@ def main():
             torch.cuda.synchronize()
 
     eng = pbccs_amd.Engine(local)
+    streams = args.streams or max(1, min(args.steps, 4))
+    eng.set_concurrency(streams)
     if not args.no_profile:
         eng.set_profiling(True)   # HIP events on the engine stream + in-kernel algorithmic counters
     settings = pbccs_amd.ConsensusSettings()
@@ -119,9 +125,8 @@ def main():
     barrier()
     sync()
     t0 = time.perf_counter()
-    for k, b in enumerate(batches):
-        b.polish()
-        log(rank, f"[bench] step {k} done t={time.perf_counter() - t0:.2f}s")
+    pbccs_amd.polish_many(batches)   # the K steps, pipelined over `streams` HIP streams / host threads
+    log(rank, f"[bench] {args.steps} steps done t={time.perf_counter() - t0:.2f}s")
     sync()
     barrier()
     t1 = time.perf_counter()
@@ -176,6 +181,7 @@ def main():
                                f"{args.zmws_per_step * args.steps} ZMWs per GPU "
                                f"({args.steps} steps x {args.zmws_per_step})",
                    "zmws_per_step": args.zmws_per_step, "insert_bp": args.length, "passes": args.passes,
+                   "streams": streams,
                    "parallelism": f"zmw-shard x{world}"},
         "gcups": round(gcups_local * world, 3),
         "zmw_status": statuses,

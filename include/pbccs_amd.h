@@ -180,6 +180,16 @@ int pbccs_batch_create(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
 int pbccs_batch_polish(pbccs_batch* b, pbccs_zmw_output* out);
 void pbccs_batch_destroy(pbccs_batch* b);
 
+/* Polish several batches of one engine concurrently: one host thread and one HIP stream per workspace
+ * slot, so that one batch's convergence tail (the last refine rounds of a few ZMWs) overlaps the other
+ * batches' work.  The analogue of ccs's ZMW thread pool (src/main/ccs.cpp:222-230, WorkQueue.h).
+ * outs[i] receives batch i's outputs.  Returns the first failure. */
+int pbccs_batch_polish_many(pbccs_batch* const* batches, int n, pbccs_zmw_output* const* outs);
+
+/* Number of workspace slots = batches that may polish at the same time (default 4).  Set it before
+ * creating batches; each slot holds its own resident band pools. */
+int pbccs_engine_set_concurrency(pbccs_engine* eng, int batches_in_flight);
+
 /* Work counters of the engine since the last reset (for roofline accounting). */
 typedef struct {
     long long fill_launches, score_launches, score_tasks, mutations;

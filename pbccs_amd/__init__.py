@@ -81,6 +81,10 @@ class Engine:
             self._lib.pbccs_engine_destroy(self._h)
             self._h = None
 
+    def set_concurrency(self, batches_in_flight):
+        """Workspace slots = batches polished at the same time by polish_many (set before creating batches)."""
+        _lib_mod.check(load().pbccs_engine_set_concurrency(self._h, int(batches_in_flight)))
+
     def set_profiling(self, on=True):
         _lib_mod.check(load().pbccs_engine_set_profiling(self._h, 1 if on else 0))
 
@@ -232,10 +236,10 @@ def QVsToASCII(qvs):
     return "".join(chr(min(max(0, q), 93) + 33) for q in qvs)
 
 
-from .polish import ConsensusSettings, PreparedBatch, polish_zmws  # noqa: E402  (batched ccs driver)
+from .polish import ConsensusSettings, PreparedBatch, polish_many, polish_zmws  # noqa: E402  (batched ccs driver)
 
 __all__ = [
     "ArrowConfig", "ArrowMultiReadMutationScorer", "ConsensusQVs", "ConsensusSettings", "Engine", "Mutation",
-    "PbccsError", "QVsToASCII", "RefineConsensus", "polish_zmws", "INSERTION", "DELETION", "SUBSTITUTION",
+    "PbccsError", "QVsToASCII", "RefineConsensus", "polish_many", "polish_zmws", "INSERTION", "DELETION", "SUBSTITUTION",
     "FORWARD_STRAND", "REVERSE_STRAND",
 ]

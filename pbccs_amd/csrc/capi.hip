@@ -11,6 +11,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine.hpp"
@@ -22,11 +23,21 @@ struct pbccs_engine {
     Counters counters;
     bool profiling = false;
     KernelStat stats[kKernelKinds];
-    Workspace ws;   // resident pools shared by the engine's batches (they polish one at a time)
+    // Resident pools.  Batches are dealt round-robin onto `concurrency` workspace slots; batches that
+    // share a slot never polish at the same time (pbccs_batch_polish_many runs one slot per thread).
+    int concurrency = 4;
+    int nextSlot = 0;
+    std::vector<std::unique_ptr<Workspace>> slots;
+    Workspace* Slot(int s)
+    {
+        while ((int)slots.size() <= s) slots.emplace_back(new Workspace());
+        return slots[s].get();
+    }
 };
 
 struct pbccs_batch {
     pbccs_engine* eng = nullptr;
+    int slot = 0;
     std::unique_ptr<ArrowBatch> B;
     pbccs_polish_options o;
     int n = 0;
@@ -385,7 +396,8 @@ int pbccs_batch_create(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
         pbccs_polish_options_default(&b->o);
         if (opts) b->o = *opts;
         b->n = n;
-        b->B.reset(new ArrowBatch(eng->device, &eng->ws));
+        b->slot = eng->nextSlot++ % std::max(1, eng->concurrency);
+        b->B.reset(new ArrowBatch(eng->device, eng->Slot(b->slot)));
         b->B->SetProfiling(eng->profiling);
         ArrowOptions ao;
         ao.scoreDiff = b->o.score_diff;
@@ -420,11 +432,12 @@ int pbccs_batch_create(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
 
 void pbccs_batch_destroy(pbccs_batch* b) { delete b; }
 
-int pbccs_batch_polish(pbccs_batch* b, pbccs_zmw_output* out)
+static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
 {
     if (!b || (b->n > 0 && !out)) return fail(PBCCS_EINVAL, "bad argument");
     if (b->polished) return fail(PBCCS_ESTATE, "a batch polishes once");
     return guarded([&] {
+        if (hipSetDevice(b->eng->device) != hipSuccess) return fail(PBCCS_EDEVICE, "hipSetDevice failed");
         b->polished = true;
         ArrowBatch& B = *b->B;
         const pbccs_polish_options& o = b->o;
@@ -505,9 +518,57 @@ int pbccs_batch_polish(pbccs_batch* b, pbccs_zmw_output* out)
             if (q.qvs) std::copy(qvs[k].begin(), qvs[k].end(), q.qvs);
             q.status = (acc < o.min_predicted_accuracy) ? PBCCS_ZMW_POOR_QUALITY : PBCCS_ZMW_SUCCESS;
         }
-        merge_engine_stats(b->eng, B);
         return PBCCS_OK;
     });
+}
+
+int pbccs_batch_polish(pbccs_batch* b, pbccs_zmw_output* out)
+{
+    const int rc = polish_one(b, out);
+    if (b && b->B) merge_engine_stats(b->eng, *b->B);
+    return rc;
+}
+
+int pbccs_batch_polish_many(pbccs_batch* const* batches, int n, pbccs_zmw_output* const* outs)
+{
+    if (n < 0 || (n > 0 && (!batches || !outs))) return fail(PBCCS_EINVAL, "bad argument");
+    if (n == 0) return PBCCS_OK;
+    pbccs_engine* eng = batches[0] ? batches[0]->eng : nullptr;
+    for (int i = 0; i < n; ++i)
+        if (!batches[i] || batches[i]->eng != eng || (batches[i]->n > 0 && !outs[i]))
+            return fail(PBCCS_EINVAL, "batches must be non-null and belong to one engine");
+    // one host thread (and HIP stream: each ArrowBatch owns one) per workspace slot
+    std::vector<std::vector<int>> bySlot;
+    for (int i = 0; i < n; ++i) {
+        const int s = batches[i]->slot;
+        if ((int)bySlot.size() <= s) bySlot.resize(s + 1);
+        bySlot[s].push_back(i);
+    }
+    std::vector<int> rc(n, PBCCS_OK);
+    std::vector<std::string> err(n);
+    std::vector<std::thread> pool;
+    for (const std::vector<int>& list : bySlot) {
+        if (list.empty()) continue;
+        pool.emplace_back([&, list] {
+            for (int i : list) {
+                rc[i] = polish_one(batches[i], outs[i]);
+                if (rc[i] != PBCCS_OK) err[i] = g_lastError;
+            }
+        });
+    }
+    for (std::thread& t : pool) t.join();
+    for (int i = 0; i < n; ++i)
+        if (batches[i]->B) merge_engine_stats(eng, *batches[i]->B);
+    for (int i = 0; i < n; ++i)
+        if (rc[i] != PBCCS_OK) return fail(rc[i], err[i].c_str());
+    return PBCCS_OK;
+}
+
+int pbccs_engine_set_concurrency(pbccs_engine* eng, int batches_in_flight)
+{
+    if (!eng || batches_in_flight < 1 || batches_in_flight > 64) return fail(PBCCS_EINVAL, "bad argument");
+    eng->concurrency = batches_in_flight;
+    return PBCCS_OK;
 }
 
 int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
@@ -528,13 +589,24 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
         const double perZmw = n > 0 ? bytes / n : 1.0;
         per = (int)std::max(1.0, std::min((double)n, budget / std::max(perZmw, 1.0)));
     }
-    for (int b = 0; b < n; b += per) {
-        const int m = std::min(per, n - b);
-        pbccs_batch* h = nullptr;
-        int rc = pbccs_batch_create(eng, in + b, m, &o, &h);
-        if (rc != PBCCS_OK) return rc;
-        rc = pbccs_batch_polish(h, out + b);
-        pbccs_batch_destroy(h);
+    // split so that every workspace slot gets work, then polish `concurrency` chunks at a time
+    const int slots = std::max(1, eng->concurrency);
+    if (n >= 64 * slots) per = std::min(per, (n + slots - 1) / slots);
+    for (int b0 = 0; b0 < n;) {
+        std::vector<pbccs_batch*> wave;
+        std::vector<pbccs_zmw_output*> outs;
+        int rc = PBCCS_OK;
+        for (int k = 0; k < slots && b0 < n; ++k) {
+            const int m = std::min(per, n - b0);
+            pbccs_batch* h = nullptr;
+            rc = pbccs_batch_create(eng, in + b0, m, &o, &h);
+            if (rc != PBCCS_OK) break;
+            wave.push_back(h);
+            outs.push_back(out + b0);
+            b0 += m;
+        }
+        if (rc == PBCCS_OK) rc = pbccs_batch_polish_many(wave.data(), (int)wave.size(), outs.data());
+        for (pbccs_batch* h : wave) pbccs_batch_destroy(h);
         if (rc != PBCCS_OK) return rc;
     }
     return PBCCS_OK;

@@ -26,11 +26,12 @@ const char* const kKernelNames[kKernelKinds] = {"k_fill", "k_suffix", "k_enumera
 
 namespace {
 
-constexpr int kInitialBandHeight = 20;         // compact band values per column, first estimate
+constexpr int kInitialBandHeight = 16;         // compact band values per column, first estimate
 constexpr int kFillBandHeight = 28;            // fill scratch values per column (doubled on overflow)
 constexpr double kFillScratchBudget = 24.0 * (1ull << 30);
 constexpr int kCoopNarrowRows = 64;           // LDS column rows of the 16-lane fill path
-constexpr size_t kCoopLdsBytes = 64 * 1024;    // LDS budget of one 64-lane fill group
+constexpr int kCoopTallRows = 1024;           // LDS column rows of the first 64-lane fill path
+constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill block (hard limit 64 KB)
 constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
 
 template <class T>
@@ -48,6 +49,70 @@ void download(std::vector<T>& h, const DevVec<T>& d, size_t n, hipStream_t s)
 }
 
 }  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// VmPool
+// ------------------------------------------------------------------------------------------------
+void VmPool::reserve(size_t n, bool keep)
+{
+    if (n <= cap) return;
+    if (!tried_) {
+        tried_ = true;
+        void* va = nullptr;
+        vmm_ = hipMemAddressReserve(&va, kVaBytes, 0, nullptr, 0) == hipSuccess && va != nullptr;
+        if (vmm_) ptr = static_cast<double*>(va);
+        else (void)hipGetLastError();
+    }
+    if (!vmm_) {
+        fallback_.reserve(n, keep);
+        ptr = fallback_.ptr;
+        cap = fallback_.cap;
+        return;
+    }
+    const size_t want = n * sizeof(double);
+    if (want > kVaBytes) throw DeviceError("band pool exceeds its address reservation");
+    int dev = 0;
+    PBCCS_HIP(hipGetDevice(&dev));
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    hipMemAccessDesc desc = {};
+    desc.location = prop.location;
+    desc.flags = hipMemAccessFlagsProtReadWrite;
+    while (mappedBytes_ < want) {
+        const size_t bytes = std::min(kChunkBytes, kVaBytes - mappedBytes_);
+        hipMemGenericAllocationHandle_t h;
+        if (hipMemCreate(&h, bytes, &prop, 0) != hipSuccess) throw DeviceError("hipMemCreate failed (device memory)");
+        char* at = reinterpret_cast<char*>(ptr) + mappedBytes_;
+        if (hipMemMap(at, bytes, 0, h, 0) != hipSuccess) {
+            (void)hipMemRelease(h);
+            throw DeviceError("hipMemMap failed");
+        }
+        if (hipMemSetAccess(at, bytes, &desc, 1) != hipSuccess) {
+            (void)hipMemUnmap(at, bytes);
+            (void)hipMemRelease(h);
+            throw DeviceError("hipMemSetAccess failed");
+        }
+        handles_.push_back(h);
+        sizes_.push_back(bytes);
+        mappedBytes_ += bytes;
+    }
+    cap = mappedBytes_ / sizeof(double);
+}
+
+VmPool::~VmPool()
+{
+    if (!vmm_) return;
+    (void)hipDeviceSynchronize();
+    size_t off = 0;
+    for (size_t k = 0; k < handles_.size(); ++k) {
+        (void)hipMemUnmap(reinterpret_cast<char*>(ptr) + off, sizes_[k]);
+        (void)hipMemRelease(handles_[k]);
+        off += sizes_[k];
+    }
+    (void)hipMemAddressFree(ptr, kVaBytes);
+}
 
 ArrowBatch::ArrowBatch(int device, Workspace* shared)
     : device_(device),
@@ -396,47 +461,56 @@ DevBatch ArrowBatch::View() const
 // the kernel reported.  Bands land directly in the compact layout; k_suffix adds the log-scale sums.
 void ArrowBatch::FillReads(const std::vector<int>& readsIn)
 {
+    constexpr int kPaths = 3;   // 0: 16 lanes / 64 rows; 1: 64 lanes / 1024 rows; 2: 64 lanes / all rows
     for (int r : readsIn) EnsureCapacity(r);
-    std::vector<int> todo[2], serial, done;
+    std::vector<int> todo[kPaths], serial, done;
     for (int r : readsIn) {
         const int p = reads_[r].fillPath;
-        if (p >= 2) serial.push_back(r);
+        if (p >= kPaths) serial.push_back(r);
         else todo[p].push_back(r);
     }
-    for (int attempt = 0; !todo[0].empty() || !todo[1].empty(); ++attempt) {
-        if (attempt > 8) throw DeviceError("band storage keeps overflowing");
-        for (auto& v : todo)   // similar lengths share a launch (LDS is sized by the longest)
-            std::stable_sort(v.begin(), v.end(), [&](int x, int y) {
-                return reads_[x].te - reads_[x].ts > reads_[y].te - reads_[y].ts;
-            });
-        // LDS fit: four 16-lane groups per block, or one 64-lane group with at least one chunk of rows
-        auto words = [&](int r) {
-            return (int)(reads_[r].seq.size() + 7) / 8 + (reads_[r].te - reads_[r].ts + 8) / 8;
-        };
-        for (int p = 0; p < 2; ++p) {
+    auto words = [&](int r) {
+        return (int)(reads_[r].seq.size() + 7) / 8 + (reads_[r].te - reads_[r].ts + 8) / 8;
+    };
+    // rows a column buffer of path p gets for reads with these sizes (0: does not fit in LDS)
+    auto rows_for = [&](int p, int maxI, int w) -> int {
+        if (p == 0) return 4 * coop_group_bytes(kCoopNarrowRows, w, 0) <= kCoopLdsBytes ? kCoopNarrowRows : 0;
+        const long long room = ((long long)kCoopLdsBytes - (long long)coop_group_bytes(0, w, 0)) / 16 / 64 * 64;
+        const long long full = (maxI + 64) / 64 * 64;   // a column never exceeds I + 1 rows
+        const long long want = p == 1 ? std::min<long long>(kCoopTallRows, full) : full;
+        return room >= want ? (int)want : (p == 2 && room >= 64 ? (int)room : 0);
+    };
+    for (int attempt = 0;; ++attempt) {
+        // route reads whose buffers do not fit this path's LDS budget to the next path
+        for (int p = 0; p < kPaths; ++p) {
             std::vector<int> keep;
             for (int r : todo[p]) {
-                const size_t need = p == 0 ? 4 * coop_group_bytes(kCoopNarrowRows, words(r), 0)
-                                           : coop_group_bytes(64, words(r), 0);
-                if (need <= kCoopLdsBytes) keep.push_back(r);
-                else if (p == 0) todo[1].push_back(r);
+                if (rows_for(p, (int)reads_[r].seq.size(), words(r)) > 0) keep.push_back(r);
+                else if (p + 1 < kPaths) todo[p + 1].push_back(r);
                 else {
-                    reads_[r].fillPath = 2;
+                    reads_[r].fillPath = kPaths;
                     serial.push_back(r);
                 }
             }
             todo[p].swap(keep);
         }
+        if (todo[0].empty() && todo[1].empty() && todo[2].empty()) break;
+        if (attempt > 8) throw DeviceError("band storage keeps overflowing");
+        for (auto& v : todo)   // similar lengths share a launch (LDS is sized by the longest)
+            std::stable_sort(v.begin(), v.end(), [&](int x, int y) {
+                return reads_[x].te - reads_[x].ts > reads_[y].te - reads_[y].ts;
+            });
         UploadDescriptors();
         const size_t R = reads_.size();
         dUsedA_.reserve(std::max<size_t>(R, 1), true);
         dUsedB_.reserve(std::max<size_t>(R, 1), true);
-        std::vector<int> list(todo[0]);
-        list.insert(list.end(), todo[1].begin(), todo[1].end());
+        std::vector<int> list;
+        for (auto& v : todo) list.insert(list.end(), v.begin(), v.end());
         upload(dList_, list, stream_);
         const DevBatch B = View();
         size_t off = 0;
-        for (int p = 0; p < 2; ++p) {
+        int hcapOf[kPaths] = {0, 0, 0};
+        for (int p = 0; p < kPaths; ++p) {
             const int n = (int)todo[p].size();
             if (n == 0) continue;
             int maxI = 1, maxJ = 1;
@@ -449,13 +523,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.usedB = dUsedB_.ptr;
             F.readWords = (maxI + 7) / 8;
             F.tplWords = (maxJ + 8) / 8;
-            if (p == 0) {
-                F.hcap = kCoopNarrowRows;
-            } else {   // as tall as 64 KB of LDS allows (columns never exceed I + 1 rows)
-                const size_t rest = coop_group_bytes(0, F.readWords, F.tplWords);
-                const long long room = ((long long)kCoopLdsBytes - (long long)rest) / 16;
-                F.hcap = (int)std::min<long long>(std::max<long long>(64, room / 64 * 64), (maxI + 64) / 64 * 64);
-            }
+            F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
+            hcapOf[p] = F.hcap;
             F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);
             const int* lp = dList_.ptr + off;
             Timed(kKFill, [&] { launch_fill_coop(p == 0 ? 16 : 64, B, F, lp, n, stream_); });
@@ -471,19 +540,22 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         download(ua, dUsedA_, R, stream_);
         download(ub, dUsedB_, R, stream_);
         PBCCS_HIP(hipStreamSynchronize(stream_));
-        std::vector<int> next[2];
-        for (int p = 0; p < 2; ++p) {
+        std::vector<int> next[kPaths];
+        for (int p = 0; p < kPaths; ++p) {
             for (int r : todo[p]) {
                 HRead& h = reads_[r];
                 if (st[r] == kFillTall) {
-                    h.fillPath = p + 1;
-                    if (h.fillPath >= 2) serial.push_back(r);
-                    else next[1].push_back(r);
+                    // skip a path whose buffer would be no taller than the one that just failed
+                    int q = p + 1;
+                    if (q == 2 && hcapOf[1] > 0 && rows_for(2, (int)h.seq.size(), words(r)) <= hcapOf[1]) ++q;
+                    h.fillPath = q;
+                    if (q >= kPaths) serial.push_back(r);
+                    else next[q].push_back(r);
                     continue;
                 }
                 if (st[r] == kFillOverflow) {
                     const long long need = std::max(ua[r], ub[r]);
-                    h.valCap = std::max(need + need / 4 + 64, h.valCap + 1);
+                    h.valCap = std::max(need + need / 16 + 64, h.valCap + 1);
                     h.valA = valTop_;
                     h.valB = valTop_ + h.valCap;
                     valTop_ += 2 * h.valCap;
@@ -498,8 +570,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 if (st[r] == kFillOk || st[r] == kFillMismatch) done.push_back(r);
             }
         }
-        todo[0].swap(next[0]);
-        todo[1].swap(next[1]);
+        for (int p = 0; p < kPaths; ++p) todo[p].swap(next[p]);
     }
     if (!done.empty()) {
         upload(dList_, done, stream_);

@@ -78,6 +78,28 @@ struct DevVec {
     ~DevVec() { release(); }
 };
 
+// Band value pool: a large virtual-address reservation whose physical backing is mapped in 1 GB
+// granules as the batch's bands grow (hipMemAddressReserve / hipMemCreate / hipMemMap).  Growth never
+// copies and never needs old + new copies side by side, so several batches can keep tens of GB of bands
+// resident each.  Falls back to DevVec growth where the virtual-memory API is unavailable.
+struct VmPool {
+    double* ptr = nullptr;
+    size_t cap = 0;   // doubles mapped
+    void reserve(size_t n, bool keep);
+    ~VmPool();
+    VmPool() = default;
+    VmPool(const VmPool&) = delete;
+    VmPool& operator=(const VmPool&) = delete;
+private:
+    static constexpr size_t kVaBytes = 1ull << 39;      // 512 GB of address space
+    static constexpr size_t kChunkBytes = 1ull << 30;   // mapping granule
+    bool tried_ = false, vmm_ = false;
+    size_t mappedBytes_ = 0;
+    std::vector<hipMemGenericAllocationHandle_t> handles_;
+    std::vector<size_t> sizes_;
+    DevVec<double> fallback_;
+};
+
 struct Counters {   // work counters for the roofline report (bench.py)
     long long fillCells = 0, fillLaunches = 0;
     long long scoreTasks = 0, scoreLaunches = 0;
@@ -101,7 +123,7 @@ struct Workspace {
     DevVec<int2> aRange, bRange;
     DevVec<int> aOff, bOff;
     DevVec<double> aLs, bLs, aPre, bSuf;
-    DevVec<double> val;
+    VmPool val;
     // lane-interleaved fill scratch
     DevVec<double> fVal, fLs, fPre;
     DevVec<int2> fRange;
@@ -241,7 +263,7 @@ private:
     DevVec<double>& dBLs_;
     DevVec<double>& dAPre_;
     DevVec<double>& dBSuf_;
-    DevVec<double>& dVal_;
+    VmPool& dVal_;
     DevVec<int>& dCodes_;
     DevVec<int>& dPosOff_;
     DevVec<int>& dQv_;

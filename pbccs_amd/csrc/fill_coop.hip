@@ -21,6 +21,8 @@
 #include "arrow_device.hpp"
 #include "arrow_kernels.hpp"
 
+#include <stdexcept>
+
 namespace pbccs {
 namespace {
 
@@ -134,13 +136,22 @@ __device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide
     int prevCtx = kCtxZero;
     int curBase = T.TBase(0), curCtx = T.TCtx(0);
     double s = 0.0;   // 0.0 + L(0)
-    int2 gR = make_int2(0, 0), sR = make_int2(0, 0);
+    // ranges of the guide and of this matrix's previous pass, prefetched one G-column block ahead
+    // (a.R(jj) of a later block is read before this pass overwrites it)
+    int2 gR = make_int2(0, 0), sR = make_int2(0, 0), gN = make_int2(0, 0), sN = make_int2(0, 0);
+    {
+        const int jj = 1 + lane;
+        if (guide && jj < J) gN = guide->R(jj);
+        if (selfValid && jj < J) sN = a.R(jj);
+    }
     for (int j = 1; j < J; ++j) {
         const int jb = (j - 1) & (G - 1);
-        if (jb == 0) {   // ranges of columns [j, j + G): the guide's, and this matrix's previous ones
-            const int jj = j + lane;
-            if (guide) gR = (jj < J) ? guide->R(jj) : make_int2(0, 0);
-            if (selfValid) sR = (jj < J) ? a.R(jj) : make_int2(0, 0);
+        if (jb == 0) {
+            gR = gN;
+            sR = sN;
+            const int jj = j + G + lane;
+            if (guide && jj < J) gN = guide->R(jj);
+            if (selfValid && jj < J) sN = a.R(jj);
         }
         if (guide) {   // RangeGuide (SimpleRecursor.cpp:728-757)
             const int gx = T.g.bcast(gR.x, jb), gy = T.g.bcast(gR.y, jb);
@@ -273,13 +284,20 @@ __device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide
     long long used = 1;
     int hb = I, he = I;
     int nextBase = T.TBase(J - 1);
-    int2 gR = make_int2(0, 0), sR = make_int2(0, 0);
+    int2 gR = make_int2(0, 0), sR = make_int2(0, 0), gN = make_int2(0, 0), sN = make_int2(0, 0);
+    {
+        const int jj = J - 1 - lane;
+        if (guide && jj > 0) gN = guide->R(jj);
+        if (selfValid && jj > 0) sN = bm.R(jj);
+    }
     for (int j = J - 1; j > 0; --j) {
         const int jb = (J - 1 - j) & (G - 1);
-        if (jb == 0) {   // ranges of columns (j - G, j]
-            const int jj = j - lane;
-            if (guide) gR = (jj > 0) ? guide->R(jj) : make_int2(0, 0);
-            if (selfValid) sR = (jj > 0) ? bm.R(jj) : make_int2(0, 0);
+        if (jb == 0) {   // block of columns (j - G, j]; prefetch the next one
+            gR = gN;
+            sR = sN;
+            const int jj = j - G - lane;
+            if (guide && jj > 0) gN = guide->R(jj);
+            if (selfValid && jj > 0) sN = bm.R(jj);
         }
         const int curBase = T.TBase(j - 1), curCtx = T.TCtx(j - 1);
         if (guide) {
@@ -381,8 +399,17 @@ __device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide
         bm.O(0) = (int)used;
         bm.L(0) = ls;
         // accumulate(logScales, 0.0) in column order; lane 0 wrote every L(j) of this pass itself
+        // (loads batched 32 at a time so the serial adds, not the load latency, set the pace)
         s = s + ls;
-        for (int k = 1; k <= J; ++k) s = s + bm.L(k);
+        int k = 1;
+        for (; k + 31 <= J; k += 32) {
+            double v[32];
+#pragma unroll
+            for (int q = 0; q < 32; ++q) v[q] = bm.L(k + q);
+#pragma unroll
+            for (int q = 0; q < 32; ++q) s = s + v[q];
+        }
+        for (; k <= J; ++k) s = s + bm.L(k);
     }
     out.used = used + 1;
     out.last = v;
@@ -568,6 +595,7 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     if (n <= 0) return;
     const int per = 64 / G;
     const size_t lds = (size_t)per * F.groupBytes;
+    if (lds > 64 * 1024) throw std::runtime_error("fill block needs more than 64 KB of LDS");
     const dim3 grid((n + per - 1) / per);
     if (G == 16) hipLaunchKernelGGL(k_fill_coop<16>, grid, dim3(64), lds, s, B, F, reads, n);
     else hipLaunchKernelGGL(k_fill_coop<64>, grid, dim3(64), lds, s, B, F, reads, n);

@@ -102,6 +102,8 @@ SIGNATURES = {
     "pbccs_batch_create": (I, [P, ctypes.POINTER(CZmwInput), I, ctypes.POINTER(CPolishOptions), ctypes.POINTER(P)]),
     "pbccs_batch_polish": (I, [P, ctypes.POINTER(CZmwOutput)]),
     "pbccs_batch_destroy": (None, [P]),
+    "pbccs_batch_polish_many": (I, [ctypes.POINTER(P), I, ctypes.POINTER(ctypes.POINTER(CZmwOutput))]),
+    "pbccs_engine_set_concurrency": (I, [P, I]),
     "pbccs_engine_set_profiling": (I, [P, I]),
     "pbccs_engine_kernel_stats": (I, [P, ctypes.POINTER(CKernelStat), I, PI, I]),
 }

@@ -121,6 +121,16 @@ class PreparedBatch:
         self.close()
 
 
+def polish_many(batches):
+    """Polish several PreparedBatches of one engine concurrently (pbccs_batch_polish_many)."""
+    if not batches:
+        return
+    n = len(batches)
+    hs = (ctypes.c_void_p * n)(*[b._h.value for b in batches])
+    outs = (ctypes.POINTER(L.CZmwOutput) * n)(*[ctypes.cast(b._outs, ctypes.POINTER(L.CZmwOutput)) for b in batches])
+    L.check(batches[0]._lib.pbccs_batch_polish_many(hs, n, outs))
+
+
 def polish_zmws(zmws, settings=None, engine=None):
     """Polish ZMWs on the GPU (upload, hot path, download).
 
