@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=16, help="ZMWs polished by the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--streams", type=int, default=0,
-                    help="batches polished concurrently (0 = min(steps, 4)); each has its own HIP stream")
+                    help="batches polished concurrently (0 = min(steps, 8)); each has its own HIP stream")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
@@ -96,7 +96,7 @@ def main():
             torch.cuda.synchronize()
 
     eng = pbccs_amd.Engine(local)
-    streams = args.streams or max(1, min(args.steps, 4))
+    streams = args.streams or max(1, min(args.steps, 8))
     eng.set_concurrency(streams)
     if not args.no_profile:
         eng.set_profiling(True)   # HIP events on the engine stream + in-kernel algorithmic counters

@@ -1360,3 +1360,25 @@ extern "C" int orc_scorer_band_stats(void* h, int r, long long* aUsed, long long
     stats(rs.scorer->beta, bUsed, bMaxH);
     return 0;
 }
+
+// Diagnostics (test infrastructure): cells of read r's alpha band that are exactly zero, and cells whose
+// whole 64-row chunk (rows counted from each column's first used row) is zero.
+extern "C" int orc_scorer_band_zeros(void* h, int r, long long* zeros, long long* zeroChunkCells)
+{
+    MultiReadScorer* s = static_cast<MultiReadScorer*>(h);
+    const ReadState& rs = s->reads.at(r);
+    if (!rs.scorer) return -1;
+    const BandMatrix& m = rs.scorer->alpha;
+    *zeros = 0;
+    *zeroChunkCells = 0;
+    for (int j = 0; j < m.cols; ++j) {
+        for (int c0 = m.ub[j]; c0 < m.ue[j]; c0 += 64) {
+            const int c1 = std::min(c0 + 64, m.ue[j]);
+            int z = 0;
+            for (int i = c0; i < c1; ++i) z += (m.Get(i, j) == 0.0);
+            *zeros += z;
+            if (z == c1 - c0) *zeroChunkCells += z;
+        }
+    }
+    return 0;
+}

@@ -226,7 +226,7 @@ private:
     void TraceSummary(size_t n, int H, long long capSlots);
     void MeanVar(const HZmw& z, int strand, int ts, int te, double* mean, double* var) const;
     template <class F>
-    void Timed(KernelKind k, F&& launch);
+    void Timed(KernelKind k, F&& launch, hipStream_t st = nullptr);
     void ResolveEvents();
     // one scoring round on the device; codes==nullptr => device enumeration of all mutations
     void RunRound(const std::vector<int>& zmws, const std::vector<std::vector<int>>* codes, double fastThr,
@@ -234,6 +234,8 @@ private:
 
     int device_ = 0;
     hipStream_t stream_ = nullptr;
+    hipStream_t stream2_ = nullptr;      // second stream for the tall-band fill path
+    hipEvent_t evFork_ = nullptr, evJoin_ = nullptr;
     std::unique_ptr<Workspace> ownWs_;
     Workspace* ws_;
     std::vector<HZmw> zmws_;

@@ -183,10 +183,14 @@ __device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide
                 const double k = (i > 1) ? (rb == nextBase ? cBranch : cStick3) : 0.0;
                 const double d = (j > 1) ? left * pDel : 0.0;
                 double x = 0.0, up = carry;   // lane 0's `up` stays the carry: DPP leaves it untouched
+                // a chunk whose inputs are all exactly zero stays zero: skip its chain (bit-exact; common
+                // in the far rows of tall bands)
+                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0) {
 #pragma unroll
-                for (int q = 0; q < G; ++q) {
-                    up = shift_up<G>(x, up);
-                    x = (m + up * k) + d;
+                    for (int q = 0; q < G; ++q) {
+                        up = shift_up<G>(x, up);
+                        x = (m + up * k) + d;
+                    }
                 }
                 const double pm = fmax(mx, prefix_max<G>(x));
                 const double thr = pm / T.sdn;
@@ -329,10 +333,14 @@ __device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide
                 const double k = (i < I - 1 && i > 0) ? (same ? cBranch : cStick3) : 0.0;
                 const double d = (j < J - 1 && j > 0) ? left * cDel : 0.0;
                 double x = 0.0, up = carry;   // lane 0's `up` stays the carry: DPP leaves it untouched
+                // a chunk whose inputs are all exactly zero stays zero: skip its chain (bit-exact; common
+                // in the far rows of tall bands)
+                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0) {
 #pragma unroll
-                for (int q = 0; q < G; ++q) {
-                    up = shift_up<G>(x, up);
-                    x = (m + up * k) + d;
+                    for (int q = 0; q < G; ++q) {
+                        up = shift_up<G>(x, up);
+                        x = (m + up * k) + d;
+                    }
                 }
                 const double pm = fmax(mx, prefix_max<G>(x));
                 const double thr = pm / T.sdn;
