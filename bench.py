@@ -20,6 +20,10 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Every batch in flight polishes on its own HIP streams; with HIP's default of 4 hardware queues the
+# streams of different batches share queues and a long fill of one batch blocks the others' short
+# kernels.  Must be set before the HIP runtime initialises (measured: 634 -> 1180 ZMWs/s).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
@@ -35,7 +39,7 @@ def parse():
     ap.add_argument("--length", type=int, default=2000)
     ap.add_argument("--passes", type=int, default=10)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-sample", type=int, default=16, help="ZMWs polished by the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=192, help="ZMWs polished by the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--streams", type=int, default=0,
                     help="batches polished concurrently (0 = min(steps, 8)); each has its own HIP stream")

@@ -9,6 +9,11 @@ import ctypes
 import math
 import os
 
+# Batches in flight each polish on their own HIP streams; HIP's default of 4 hardware queues makes the
+# streams of different batches share queues (a long fill of one batch then blocks the others).  Takes
+# effect only if the HIP runtime has not been initialised yet in this process.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 from . import lib as _lib_mod
 from .lib import PbccsError, load
 

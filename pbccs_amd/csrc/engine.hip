@@ -250,6 +250,10 @@ void ArrowBatch::Prepare()
     dDelta_.reserve(std::max<long long>(delta, 1), false);
     dPosOff_.reserve(std::max<long long>(pos, 1), false);
     dQv_.reserve(std::max<long long>(pos, 1), false);
+    ws_->sel.reserve(std::max<long long>(mut, 1), false);
+    ws_->selScore.reserve(std::max<long long>(mut, 1), false);
+    ws_->selCode.reserve(std::max<long long>(mut, 1), false);
+    ws_->selCount.reserve(2, false);
     PBCCS_HIP(hipStreamSynchronize(stream_));
 }
 
@@ -1016,9 +1020,9 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
         for (size_t a = 0; a < act.size(); ++a) (*nTested)[idx[a]] += rNMut_[a];
 
         // favourable mutations, compacted on the device in list order
-        DevVec<long long> dSel;
-        DevVec<double> dSelScore;
-        DevVec<long long> dCount;
+        DevVec<long long>& dSel = ws_->sel;
+        DevVec<double>& dSelScore = ws_->selScore;
+        DevVec<long long>& dCount = ws_->selCount;
         dSel.reserve(std::max<long long>(rTotalMut_, 1), false);
         dSelScore.reserve(std::max<long long>(rTotalMut_, 1), false);
         dCount.reserve(2, false);
@@ -1028,7 +1032,7 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
                                                 (int)rTotalMut_, stream_));
         PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmpBytes2, dScore_.ptr, dFav_.ptr, dSelScore.ptr,
                                                 dCount.ptr + 1, (int)rTotalMut_, stream_));
-        DevVec<unsigned char> tmp;
+        DevVec<unsigned char>& tmp = ws_->selTmp;
         tmp.reserve(std::max<size_t>(std::max(tmpBytes, tmpBytes2), 1), false);
         PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tmpBytes, it, dFav_.ptr, dSel.ptr, dCount.ptr,
                                                 (int)rTotalMut_, stream_));
@@ -1044,7 +1048,7 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
         download(selScore, dSelScore, cnt[0], stream_);
         if (iter == 0) {
             // the enumerated codes live only on the device: select them too
-            DevVec<int> dSelCode;
+            DevVec<int>& dSelCode = ws_->selCode;
             dSelCode.reserve(std::max<long long>(cnt[0], 1), false);
             size_t tb = 0;
             PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,

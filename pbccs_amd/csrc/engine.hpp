@@ -135,6 +135,11 @@ struct Workspace {
     DevVec<double> scratch;
     DevVec<unsigned long long> scratchTop;
     DevVec<int> scratchOverflow;
+    // favourable-mutation selection (persistent: a per-round hipFree would synchronise the whole device)
+    DevVec<long long> sel, selCount;
+    DevVec<double> selScore;
+    DevVec<int> selCode;
+    DevVec<unsigned char> selTmp;
 };
 
 class ArrowBatch {
