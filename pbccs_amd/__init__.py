@@ -12,7 +12,8 @@ import os
 # Batches in flight each polish on their own HIP streams; HIP's default of 4 hardware queues makes the
 # streams of different batches share queues (a long fill of one batch then blocks the others).  Takes
 # effect only if the HIP runtime has not been initialised yet in this process.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export HIP's default (4)
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 from . import lib as _lib_mod
 from .lib import PbccsError, load

@@ -30,7 +30,7 @@ struct pbccs_engine {
     std::vector<std::unique_ptr<Workspace>> slots;
     Workspace* Slot(int s)
     {
-        while ((int)slots.size() <= s) slots.emplace_back(new Workspace());
+        while ((int)slots.size() <= s) slots.emplace_back(new Workspace(true));
         return slots[s].get();
     }
 };

@@ -56,7 +56,7 @@ void download(std::vector<T>& h, const DevVec<T>& d, size_t n, hipStream_t s)
 void VmPool::reserve(size_t n, bool keep)
 {
     if (n <= cap) return;
-    if (!tried_) {
+    if (!tried_ && allowVmm) {
         tried_ = true;
         void* va = nullptr;
         vmm_ = hipMemAddressReserve(&va, kVaBytes, 0, nullptr, 0) == hipSuccess && va != nullptr;

@@ -85,6 +85,7 @@ struct DevVec {
 struct VmPool {
     double* ptr = nullptr;
     size_t cap = 0;   // doubles mapped
+    bool allowVmm = false;   // only long-lived engine workspaces map 1 GB granules; scorers use hipMalloc
     void reserve(size_t n, bool keep);
     ~VmPool();
     VmPool() = default;
@@ -119,6 +120,7 @@ struct KernelStat {
 // Large device pools.  A batch either owns one (fine-grained scorers) or borrows its engine's (batch
 // polish): batches polish one after another, so they stream through one resident workspace.
 struct Workspace {
+    explicit Workspace(bool vmm = false) { val.allowVmm = vmm; }
     // per-read compact bands (what scoring reads)
     DevVec<int2> aRange, bRange;
     DevVec<int> aOff, bOff;

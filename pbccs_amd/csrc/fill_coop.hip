@@ -112,6 +112,7 @@ struct PassOut {
     double last;      // alpha(I, J) or beta(0, 0)
     double sumL;      // accumulate(logScales, 0.0) left to right
     bool tall;        // a column exceeded the LDS buffer
+    bool changed;     // some column's [begin, end) differs from the previous pass of this matrix
 };
 
 // ---- FillAlpha (SimpleRecursor.cpp:60-181) --------------------------------------------------------
@@ -119,7 +120,7 @@ template <int G>
 __device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide, bool selfValid, bool& ovf)
 {
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0.0, 0.0, false};
+    PassOut out{0, 0.0, 0.0, false, !selfValid};
     if (a.cap < 1) ovf = true;
     if (lane == 0) {
         if (!ovf) a.V(0) = 1.0;
@@ -157,8 +158,10 @@ __device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide
             const int gx = T.g.bcast(gR.x, jb), gy = T.g.bcast(gR.y, jb);
             if (gx < gy) { hb = min(gx, hb); he = max(gy, he); }
         }
+        int sx = 0, sy = 0;
         if (selfValid) {
-            const int sx = T.g.bcast(sR.x, jb), sy = T.g.bcast(sR.y, jb);
+            sx = T.g.bcast(sR.x, jb);
+            sy = T.g.bcast(sR.y, jb);
             if (sx < sy) { hb = min(sx, hb); he = max(sy, he); }
         }
         const int reqEnd = min(I, he);
@@ -229,6 +232,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide
             }
         }
         if (used + (e - b) > a.cap) ovf = true;
+        out.changed = out.changed || b != sx || e != sy;
         const double lsj = scale ? log(mx) : 0.0;
         if (lane == 0) {
             a.R(j) = make_int2(b, e);
@@ -272,7 +276,7 @@ template <int G>
 __device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide, bool selfValid, bool& ovf)
 {
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0.0, 0.0, false};
+    PassOut out{0, 0.0, 0.0, false, !selfValid};
     if (bm.cap < 1) ovf = true;
     if (lane == 0) {
         if (!ovf) bm.V(0) = 1.0;
@@ -308,8 +312,10 @@ __device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide
             const int gx = T.g.bcast(gR.x, jb), gy = T.g.bcast(gR.y, jb);
             if (gx < gy) { hb = min(gx, hb); he = max(gy, he); }
         }
+        int sx = 0, sy = 0;
         if (selfValid) {
-            const int sx = T.g.bcast(sR.x, jb), sy = T.g.bcast(sR.y, jb);
+            sx = T.g.bcast(sR.x, jb);
+            sy = T.g.bcast(sR.y, jb);
             if (sx < sy) { hb = min(sx, hb); he = max(sy, he); }
         }
         const int reqBegin = max(0, hb);
@@ -378,6 +384,7 @@ __device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide
             }
         }
         if (used + (e - b) > bm.cap) ovf = true;
+        out.changed = out.changed || b != sx || e != sy;
         const double lsj = scale ? log(mx) : 0.0;
         if (lane == 0) {
             bm.R(j) = make_int2(b, e);
@@ -553,22 +560,35 @@ __global__ void __launch_bounds__(64) k_fill_coop(DevBatch B, CoopFill F, const 
     double bv = log(pb.last) + pb.sumL;
     // NB: alphaV / betaV are not re-evaluated inside the loop (SimpleRecursor.cpp:667-679)
     const bool mismatched = fabs(av - bv) > kAlphaBetaTol;
+    // Flip-flop fixed point: a pass depends only on the band ranges of the other matrix (guide) and of
+    // its own previous pass (hint), never on previous values.  Once an alpha pass and the beta pass after
+    // it both reproduce their predecessors' ranges, every later pass repeats them bit for bit, so the
+    // remaining flip-flops are skipped and only the count the reference reports is kept.
+    int unchanged = 0;
     while (mismatched && flips <= kMaxFlipFlops) {
+        bool changed;
         if (flips % 2 == 0) {
             pa = coop_alpha<G>(T, a, &bm, true, ovf);
             if (pa.tall) return fail_tall();
             needA = max(needA, pa.used);
             cells += pa.used;
             ua = pa.used;
+            changed = pa.changed;
         } else {
             pb = coop_beta<G>(T, bm, &a, true, ovf);
             if (pb.tall) return fail_tall();
             needB = max(needB, pb.used);
             cells += pb.used;
             ub = pb.used;
+            changed = pb.changed;
         }
         passes += 1;
         ++flips;
+        unchanged = changed ? 0 : unchanged + 1;
+        if (unchanged >= 2) {
+            flips = kMaxFlipFlops + 1;
+            break;
+        }
     }
     av = log(pa.last) + pa.sumL;
     bv = log(pb.last) + pb.sumL;

@@ -172,3 +172,31 @@ def test_zmw6251_reference_record_on_gpu(P):
     assert abs(r["predicted_accuracy"] - e["pred_acc"]) < tol["pred_acc"]
     o = O.polish_zmw(z["draft"], z["reads"], z["snr"], z["min_zscore"])
     assert r["consensus"] == o["template"]
+
+
+def test_fills_2kb_match_oracle(P):
+    """Full-size (configs[1]) fills: per-read LL and flip-flop counts, including the reads whose first
+    band explodes past 4% of the matrix (the 5-pass reband path, ~one read per ZMW at 2 kb) and the
+    6-flip-flop reads whose trailing passes the engine skips at the band fixed point."""
+    from pbccs_amd import synth
+    zs = synth.make_zmws(3, 2000, 10, seed=61)
+    for z in zs:
+        g, o, rg, ro = _scorers(P, z["draft"], z["reads"])
+        assert rg == ro
+        assert g.NumFlipFlops() == [o.read_info(k)["flipflops"] for k in range(len(z["reads"]))]
+        for x, y in zip(g.BaselineScores(), [o.read_info(k)["ll"] for k in range(len(z["reads"]))]):
+            assert _close(x, y, 1e-12, 1e-12)
+
+
+def test_polish_2kb_batch_matches_oracle(P):
+    """configs[1] ZMWs (2 kb insert, 10 passes) through the batch entry point: bit-exact consensus,
+    nTested/nApplied and AddRead results; QVs within +-1."""
+    from pbccs_amd import synth
+    zs = synth.make_zmws(6, 2000, 10, seed=71)
+    res = P.polish_zmws(zs)
+    for z, r in zip(zs, res):
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+        assert r["add_read_results"] == e["add_read_results"]
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        assert r["consensus"] == e["template"]
+        assert max(abs(a - b) for a, b in zip(r["qvs"], e["qvs"])) <= 1
