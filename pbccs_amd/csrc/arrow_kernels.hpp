@@ -55,6 +55,9 @@ struct CoopFill {
     int readWords = 0;       // nibble-packed read words per group (>= ceil(I / 8) of every read)
     int tplWords = 0;        // nibble-packed template words per group (>= ceil((J + 1) / 8))
     size_t groupBytes = 0;   // coop_group_bytes(hcap, readWords, tplWords)
+    unsigned long long* chainStats = nullptr;   // diagnostics (PBCCS_CHAIN_STATS): [chunks, sweeps, cycles, stops]
+    bool jacobi = false;     // G = 64 chain by Jacobi sweeps (see fill_coop.hip)
+    bool prio = true;        // G = 64 waves at raised issue priority
 };
 size_t coop_group_bytes(int hcap, int readWords, int tplWords);
 void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* reads, int n, hipStream_t s);

@@ -490,7 +490,7 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
         ro.mutationNeighborhood = o.refine.mutation_neighborhood;
         std::vector<int> conv;
         std::vector<long long> nt, na;
-        B.Refine(refineZ, ro, &conv, &nt, &na);
+        B.Refine(refineZ, ro, &conv, &nt, &na, false);
         std::vector<int> qvZ, qvIdx;
         for (size_t k = 0; k < refineZ.size(); ++k) {
             pbccs_zmw_output& q = out[refineIdx[k]];

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <numeric>
 #include <stdexcept>
+#include <chrono>
 #include <unordered_set>
 
 namespace pbccs {
@@ -204,6 +205,14 @@ void ArrowBatch::ResolveEvents()
 void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
 {
     ResolveEvents();
+    if (chainInit_) {
+        unsigned long long c[4];
+        PBCCS_HIP(hipMemcpyAsync(c, dChain_.ptr, sizeof(c), hipMemcpyDeviceToHost, stream_));
+        PBCCS_HIP(hipStreamSynchronize(stream_));
+        std::fprintf(stderr, "[chain64] chunks=%llu sweeps/chunk=%.2f cycles/sweep=%.1f stop-exits=%.3f\n", c[0],
+                     c[0] ? (double)c[1] / c[0] : 0.0, c[1] ? (double)c[2] / c[1] : 0.0, c[0] ? (double)c[3] / c[0] : 0.0);
+        PBCCS_HIP(hipMemsetAsync(dChain_.ptr, 0, sizeof(c), stream_));
+    }
     if (profiling_) {
         unsigned long long h[16];
         PBCCS_HIP(hipMemcpyAsync(h, dStats_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
@@ -254,6 +263,17 @@ void ArrowBatch::Prepare()
     ws_->selScore.reserve(std::max<long long>(mut, 1), false);
     ws_->selCode.reserve(std::max<long long>(mut, 1), false);
     ws_->selCount.reserve(2, false);
+    {   // hipCUB temp storage of the refine rounds' selections (a later growth would synchronise the device)
+        size_t a = 0, b = 0, c = 0;
+        const int nm = (int)std::min<long long>(std::max<long long>(mut, 1), INT_MAX);
+        hipcub::CountingInputIterator<long long> it(0);
+        PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, a, it, dFav_.ptr, ws_->sel.ptr, ws_->selCount.ptr, nm, stream_));
+        PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, b, dScore_.ptr, dFav_.ptr, ws_->selScore.ptr,
+                                                ws_->selCount.ptr + 1, nm, stream_));
+        PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, c, dCodes_.ptr, dFav_.ptr, ws_->selCode.ptr,
+                                                ws_->selCount.ptr + 1, nm, stream_));
+        ws_->selTmp.reserve(std::max<size_t>(std::max(a, std::max(b, c)), 1), false);
+    }
     PBCCS_HIP(hipStreamSynchronize(stream_));
 }
 
@@ -523,8 +543,13 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         size_t off = 0;
         int hcapOf[kPaths] = {0, 0, 0};
         // the 64-lane (tall) launches run on a second stream beside the 16-lane one: a round's latency
-        // is then the slower of the two, not their sum
-        bool forked = false;
+        // is then the slower of the two, not their sum.  Fork before the first launch (after the list
+        // upload), so the tall fills do not wait for the 16-lane fill.
+        const bool forked = !todo[1].empty() || !todo[2].empty();
+        if (forked) {
+            PBCCS_HIP(hipEventRecord(evFork_, stream_));
+            PBCCS_HIP(hipStreamWaitEvent(stream2_, evFork_, 0));
+        }
         for (int p = 0; p < kPaths; ++p) {
             const int n = (int)todo[p].size();
             if (n == 0) continue;
@@ -541,16 +566,25 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
             hcapOf[p] = F.hcap;
             F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);
-            const int* lp = dList_.ptr + off;
-            hipStream_t st = stream_;
-            if (p > 0) {
-                if (!forked) {
-                    PBCCS_HIP(hipEventRecord(evFork_, stream_));
-                    PBCCS_HIP(hipStreamWaitEvent(stream2_, evFork_, 0));
-                    forked = true;
+            static const bool chainStats = std::getenv("PBCCS_CHAIN_STATS") != nullptr;
+            static const char* chainMode = std::getenv("PBCCS_CHAIN_MODE");   // "serial" | "jacobi"
+            static const char* prioEnv = std::getenv("PBCCS_TALL_PRIO");      // "0" disables
+            // Jacobi sweeps cut a tall chunk's latency but not its instruction count: use them when the
+            // launch is latency-bound (few tall reads, e.g. a batch's convergence tail), serial steps when
+            // the tall fills compete for issue slots with a full device.
+            static const int jacobiMax = std::getenv("PBCCS_JACOBI_MAX") ? std::atoi(std::getenv("PBCCS_JACOBI_MAX")) : 64;
+            F.jacobi = chainMode ? std::strcmp(chainMode, "jacobi") == 0 : (p > 0 && n <= jacobiMax);
+            F.prio = !(prioEnv && std::strcmp(prioEnv, "0") == 0);
+            if (chainStats && p > 0) {
+                dChain_.reserve(4, false);
+                if (!chainInit_) {
+                    PBCCS_HIP(hipMemsetAsync(dChain_.ptr, 0, 4 * sizeof(unsigned long long), stream_));
+                    chainInit_ = true;
                 }
-                st = stream2_;
+                F.chainStats = dChain_.ptr;
             }
+            const int* lp = dList_.ptr + off;
+            const hipStream_t st = (p > 0) ? stream2_ : stream_;
             Timed(kKFill, [&] { launch_fill_coop(p == 0 ? 16 : 64, B, F, lp, n, st); }, st);
             PBCCS_HIP(hipGetLastError());
             counters_.fillLaunches += 1;
@@ -993,7 +1027,7 @@ std::vector<Scored> best_subset(std::vector<Scored> in, int sep)   // Consensus-
 }  // namespace
 
 void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std::vector<int>* converged,
-                        std::vector<long long>* nTested, std::vector<long long>* nApplied)
+                        std::vector<long long>* nTested, std::vector<long long>* nApplied, bool needFinalState)
 {
     const int n = (int)zl.size();
     converged->assign(n, 0);
@@ -1002,14 +1036,150 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
     std::vector<char> done(n, 0);
     std::vector<std::unordered_set<std::string>> history(n);
     std::vector<std::vector<int>> centers(n);
+    std::vector<int> zit(n, 0);   // per-ZMW iteration of AbstractRefineConsensus
+    // Iteration memo (replay of the reference's non-converging tails).
+    //   An iteration's scoring outcome (the favourable list with its float scores) is a function of the
+    //   loop state entering it, *relative* to the leftmost read window start a: the template from a - 1
+    //   on (window bases plus the context base before a, which the reverse strand reads), the windows and
+    //   active flags relative to a, and the previous favourable positions relative to a.  Template bases
+    //   left of a - 1 are never read by a fill or scored by a read.  When the state entering iteration i
+    //   equals (relative) the state entering iteration i - p, iteration i repeats iteration i - p's
+    //   favourable list shifted by the change of a: the host then replays the iteration exactly -- nTested
+    //   from the enumeration of the real template, BestSubset, the cycle check against the real history,
+    //   ApplyMutations and the window remap -- with no fills and no scoring, and keeps going while the
+    //   states keep matching.  This covers the two NonConvergent shapes seen at 2 kb: period-2
+    //   oscillations and period-1 "crawls" that insert one base before the windows per iteration.
+    struct Memo {
+        int anchor = 0;
+        std::string rtpl;
+        std::vector<int> rwin;   // per read: ts - a, te - a, active
+        std::vector<int> rcen;
+        std::vector<Scored> fav;
+        bool same(const Memo& o) const { return rtpl == o.rtpl && rwin == o.rwin && rcen == o.rcen; }
+    };
+    std::vector<std::vector<Memo>> memo(n);
+    static const bool noReplay = std::getenv("PBCCS_NO_CYCLE_REPLAY") != nullptr;
+    constexpr int kMaxPeriod = 4;
+    auto make_memo = [&](int k) {
+        const HZmw& z = zmws_[zl[k]];
+        Memo m;
+        int a = (int)z.tpl.size();
+        for (int q = 0; q < z.nReads; ++q) a = std::min(a, reads_[z.readBegin + q].ts);
+        m.anchor = a;
+        m.rtpl = z.tpl.substr(std::max(0, a - 1));
+        for (int q = 0; q < z.nReads; ++q) {
+            const HRead& r = reads_[z.readBegin + q];
+            m.rwin.push_back(r.ts - a);
+            m.rwin.push_back(r.te - a);
+            m.rwin.push_back(r.active ? 1 : 0);
+        }
+        for (int c : centers[k]) m.rcen.push_back(c - a);
+        return m;
+    };
+    auto match = [&](int k, const Memo& cur) -> int {   // period p of a matching earlier state, or 0
+        const int i = zit[k];
+        for (int p = 1; p <= kMaxPeriod && p <= i; ++p)
+            if (cur.same(memo[k][i - p])) return p;
+        return 0;
+    };
     const double fastThr = zl.empty() ? -12.5 : zmws_[zl[0]].opt.fastScoreThreshold;
-    for (int iter = 0; iter < ro.maxIterations; ++iter) {
+    // PBCCS_ROUND_TRACE=1: one stderr line per round (active ZMWs, refilled reads, phase wall times)
+    static const bool roundTrace = std::getenv("PBCCS_ROUND_TRACE") != nullptr;
+    using Clock = std::chrono::steady_clock;
+    auto ms = [](Clock::time_point a, Clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    std::vector<int> finalRefill;
+    long long replayed = 0;
+    for (int round = 0;; ++round) {
+        const Clock::time_point t0 = Clock::now();
+        // ---- memo: record the state entering each ZMW's iteration; replay matching iterations on the host
+        std::vector<int> preRefill;
+        for (int k = 0; k < n; ++k) {
+            if (done[k]) continue;
+            Memo cur = make_memo(k);
+            int p = (noReplay || zit[k] == 0) ? 0 : match(k, cur);
+            if (p == 0) {
+                memo[k].push_back(std::move(cur));
+                continue;
+            }
+            HZmw& z = zmws_[zl[k]];
+            bool ended = false;
+            while (p > 0) {
+                const int i = zit[k];
+                memo[k].push_back(std::move(cur));   // memo[k][i]: the state entering this iteration
+                const int shift = memo[k][i].anchor - memo[k][i - p].anchor;
+                std::vector<Scored> fav;
+                for (const Scored& f : memo[k][i - p].fav)
+                    fav.push_back({mut_code(mut_pos(f.code) + shift, mut_type(f.code), mut_base(f.code)), f.score});
+                memo[k][i].fav = fav;
+                // active flags after the refill = those the memoised transition's refill produced
+                // (memo[k][i - p + 1] is memo[k][i] itself when p = 1)
+                std::vector<char> succActive(z.nReads);
+                for (int q = 0; q < z.nReads; ++q) succActive[q] = memo[k][i - p + 1].rwin[3 * q + 2] != 0;
+                std::vector<int> tried;
+                nearby_mutations(z.tpl, centers[k], ro.mutationNeighborhood, &tried);
+                (*nTested)[k] += (long long)tried.size();
+                std::vector<Scored> best = best_subset(fav, ro.mutationSeparation);
+                std::vector<Mutation> muts;
+                for (const Scored& b : best) muts.push_back(mutation_from_code(b.code));
+                if (best.size() > 1) {
+                    std::string next;
+                    std::vector<int> mtp;
+                    if (apply_mutations(z.tpl, muts, &next, &mtp) && history[k].count(next)) {
+                        best.resize(1);
+                        muts.resize(1);
+                    }
+                }
+                (*nApplied)[k] += (long long)best.size();
+                history[k].insert(z.tpl);
+                centers[k].clear();
+                for (const Scored& f : fav) centers[k].push_back(mut_pos(f.code));
+                std::vector<int> mtp;
+                if (!apply_host(&z.tpl, muts, &mtp)) {
+                    done[k] = 1;
+                    converged->at(k) = -1;
+                    ended = true;
+                    break;
+                }
+                for (int q = 0; q < z.nReads; ++q) {   // refill outcome = the memoised transition's
+                    HRead& r = reads_[z.readBegin + q];
+                    r.ts = mtp[r.ts];
+                    r.te = mtp[r.te];
+                    r.active = succActive[q] != 0;
+                }
+                ++replayed;
+                if (++zit[k] >= ro.maxIterations) {
+                    done[k] = 1;   // NonConvergent
+                    ended = true;
+                    break;
+                }
+                cur = make_memo(k);
+                p = match(k, cur);
+            }
+            UploadTemplate(zl[k]);
+            descDirty_ = true;
+            if (!ended) memo[k].push_back(std::move(cur));   // a real iteration follows from this state
+            std::vector<int>& dst = ended ? finalRefill : preRefill;
+            if (ended && !needFinalState) continue;
+            for (int q = 0; q < z.nReads; ++q)
+                if (reads_[z.readBegin + q].active) {
+                    EnsureCapacity(z.readBegin + q);
+                    dst.push_back(z.readBegin + q);
+                }
+        }
+        if (!preRefill.empty()) {
+            FillReads(preRefill);
+            for (int r : preRefill)
+                if (reads_[r].status != kFillOk) reads_[r].active = false;
+            descDirty_ = true;
+        }
         std::vector<int> act, idx;
         for (int k = 0; k < n; ++k)
             if (!done[k]) { act.push_back(zl[k]); idx.push_back(k); }
         if (act.empty()) break;
         std::vector<std::vector<int>> lists;
-        if (iter == 0) {
+        if (round == 0) {
             RunRound(act, nullptr, fastThr, false);
         } else {
             lists.resize(act.size());
@@ -1018,6 +1188,7 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
             RunRound(act, &lists, fastThr, false);
         }
         for (size_t a = 0; a < act.size(); ++a) (*nTested)[idx[a]] += rNMut_[a];
+        const Clock::time_point t1 = Clock::now();
 
         // favourable mutations, compacted on the device in list order
         DevVec<long long>& dSel = ws_->sel;
@@ -1046,7 +1217,7 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
         std::vector<int> selCode;
         download(sel, dSel, cnt[0], stream_);
         download(selScore, dSelScore, cnt[0], stream_);
-        if (iter == 0) {
+        if (round == 0) {
             // the enumerated codes live only on the device: select them too
             DevVec<int>& dSelCode = ws_->selCode;
             dSelCode.reserve(std::max<long long>(cnt[0], 1), false);
@@ -1066,13 +1237,14 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
             const long long g = sel[q];
             const size_t a = std::upper_bound(rMutStart_.begin(), rMutStart_.end(), g) - rMutStart_.begin() - 1;
             const long long m = g - rMutStart_[a];
-            const int code = (iter == 0) ? selCode[q] : lists[a][m];
+            const int code = (round == 0) ? selCode[q] : lists[a][m];
             fav[a].push_back({code, (float)selScore[q]});
         }
         std::vector<int> changed;
         for (size_t a = 0; a < act.size(); ++a) {
             const int k = idx[a];
             const int zi = act[a];
+            memo[k].back().fav = fav[a];
             if (fav[a].empty()) {
                 converged->at(k) = 1;
                 done[k] = 1;
@@ -1111,15 +1283,29 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
                     changed.push_back(z.readBegin + q);
                 }
             }
-            if (iter + 1 >= ro.maxIterations) done[k] = 1;   // NonConvergent
+            if (++zit[k] >= ro.maxIterations) done[k] = 1;   // NonConvergent
         }
         descDirty_ = true;
+        const Clock::time_point t2 = Clock::now();
         if (!changed.empty()) {
             FillReads(changed);
             for (int r : changed)
                 if (reads_[r].status != kFillOk) reads_[r].active = false;
             descDirty_ = true;
         }
+        if (roundTrace) {
+            const Clock::time_point t3 = Clock::now();
+            std::fprintf(stderr, "[round] batch=%p round=%d zmws=%zu muts=%lld refill=%zu prerefill=%zu replayed=%lld "
+                                 "score=%.1fms select=%.1fms fill=%.1fms\n",
+                         (void*)this, round, act.size(), rTotalMut_, changed.size(), preRefill.size(), replayed,
+                         ms(t0, t1), ms(t1, t2), ms(t2, t3));
+        }
+    }
+    if (!finalRefill.empty()) {   // the scorer API observes the final state: give replayed ZMWs their bands
+        FillReads(finalRefill);
+        for (int r : finalRefill)
+            if (reads_[r].status != kFillOk) reads_[r].active = false;
+        descDirty_ = true;
     }
 }
 

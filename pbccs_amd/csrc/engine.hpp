@@ -167,8 +167,10 @@ public:
     void ScoreLists(const std::vector<int>& zmws, const std::vector<std::vector<int>>& codes, double fastThr,
                     std::vector<std::vector<double>>* scores, std::vector<std::vector<double>>* perRead = nullptr);
     // RefineConsensus for the listed ZMWs (all in lock-step rounds).
+    // needFinalState = false: ZMWs that end NonConvergent may be left without the bands of their final
+    // template (the batch polish never reads them).
     void Refine(const std::vector<int>& zmws, const RefineOptions& ro, std::vector<int>* converged,
-                std::vector<long long>* nTested, std::vector<long long>* nApplied);
+                std::vector<long long>* nTested, std::vector<long long>* nApplied, bool needFinalState = true);
     // ConsensusQVs for the listed ZMWs.
     void QVs(const std::vector<int>& zmws, std::vector<std::vector<int>>* qvs);
     // ApplyMutations (MultiReadMutationScorer.cpp:235-267).  Returns false on an invalid edit.
@@ -294,6 +296,8 @@ private:
     bool profiling_ = false;
     DevVec<unsigned long long> dStats_;
     DevVec<long long> dTrace_;   // PBCCS_FILL_TRACE diagnostics
+    DevVec<unsigned long long> dChain_;   // PBCCS_CHAIN_STATS diagnostics
+    bool chainInit_ = false;
     struct Pending {
         int kind;
         hipEvent_t a, b;

@@ -87,6 +87,70 @@ struct Group {
     __device__ __forceinline__ int bcast(int x, int src) const { return __shfl(x, src, G); }
 };
 
+// The in-column insertion chain x_i = (m_i + x_{i-1} k_i) + d_i over the G rows of a chunk (lane l = row
+// l; lane 0's predecessor is `carry`), in the reference's operation order (SimpleRecursor.cpp:117-150).
+//  G = 16: G serial shift-by-one DPP steps; after step q lanes <= q hold their final value.
+//  G = 64: Jacobi sweeps -- every lane recomputes its row from its neighbour's current value at once.
+//          Lanes below `exact` hold the serial result: each sweep extends that prefix by one lane, and
+//          a prefix of lanes whose bits did not move in a sweep satisfies the recurrence from `carry`,
+//          whose solution is unique, so it IS the serial result bit for bit.  Influence decays along
+//          the chain (k_i << 1), so inside a tall band the prefix jumps to the whole chunk after ~7
+//          sweeps instead of 64 serial steps.  Rows past the band end decay without damping relative to
+//          themselves and would settle only one per sweep; they are never stored, so the sweeps stop as
+//          soon as the band-end row (`stop_bits`, checked every 4 sweeps) lies inside the exact prefix.
+//          At most G sweeps in any case.
+template <int G, class StopBits>
+__device__ __forceinline__ double insertion_chain(const Group<G>& g, double m, double k, double d, double carry,
+                                                  StopBits stop_bits, bool jacobi, unsigned long long* dbg)
+{
+    if constexpr (G == 64) {
+        if (jacobi) {
+            const long long c0 = dbg ? clock64() : 0;
+            double x = m + d;
+            int exact = 0, q = 0;
+            bool stopped = false;
+            // blocks of 4 sweeps with one convergence test each (a VALU -> SALU round trip per test)
+            while (q < G) {
+                double prev = x;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    prev = x;
+                    x = (m + shift_up<G>(x, carry) * k) + d;
+                }
+                q += 4;
+                // lanes that did not move in the last sweep form a fixed-point prefix
+                const unsigned long long moved = g.bits(__double_as_longlong(x) != __double_as_longlong(prev));
+                exact = max(exact + 4, moved ? __ffsll((long long)moved) - 1 : G);
+                if (exact >= G) break;
+                if ((q & 7) == 0) {
+                    const unsigned long long st = stop_bits(x);
+                    if (st && __ffsll((long long)st) - 1 < exact) {
+                        stopped = true;
+                        break;
+                    }
+                }
+            }
+            if (dbg && g.lane == 0) {
+                atomicAdd(dbg + 0, 1ull);
+                atomicAdd(dbg + 1, (unsigned long long)q);
+                atomicAdd(dbg + 2, (unsigned long long)(clock64() - c0));
+                atomicAdd(dbg + 3, stopped ? 1ull : 0ull);
+            }
+            return x;
+        }
+    }
+    (void)stop_bits;
+    (void)jacobi;
+    (void)dbg;
+    double x = 0.0, up = carry;   // lane 0's `up` stays the carry: DPP leaves it untouched
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+        up = shift_up<G>(x, up);
+        x = (m + up * k) + d;
+    }
+    return x;
+}
+
 // Everything a group needs about its read (group-uniform values) + LDS views.
 template <int G>
 struct Task {
@@ -98,6 +162,8 @@ struct Task {
     double* col0;
     double* col1;
     int hcap;              // rows per LDS column buffer
+    unsigned long long* dbg;   // chain diagnostics (nullptr: off)
+    bool jacobi;               // G = 64: Jacobi sweeps instead of 64 serial DPP steps
     double prNot, prThird, sdn;
 
     __device__ __forceinline__ int TBase(int idx) const { return nib(tpW, idx); }
@@ -185,16 +251,15 @@ __device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide
                 const double m = (i == 1 && j == 1) ? mpe : ((i != 1 && j != 1) ? mpe * pMatch : 0.0);
                 const double k = (i > 1) ? (rb == nextBase ? cBranch : cStick3) : 0.0;
                 const double d = (j > 1) ? left * pDel : 0.0;
-                double x = 0.0, up = carry;   // lane 0's `up` stays the carry: DPP leaves it untouched
+                double x = 0.0;
                 // a chunk whose inputs are all exactly zero stays zero: skip its chain (bit-exact; common
                 // in the far rows of tall bands)
-                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0) {
-#pragma unroll
-                    for (int q = 0; q < G; ++q) {
-                        up = shift_up<G>(x, up);
-                        x = (m + up * k) + d;
-                    }
-                }
+                auto stop_bits = [&](double xv) {   // the reference loop's continue test (:110-112), per row
+                    const double pmv = fmax(mx, prefix_max<G>(xv));
+                    return T.g.bits(!((i + 1 < I) && (xv >= pmv / T.sdn || i + 1 < reqEnd)));
+                };
+                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0)
+                    x = insertion_chain<G>(T.g, m, k, d, carry, stop_bits, T.jacobi, T.dbg);
                 const double pm = fmax(mx, prefix_max<G>(x));
                 const double thr = pm / T.sdn;
                 const bool cont = (i + 1 < I) && (x >= thr || i + 1 < reqEnd);
@@ -338,16 +403,15 @@ __device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide
                 const double m = (i < I - 1) ? mpe * cMatch : ((i == I - 1 && j == J - 1) ? mpe : 0.0);
                 const double k = (i < I - 1 && i > 0) ? (same ? cBranch : cStick3) : 0.0;
                 const double d = (j < J - 1 && j > 0) ? left * cDel : 0.0;
-                double x = 0.0, up = carry;   // lane 0's `up` stays the carry: DPP leaves it untouched
+                double x = 0.0;
                 // a chunk whose inputs are all exactly zero stays zero: skip its chain (bit-exact; common
                 // in the far rows of tall bands)
-                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0) {
-#pragma unroll
-                    for (int q = 0; q < G; ++q) {
-                        up = shift_up<G>(x, up);
-                        x = (m + up * k) + d;
-                    }
-                }
+                auto stop_bits = [&](double xv) {   // the reference loop's continue test (:227-229), per row
+                    const double pmv = fmax(mx, prefix_max<G>(xv));
+                    return T.g.bits(!((i - 1 > 0) && (xv >= pmv / T.sdn || i - 1 >= reqBegin)));
+                };
+                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0)
+                    x = insertion_chain<G>(T.g, m, k, d, carry, stop_bits, T.jacobi, T.dbg);
                 const double pm = fmax(mx, prefix_max<G>(x));
                 const double thr = pm / T.sdn;
                 const bool cont = (i - 1 > 0) && (x >= thr || i - 1 >= reqBegin);
@@ -443,6 +507,9 @@ template <int G>
 __global__ void __launch_bounds__(64) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
 {
     extern __shared__ __align__(16) unsigned char smem[];
+    // tall reads are the latency-critical path of every refine round: issue ahead of the 16-lane fills
+    // and score waves that share the SIMD (F.prio = 0 leaves the default priority)
+    if (G == 64 && F.prio) __builtin_amdgcn_s_setprio(3);
     const int grp = threadIdx.x / G;
     const int t = blockIdx.x * (64 / G) + grp;
     const int lane = threadIdx.x & (G - 1);
@@ -506,6 +573,8 @@ __global__ void __launch_bounds__(64) k_fill_coop(DevBatch B, CoopFill F, const 
     T.col0 = col;
     T.col1 = col + F.hcap;
     T.hcap = F.hcap;
+    T.dbg = F.chainStats;
+    T.jacobi = F.jacobi;
     T.prNot = B.prNot;
     T.prThird = B.prThird;
     T.sdn = B.sdn;

@@ -200,3 +200,43 @@ def test_polish_2kb_batch_matches_oracle(P):
         assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
         assert r["consensus"] == e["template"]
         assert max(abs(a - b) for a, b in zip(r["qvs"], e["qvs"])) <= 1
+
+
+# configs[1] ZMWs (seed 1, the bench's first step) that the reference loop leaves NonConvergent: their
+# templates oscillate until MaximumIterations, which the engine replays instead of re-running
+# (engine.hip, Refine: cycle replay).  Found with tools/find_nonconvergent.py 2000 2000 10 1.
+NONCONVERGENT_2KB = (1, (820, 880, 1324, 1962))
+
+
+def test_nonconvergent_cycles_batch_match_oracle(P):
+    from pbccs_amd import synth
+    seed, idx = NONCONVERGENT_2KB
+    allz = synth.make_zmws(max(idx) + 1, 2000, 10, seed=seed)
+    zs = [allz[i] for i in idx]
+    res = P.polish_zmws(zs)
+    for z, r in zip(zs, res):
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+        assert not e["converged"]
+        assert r["status"] == "NonConvergent"
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+
+
+def test_nonconvergent_cycle_final_state_matches_oracle(P):
+    """Through the scorer API the state after RefineConsensus is observable: the replayed cycle must end
+    on the reference's final template (MaximumIterations - i mod period real iterations are run)."""
+    from pbccs_amd import synth
+    seed, idx = NONCONVERGENT_2KB
+    z = synth.make_zmws(idx[0] + 1, 2000, 10, seed=seed)[idx[0]]
+    g, o, rg, ro = _scorers(P, z["draft"], z["reads"], threshold=-5.0)
+    assert rg == ro
+    conv, nt, na = P.RefineConsensus(g)
+    ref = o.refine()
+    assert (conv, nt, na) == (ref["converged"], ref["n_tested"], ref["n_applied"])
+    assert g.Template() == o.template()
+    assert _close(g.BaselineScore(), o.baseline(), 1e-9)
+    for odd in (39, 38):   # both parities of the iterations left after the cycle is detected
+        g, o, _, _ = _scorers(P, z["draft"], z["reads"], threshold=-5.0)
+        conv, nt, na = P.RefineConsensus(g, max_iterations=odd)
+        ref = o.refine(max_iter=odd)
+        assert (conv, nt, na) == (ref["converged"], ref["n_tested"], ref["n_applied"])
+        assert g.Template() == o.template()
