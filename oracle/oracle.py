@@ -210,3 +210,160 @@ def polish_zmw(draft, reads, snr, min_zscore=-5.0, max_iter=40, separation=10, n
         out["qvs"] = q
         out["pred_acc"] = 1.0 - sum(10.0 ** (v / -10.0) for v in q) / max(1, len(q))
     return out
+
+
+# ================================================================ Quiver family (oracle/quiver_oracle.cpp)
+QV_PARAM_NAMES = ("Match", "Mismatch", "MismatchS", "Branch", "BranchS", "DeletionN", "DeletionWithTag",
+                  "DeletionWithTagS", "Nce", "NceS")
+INCORPORATE, EXTRA, DELETE, MERGE = 1, 2, 4, 8
+BASIC_MOVES, ALL_MOVES = 7, 15
+
+
+def _qlib():
+    L = lib()
+    if not getattr(L, "_q_ready", False):
+        c_f, c_i, c_p, c_s = ctypes.c_float, ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p
+        F = ctypes.POINTER(ctypes.c_float)
+        I = ctypes.POINTER(ctypes.c_int)
+        LL = ctypes.POINTER(ctypes.c_longlong)
+        Lg = ctypes.POINTER(ctypes.c_long)
+        for n in ("qorc_log_add",):
+            getattr(L, n).restype = c_f
+            getattr(L, n).argtypes = [c_f, c_f]
+        for n in ("qorc_exp_ps", "qorc_log_ps"):
+            getattr(L, n).restype = c_f
+            getattr(L, n).argtypes = [c_f]
+        L.qorc_scorer_new.restype = c_p
+        L.qorc_scorer_new.argtypes = [c_s, F, c_i, c_f, c_f, c_f, c_i]
+        L.qorc_scorer_free.argtypes = [c_p]
+        L.qorc_scorer_add_read.argtypes = [c_p, c_s, F, F, F, F, F, c_i, c_i, c_i, c_f, c_i]
+        L.qorc_scorer_score.restype = c_f
+        L.qorc_scorer_score.argtypes = [c_p, c_i, c_i, c_i, c_s, c_i]
+        L.qorc_ms_score.restype = c_f
+        L.qorc_ms_score.argtypes = [c_p, c_i, c_i, c_i, c_i, c_s]
+        L.qorc_scorer_scores.argtypes = [c_p, c_i, c_i, c_i, c_s, c_f, F]
+        L.qorc_scorer_is_favorable.argtypes = [c_p, c_i, c_i, c_i, c_s, c_i]
+        L.qorc_scorer_baseline.restype = c_f
+        L.qorc_scorer_baseline.argtypes = [c_p]
+        L.qorc_scorer_num_reads.argtypes = [c_p]
+        L.qorc_scorer_read_info.argtypes = [c_p, c_i, I, I, I, F, I, LL, LL, LL, LL]
+        L.qorc_scorer_cell.restype = c_f
+        L.qorc_scorer_cell.argtypes = [c_p, c_i, c_i, c_i, c_i]
+        L.qorc_scorer_template.argtypes = [c_p, c_s, c_i]
+        L.qorc_scorer_apply.argtypes = [c_p, c_i, I, I, I, c_s]
+        L.qorc_refine.argtypes = [c_p, c_i, c_i, c_i, Lg, Lg]
+        L.qorc_qvs.argtypes = [c_p, I, c_i]
+        L._q_ready = True
+    return L
+
+
+def _farr(vals):
+    return (ctypes.c_float * len(vals))(*vals)
+
+
+def qv_params(d):
+    """QvModelParams as the 20 floats of the C ABI (dict keys as in QuiverConfig.hpp:79-92; Merge/MergeS
+    may be scalars or 4-lists)."""
+    out = [float(d[k]) for k in QV_PARAM_NAMES]
+    for k in ("Merge", "MergeS"):
+        v = d[k]
+        out += [float(x) for x in v] if isinstance(v, (list, tuple)) else [float(v)] * 4
+    return out
+
+
+class QuiverScorer:
+    """Mirror of ConsensusCore::MultiReadMutationScorer<SparseSse{Qv,QvSumProduct}Recursor> (CPU restatement)."""
+
+    def __init__(self, tpl, params, moves=ALL_MOVES, score_diff=12.5, fast_threshold=-12.5, add_threshold=1.0,
+                 sum_product=False):
+        self._h = _qlib().qorc_scorer_new(tpl.encode(), _farr(qv_params(params)), moves, score_diff, fast_threshold,
+                                          add_threshold, 1 if sum_product else 0)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _qlib().qorc_scorer_free(self._h)
+            self._h = None
+
+    def add_read(self, seq, strand=FORWARD, ts=0, te=None, features=None, threshold=None):
+        """features: dict with optional ins/subs/del/del_tag/merge lists (del_tag as characters)."""
+        if te is None:
+            te = len(self.template())
+        f = features or {}
+        arrs = []
+        for k in ("ins", "subs", "del", "del_tag", "merge"):
+            v = f.get(k)
+            if v is None:
+                arrs.append(None)
+            elif k == "del_tag":
+                arrs.append(_farr([float(ord(c)) if isinstance(c, str) else float(c) for c in v]))
+            else:
+                arrs.append(_farr([float(x) for x in v]))
+        use_cfg = 1 if threshold is None else 0
+        return _qlib().qorc_scorer_add_read(self._h, seq.encode(), *arrs, strand, ts, te,
+                                             0.0 if threshold is None else threshold, use_cfg)
+
+    def score(self, mtype, start, base="-", fast=False, end=None):
+        nb = b"" if mtype == DELETION else base.encode()
+        return _qlib().qorc_scorer_score(self._h, mtype, start, end if end is not None else mutation_end(mtype, start),
+                                         nb, 1 if fast else 0)
+
+    def read_score_mutation(self, r, mtype, start, base="-"):
+        nb = b"" if mtype == DELETION else base.encode()
+        return _qlib().qorc_ms_score(self._h, r, mtype, start, mutation_end(mtype, start), nb)
+
+    def scores(self, mtype, start, base="-", unscored=0.0):
+        out = (ctypes.c_float * max(1, self.num_reads()))()
+        nb = b"" if mtype == DELETION else base.encode()
+        n = _qlib().qorc_scorer_scores(self._h, mtype, start, mutation_end(mtype, start), nb, unscored, out)
+        return list(out[:n])
+
+    def is_favorable(self, mtype, start, base="-", fast=False):
+        nb = b"" if mtype == DELETION else base.encode()
+        return bool(_qlib().qorc_scorer_is_favorable(self._h, mtype, start, mutation_end(mtype, start), nb,
+                                                      1 if fast else 0))
+
+    def baseline(self):
+        return _qlib().qorc_scorer_baseline(self._h)
+
+    def num_reads(self):
+        return _qlib().qorc_scorer_num_reads(self._h)
+
+    def read_info(self, r):
+        a, ts, te, fl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        sc = ctypes.c_float()
+        ua, ub, aa, ab = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong()
+        _qlib().qorc_scorer_read_info(self._h, r, ctypes.byref(a), ctypes.byref(ts), ctypes.byref(te), ctypes.byref(sc),
+                                      ctypes.byref(fl), ctypes.byref(ua), ctypes.byref(ub), ctypes.byref(aa),
+                                      ctypes.byref(ab))
+        return {"active": bool(a.value), "ts": ts.value, "te": te.value, "score": sc.value, "flipflops": fl.value,
+                "used": (ua.value, ub.value), "allocated": (aa.value, ab.value)}
+
+    def cell(self, r, which, i, j):
+        return _qlib().qorc_scorer_cell(self._h, r, which, i, j)
+
+    def template(self):
+        buf = ctypes.create_string_buffer(1 << 20)
+        _qlib().qorc_scorer_template(self._h, buf, len(buf))
+        return buf.value.decode()
+
+    def apply(self, muts):
+        types = _iarr([m[0] for m in muts])
+        starts = _iarr([m[1] for m in muts])
+        ends = _iarr([mutation_end(m[0], m[1]) for m in muts])
+        bases = "".join(m[2] if m[0] != DELETION else "-" for m in muts).encode()
+        return _qlib().qorc_scorer_apply(self._h, len(muts), types, starts, ends, bases)
+
+    def refine(self, max_iter=40, separation=10, neighborhood=20):
+        nt, na = ctypes.c_long(), ctypes.c_long()
+        conv = _qlib().qorc_refine(self._h, max_iter, separation, neighborhood, ctypes.byref(nt), ctypes.byref(na))
+        return {"converged": conv == 1, "error": conv < 0, "n_tested": nt.value, "n_applied": na.value}
+
+    def qvs(self):
+        L = len(self.template())
+        out = (ctypes.c_int * max(1, L))()
+        n = _qlib().qorc_qvs(self._h, out, L)
+        return list(out[:n])
+
+
+def quiver_log_add(a, b):
+    return _qlib().qorc_log_add(a, b)

@@ -96,6 +96,91 @@ def make_zmw6251():
     }
 
 
+def _testing_params():
+    """TestingParams (ConsensusCore/src/Tests/ParameterSettings.cpp:47-63), read from the test source."""
+    src = open(os.path.join(REF, "ConsensusCore/src/Tests/ParameterSettings.cpp")).read()
+    body = src[src.index("QvModelParams TestingParams"):src.index("QuiverConfig TestingConfig")]
+    vals = [float(v.rstrip("f")) for v in re.findall(r"(-?[0-9.]+f),\s*//|(?<=\s)(-?[0-9.]+f)\);", body) for v in v if v]
+    names = ["Match", "Mismatch", "MismatchS", "Branch", "BranchS", "DeletionN", "DeletionWithTag",
+             "DeletionWithTagS", "Nce", "NceS", "Merge", "MergeS"]
+    assert len(vals) == len(names), vals
+    return dict(zip(names, vals))
+
+
+def make_quiver_kats():
+    """The Quiver gtest known answers, transcribed as data (inputs + expected outputs), values from
+    TestingParams.  Viterbi recursor unless noted (SparseSseQvRecursor, the MultiReadMutationScorer type
+    of Quiver/MultiReadMutationScorer.hpp:242)."""
+    P = _testing_params()
+    INS, DEL, SUB = 0, 1, 2
+    nb, std = 1e9, 200.0   # BandingOptions(0, 1e9) "noBanding", BandingOptions(4, 200) (TestRecursors.cpp:78-80)
+    medium_tpl = "GATTACA" * 10
+    medium_read = "GATTACA" * 3 + "GATTTTTTACA" * 4 + "GATTACA" * 3
+
+    def case(name, source, tpl, reads, checks, moves=15, score_diff=std, fast=-12.5):
+        return {"name": name, "source": source, "tpl": tpl, "moves": moves, "score_diff": score_diff,
+                "fast_threshold": fast, "reads": reads, "checks": checks}
+
+    def rd(seq, strand=0, ts=0, te=None):
+        return {"seq": seq, "strand": strand, "ts": ts, "te": te}
+
+    def sc(t, pos, base, exp):
+        return {"kind": "score", "mut": [t, pos, base], "expected": exp}
+
+    def ms(t, pos, base, exp):   # single-read MutationScorer::ScoreMutation (read 0)
+        return {"kind": "read_score_mutation", "mut": [t, pos, base], "expected": exp}
+
+    kats = [
+        case("SmallMatch", "src/Tests/TestRecursors.cpp:99-126", "GATG", [rd("GATG")],
+             [{"kind": "baseline", "expected": 0.0}], moves=7, score_diff=nb),
+        case("SmallMismatch", "src/Tests/TestRecursors.cpp:128-152", "GATG", [rd("GATC")],
+             [{"kind": "baseline", "expected": -10.0}], moves=7, score_diff=nb),
+        case("SmallMerge", "src/Tests/TestRecursors.cpp:154-182", "GATT", [rd("GAT")],
+             [{"kind": "baseline", "expected": -2.0}], moves=15, score_diff=nb),
+        case("MediumSized", "src/Tests/TestRecursors.cpp:184-204 (FillAlphaBeta)", medium_tpl, [rd(medium_read)],
+             [{"kind": "baseline", "expected": -80.0}], moves=7, score_diff=std),
+        case("MutationScorer.Basic", "src/Tests/TestMutationScorer.cpp:100-124", "GATTACA", [rd("GATTACA")],
+             [{"kind": "baseline", "expected": 0.0},
+              ms(INS, 4, "A", P["Merge"]), ms(INS, 4, "G", P["DeletionN"]),
+              ms(SUB, 4, "T", P["Mismatch"]), ms(DEL, 4, "-", P["Nce"])]),
+        case("MutationScorer.AtBeginning", "src/Tests/TestMutationScorer.cpp:138-158", "GATTACA", [rd("GATTACA")],
+             [ms(INS, 0, "A", P["DeletionN"]), ms(INS, 1, "G", P["Merge"]), ms(INS, 1, "A", P["Merge"]),
+              ms(INS, 1, "T", P["DeletionN"]), ms(SUB, 0, "T", P["Mismatch"]), ms(DEL, 0, "-", P["Nce"])]),
+        case("MutationScorer.AtEnd", "src/Tests/TestMutationScorer.cpp:160-176", "GATTACA", [rd("GATTACA")],
+             [ms(INS, 7, "A", P["Merge"]), ms(INS, 7, "G", P["DeletionN"]), ms(SUB, 6, "T", P["Mismatch"]),
+              ms(DEL, 6, "-", P["Nce"])]),
+        case("MutationScorer.TinyTemplate", "src/Tests/TestMutationScorer.cpp:179-202", "GTGC", [rd("GTGC")],
+             [ms(DEL, 0, "-", P["Nce"]), ms(DEL, 3, "-", P["Nce"]), ms(INS, 0, "T", P["DeletionN"]),
+              ms(INS, 4, "T", P["DeletionN"])] + [ms(SUB, p, "A", P["Mismatch"]) for p in range(4)]),
+        case("MRMS.Basic", "src/Tests/TestMultiReadMutationScorer.cpp:275-319 (FastScoreThreshold -500)",
+             "TTGATTACATT", [rd("TTGATTACATT")],
+             [sc(SUB, 6, "A", 0.0), sc(INS, 6, "A", P["Merge"]), sc(SUB, 6, "T", P["Mismatch"]),
+              sc(DEL, 6, "-", P["Nce"]),
+              {"kind": "add_read", "read": rd("TTGATTACATT")},
+              sc(SUB, 6, "A", 0.0), sc(INS, 6, "A", -4.0), sc(SUB, 6, "T", -20.0), sc(DEL, 6, "-", -16.0),
+              {"kind": "apply", "muts": [[INS, 6, "A"]], "template": "TTGATTAACATT"},
+              sc(SUB, 6, "A", 0.0)], fast=-500.0),
+        case("MRMS.ReverseStrand", "src/Tests/TestMultiReadMutationScorer.cpp:395-437", "AATGTAATCAA",
+             [rd("TTGATTACATT", 1)],
+             [sc(SUB, 4, "T", 0.0), sc(INS, 5, "T", P["Merge"]), sc(SUB, 4, "A", P["Mismatch"]),
+              sc(DEL, 4, "-", P["Nce"]),
+              {"kind": "add_read", "read": rd("TTGATTACATT", 1)},
+              sc(SUB, 4, "T", 0.0), sc(INS, 5, "T", 2 * P["Merge"]), sc(SUB, 4, "A", 2 * P["Mismatch"]),
+              sc(DEL, 4, "-", 2 * P["Nce"]),
+              {"kind": "apply", "muts": [[INS, 5, "T"]], "template": "AATGTTAATCAA"},
+              sc(SUB, 4, "T", 0.0)], fast=-500.0),
+        case("MRMS.MutationsAtBeginning", "src/Tests/TestMultiReadMutationScorer.cpp:440-460", "TTGATTACATT",
+             [rd("TTGATTACATT")],
+             [sc(SUB, 0, "T", 0.0), sc(INS, 0, "A", 0.0), sc(INS, 1, "A", P["DeletionN"]),
+              sc(DEL, 0, "-", P["Branch"])], fast=-500.0),
+        case("MRMS.MutationsAtEnd", "src/Tests/TestMultiReadMutationScorer.cpp:462-483", "TTGATTACATT",
+             [rd("TTGATTACATT")],
+             [sc(SUB, 10, "T", 0.0), sc(INS, 11, "A", P["DeletionN"]), sc(INS, 12, "A", 0.0),
+              sc(DEL, 10, "-", P["Branch"])], fast=-500.0),
+    ]
+    return {"params": P, "tolerance_abs": 0.0, "kats": kats}
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference tree not present; fixtures are committed, nothing to regenerate")
@@ -103,7 +188,9 @@ def main():
         json.dump(make_kats(), f, indent=1)
     with open(os.path.join(HERE, "zmw6251.json"), "w") as f:
         json.dump(make_zmw6251(), f, indent=1)
-    print("wrote arrow_kats.json, zmw6251.json")
+    with open(os.path.join(HERE, "quiver_kats.json"), "w") as f:
+        json.dump(make_quiver_kats(), f, indent=1)
+    print("wrote arrow_kats.json, zmw6251.json, quiver_kats.json")
 
 
 if __name__ == "__main__":
