@@ -209,6 +209,64 @@ typedef struct {
 int pbccs_engine_set_profiling(pbccs_engine* eng, int on);
 int pbccs_engine_kernel_stats(pbccs_engine* eng, pbccs_kernel_stat* out, int cap, int* n, int reset);
 
+
+/* ---- Quiver family (ConsensusCore/include/ConsensusCore/Quiver/) ---------------------------------
+ * ccs does not call it; the north_star names it (QuiverConfig, QvEvaluator, SseRecursor).  One scorer =
+ * MultiReadMutationScorer<SparseSseQvRecursor> (Viterbi) or <SparseSseQvSumProductRecursor>
+ * (Quiver/MultiReadMutationScorer.hpp:242-245).  Scores are FP32 log-likelihoods. */
+typedef struct pbccs_quiver_scorer pbccs_quiver_scorer;
+
+/* QvModelParams (Quiver/QuiverConfig.hpp:79-176); merge / merge_s per template base A, C, G, T */
+typedef struct {
+    float match, mismatch, mismatch_s, branch, branch_s, deletion_n, deletion_with_tag, deletion_with_tag_s, nce,
+        nce_s;
+    float merge[4], merge_s[4];
+} pbccs_qv_model_params;
+
+/* QuiverConfig (QuiverConfig.hpp:181-199) + the recursor's combiner */
+typedef struct {
+    pbccs_qv_model_params params;
+    int moves_available;         /* Move bits: INCORPORATE 1, EXTRA 2, DELETE 4, MERGE 8 (ALL_MOVES 15) */
+    float score_diff;            /* BandingOptions::ScoreDiff (the diagonal-cross argument is ignored) */
+    float fast_score_threshold;  /* QuiverConfig::FastScoreThreshold */
+    float add_threshold;         /* QuiverConfig::AddThreshold (1.0 = no memory gate) */
+    int sum_product;             /* 0: Viterbi (SparseSseQvRecursor), 1: sum-product (logAdd) */
+} pbccs_quiver_config;
+
+/* MultiReadMutationScorer(const QuiverConfigTable&, std::string tpl)  (Quiver/MultiReadMutationScorer.cpp:123-136)
+ * The table: n configs with their chemistry names ("*" = the InsertDefault fallback, QuiverConfig.cpp:67-138). */
+int pbccs_quiver_scorer_create(pbccs_engine* eng, const pbccs_quiver_config* configs, const char* const* chemistries,
+                               int n_configs, const char* tpl, int tpl_len, pbccs_quiver_scorer** out);
+void pbccs_quiver_scorer_destroy(pbccs_quiver_scorer* s);
+/* bool AddRead(const MappedQvRead&, float threshold)                                    (.cpp:246-290)
+ * QvSequenceFeatures tracks of len floats each (NULL = zeros); del_tag holds the tag bases as float(char).
+ * threshold NaN = the read's config AddThreshold (the one-argument overload). *active = the return value. */
+int pbccs_quiver_scorer_add_read(pbccs_quiver_scorer* s, const char* seq, int len, const float* ins_qv,
+                                 const float* subs_qv, const float* del_qv, const float* del_tag,
+                                 const float* merge_qv, const char* chemistry, int strand, int tstart, int tend,
+                                 float threshold, int* active);
+/* float Score(m) / FastScore(m) (.cpp:312-353); many at once */
+int pbccs_quiver_scorer_score_many(pbccs_quiver_scorer* s, const pbccs_mutation* m, int n, int fast, float* scores);
+/* MutationScorer<R>::ScoreMutation (Quiver/MutationScorer.cpp:113-226) on read i's own scorer: the mutation is
+ * in the read's window coordinates and the absolute score of the mutated window is returned */
+int pbccs_quiver_scorer_read_score_mutation(pbccs_quiver_scorer* s, int i, const pbccs_mutation* m, float* score);
+/* std::vector<float> Scores(m, unscoredValue) (.cpp:355-371); per_read holds NumReads() entries */
+int pbccs_quiver_scorer_scores(pbccs_quiver_scorer* s, const pbccs_mutation* m, float unscored, float* per_read);
+/* IsFavorable / FastIsFavorable (.cpp:382-409) */
+int pbccs_quiver_scorer_is_favorable(pbccs_quiver_scorer* s, const pbccs_mutation* m, int fast, int* favorable);
+int pbccs_quiver_scorer_apply_mutations(pbccs_quiver_scorer* s, const pbccs_mutation* m, int n);   /* (.cpp:205-239) */
+int pbccs_quiver_scorer_template(pbccs_quiver_scorer* s, int strand, char* out, int cap, int* len);
+int pbccs_quiver_scorer_num_reads(pbccs_quiver_scorer* s);
+int pbccs_quiver_scorer_read_info(pbccs_quiver_scorer* s, int i, int* active, int* strand, int* tstart, int* tend);
+int pbccs_quiver_scorer_baseline_score(pbccs_quiver_scorer* s, float* score);          /* (.cpp:467-476) */
+int pbccs_quiver_scorer_baseline_scores(pbccs_quiver_scorer* s, float* out, int cap, int* n);
+int pbccs_quiver_scorer_num_flipflops(pbccs_quiver_scorer* s, int* out);
+/* AllocatedEntries of read i's alpha / beta (SparseMatrix-inl.hpp:275-284) */
+int pbccs_quiver_scorer_allocated_entries(pbccs_quiver_scorer* s, int i, long long* alpha, long long* beta);
+int pbccs_quiver_refine_consensus(pbccs_quiver_scorer* s, const pbccs_refine_options* opts, long long* n_tested,
+                                  long long* n_applied, int* converged);
+int pbccs_quiver_consensus_qvs(pbccs_quiver_scorer* s, int* qvs, int cap, int* n);
+
 #ifdef __cplusplus
 }
 #endif

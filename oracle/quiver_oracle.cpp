@@ -780,7 +780,7 @@ struct MultiReadScorer {
                 sum += Delta(rs, m);
                 if (sum < fastThreshold) return false;
             }
-        return sum > 0.04f;
+        return (double)sum > 0.04;   // MIN_FAVORABLE_SCOREDIFF is a double literal (:52)
     }
     std::vector<float> Scores(const Mut& m, float unscored)
     {
@@ -956,7 +956,7 @@ int qorc_scorer_is_favorable(void* h, int type, int start, int end, const char* 
 {
     MultiReadScorer* s = static_cast<MultiReadScorer*>(h);
     const Mut m = MakeMut(type, start, end, bases);
-    return fast ? (s->FastIsFavorable(m) ? 1 : 0) : (s->Score(m) > 0.04f ? 1 : 0);
+    return fast ? (s->FastIsFavorable(m) ? 1 : 0) : ((double)s->Score(m) > 0.04 ? 1 : 0);
 }
 
 // MutationScorer<R>::ScoreMutation on read r's own scorer (read coordinates; absolute score)

@@ -221,7 +221,10 @@ class ArrowMultiReadMutationScorer:
 
 
 def RefineConsensus(mms, max_iterations=40, mutation_separation=10, mutation_neighborhood=20):
-    """bool RefineConsensus(MRMS&, size_t* nTested, size_t* nApplied, const RefineOptions&) -> (converged, nT, nA)."""
+    """bool RefineConsensus(MRMS&, size_t* nTested, size_t* nApplied, const RefineOptions&) -> (converged, nT, nA).
+    Templated on the scorer in the reference (Consensus.hpp:63-67): Arrow or Quiver scorers."""
+    if isinstance(mms, _quiver.QuiverMultiReadMutationScorer):
+        return _quiver.RefineConsensus(mms, max_iterations, mutation_separation, mutation_neighborhood)
     o = _lib_mod.CRefineOptions(max_iterations, mutation_separation, mutation_neighborhood)
     nt, na, conv = ctypes.c_longlong(0), ctypes.c_longlong(0), ctypes.c_int()
     _lib_mod.check(load().pbccs_refine_consensus(mms._h, ctypes.byref(o), ctypes.byref(nt), ctypes.byref(na),
@@ -230,6 +233,8 @@ def RefineConsensus(mms, max_iterations=40, mutation_separation=10, mutation_nei
 
 
 def ConsensusQVs(mms):
+    if isinstance(mms, _quiver.QuiverMultiReadMutationScorer):
+        return _quiver.ConsensusQVs(mms)
     cap = mms.TemplateLength()
     out = (ctypes.c_int * max(1, cap))()
     n = ctypes.c_int()
@@ -243,6 +248,9 @@ def QVsToASCII(qvs):
 
 
 from .polish import ConsensusSettings, PreparedBatch, polish_many, polish_zmws  # noqa: E402  (batched ccs driver)
+from . import quiver as _quiver  # noqa: E402
+from .quiver import (QvModelParams, QuiverConfig, QuiverConfigTable,  # noqa: E402,F401
+                     QuiverMultiReadMutationScorer, ALL_MOVES, BASIC_MOVES)
 
 __all__ = [
     "ArrowConfig", "ArrowMultiReadMutationScorer", "ConsensusQVs", "ConsensusSettings", "Engine", "Mutation",

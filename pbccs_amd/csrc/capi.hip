@@ -637,3 +637,287 @@ int pbccs_engine_kernel_stats(pbccs_engine* eng, pbccs_kernel_stat* out, int cap
 }
 
 }  // extern "C"
+
+// ================================================================ Quiver family
+#include "quiver_engine.hpp"
+
+struct pbccs_quiver_scorer {
+    pbccs_engine* eng = nullptr;
+    std::unique_ptr<quiver::QuiverBatch> batch;
+    std::vector<std::pair<std::string, int>> table;   // QuiverConfigTable: chemistry -> config index
+    std::vector<pbccs_quiver_config> cfgs;
+    int z = 0;
+};
+
+namespace {
+
+quiver::QParams qparams(const pbccs_quiver_config& c)
+{
+    quiver::QParams p;
+    const pbccs_qv_model_params& m = c.params;
+    p.Match = m.match;
+    p.Mismatch = m.mismatch;
+    p.MismatchS = m.mismatch_s;
+    p.Branch = m.branch;
+    p.BranchS = m.branch_s;
+    p.DeletionN = m.deletion_n;
+    p.DeletionWithTag = m.deletion_with_tag;
+    p.DeletionWithTagS = m.deletion_with_tag_s;
+    p.Nce = m.nce;
+    p.NceS = m.nce_s;
+    for (int k = 0; k < 4; ++k) {
+        p.Merge[k] = m.merge[k];
+        p.MergeS[k] = m.merge_s[k];
+    }
+    p.scoreDiff = c.score_diff;
+    p.fastThreshold = c.fast_score_threshold;
+    p.addThreshold = c.add_threshold;
+    p.moves = c.moves_available;
+    p.sumProduct = c.sum_product ? 1 : 0;
+    return p;
+}
+
+// Quiver mutations may lie past the template end: no read scores them (ReadScoresMutation, :60-71)
+bool to_quiver_mutation(const pbccs_mutation& in, Mutation* out)
+{
+    if (in.type < 0 || in.type > 2 || in.start < 0) return false;
+    const int width = in.end - in.start;
+    if (in.type == PBCCS_INSERTION ? width != 0 : width != 1) return false;   // single-base only
+    if (in.type != PBCCS_DELETION && !(in.new_base == 'A' || in.new_base == 'C' || in.new_base == 'G' || in.new_base == 'T'))
+        return false;
+    *out = Mutation::Make(in.type, in.start, in.new_base);
+    return true;
+}
+
+int quiver_codes(const pbccs_mutation* m, int n, std::vector<int>* codes)
+{
+    for (int i = 0; i < n; ++i) {
+        Mutation mu;
+        if (!to_quiver_mutation(m[i], &mu)) return fail(PBCCS_EINVAL, "invalid single-base mutation");
+        codes->push_back(mutation_code(mu));
+    }
+    return PBCCS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pbccs_quiver_scorer_create(pbccs_engine* eng, const pbccs_quiver_config* configs, const char* const* chemistries,
+                               int n_configs, const char* tpl, int tpl_len, pbccs_quiver_scorer** out)
+{
+    if (!eng || !configs || n_configs < 1 || !tpl || tpl_len <= 0 || !out) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::unique_ptr<pbccs_quiver_scorer> s(new pbccs_quiver_scorer());
+        s->eng = eng;
+        s->batch.reset(new quiver::QuiverBatch(eng->device));
+        float fast = 0.0f;   // min over the table, starting at 0 (:129-135)
+        for (int k = 0; k < n_configs; ++k) {
+            const std::string name = (chemistries && chemistries[k]) ? chemistries[k] : "*";
+            bool dup = false;
+            for (auto& kv : s->table) dup = dup || kv.first == name;
+            if (dup) continue;   // InsertAs_ keeps the first entry of a name (QuiverConfig.cpp:67-78)
+            s->table.emplace_back(name, s->batch->AddConfig(qparams(configs[k])));
+            s->cfgs.push_back(configs[k]);
+            fast = std::min(fast, configs[k].fast_score_threshold);
+        }
+        s->z = s->batch->AddZmw(std::string(tpl, tpl_len), fast);
+        *out = s.release();
+        return PBCCS_OK;
+    });
+}
+
+void pbccs_quiver_scorer_destroy(pbccs_quiver_scorer* s) { delete s; }
+
+int pbccs_quiver_scorer_add_read(pbccs_quiver_scorer* s, const char* seq, int len, const float* ins_qv,
+                                 const float* subs_qv, const float* del_qv, const float* del_tag,
+                                 const float* merge_qv, const char* chemistry, int strand, int tstart, int tend,
+                                 float threshold, int* active)
+{
+    if (!s || !seq || len <= 0 || !active || (strand != 0 && strand != 1)) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        // QuiverConfigTable::At: exact chemistry, else "*" (QuiverConfig.cpp:112-127)
+        const std::string chem = chemistry ? chemistry : "*";
+        int cfg = -1;
+        size_t pos = 0;
+        for (size_t k = 0; k < s->table.size(); ++k)
+            if (s->table[k].first == chem) { cfg = s->table[k].second; pos = k; }
+        if (cfg < 0)
+            for (size_t k = 0; k < s->table.size(); ++k)
+                if (s->table[k].first == "*") { cfg = s->table[k].second; pos = k; }
+        if (cfg < 0) return fail(PBCCS_EINVAL, "Chemistry not found in QuiverConfigTable");
+        quiver::QReadFeatures f;
+        f.seq.assign(seq, len);
+        auto track = [&](std::vector<float>& v, const float* src) {
+            v.assign(len, 0.0f);
+            if (src) std::copy(src, src + len, v.begin());
+        };
+        track(f.ins, ins_qv);
+        track(f.subs, subs_qv);
+        track(f.del, del_qv);
+        track(f.tag, del_tag);
+        track(f.merge, merge_qv);
+        const float thr = std::isnan(threshold) ? s->cfgs[pos].add_threshold : threshold;
+        *active = s->batch->AddRead(s->z, f, strand, tstart, tend, cfg, thr) ? 1 : 0;
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_quiver_scorer_score_many(pbccs_quiver_scorer* s, const pbccs_mutation* m, int n, int fast, float* scores)
+{
+    if (!s || n < 0 || (n > 0 && (!m || !scores))) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::vector<int> codes;
+        if (quiver_codes(m, n, &codes) != PBCCS_OK) return PBCCS_EINVAL;
+        std::vector<float> d;
+        s->batch->Deltas(s->z, codes, &d);
+        for (int i = 0; i < n; ++i) scores[i] = s->batch->Score(s->z, d, i, fast != 0);
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_quiver_scorer_read_score_mutation(pbccs_quiver_scorer* s, int i, const pbccs_mutation* m, float* score)
+{
+    if (!s || !m || !score || i < 0 || i >= s->batch->NumReads(s->z)) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::vector<int> codes;
+        if (quiver_codes(m, 1, &codes) != PBCCS_OK) return PBCCS_EINVAL;
+        *score = s->batch->ReadScoreMutation(s->batch->ReadIndex(s->z, i), codes[0]);
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_quiver_scorer_scores(pbccs_quiver_scorer* s, const pbccs_mutation* m, float unscored, float* per_read)
+{
+    if (!s || !m || !per_read) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::vector<int> codes;
+        if (quiver_codes(m, 1, &codes) != PBCCS_OK) return PBCCS_EINVAL;
+        std::vector<float> d;
+        s->batch->Deltas(s->z, codes, &d);
+        const int nr = s->batch->NumReads(s->z);
+        for (int k = 0; k < nr; ++k) per_read[k] = std::isnan(d[k]) ? unscored : d[k];
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_quiver_scorer_is_favorable(pbccs_quiver_scorer* s, const pbccs_mutation* m, int fast, int* favorable)
+{
+    if (!s || !m || !favorable) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::vector<int> codes;
+        if (quiver_codes(m, 1, &codes) != PBCCS_OK) return PBCCS_EINVAL;
+        std::vector<float> d;
+        s->batch->Deltas(s->z, codes, &d);
+        *favorable = fast ? (s->batch->FastIsFavorable(s->z, d, 0) ? 1 : 0)
+                          : ((double)s->batch->Score(s->z, d, 0, false) > 0.04 ? 1 : 0);
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_quiver_scorer_apply_mutations(pbccs_quiver_scorer* s, const pbccs_mutation* m, int n)
+{
+    if (!s || n < 0 || (n > 0 && !m)) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::vector<Mutation> muts;
+        for (int i = 0; i < n; ++i) {
+            Mutation mu;
+            if (!to_quiver_mutation(m[i], &mu)) return fail(PBCCS_EINVAL, "invalid mutation");
+            muts.push_back(mu);
+        }
+        if (!s->batch->ApplyMutations(s->z, muts)) return fail(PBCCS_EINVAL, "mutation outside the template");
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_quiver_scorer_template(pbccs_quiver_scorer* s, int strand, char* out, int cap, int* len)
+{
+    if (!s || !out || !len) return fail(PBCCS_EINVAL, "bad argument");
+    const std::string t = strand ? reverse_complement(s->batch->Template(s->z)) : s->batch->Template(s->z);
+    *len = (int)t.size();
+    if ((int)t.size() + 1 > cap) return fail(PBCCS_ERANGE, "buffer too small");
+    std::memcpy(out, t.c_str(), t.size() + 1);
+    return PBCCS_OK;
+}
+
+int pbccs_quiver_scorer_num_reads(pbccs_quiver_scorer* s) { return s ? s->batch->NumReads(s->z) : -1; }
+
+int pbccs_quiver_scorer_read_info(pbccs_quiver_scorer* s, int i, int* active, int* strand, int* tstart, int* tend)
+{
+    if (!s || i < 0 || i >= s->batch->NumReads(s->z)) return fail(PBCCS_EINVAL, "bad argument");
+    const int r = s->batch->ReadIndex(s->z, i);
+    if (active) *active = s->batch->Active(r) ? 1 : 0;
+    if (strand) *strand = s->batch->Strand(r);
+    if (tstart) *tstart = s->batch->Ts(r);
+    if (tend) *tend = s->batch->Te(r);
+    return PBCCS_OK;
+}
+
+int pbccs_quiver_scorer_baseline_score(pbccs_quiver_scorer* s, float* score)
+{
+    if (!s || !score) return fail(PBCCS_EINVAL, "bad argument");
+    *score = s->batch->BaselineScore(s->z);
+    return PBCCS_OK;
+}
+
+int pbccs_quiver_scorer_baseline_scores(pbccs_quiver_scorer* s, float* out, int cap, int* n)
+{
+    if (!s || !n) return fail(PBCCS_EINVAL, "bad argument");
+    std::vector<float> v;
+    for (int k = 0; k < s->batch->NumReads(s->z); ++k) {
+        const int r = s->batch->ReadIndex(s->z, k);
+        if (s->batch->Active(r)) v.push_back(s->batch->ReadScore(r));
+    }
+    *n = (int)v.size();
+    if ((int)v.size() > cap || (!out && !v.empty())) return fail(PBCCS_ERANGE, "buffer too small");
+    std::copy(v.begin(), v.end(), out);
+    return PBCCS_OK;
+}
+
+int pbccs_quiver_scorer_num_flipflops(pbccs_quiver_scorer* s, int* out)
+{
+    if (!s || !out) return fail(PBCCS_EINVAL, "bad argument");
+    for (int k = 0; k < s->batch->NumReads(s->z); ++k) out[k] = s->batch->Flips(s->batch->ReadIndex(s->z, k));
+    return PBCCS_OK;
+}
+
+int pbccs_quiver_scorer_allocated_entries(pbccs_quiver_scorer* s, int i, long long* alpha, long long* beta)
+{
+    if (!s || i < 0 || i >= s->batch->NumReads(s->z) || !alpha || !beta) return fail(PBCCS_EINVAL, "bad argument");
+    const int r = s->batch->ReadIndex(s->z, i);
+    *alpha = s->batch->Allocated(r, 0);
+    *beta = s->batch->Allocated(r, 1);
+    return PBCCS_OK;
+}
+
+int pbccs_quiver_refine_consensus(pbccs_quiver_scorer* s, const pbccs_refine_options* opts, long long* n_tested,
+                                  long long* n_applied, int* converged)
+{
+    if (!s || !n_tested || !n_applied || !converged) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        RefineOptions ro;
+        if (opts) {
+            ro.maxIterations = opts->max_iterations;
+            ro.mutationSeparation = opts->mutation_separation;
+            ro.mutationNeighborhood = opts->mutation_neighborhood;
+        }
+        bool conv = false;
+        if (!s->batch->Refine(s->z, ro, n_tested, n_applied, &conv)) return fail(PBCCS_EINVAL, "invalid edit");
+        *converged = conv ? 1 : 0;
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_quiver_consensus_qvs(pbccs_quiver_scorer* s, int* qvs, int cap, int* n)
+{
+    if (!s || !n) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        const std::vector<int> q = s->batch->QVs(s->z);
+        *n = (int)q.size();
+        if ((int)q.size() > cap || !qvs) return fail(PBCCS_ERANGE, "buffer too small");
+        std::copy(q.begin(), q.end(), qvs);
+        return PBCCS_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,507 @@
+// pbccs_amd/csrc/quiver_engine.hip -- QuiverBatch (quiver_engine.hpp).
+#include "quiver_engine.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <set>
+#include <stdexcept>
+
+namespace pbccs {
+namespace quiver {
+namespace {
+
+#define QHIP(x)                                                              \
+    do {                                                                     \
+        hipError_t e_ = (x);                                                 \
+        if (e_ != hipSuccess) throw DeviceError(hipGetErrorString(e_));      \
+    } while (0)
+
+template <class T>
+void put(DevVec<T>& d, const std::vector<T>& h, hipStream_t s)
+{
+    d.reserve(std::max<size_t>(h.size(), 1), false);
+    if (!h.empty()) QHIP(hipMemcpyAsync(d.ptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
+}
+
+template <class T>
+void get(std::vector<T>& h, const DevVec<T>& d, size_t n, hipStream_t s)
+{
+    h.resize(n);
+    if (n) QHIP(hipMemcpyAsync(h.data(), d.ptr, n * sizeof(T), hipMemcpyDeviceToHost, s));
+}
+
+constexpr int kInitialBand = 24;   // values per column per arena to start with
+
+struct ScoredMut {
+    int code;
+    float score;
+};
+
+std::vector<ScoredMut> best_subset(std::vector<ScoredMut> in, int sep)   // Consensus-inl.hpp:98-118
+{
+    if (sep == 0) return in;
+    std::vector<ScoredMut> out;
+    while (!in.empty()) {
+        size_t best = 0;
+        for (size_t k = 1; k < in.size(); ++k)
+            if (in[best].score < in[k].score) best = k;
+        const ScoredMut b = in[best];
+        out.push_back(b);
+        const int lo = mut_pos(b.code) - sep, hi = mut_pos(b.code) + sep;
+        std::vector<ScoredMut> keep;
+        for (const ScoredMut& s : in)
+            if (!(lo <= mut_pos(s.code) && mut_pos(s.code) <= hi)) keep.push_back(s);
+        in.swap(keep);
+    }
+    return out;
+}
+
+}  // namespace
+
+QuiverBatch::QuiverBatch(int device) : device_(device)
+{
+    QHIP(hipSetDevice(device_));
+    QHIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    dScratchTop_.reserve(1, false);
+    dOverflow_.reserve(1, false);
+    dScratch_.reserve(1 << 20, false);
+}
+
+QuiverBatch::~QuiverBatch()
+{
+    if (stream_) {
+        (void)hipStreamSynchronize(stream_);
+        (void)hipStreamDestroy(stream_);
+    }
+}
+
+int QuiverBatch::AddConfig(const QParams& p)
+{
+    if (!(p.scoreDiff >= 0.0f)) throw std::invalid_argument("ScoreDiff must be positive");
+    configs_.push_back(p);
+    dirty_ = true;
+    return (int)configs_.size() - 1;
+}
+
+int QuiverBatch::AddZmw(const std::string& tpl, float fastScoreThreshold)
+{
+    if (tpl.empty() || !is_acgt(tpl)) throw std::invalid_argument("template must be a non-empty ACGT string");
+    HZmw z;
+    z.tpl = tpl;
+    z.fastThreshold = fastScoreThreshold;
+    zmws_.push_back(z);
+    dirty_ = true;
+    return (int)zmws_.size() - 1;
+}
+
+void QuiverBatch::EnsureCapacity(int ri)
+{
+    HRead& r = reads_[ri];
+    const int J = r.te - r.ts;
+    if (J + 1 > r.colCap) {
+        r.colCap = J + J / 4 + 16;
+        r.colBase = colTop_;
+        colTop_ += 4LL * r.colCap;
+        dirty_ = true;
+    }
+    const long long want = (long long)(J + 1) * kInitialBand;
+    if (r.valCap < want) {
+        r.valCap = want + want / 4;
+        r.valBase = valTop_;
+        valTop_ += 4 * r.valCap;
+        dirty_ = true;
+    }
+}
+
+bool QuiverBatch::AddRead(int zi, const QReadFeatures& f, int strand, int ts, int te, int config, float threshold)
+{
+    HZmw& z = zmws_.at(zi);
+    const int L = (int)z.tpl.size();
+    const size_t I = f.seq.size();
+    if (ts < 0 || te > L || ts > te || I < 1 || config < 0 || config >= (int)configs_.size())
+        throw std::invalid_argument("read window outside the template or bad config");
+    if (f.ins.size() != I || f.subs.size() != I || f.del.size() != I || f.tag.size() != I || f.merge.size() != I)
+        throw std::invalid_argument("QV feature tracks must match the read length");
+    HRead r;
+    r.zmw = zi;
+    r.config = config;
+    r.strand = strand;
+    r.ts = ts;
+    r.te = te;
+    r.seqOff = (long long)hSeq_.size();
+    hSeq_.insert(hSeq_.end(), f.seq.begin(), f.seq.end());
+    for (const std::vector<float>* t : {&f.ins, &f.subs, &f.del, &f.tag, &f.merge})
+        hFeat_.insert(hFeat_.end(), t->begin(), t->end());
+    r.colBuf = -1;
+    reads_.push_back(r);
+    const int ri = (int)reads_.size() - 1;
+    z.reads.push_back(ri);
+    HRead& h = reads_[ri];
+    h.colBuf = valTop_;
+    valTop_ += (long long)I + 8;
+    EnsureCapacity(ri);
+    dirty_ = true;
+    Fill({ri});
+    // AddRead: a scorer whose construction threw (alpha/beta mismatch) is dropped; so is one whose
+    // matrices allocate more than `threshold` of the full matrix (:263-276)
+    h.hasScorer = h.active;
+    if (h.active && threshold < 1.0f) {
+        const int J = te - ts;
+        // float threshold * int * int is float; 0.5 + float is double (:268)
+        const int maxSize = static_cast<int>(0.5 + threshold * (float)(int)(I + 1) * (float)(J + 1));
+        if (h.alloc[0] >= maxSize || h.alloc[1] >= maxSize) h.active = h.hasScorer = false;
+    }
+    return h.active;
+}
+
+void QuiverBatch::Upload()
+{
+    if (!dirty_) return;
+    std::vector<long long> zf, zr;
+    std::vector<int> zl;
+    std::vector<char> tp;
+    for (const HZmw& z : zmws_) {
+        zf.push_back((long long)tp.size());
+        tp.insert(tp.end(), z.tpl.begin(), z.tpl.end());
+        tp.push_back('\0');
+        const std::string rc = reverse_complement(z.tpl);
+        zr.push_back((long long)tp.size());
+        tp.insert(tp.end(), rc.begin(), rc.end());
+        tp.push_back('\0');
+        zl.push_back((int)z.tpl.size());
+    }
+    const size_t R = reads_.size();
+    std::vector<int> rz(R), rp(R), rs(R), rts(R), rte(R), rl(R), rcc(R);
+    std::vector<long long> rso(R), rcb(R), rvb(R), rvc(R), rcbuf(R);
+    for (size_t i = 0; i < R; ++i) {
+        const HRead& r = reads_[i];
+        rz[i] = r.zmw;
+        rp[i] = r.config;
+        rs[i] = r.strand;
+        rts[i] = r.ts;
+        rte[i] = r.te;
+        rso[i] = r.seqOff;
+        rcb[i] = r.colBase;
+        rcc[i] = r.colCap;
+        rvb[i] = r.valBase;
+        rvc[i] = r.valCap;
+        rcbuf[i] = r.colBuf;
+    }
+    for (size_t i = 0; i < R; ++i) {
+        const HRead& r = reads_[i];
+        const size_t I = (i + 1 < R ? reads_[i + 1].seqOff : (long long)hSeq_.size()) - r.seqOff;
+        rl[i] = (int)I;
+    }
+    put(dZFwd_, zf, stream_);
+    put(dZRev_, zr, stream_);
+    put(dZLen_, zl, stream_);
+    put(dTpl_, tp, stream_);
+    put(dParams_, configs_, stream_);
+    put(dRZmw_, rz, stream_);
+    put(dRParam_, rp, stream_);
+    put(dRStrand_, rs, stream_);
+    put(dRTs_, rts, stream_);
+    put(dRTe_, rte, stream_);
+    put(dRLen_, rl, stream_);
+    put(dRSeq_, rso, stream_);
+    put(dRColBase_, rcb, stream_);
+    put(dRColCap_, rcc, stream_);
+    put(dRValBase_, rvb, stream_);
+    put(dRValCap_, rvc, stream_);
+    put(dRColBuf_, rcbuf, stream_);
+    put(dSeq_, hSeq_, stream_);
+    put(dFeat_, hFeat_, stream_);
+    dRange_.reserve(std::max<long long>(colTop_, 1), true);
+    dOff_.reserve(std::max<long long>(colTop_, 1), true);
+    dAlloc_.reserve(std::max<long long>(colTop_ / 2, 1), true);
+    dVal_.reserve(std::max<long long>(valTop_, 1), true);
+    dRCurA_.reserve(std::max<size_t>(R, 1), true);
+    dRCurB_.reserve(std::max<size_t>(R, 1), true);
+    dRScore_.reserve(std::max<size_t>(R, 1), true);
+    dRFlips_.reserve(std::max<size_t>(R, 1), true);
+    dRStatus_.reserve(std::max<size_t>(R, 1), true);
+    dRUsed_.reserve(std::max<size_t>(2 * R, 1), true);
+    dRAlloc_.reserve(std::max<size_t>(2 * R, 1), true);
+    QHIP(hipStreamSynchronize(stream_));
+    dirty_ = false;
+}
+
+QBatch QuiverBatch::View()
+{
+    QBatch b;
+    b.zFwd = dZFwd_.ptr;
+    b.zRev = dZRev_.ptr;
+    b.zLen = dZLen_.ptr;
+    b.tplPool = dTpl_.ptr;
+    b.params = dParams_.ptr;
+    b.rZmw = dRZmw_.ptr;
+    b.rParam = dRParam_.ptr;
+    b.rStrand = dRStrand_.ptr;
+    b.rTs = dRTs_.ptr;
+    b.rTe = dRTe_.ptr;
+    b.rLen = dRLen_.ptr;
+    b.rSeq = dRSeq_.ptr;
+    b.seqPool = dSeq_.ptr;
+    b.featPool = dFeat_.ptr;
+    b.rColBase = dRColBase_.ptr;
+    b.rColCap = dRColCap_.ptr;
+    b.rValBase = dRValBase_.ptr;
+    b.rValCap = dRValCap_.ptr;
+    b.rColBuf = dRColBuf_.ptr;
+    b.range = dRange_.ptr;
+    b.off = dOff_.ptr;
+    b.alloc = dAlloc_.ptr;
+    b.valPool = dVal_.ptr;
+    b.rCurA = dRCurA_.ptr;
+    b.rCurB = dRCurB_.ptr;
+    b.rScore = dRScore_.ptr;
+    b.rFlips = dRFlips_.ptr;
+    b.rStatus = dRStatus_.ptr;
+    b.rUsed = dRUsed_.ptr;
+    b.rAlloc = dRAlloc_.ptr;
+    return b;
+}
+
+// MutationScorer ctor / Template(): FillAlphaBeta; grows a read's arenas and re-runs it on overflow.
+void QuiverBatch::Fill(const std::vector<int>& readsIn)
+{
+    std::vector<int> todo(readsIn);
+    for (int attempt = 0; !todo.empty(); ++attempt) {
+        if (attempt > 8) throw DeviceError("quiver band storage keeps overflowing");
+        Upload();
+        put(dList_, todo, stream_);
+        const QBatch B = View();
+        launch_qfill(B, dList_.ptr, (int)todo.size(), stream_);
+        QHIP(hipGetLastError());
+        const size_t R = reads_.size();
+        std::vector<int> st, ca, cb, fl;
+        std::vector<float> sc;
+        std::vector<long long> used, al;
+        get(st, dRStatus_, R, stream_);
+        get(ca, dRCurA_, R, stream_);
+        get(cb, dRCurB_, R, stream_);
+        get(fl, dRFlips_, R, stream_);
+        get(sc, dRScore_, R, stream_);
+        get(used, dRUsed_, 2 * R, stream_);
+        get(al, dRAlloc_, 2 * R, stream_);
+        QHIP(hipStreamSynchronize(stream_));
+        std::vector<int> next;
+        for (int r : todo) {
+            HRead& h = reads_[r];
+            if (st[r] == kQOverflow) {
+                const long long need = std::max(used[2 * r], used[2 * r + 1]);
+                h.valCap = std::max(need + need / 4 + 64, h.valCap + 1);
+                h.valBase = valTop_;
+                valTop_ += 4 * h.valCap;
+                dirty_ = true;
+                next.push_back(r);
+                continue;
+            }
+            h.active = st[r] == kQOk;   // AlphaBetaMismatchException -> no scorer / inactive
+            h.curA = ca[r];
+            h.curB = cb[r];
+            h.flips = fl[r];
+            h.score = sc[r];
+            h.alloc[0] = al[2 * r];
+            h.alloc[1] = al[2 * r + 1];
+        }
+        todo.swap(next);
+    }
+    // the device copies of curA / curB are what k_qscore reads: they were written by the kernel itself
+}
+
+void QuiverBatch::Deltas(int zi, const std::vector<int>& codes, std::vector<float>* out)
+{
+    const HZmw& z = zmws_.at(zi);
+    const int nr = (int)z.reads.size();
+    const long long M = (long long)codes.size();
+    out->assign((size_t)M * nr, std::numeric_limits<float>::quiet_NaN());
+    if (M == 0 || nr == 0) return;
+    std::vector<int> tr, tm;
+    std::vector<long long> slot;
+    for (long long m = 0; m < M; ++m)
+        for (int k = 0; k < nr; ++k) {
+            if (!reads_[z.reads[k]].active) continue;
+            tr.push_back(z.reads[k]);
+            tm.push_back((int)m);
+            slot.push_back(m * nr + k);
+        }
+    if (tr.empty()) return;
+    std::vector<float> d;
+    RunScore(tr, tm, codes, false, &d);
+    for (size_t t = 0; t < tr.size(); ++t) (*out)[slot[t]] = d[t];
+}
+
+void QuiverBatch::RunScore(const std::vector<int>& tr, const std::vector<int>& tm, const std::vector<int>& codes,
+                           bool raw, std::vector<float>* out)
+{
+    Upload();
+    put(dTaskRead_, tr, stream_);
+    put(dTaskMut_, tm, stream_);
+    put(dCodes_, codes, stream_);
+    dDelta_.reserve(std::max<size_t>(tr.size(), 1), false);
+    for (int attempt = 0;; ++attempt) {
+        QHIP(hipMemsetAsync(dScratchTop_.ptr, 0, sizeof(unsigned long long), stream_));
+        QHIP(hipMemsetAsync(dOverflow_.ptr, 0, sizeof(int), stream_));
+        QScoreWork W;
+        W.taskRead = dTaskRead_.ptr;
+        W.taskMut = dTaskMut_.ptr;
+        W.codes = dCodes_.ptr;
+        W.delta = dDelta_.ptr;
+        W.scratch = dScratch_.ptr;
+        W.scratchTop = dScratchTop_.ptr;
+        W.scratchCap = dScratch_.cap;
+        W.overflow = dOverflow_.ptr;
+        W.nTasks = (long long)tr.size();
+        W.raw = raw ? 1 : 0;
+        launch_qscore(View(), W, stream_);
+        QHIP(hipGetLastError());
+        int ovf = 0;
+        QHIP(hipMemcpyAsync(&ovf, dOverflow_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
+        QHIP(hipStreamSynchronize(stream_));
+        if (!ovf) break;
+        if ((ovf & 2) || attempt > 6) throw DeviceError("quiver extend buffer exceeds 8 columns / scratch");
+        dScratch_.reserve(dScratch_.cap * 4, false);
+    }
+    get(*out, dDelta_, tr.size(), stream_);
+    QHIP(hipStreamSynchronize(stream_));
+}
+
+float QuiverBatch::ReadScoreMutation(int r, int code)
+{
+    if (!reads_.at(r).hasScorer) return 0.0f;
+    std::vector<float> d;
+    RunScore({r}, {0}, {code}, true, &d);
+    return d[0];
+}
+
+// Score / FastScore (Quiver/MultiReadMutationScorer.cpp:312-353): float sum in read order; NaN = the read
+// does not score the mutation (or is inactive).
+float QuiverBatch::Score(int zi, const std::vector<float>& deltas, int m, bool fast) const
+{
+    const HZmw& z = zmws_[zi];
+    const int nr = (int)z.reads.size();
+    float sum = 0;
+    for (int k = 0; k < nr; ++k) {
+        const float d = deltas[(size_t)m * nr + k];
+        if (std::isnan(d)) continue;
+        sum += d;
+        if (fast && sum < z.fastThreshold) return sum;
+    }
+    return sum;
+}
+
+bool QuiverBatch::FastIsFavorable(int zi, const std::vector<float>& deltas, int m) const   // :392-409
+{
+    const HZmw& z = zmws_[zi];
+    const int nr = (int)z.reads.size();
+    float sum = 0;
+    for (int k = 0; k < nr; ++k) {
+        const float d = deltas[(size_t)m * nr + k];
+        if (std::isnan(d)) continue;
+        sum += d;
+        if (sum < z.fastThreshold) return false;
+    }
+    return (double)sum > 0.04;   // MIN_FAVORABLE_SCOREDIFF (:52), a double
+}
+
+float QuiverBatch::BaselineScore(int zi) const   // :467-476
+{
+    float sum = 0;
+    for (int r : zmws_[zi].reads)
+        if (reads_[r].active) sum += reads_[r].score;
+    return sum;
+}
+
+bool QuiverBatch::ApplyMutations(int zi, const std::vector<Mutation>& muts)   // :205-239
+{
+    HZmw& z = zmws_.at(zi);
+    std::string next;
+    std::vector<int> mtp;
+    if (!apply_mutations(z.tpl, muts, &next, &mtp)) return false;
+    z.tpl = next;
+    std::vector<int> refill;
+    for (int r : z.reads) {
+        HRead& h = reads_[r];
+        h.ts = mtp[h.ts];
+        h.te = mtp[h.te];
+        if (h.active) {
+            EnsureCapacity(r);
+            refill.push_back(r);
+        }
+    }
+    dirty_ = true;
+    Fill(refill);   // a refill that mismatches marks the read inactive
+    return true;
+}
+
+// AbstractRefineConsensus (Consensus-inl.hpp:159-251) with Quiver's float scores.
+bool QuiverBatch::Refine(int zi, const RefineOptions& ro, long long* nTested, long long* nApplied, bool* converged)
+{
+    *nTested = 0;
+    *nApplied = 0;
+    *converged = false;
+    std::set<std::string> history;
+    std::vector<int> centers;
+    for (int iter = 0; iter < ro.maxIterations; ++iter) {
+        const std::string tpl = zmws_[zi].tpl;
+        std::vector<int> codes;
+        if (iter == 0) unique_mutations(tpl, 0, (int)tpl.size(), &codes);
+        else nearby_mutations(tpl, centers, ro.mutationNeighborhood, &codes);
+        *nTested += (long long)codes.size();
+        std::vector<float> d;
+        Deltas(zi, codes, &d);
+        std::vector<ScoredMut> fav;
+        for (int m = 0; m < (int)codes.size(); ++m)
+            if (FastIsFavorable(zi, d, m)) fav.push_back({codes[m], Score(zi, d, m, false)});
+        if (fav.empty()) {
+            *converged = true;
+            break;
+        }
+        std::vector<ScoredMut> best = best_subset(fav, ro.mutationSeparation);
+        std::vector<Mutation> muts;
+        for (const ScoredMut& s : best) muts.push_back(mutation_from_code(s.code));
+        if (best.size() > 1) {
+            std::string nx;
+            std::vector<int> mtp;
+            if (apply_mutations(tpl, muts, &nx, &mtp) && history.count(nx)) {
+                best.resize(1);
+                muts.resize(1);
+            }
+        }
+        *nApplied += (long long)best.size();
+        history.insert(tpl);
+        centers.clear();
+        for (const ScoredMut& s : fav) centers.push_back(mut_pos(s.code));
+        if (!ApplyMutations(zi, muts)) return false;
+    }
+    return true;
+}
+
+std::vector<int> QuiverBatch::QVs(int zi)   // ConsensusQVs (Consensus-inl.hpp:274-295)
+{
+    const std::string tpl = zmws_[zi].tpl;
+    std::vector<int> codes, posOff;
+    for (int p = 0; p < (int)tpl.size(); ++p) {
+        posOff.push_back((int)codes.size());
+        unique_mutations(tpl, p, p + 1, &codes);
+    }
+    posOff.push_back((int)codes.size());
+    std::vector<float> d;
+    Deltas(zi, codes, &d);
+    std::vector<int> qv;
+    for (int p = 0; p < (int)tpl.size(); ++p) {
+        double sum = 0.0;
+        for (int m = posOff[p]; m < posOff[p + 1]; ++m) {
+            const double s = Score(zi, d, m, false);
+            if (s < 0.0) sum += std::exp(s);
+        }
+        qv.push_back(probability_to_qv(1.0 - 1.0 / (1.0 + sum)));
+    }
+    return qv;
+}
+
+}  // namespace quiver
+}  // namespace pbccs

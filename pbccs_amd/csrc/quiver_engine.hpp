@@ -1,0 +1,109 @@
+// pbccs_amd/csrc/quiver_engine.hpp -- host side of the Quiver engine (ConsensusCore Quiver family).
+//
+// QuiverBatch keeps Quiver scorers (a template + mapped QV-feature reads each) resident in HBM and runs
+// the MultiReadMutationScorer surface on them (Quiver/MultiReadMutationScorer.cpp:60-504): AddRead with
+// the memory-fraction gate, Score / FastScore / Scores / (Fast)IsFavorable, ApplyMutations + refills,
+// BaselineScore(s), and RefineConsensus / ConsensusQVs on top (Consensus-inl.hpp:159-295).  Fills and
+// mutation scores run on the GPU (quiver_kernels.hip); the read-ordered float sums run on the host.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "arrow_model.hpp"
+#include "engine.hpp"
+#include "quiver_kernels.hpp"
+
+namespace pbccs {
+namespace quiver {
+
+struct QReadFeatures {
+    std::string seq;
+    std::vector<float> ins, subs, del, tag, merge;   // tag: DelTag as float(char)
+};
+
+class QuiverBatch {
+public:
+    explicit QuiverBatch(int device);
+    ~QuiverBatch();
+    QuiverBatch(const QuiverBatch&) = delete;
+    QuiverBatch& operator=(const QuiverBatch&) = delete;
+
+    int AddConfig(const QParams& p);
+    int AddZmw(const std::string& tpl, float fastScoreThreshold);
+    // AddRead (Quiver/MultiReadMutationScorer.cpp:246-283): fills the read; returns whether it is active.
+    bool AddRead(int z, const QReadFeatures& f, int strand, int ts, int te, int config, float threshold);
+
+    // per (mutation, read) deltas ScoreMutation(oriented) - Score(), NaN where the read does not score it;
+    // out[m * nReads + k]
+    void Deltas(int z, const std::vector<int>& codes, std::vector<float>* out);
+    // MutationScorer<R>::ScoreMutation on read r's own scorer, mutation in the read's window coordinates
+    float ReadScoreMutation(int r, int code);
+    float Score(int z, const std::vector<float>& deltas, int m, bool fast) const;   // read-ordered float sum
+    bool FastIsFavorable(int z, const std::vector<float>& deltas, int m) const;
+    bool ApplyMutations(int z, const std::vector<Mutation>& muts);
+    bool Refine(int z, const RefineOptions& ro, long long* nTested, long long* nApplied, bool* converged);
+    std::vector<int> QVs(int z);
+
+    const std::string& Template(int z) const { return zmws_[z].tpl; }
+    int NumReads(int z) const { return (int)zmws_[z].reads.size(); }
+    int ReadIndex(int z, int k) const { return zmws_[z].reads[k]; }
+    bool Active(int r) const { return reads_[r].active; }
+    int Ts(int r) const { return reads_[r].ts; }
+    int Te(int r) const { return reads_[r].te; }
+    int Strand(int r) const { return reads_[r].strand; }
+    int Flips(int r) const { return reads_[r].flips; }
+    float ReadScore(int r) const { return reads_[r].score; }
+    long long Allocated(int r, int which) const { return reads_[r].alloc[which]; }
+    float BaselineScore(int z) const;
+
+private:
+    struct HZmw {
+        std::string tpl;
+        float fastThreshold = 0.0f;
+        std::vector<int> reads;
+    };
+    struct HRead {
+        int zmw = 0, config = 0, strand = 0, ts = 0, te = 0;
+        bool active = false, hasScorer = false;
+        long long seqOff = 0;
+        long long colBase = 0;
+        int colCap = 0;
+        long long valBase = 0, valCap = 0, colBuf = 0;
+        int curA = 0, curB = 0, flips = 0;
+        float score = 0.0f;
+        long long alloc[2] = {0, 0};
+    };
+    void Upload();
+    void EnsureCapacity(int r);
+    QBatch View();
+    void Fill(const std::vector<int>& reads);
+    void RunScore(const std::vector<int>& taskRead, const std::vector<int>& taskMut, const std::vector<int>& codes,
+                  bool raw, std::vector<float>* d);
+
+    int device_ = 0;
+    hipStream_t stream_ = nullptr;
+    std::vector<QParams> configs_;
+    std::vector<HZmw> zmws_;
+    std::vector<HRead> reads_;
+    std::vector<char> hSeq_;
+    std::vector<float> hFeat_;
+    long long colTop_ = 0, valTop_ = 0;
+    bool dirty_ = true;
+    // device
+    DevVec<long long> dZFwd_, dZRev_, dRSeq_, dRColBase_, dRValBase_, dRValCap_, dRColBuf_, dRUsed_, dRAlloc_;
+    DevVec<int> dZLen_, dRZmw_, dRParam_, dRStrand_, dRTs_, dRTe_, dRLen_, dRColCap_, dRCurA_, dRCurB_, dRFlips_,
+        dRStatus_, dList_, dTaskRead_, dTaskMut_, dCodes_, dOverflow_, dOff_;
+    DevVec<char> dTpl_, dSeq_;
+    DevVec<float> dFeat_, dRScore_, dDelta_, dScratch_;
+    DevVec<QParams> dParams_;
+    DevVec<int2> dRange_;
+    DevVec<QAlloc> dAlloc_;
+    DevVec<float> dVal_;
+    DevVec<unsigned long long> dScratchTop_;
+};
+
+}  // namespace quiver
+}  // namespace pbccs

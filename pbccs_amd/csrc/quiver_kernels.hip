@@ -1,0 +1,567 @@
+// pbccs_amd/csrc/quiver_kernels.hip -- Quiver recursions on gfx950.
+//
+//   k_qfill    one lane per read: RecursorBase::FillAlphaBeta (detail/RecursorBase.cpp:70-116) over the
+//              SSE recursor's fills (SseRecursor.cpp:73-353) into double-buffered band arenas.
+//   k_qscore   one lane per (mutation, read): MutationScorer::ScoreMutation (Quiver/MutationScorer.cpp:
+//              113-226) -- ExtendAlpha + LinkAlphaBeta in the middle, ExtendAlpha to the end, ExtendBeta
+//              (SimpleRecursor.cpp:407-495) at the start, a whole FillAlpha for tiny windows.
+// The 4-row SSE blocks are evaluated row by row in the reference's order: the block terms (Inc, Merge,
+// Del, each combined from -FLT_MAX), then the serial Extra cascade, then the block's min / max for the
+// band test -- every value equals the SSE lane's.
+#include "quiver_kernels.hpp"
+
+namespace pbccs {
+namespace quiver {
+namespace {
+
+// ---- RangeGuide / RowRange (detail/RecursorBase-inl.hpp:49-114) ----------------------------------------
+__device__ void row_range(const QBand& m, int j, float scoreDiff, int* ob, int* oe)
+{
+    int b = m.range[j].x, e = m.range[j].y;
+    int maxRow = b;
+    float maxScore = m.Get(maxRow, j);
+    for (int i = b + 1; i < e; ++i) {
+        const float s = m.Get(i, j);
+        if (s > maxScore) { maxRow = i; maxScore = s; }
+    }
+    const float thr = maxScore - scoreDiff;
+    int i;
+    for (i = b; i < maxRow && m.Get(i, j) < thr; ++i) {}
+    b = i;
+    for (i = e - 1; i >= maxRow && m.Get(i, j) < thr; --i) {}
+    *ob = b;
+    *oe = i + 1;
+}
+
+__device__ void range_guide(int j, const QBand* guide, const QBand* self, float scoreDiff, int* hb, int* he)
+{
+    const bool useG = guide && !guide->Empty(j);
+    const bool useS = self && !self->Empty(j);
+    if (!useG && !useS) return;
+    int b = *hb, e = *he, rb, re;
+    if (useG) { row_range(*guide, j, scoreDiff, &rb, &re); b = min(rb, b); e = max(re, e); }
+    if (useS) { row_range(*self, j, scoreDiff, &rb, &re); b = min(rb, b); e = max(re, e); }
+    *hb = b;
+    *he = e;
+}
+
+__device__ __forceinline__ void put(const QBand& m, long long k, float v, bool& ovf)
+{
+    if (k < m.cap) m.val[k] = v;
+    else ovf = true;
+}
+
+// ---- SseRecursor::FillAlpha (SseRecursor.cpp:73-213) -----------------------------------------------------
+// `prev`: this matrix's previous pass (RangeGuide's self hint); `out`: the arena written now.  Rows come
+// top-down, so column j's cells are appended at `used` as they are produced.
+__device__ long long fill_alpha(const QEval& e, const QBand* guide, const QBand* prev, const QBand& out,
+                                QAlloc* alloc, bool allocExists, bool& ovf)
+{
+    const int I = e.I(), J = e.J();
+    const bool sp = e.p->sumProduct != 0;
+    const bool merge = (e.p->moves & kMerge) != 0;
+    const float sd = e.p->scoreDiff;
+    long long used = 0;
+    int hb = 0, he = 0;
+    for (int j = 0; j <= J; ++j) {
+        range_guide(j, guide, prev, sd, &hb, &he);
+        const int reqEnd = min(I + 1, he);
+        float score = kNegInf, thr = kNegInf, mx = kNegInf;
+        if (alloc) alloc_start(alloc[j], allocExists, hb, he, I + 1);
+        const int beginRow = hb;
+        out.off[j] = (int)min(used, (long long)0x7fffffff);
+        out.range[j] = make_int2(beginRow, beginRow);   // grows with each row, so reads of it stay exact
+        auto set = [&](int r, float v) {
+            put(out, used + (r - beginRow), v, ovf);
+            out.range[j].y = r + 1;
+            if (alloc) alloc_set(alloc[j], r, I + 1);
+        };
+        int i;
+        for (i = beginRow; (i == 0 || (I - i + 1) % 4 != 0) && i <= I; i++) {
+            score = kNegInf;
+            if (i == 0 && j == 0) score = 0.0f;
+            if (i > 0 && j > 0) score = comb(sp, score, out.Get(i - 1, j - 1) + e.Inc(i - 1, j - 1));
+            if (merge && i > 0 && j > 1) score = comb(sp, score, out.Get(i - 1, j - 2) + e.Merge(i - 1, j - 2));
+            if (j > 0) score = comb(sp, score, out.Get(i, j - 1) + e.Del(i, j - 1));
+            if (i > 0) score = comb(sp, score, out.Get(i - 1, j) + e.Extra(i - 1, j));
+            set(i, score);
+            if (score > mx) { mx = score; thr = mx - sd; }
+        }
+        for (; i <= I && (score >= thr || i < reqEnd); i += 4) {
+            float s5[5];
+            s5[0] = out.Get(i - 1, j);
+            for (int k = 0; k < 4; ++k) {
+                const int r = i + k;
+                float v = kNegInf;
+                if (j > 0) v = comb4(sp, v, out.Get(r - 1, j - 1) + e.Inc(r - 1, j - 1));
+                if (merge && j >= 2) v = comb4(sp, v, out.Get(r - 1, j - 2) + e.Merge(r - 1, j - 2));
+                if (j > 0) v = comb4(sp, v, out.Get(r, j - 1) + e.Del(r, j - 1));
+                s5[k + 1] = v;
+            }
+            for (int ii = 1; ii < 5; ++ii) {   // Extra cascade (:175-183)
+                s5[ii] = comb(sp, s5[ii], s5[ii - 1] + e.Extra(i + ii - 2, j));
+                set(i + ii - 1, s5[ii]);
+            }
+            float pmax = s5[1], pmin = s5[1];   // std::max_element / std::min_element
+            for (int ii = 2; ii < 5; ++ii) {
+                if (pmax < s5[ii]) pmax = s5[ii];
+                if (s5[ii] < pmin) pmin = s5[ii];
+            }
+            score = pmin;
+            if (pmax > mx) { mx = pmax; thr = mx - sd; }
+        }
+        const int endRow = i;
+        out.range[j] = make_int2(beginRow, endRow);
+        used += endRow - beginRow;
+        he = endRow;
+        for (i = beginRow; i < endRow && out.Get(i, j) < thr; ++i) {}
+        hb = i;
+    }
+    return used;
+}
+
+// ---- SseRecursor::FillBeta (SseRecursor.cpp:216-353) -----------------------------------------------------
+// Rows come bottom-up and the column's first row is known only at its end: cells go to the read's column
+// buffer (indexed by row) and are copied top-down into the arena when the column is finished.
+__device__ long long fill_beta(const QEval& e, const QBand* guide, const QBand* prev, const QBand& out,
+                               float* colbuf, QAlloc* alloc, bool allocExists, bool& ovf)
+{
+    const int I = e.I(), J = e.J();
+    const bool sp = e.p->sumProduct != 0;
+    const bool merge = (e.p->moves & kMerge) != 0;
+    const float sd = e.p->scoreDiff;
+    long long used = 0;
+    int hb = I + 1, he = I + 1;
+    for (int j = J; j >= 0; --j) {
+        range_guide(j, guide, prev, sd, &hb, &he);
+        const int reqBegin = max(0, hb);
+        float score = kNegInf, thr = kNegInf, mx = kNegInf;
+        if (alloc) alloc_start(alloc[j], allocExists, hb, he, I + 1);
+        const int endRow = he;
+        int lo = endRow;   // rows [lo, endRow) of this column are in colbuf
+        auto get = [&](int r, int c) -> float {
+            if (c == j) return (r >= lo && r < endRow) ? colbuf[r] : kNegInf;
+            return out.Get(r, c);
+        };
+        auto set = [&](int r, float v) {
+            colbuf[r] = v;
+            lo = r;
+            if (alloc) alloc_set(alloc[j], r, I + 1);
+        };
+        int i;
+        for (i = endRow - 1; (i == I || (i + 1) % 4 != 0) && i >= 0; i--) {
+            score = kNegInf;
+            if (i == I && j == J) score = 0.0f;
+            if (i < I && j < J) score = comb(sp, score, get(i + 1, j + 1) + e.Inc(i, j));
+            if (merge && j < J - 1 && i < I) score = comb(sp, score, get(i + 1, j + 2) + e.Merge(i, j));
+            if (j < J) score = comb(sp, score, get(i, j + 1) + e.Del(i, j));
+            if (i < I) score = comb(sp, score, get(i + 1, j) + e.Extra(i, j));
+            set(i, score);
+            if (score > mx) { mx = score; thr = mx - sd; }
+        }
+        i = i - 3;
+        for (; i >= 0 && (score >= thr || i >= reqBegin); i -= 4) {
+            float s5[5];
+            for (int k = 0; k < 4; ++k) {
+                const int r = i + k;
+                float v = kNegInf;
+                if (i < I && j < J) v = comb4(sp, v, get(r + 1, j + 1) + e.Inc(r, j));
+                if (merge && j < J - 1 && i < I) v = comb4(sp, v, get(r + 1, j + 2) + e.Merge(r, j));
+                if (j < J) v = comb4(sp, v, get(r, j + 1) + e.Del(r, j));
+                s5[k] = v;
+            }
+            s5[4] = get(i + 4, j);
+            for (int ii = 3; ii >= 0; ii--) {
+                s5[ii] = comb(sp, s5[ii], s5[ii + 1] + e.Extra(i + ii, j));
+                set(i + ii, s5[ii]);
+            }
+            float pmax = s5[0], pmin = s5[0];
+            for (int ii = 1; ii < 4; ++ii) {
+                if (pmax < s5[ii]) pmax = s5[ii];
+                if (s5[ii] < pmin) pmin = s5[ii];
+            }
+            score = pmin;
+            if (pmax > mx) { mx = pmax; thr = mx - sd; }
+        }
+        const int beginRow = i + 4;
+        out.off[j] = (int)min(used, (long long)0x7fffffff);
+        for (int r = beginRow; r < endRow; ++r) put(out, used + (r - beginRow), colbuf[r], ovf);
+        out.range[j] = make_int2(beginRow, endRow);
+        used += endRow - beginRow;
+        hb = beginRow;
+        for (i = endRow; i > beginRow && out.Get(i - 1, j) < thr; i--) {}
+        he = i;
+    }
+    return used;
+}
+
+// ---- SseRecursor::ExtendAlpha (SseRecursor.cpp:433-551) --------------------------------------------------
+__device__ void extend_alpha(const QEval& e, const QBand& a, int beginColumn, const QBand& ext, int numExt, bool& ovf)
+{
+    const bool sp = e.p->sumProduct != 0;
+    const bool merge = (e.p->moves & kMerge) != 0;
+    long long used = 0;
+    for (int c = 0; c < numExt; c++) {
+        const int j = beginColumn + c;
+        int beginRow, endRow;
+        if (j < a.cols) { beginRow = a.range[j].x; endRow = a.range[j].y; }
+        else { beginRow = a.range[a.cols - 1].x; endRow = e.I() + 1; }
+        ext.off[c] = (int)used;
+        ext.range[c] = make_int2(beginRow, beginRow);
+        auto set = [&](int r, float v) {
+            put(ext, used + (r - beginRow), v, ovf);
+            ext.range[c].y = r + 1;
+        };
+        auto prevCol = [&](int r) { return c == 0 ? a.Get(r, j - 1) : ext.Get(r, c - 1); };
+        int i;
+        for (i = beginRow; (i == 0 || (endRow - i) % 4 != 0) && i < endRow; i++) {
+            float score = kNegInf;
+            if (i > 0) {
+                score = comb(sp, score, prevCol(i - 1) + e.Inc(i - 1, j - 1));
+                score = comb(sp, score, ext.Get(i - 1, c) + e.Extra(i - 1, j));
+                if (merge) score = comb(sp, score, a.Get(i - 1, j - 2) + e.Merge(i - 1, j - 2));
+            }
+            score = comb(sp, score, prevCol(i) + e.Del(i, j - 1));
+            set(i, score);
+        }
+        for (; i < endRow - 3; i += 4) {
+            float s5[5];
+            s5[0] = ext.Get(i - 1, c);
+            for (int k = 0; k < 4; ++k) {
+                const int r = i + k;
+                float v = kNegInf;
+                v = comb4(sp, v, prevCol(r - 1) + e.Inc(r - 1, j - 1));
+                if (merge && j >= 2) v = comb4(sp, v, a.Get(r - 1, j - 2) + e.Merge(r - 1, j - 2));
+                v = comb4(sp, v, prevCol(r) + e.Del(r, j - 1));
+                s5[k + 1] = v;
+            }
+            for (int ii = 1; ii < 5; ii++) {
+                s5[ii] = comb(sp, s5[ii], s5[ii - 1] + e.Extra(i + ii - 2, j));
+                set(i + ii - 1, s5[ii]);
+            }
+        }
+        ext.range[c] = make_int2(beginRow, endRow);
+        used += endRow - beginRow;
+    }
+}
+
+// ---- SimpleRecursor::ExtendBeta (Quiver/SimpleRecursor.cpp:407-495) ---------------------------------------
+__device__ void extend_beta(const QEval& e, const QBand& b, int lastColumn, const QBand& ext, int numExt,
+                            int lengthDiff, bool& ovf)
+{
+    const bool sp = e.p->sumProduct != 0;
+    const bool merge = (e.p->moves & kMerge) != 0;
+    const int I = e.I();
+    const int J = b.cols - 1;
+    const int lastExt = numExt - 1;
+    long long used = 0;
+    for (int j = lastColumn; j > lastColumn - numExt; j--) {
+        const int jp = j + lengthDiff;
+        const int c = lastExt - (lastColumn - j);
+        int beginRow, endRow;
+        if (j < 0) { beginRow = 0; endRow = b.range[0].y; }
+        else { beginRow = b.range[j].x; endRow = b.range[j].y; }
+        ext.off[c] = (int)used;
+        // rows are produced bottom-up and only rows below the one being computed are still unset; they are
+        // never read (the column's reads are ext(i + 1, c)), so the final range is valid from the start
+        ext.range[c] = make_int2(beginRow, endRow);
+        for (int i = endRow - 1; i >= beginRow; i--) {
+            float score = kNegInf;
+            if (i < I && j < J) {
+                const float prev = (c == lastExt) ? b.Get(i + 1, j + 1) : ext.Get(i + 1, c + 1);
+                score = comb(sp, score, prev + e.Inc(i, jp));
+            }
+            if (i < I) score = comb(sp, score, ext.Get(i + 1, c) + e.Extra(i, jp));
+            if (j < J) {
+                const float prev = (c == lastExt) ? b.Get(i, j + 1) : ext.Get(i, c + 1);
+                score = comb(sp, score, prev + e.Del(i, jp));
+            }
+            if (merge && j < J - 1 && i < I) score = comb(sp, score, b.Get(i + 1, j + 2) + e.Merge(i, jp));
+            put(ext, used + (i - beginRow), score, ovf);
+        }
+        used += max(0, endRow - beginRow);
+    }
+}
+
+// ---- SseRecursor::LinkAlphaBeta (SseRecursor.cpp:355-431) ------------------------------------------------
+__device__ float link_alpha_beta(const QEval& e, const QBand& a, int ac, const QBand& b, int bc, int absc)
+{
+    const bool sp = e.p->sumProduct != 0;
+    const bool merge = (e.p->moves & kMerge) != 0;
+    const int I = e.I();
+    const int ub = min(min(a.range[ac - 2].x, a.range[ac - 1].x), min(b.range[bc].x, b.range[bc + 1].x));
+    const int ue = max(max(a.range[ac - 2].y, a.range[ac - 1].y), max(b.range[bc].y, b.range[bc + 1].y));
+    float v = kNegInf;
+    float v4[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
+    int i;
+    for (i = ub; i < ue - 4; i += 4) {
+        for (int k = 0; k < 4; ++k) {
+            const int r = i + k;
+            v4[k] = comb4(sp, v4[k], a.Get(r, ac - 1) + e.Inc(r, absc - 1) + b.Get(r + 1, bc));
+            if (merge) {
+                v4[k] = comb4(sp, v4[k], a.Get(r, ac - 2) + e.Merge(r, absc - 2) + b.Get(r + 1, bc));
+                v4[k] = comb4(sp, v4[k], a.Get(r, ac - 1) + e.Merge(r, absc - 1) + b.Get(r + 1, bc + 1));
+            }
+            v4[k] = comb4(sp, v4[k], a.Get(r, ac - 1) + e.Del(r, absc - 1) + b.Get(r, bc));
+        }
+    }
+    for (; i < ue; i++) {
+        if (i < I) {
+            v = comb(sp, v, a.Get(i, ac - 1) + e.Inc(i, absc - 1) + b.Get(i + 1, bc));
+            if (merge) {
+                v = comb(sp, v, a.Get(i, ac - 2) + e.Merge(i, absc - 2) + b.Get(i + 1, bc));
+                v = comb(sp, v, a.Get(i, ac - 1) + e.Merge(i, absc - 1) + b.Get(i + 1, bc + 1));
+            }
+        }
+        v = comb(sp, v, a.Get(i, ac - 1) + e.Del(i, absc - 1) + b.Get(i, bc));
+    }
+    float acc = kNegInf;   // std::accumulate(v_array, v_array + 5, NEG_INF, C::Combine)
+    for (int k = 0; k < 4; ++k) acc = comb(sp, acc, v4[k]);
+    return comb(sp, acc, v);
+}
+
+// ---- per-read views -----------------------------------------------------------------------------------
+struct ReadView {
+    QRead rd;
+    QEval ev;
+    QBand arena[4];   // alpha 0, alpha 1, beta 0, beta 1
+    QAlloc* allocA;
+    QAlloc* allocB;
+    float* colbuf;
+};
+
+__device__ ReadView read_view(const QBatch& B, int r)
+{
+    ReadView v;
+    const int z = B.rZmw[r];
+    const int I = B.rLen[r];
+    const long long so = B.rSeq[r];
+    v.rd.seq = B.seqPool + so;
+    const float* f = B.featPool + 5 * so;
+    v.rd.ins = f;
+    v.rd.subs = f + I;
+    v.rd.del = f + 2 * I;
+    v.rd.tag = f + 3 * I;
+    v.rd.merge = f + 4 * I;
+    v.rd.I = I;
+    const int ts = B.rTs[r], te = B.rTe[r], L = B.zLen[z];
+    v.ev.r = &v.rd;
+    v.ev.p = B.params + B.rParam[r];
+    v.ev.t.base = B.tplPool + (B.rStrand[r] == 0 ? B.zFwd[z] + ts : B.zRev[z] + (L - te));
+    v.ev.t.len = te - ts;
+    v.ev.t.editPos = -1;
+    const long long cb = B.rColBase[r];
+    const int cc = B.rColCap[r];
+    const long long vb = B.rValBase[r], vc = B.rValCap[r];
+    for (int k = 0; k < 4; ++k) {
+        v.arena[k].range = B.range + cb + (long long)k * cc;
+        v.arena[k].off = B.off + cb + (long long)k * cc;
+        v.arena[k].val = B.valPool + vb + (long long)k * vc;
+        v.arena[k].cap = vc;
+        v.arena[k].cols = te - ts + 1;
+    }
+    v.allocA = B.alloc + cb / 2;   // 2 x colCap alloc slots per read (colBase advances by 4 x colCap)
+    v.allocB = v.allocA + cc;
+    v.colbuf = B.valPool + B.rColBuf[r];
+    return v;
+}
+
+__device__ long long used_entries(const QBand& m)
+{
+    long long s = 0;
+    for (int j = 0; j < m.cols; ++j) s += max(0, m.range[j].y - m.range[j].x);
+    return s;
+}
+
+__device__ long long allocated_entries(const QAlloc* a, int cols)
+{
+    long long s = 0;
+    for (int j = 0; j < cols; ++j) s += a[j].capacity;
+    return s;
+}
+
+}  // namespace
+
+// ---- k_qfill: MutationScorer ctor / Template() -> FillAlphaBeta ------------------------------------------
+__global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ reads, int n)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int r = reads[t];
+    ReadView v = read_view(B, r);
+    v.ev.r = &v.rd;
+    const QEval& e = v.ev;
+    const int I = e.I(), J = e.J();
+    if (I < 1 || J < 1 || J + 1 > B.rColCap[r]) {
+        B.rStatus[r] = kQBad;
+        return;
+    }
+    for (int k = 0; k < 4; ++k)
+        for (int j = 0; j <= J; ++j) v.arena[k].range[j] = make_int2(0, 0);
+    bool ovf = false;
+    long long needA = 0, needB = 0;
+    int curA = 0, curB = 2;   // arena index of the latest alpha / beta pass
+    bool aPassed = false, bPassed = false;
+    auto passA = [&](bool guided) {
+        const int nxt = aPassed ? (curA ^ 1) : 0;
+        const long long u = fill_alpha(e, guided ? &v.arena[curB] : nullptr, aPassed ? &v.arena[curA] : nullptr,
+                                       v.arena[nxt], v.allocA, aPassed, ovf);
+        needA = max(needA, u);
+        curA = nxt;
+        aPassed = true;
+        return u;
+    };
+    auto passB = [&]() {
+        const int nxt = bPassed ? (curB ^ 1) : 2;
+        const long long u = fill_beta(e, &v.arena[curA], bPassed ? &v.arena[curB] : nullptr, v.arena[nxt], v.colbuf,
+                                      v.allocB, bPassed, ovf);
+        needB = max(needB, u);
+        curB = nxt;
+        bPassed = true;
+        return u;
+    };
+    // RecursorBase::FillAlphaBeta (detail/RecursorBase.cpp:70-116)
+    const long long ua = passA(false);
+    const long long ub = passB();
+    int flips = 0;
+    const int maxSize = (int)(0.5 + 0.04 * (I + 1) * (J + 1));   // REBANDING_THRESHOLD, double arithmetic
+    if (!ovf && (ua >= maxSize || ub >= maxSize)) {
+        passA(true);
+        passB();
+        passA(true);
+        flips += 3;
+    }
+    auto a_end = [&]() { return v.arena[curA].Get(I, J); };
+    auto b_start = [&]() { return v.arena[curB].Get(0, 0); };
+    // fabs(a(I, J) - b(0, 0)) > ALPHA_BETA_MISMATCH_TOLERANCE: a float difference against the double 0.2
+    while (!ovf && (double)fabsf(a_end() - b_start()) > 0.2 && flips <= kMaxFlipFlops) {
+        if (flips % 2 == 0) passA(true);
+        else passB();
+        flips++;
+    }
+    B.rUsed[2 * r] = needA;
+    B.rUsed[2 * r + 1] = needB;
+    if (ovf) {
+        B.rStatus[r] = kQOverflow;
+        return;
+    }
+    B.rCurA[r] = curA;
+    B.rCurB[r] = curB - 2;
+    B.rFlips[r] = flips;
+    B.rScore[r] = b_start();
+    B.rAlloc[2 * r] = allocated_entries(v.allocA, J + 1);
+    B.rAlloc[2 * r + 1] = allocated_entries(v.allocB, J + 1);
+    B.rStatus[r] = ((double)fabsf(a_end() - b_start()) > 0.2) ? kQMismatch : kQOk;
+}
+
+// ---- k_qscore: MultiReadMutationScorer::Score terms (Quiver/MultiReadMutationScorer.cpp:60-120, 312-326)
+__global__ void __launch_bounds__(64) k_qscore(QBatch B, QScoreWork W)
+{
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= W.nTasks) return;
+    const int r = W.taskRead[t];
+    const int code = W.codes[W.taskMut[t]];
+    const int type = (code >> 2) & 3, pos = code >> 4, base = code & 3;
+    const int ms = pos, me = (type == 0) ? pos : pos + 1;
+    const int ts = B.rTs[r], te = B.rTe[r];
+    const bool scores = W.raw || ((type == 0) ? (ts < ms && me <= te) : (ts < me && ms < te));   // ReadScoresMutation
+    if (!scores) {
+        W.delta[t] = __builtin_nanf("");
+        return;
+    }
+    ReadView v = read_view(B, r);
+    v.ev.r = &v.rd;
+    QEval& e = v.ev;
+    const char kB[4] = {'A', 'C', 'G', 'T'};
+    // OrientedMutation (:79-120), single-base mutations
+    int os, oe;
+    char ob;
+    if (W.raw) { os = ms; oe = me; ob = kB[base]; }
+    else if (B.rStrand[r] == 0) { os = ms - ts; oe = me - ts; ob = kB[base]; }
+    else { os = te - me; oe = te - ms; ob = kB[3 - base]; }
+    const QBand& a = v.arena[B.rCurA[r]];
+    const QBand& b = v.arena[2 + B.rCurB[r]];
+    const int J = e.J();   // unmutated window length
+    const int lengthDiff = (type == 0) ? 1 : (type == 1) ? -1 : 0;
+    // MutationScorer::ScoreMutation (Quiver/MutationScorer.cpp:113-226)
+    const int betaLinkCol = 1 + oe;
+    const int absLinkCol = 1 + oe + lengthDiff;
+    const bool atBegin = os < 3;
+    const bool atEnd = oe > J - 2;
+    e.t.editPos = os;
+    e.t.editType = type;
+    e.t.editBase = ob;
+    e.t.len = J + lengthDiff;
+    const int newLen = e.t.len;
+    // extend buffer: at most 8 columns (EXTEND_BUFFER_COLUMNS), values bump-allocated from the pool
+    int2 xr[8];
+    int xo[8];
+    QBand ext;
+    ext.range = xr;
+    ext.off = xo;
+    ext.cols = 8;
+    const int I = e.I();
+    auto alloc = [&](long long n) -> bool {
+        const unsigned long long at = atomicAdd(W.scratchTop, (unsigned long long)n);
+        if (at + n > W.scratchCap) {
+            atomicOr(W.overflow, 1);
+            return false;
+        }
+        ext.val = W.scratch + at;
+        ext.cap = n;
+        return true;
+    };
+    bool ovf = false;
+    float score;
+    if (!atBegin && !atEnd) {
+        const int extStart = (type == 1) ? os - 1 : os;
+        const int extLen = 2;
+        long long need = 0;
+        for (int c = 0; c < extLen; ++c) {
+            const int j = extStart + c;
+            need += (j < a.cols) ? (a.range[j].y - a.range[j].x) : (I + 1 - a.range[a.cols - 1].x);
+        }
+        if (!alloc(max(need, 1LL))) { W.delta[t] = __builtin_nanf(""); return; }
+        extend_alpha(e, a, extStart, ext, extLen, ovf);
+        score = link_alpha_beta(e, ext, extLen, b, betaLinkCol, absLinkCol);
+    } else if (!atBegin && atEnd) {
+        const int extStart = os - 1;
+        const int extLen = newLen - extStart + 1;
+        if (extLen > 8) { atomicOr(W.overflow, 2); W.delta[t] = __builtin_nanf(""); return; }
+        if (!alloc((long long)extLen * (I + 1))) { W.delta[t] = __builtin_nanf(""); return; }
+        extend_alpha(e, a, extStart, ext, extLen, ovf);
+        score = ext.Get(I, extLen - 1);
+    } else if (atBegin && !atEnd) {
+        const int extLast = oe;
+        const int extLen = oe + lengthDiff + 1;
+        if (extLen > 8) { atomicOr(W.overflow, 2); W.delta[t] = __builtin_nanf(""); return; }
+        if (!alloc((long long)extLen * (I + 1))) { W.delta[t] = __builtin_nanf(""); return; }
+        extend_beta(e, b, extLast, ext, extLen, lengthDiff, ovf);
+        score = ext.Get(0, 0);
+    } else {
+        // whole fill of the mutated window (tiny windows only)
+        if (newLen + 1 > 8) { atomicOr(W.overflow, 2); W.delta[t] = __builtin_nanf(""); return; }
+        if (!alloc((long long)(newLen + 1) * (I + 1))) { W.delta[t] = __builtin_nanf(""); return; }
+        ext.cols = newLen + 1;
+        for (int j = 0; j < ext.cols; ++j) xr[j] = make_int2(0, 0);
+        fill_alpha(e, nullptr, nullptr, ext, nullptr, false, ovf);
+        score = ext.Get(I, newLen);
+    }
+    if (ovf) atomicOr(W.overflow, 1);
+    W.delta[t] = W.raw ? score : score - B.rScore[r];
+}
+
+void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s)
+{
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_qfill, dim3((n + 63) / 64), dim3(64), 0, s, B, reads, n);
+}
+
+void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s)
+{
+    if (W.nTasks <= 0) return;
+    hipLaunchKernelGGL(k_qscore, dim3((unsigned)((W.nTasks + 63) / 64)), dim3(64), 0, s, B, W);
+}
+
+}  // namespace quiver
+}  // namespace pbccs

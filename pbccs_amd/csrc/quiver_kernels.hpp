@@ -1,0 +1,69 @@
+// pbccs_amd/csrc/quiver_kernels.hpp -- launch interface of the Quiver kernels (quiver_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "quiver_device.hpp"
+
+namespace pbccs {
+namespace quiver {
+
+// Batch of Quiver scorers resident in HBM (struct of arrays; see quiver_engine.hpp for the host side).
+struct QBatch {
+    // per scorer (a ZMW's template + config)
+    const long long* zFwd;     // forward template offset in tplPool
+    const long long* zRev;     // reverse-complement template offset
+    const int* zLen;
+    const char* tplPool;
+    const QParams* params;     // per read config (QuiverConfigTable lookup done on the host)
+    // per read
+    const int* rZmw;
+    const int* rParam;
+    const int* rStrand;
+    const int* rTs;
+    const int* rTe;
+    const int* rLen;
+    const long long* rSeq;     // offset of the bases in seqPool and of the 5 feature tracks in featPool
+    const char* seqPool;
+    const float* featPool;     // 5 consecutive tracks per read: ins, subs, del, tag, merge (each rLen floats)
+    const long long* rColBase; // column slots: 4 arenas (alpha 0/1, beta 0/1) x colCap + alloc slots
+    const int* rColCap;
+    const long long* rValBase; // 4 value arenas of rValCap floats each
+    const long long* rValCap;
+    const long long* rColBuf;  // beta column buffer (rLen + 1 floats) in valPool
+    int2* range;
+    int* off;
+    QAlloc* alloc;             // 2 x colCap per read (alpha, beta): AllocatedEntries bookkeeping
+    float* valPool;
+    // fill results
+    int* rCurA;                // arena (0/1) holding the final alpha / beta
+    int* rCurB;
+    float* rScore;             // MutationScorer::Score() = beta(0, 0)
+    int* rFlips;
+    int* rStatus;
+    long long* rUsed;          // [2 r] alpha / [2 r + 1] beta values needed (overflow sizing)
+    long long* rAlloc;         // [2 r] alpha / [2 r + 1] beta AllocatedEntries
+};
+
+__host__ __device__ inline int qcols(int J) { return J + 1; }
+
+// Scoring work: per (mutation, read) task of one scorer.
+struct QScoreWork {
+    const int* taskRead;       // read index
+    const int* taskMut;        // index into codes
+    const int* codes;          // pos << 4 | type << 2 | base (single-base mutations)
+    float* delta;              // ScoreMutation(oriented) - Score(), or NaN when the read does not score it
+    float* scratch;            // extend buffers, bump-allocated
+    unsigned long long* scratchTop;
+    unsigned long long scratchCap;
+    int* overflow;
+    long long nTasks;
+    int raw;                   // 1: codes are already in the read's own coordinates (MutationScorer API):
+                               //    no ReadScoresMutation / orientation, delta = the absolute score
+};
+
+void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s);
+void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s);
+
+}  // namespace quiver
+}  // namespace pbccs

@@ -64,6 +64,18 @@ class CCounters(ctypes.Structure):
                 ("score_tasks", ctypes.c_longlong), ("mutations", ctypes.c_longlong)]
 
 
+class CQvModelParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in ("match", "mismatch", "mismatch_s", "branch", "branch_s", "deletion_n",
+                                              "deletion_with_tag", "deletion_with_tag_s", "nce", "nce_s")] + \
+               [("merge", ctypes.c_float * 4), ("merge_s", ctypes.c_float * 4)]
+
+
+class CQuiverConfig(ctypes.Structure):
+    _fields_ = [("params", CQvModelParams), ("moves_available", ctypes.c_int), ("score_diff", ctypes.c_float),
+                ("fast_score_threshold", ctypes.c_float), ("add_threshold", ctypes.c_float),
+                ("sum_product", ctypes.c_int)]
+
+
 # exported symbol -> (restype, argtypes); tests check that every symbol of include/pbccs_amd.h is exported
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -72,6 +84,7 @@ PI = ctypes.POINTER(ctypes.c_int)
 PD = ctypes.POINTER(ctypes.c_double)
 PLL = ctypes.POINTER(ctypes.c_longlong)
 PM = ctypes.POINTER(CMutation)
+PF = ctypes.POINTER(ctypes.c_float)
 SIGNATURES = {
     "pbccs_engine_create": (I, [I, ctypes.POINTER(P)]),
     "pbccs_engine_destroy": (None, [P]),
@@ -106,6 +119,26 @@ SIGNATURES = {
     "pbccs_engine_set_concurrency": (I, [P, I]),
     "pbccs_engine_set_profiling": (I, [P, I]),
     "pbccs_engine_kernel_stats": (I, [P, ctypes.POINTER(CKernelStat), I, PI, I]),
+    # Quiver family
+    "pbccs_quiver_scorer_create": (I, [P, ctypes.POINTER(CQuiverConfig), ctypes.POINTER(ctypes.c_char_p), I,
+                                       ctypes.c_char_p, I, ctypes.POINTER(P)]),
+    "pbccs_quiver_scorer_destroy": (None, [P]),
+    "pbccs_quiver_scorer_add_read": (I, [P, ctypes.c_char_p, I, PF, PF, PF, PF, PF, ctypes.c_char_p, I, I, I,
+                                         ctypes.c_float, PI]),
+    "pbccs_quiver_scorer_score_many": (I, [P, PM, I, I, PF]),
+    "pbccs_quiver_scorer_scores": (I, [P, PM, ctypes.c_float, PF]),
+    "pbccs_quiver_scorer_read_score_mutation": (I, [P, I, PM, PF]),
+    "pbccs_quiver_scorer_is_favorable": (I, [P, PM, I, PI]),
+    "pbccs_quiver_scorer_apply_mutations": (I, [P, PM, I]),
+    "pbccs_quiver_scorer_template": (I, [P, I, ctypes.c_char_p, I, PI]),
+    "pbccs_quiver_scorer_num_reads": (I, [P]),
+    "pbccs_quiver_scorer_read_info": (I, [P, I, PI, PI, PI, PI]),
+    "pbccs_quiver_scorer_baseline_score": (I, [P, PF]),
+    "pbccs_quiver_scorer_baseline_scores": (I, [P, PF, I, PI]),
+    "pbccs_quiver_scorer_num_flipflops": (I, [P, PI]),
+    "pbccs_quiver_scorer_allocated_entries": (I, [P, I, PLL, PLL]),
+    "pbccs_quiver_refine_consensus": (I, [P, ctypes.POINTER(CRefineOptions), PLL, PLL, PI]),
+    "pbccs_quiver_consensus_qvs": (I, [P, PI, I, PI]),
 }
 
 

@@ -1,0 +1,219 @@
+"""Quiver family mirror (ConsensusCore/include/ConsensusCore/Quiver/): QvModelParams, QuiverConfig,
+QuiverConfigTable and MultiReadMutationScorer over the HIP engine's C ABI (include/pbccs_amd.h,
+pbccs_quiver_*).  Viterbi = SparseSseQvRecursor, sum-product = SparseSseQvSumProductRecursor
+(Quiver/MultiReadMutationScorer.hpp:242-245).  No CPU fallback."""
+import ctypes
+import math
+
+from . import lib as _lib_mod
+from .lib import load
+
+INCORPORATE, EXTRA, DELETE, MERGE = 1, 2, 4, 8
+BASIC_MOVES, ALL_MOVES = 7, 15
+_PARAM_FIELDS = ("Match", "Mismatch", "MismatchS", "Branch", "BranchS", "DeletionN", "DeletionWithTag",
+                 "DeletionWithTagS", "Nce", "NceS")
+
+
+class QvModelParams:
+    """QvModelParams (QuiverConfig.hpp:79-176): Merge / MergeS may be one rate or four per-base rates."""
+
+    def __init__(self, chemistry="*", model="", **kw):
+        self.ChemistryName, self.ModelName = chemistry, model
+        for k in _PARAM_FIELDS:
+            setattr(self, k, float(kw.get(k, 0.0)))
+        for k in ("Merge", "MergeS"):
+            v = kw.get(k, 0.0)
+            setattr(self, k, [float(x) for x in v] if isinstance(v, (list, tuple)) else [float(v)] * 4)
+
+    def _c(self):
+        c = _lib_mod.CQvModelParams()
+        for k, cn in zip(_PARAM_FIELDS, ("match", "mismatch", "mismatch_s", "branch", "branch_s", "deletion_n",
+                                         "deletion_with_tag", "deletion_with_tag_s", "nce", "nce_s")):
+            setattr(c, cn, getattr(self, k))
+        for i in range(4):
+            c.merge[i] = self.Merge[i]
+            c.merge_s[i] = self.MergeS[i]
+        return c
+
+
+class QuiverConfig:
+    """QuiverConfig (QuiverConfig.hpp:181-199); BandingOptions(diagCross, scoreDiff) -> score_diff."""
+
+    def __init__(self, params, moves=ALL_MOVES, score_diff=12.5, fast_score_threshold=-12.5, add_threshold=1.0,
+                 sum_product=False):
+        self.QvParams, self.MovesAvailable = params, moves
+        self.ScoreDiff, self.FastScoreThreshold, self.AddThreshold = score_diff, fast_score_threshold, add_threshold
+        self.SumProduct = sum_product
+
+    def _c(self):
+        c = _lib_mod.CQuiverConfig()
+        c.params = self.QvParams._c()
+        c.moves_available = self.MovesAvailable
+        c.score_diff = self.ScoreDiff
+        c.fast_score_threshold = self.FastScoreThreshold
+        c.add_threshold = self.AddThreshold
+        c.sum_product = 1 if self.SumProduct else 0
+        return c
+
+
+class QuiverConfigTable:
+    """QuiverConfigTable (QuiverConfig.cpp:67-138): Insert (by chemistry), InsertAs, InsertDefault ("*")."""
+
+    def __init__(self):
+        self.entries = []
+
+    def InsertAs(self, name, config):
+        if name == "*":
+            raise ValueError("Cannot Insert(...) a QuiverConfig with chemistry '*'")
+        return self._insert(name, config)
+
+    def Insert(self, config):
+        return self.InsertAs(config.QvParams.ChemistryName, config)
+
+    def InsertDefault(self, config):
+        return self._insert("*", config)
+
+    def _insert(self, name, config):
+        if any(n == name for n, _ in self.entries):
+            return False
+        self.entries.insert(0, (name, config))
+        return True
+
+
+class QuiverMultiReadMutationScorer:
+    """MultiReadMutationScorer<SparseSse{Qv,QvSumProduct}Recursor> (Quiver/MultiReadMutationScorer.cpp)."""
+
+    def __init__(self, configs, tpl, engine=None):
+        from . import default_engine
+        if isinstance(configs, QuiverConfig):
+            t = QuiverConfigTable()
+            t.InsertDefault(configs)
+            configs = t
+        self._eng = engine or default_engine()
+        n = len(configs.entries)
+        arr = (_lib_mod.CQuiverConfig * n)(*[c._c() for _, c in configs.entries])
+        names = (ctypes.c_char_p * n)(*[name.encode() for name, _ in configs.entries])
+        h = ctypes.c_void_p()
+        _lib_mod.check(load().pbccs_quiver_scorer_create(self._eng._h, arr, names, n, tpl.encode(), len(tpl),
+                                                          ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            load().pbccs_quiver_scorer_destroy(self._h)
+            self._h = None
+
+    def AddRead(self, seq, strand=0, template_start=0, template_end=None, ins_qv=None, subs_qv=None, del_qv=None,
+                del_tag=None, merge_qv=None, chemistry="*", threshold=None):
+        if template_end is None:
+            template_end = self.TemplateLength()
+
+        def arr(v, tag=False):
+            if v is None:
+                return None
+            vals = [float(ord(x)) if tag and isinstance(x, str) else float(x) for x in v]
+            return (ctypes.c_float * len(vals))(*vals)
+
+        active = ctypes.c_int()
+        _lib_mod.check(load().pbccs_quiver_scorer_add_read(
+            self._h, seq.encode(), len(seq), arr(ins_qv), arr(subs_qv), arr(del_qv), arr(del_tag, True),
+            arr(merge_qv), chemistry.encode(), strand, template_start, template_end,
+            float("nan") if threshold is None else threshold, ctypes.byref(active)))
+        return bool(active.value)
+
+    def ScoreMany(self, muts, fast=False):
+        n = len(muts)
+        arr = (_lib_mod.CMutation * max(1, n))(*[m._c() for m in muts])
+        out = (ctypes.c_float * max(1, n))()
+        _lib_mod.check(load().pbccs_quiver_scorer_score_many(self._h, arr, n, 1 if fast else 0, out))
+        return list(out[:n])
+
+    def Score(self, m):
+        return self.ScoreMany([m])[0]
+
+    def FastScore(self, m):
+        return self.ScoreMany([m], fast=True)[0]
+
+    def ReadScoreMutation(self, i, m):
+        """MutationScorer::ScoreMutation on read i's scorer (read coordinates, absolute score)."""
+        v = ctypes.c_float()
+        c = m._c()
+        _lib_mod.check(load().pbccs_quiver_scorer_read_score_mutation(self._h, i, ctypes.byref(c), ctypes.byref(v)))
+        return v.value
+
+    def Scores(self, m, unscored_value=0.0):
+        out = (ctypes.c_float * max(1, self.NumReads()))()
+        c = m._c()
+        _lib_mod.check(load().pbccs_quiver_scorer_scores(self._h, ctypes.byref(c), unscored_value, out))
+        return list(out[: self.NumReads()])
+
+    def IsFavorable(self, m):
+        v = ctypes.c_int()
+        c = m._c()
+        _lib_mod.check(load().pbccs_quiver_scorer_is_favorable(self._h, ctypes.byref(c), 0, ctypes.byref(v)))
+        return bool(v.value)
+
+    def FastIsFavorable(self, m):
+        v = ctypes.c_int()
+        c = m._c()
+        _lib_mod.check(load().pbccs_quiver_scorer_is_favorable(self._h, ctypes.byref(c), 1, ctypes.byref(v)))
+        return bool(v.value)
+
+    def ApplyMutations(self, muts):
+        arr = (_lib_mod.CMutation * max(1, len(muts)))(*[m._c() for m in muts])
+        _lib_mod.check(load().pbccs_quiver_scorer_apply_mutations(self._h, arr, len(muts)))
+
+    def Template(self, strand=0):
+        buf = ctypes.create_string_buffer(1 << 22)
+        n = ctypes.c_int()
+        _lib_mod.check(load().pbccs_quiver_scorer_template(self._h, strand, buf, len(buf), ctypes.byref(n)))
+        return buf.value.decode()
+
+    def TemplateLength(self):
+        return len(self.Template())
+
+    def NumReads(self):
+        return load().pbccs_quiver_scorer_num_reads(self._h)
+
+    def ReadInfo(self, i):
+        a, s, ts, te = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib_mod.check(load().pbccs_quiver_scorer_read_info(self._h, i, ctypes.byref(a), ctypes.byref(s),
+                                                             ctypes.byref(ts), ctypes.byref(te)))
+        return {"active": bool(a.value), "strand": s.value, "template_start": ts.value, "template_end": te.value}
+
+    def BaselineScore(self):
+        v = ctypes.c_float()
+        _lib_mod.check(load().pbccs_quiver_scorer_baseline_score(self._h, ctypes.byref(v)))
+        return v.value
+
+    def BaselineScores(self):
+        out = (ctypes.c_float * max(1, self.NumReads()))()
+        n = ctypes.c_int()
+        _lib_mod.check(load().pbccs_quiver_scorer_baseline_scores(self._h, out, self.NumReads(), ctypes.byref(n)))
+        return list(out[: n.value])
+
+    def NumFlipFlops(self):
+        out = (ctypes.c_int * max(1, self.NumReads()))()
+        _lib_mod.check(load().pbccs_quiver_scorer_num_flipflops(self._h, out))
+        return list(out[: self.NumReads()])
+
+    def AllocatedEntries(self, i):
+        a, b = ctypes.c_longlong(), ctypes.c_longlong()
+        _lib_mod.check(load().pbccs_quiver_scorer_allocated_entries(self._h, i, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+
+def RefineConsensus(mms, max_iterations=40, mutation_separation=10, mutation_neighborhood=20):
+    o = _lib_mod.CRefineOptions(max_iterations, mutation_separation, mutation_neighborhood)
+    nt, na, conv = ctypes.c_longlong(0), ctypes.c_longlong(0), ctypes.c_int()
+    _lib_mod.check(load().pbccs_quiver_refine_consensus(mms._h, ctypes.byref(o), ctypes.byref(nt), ctypes.byref(na),
+                                                        ctypes.byref(conv)))
+    return bool(conv.value), nt.value, na.value
+
+
+def ConsensusQVs(mms):
+    cap = mms.TemplateLength()
+    out = (ctypes.c_int * max(1, cap))()
+    n = ctypes.c_int()
+    _lib_mod.check(load().pbccs_quiver_consensus_qvs(mms._h, out, cap, ctypes.byref(n)))
+    return list(out[: n.value])

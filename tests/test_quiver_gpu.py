@@ -1,0 +1,133 @@
+"""GPU parity of the Quiver family (HIP engine through the C ABI) against the reference's Quiver gtest
+known answers and against the CPU restatement (oracle/quiver_oracle.cpp) on seeded synthetic reads with
+random QV features.  Tolerance: bit-exact FP32 (every score, baseline, flip-flop count, refine outcome and
+QV), since the engine repeats the SSE recursor's single-precision operations in order."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.test_quiver_oracle_pins import run_kat
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+KATS = json.load(open(os.path.join(GOLD, "quiver_kats.json")))
+
+
+class GpuQuiver:
+    """Adapter with the oracle's QuiverScorer call shape over pbccs_amd's QuiverMultiReadMutationScorer."""
+
+    def __init__(self, tpl, params, moves=15, score_diff=12.5, fast_threshold=-12.5, add_threshold=1.0,
+                 sum_product=False):
+        import pbccs_amd as P
+        self.P = P
+        qp = P.QvModelParams(**params)
+        cfg = P.QuiverConfig(qp, moves=moves, score_diff=score_diff, fast_score_threshold=fast_threshold,
+                             add_threshold=add_threshold, sum_product=sum_product)
+        self.s = P.QuiverMultiReadMutationScorer(cfg, tpl)
+
+    def add_read(self, seq, strand=0, ts=0, te=None, features=None, threshold=None):
+        f = features or {}
+        return self.s.AddRead(seq, strand, ts, te, ins_qv=f.get("ins"), subs_qv=f.get("subs"), del_qv=f.get("del"),
+                              del_tag=f.get("del_tag"), merge_qv=f.get("merge"), threshold=threshold)
+
+    def score(self, t, p, b="-", fast=False):
+        return self.s.ScoreMany([self.P.Mutation(t, p, b)], fast=fast)[0]
+
+    def read_score_mutation(self, r, t, p, b="-"):
+        return self.s.ReadScoreMutation(r, self.P.Mutation(t, p, b))
+
+    def baseline(self):
+        return self.s.BaselineScore()
+
+    def apply(self, muts):
+        self.s.ApplyMutations([self.P.Mutation(t, p, b) for (t, p, b) in muts])
+
+    def template(self):
+        return self.s.Template()
+
+
+@pytest.mark.parametrize("idx", range(len(KATS["kats"])))
+def test_quiver_kats_on_gpu(idx):
+    run_kat(GpuQuiver, KATS["kats"][idx], KATS["params"])
+
+
+PARAMS2 = dict(Match=-0.2, Mismatch=-8.0, MismatchS=-0.15, Branch=-3.5, BranchS=-0.12, DeletionN=-7.5,
+               DeletionWithTag=-4.5, DeletionWithTagS=-0.2, Nce=-6.0, NceS=-0.1, Merge=[-3.0, -3.2, -2.9, -3.1],
+               MergeS=[-0.1, -0.12, -0.09, -0.11])
+
+
+def _features(rng, seq):
+    n = len(seq)
+    tags = rng.choice(list("ACGTN"), size=n)
+    return {"ins": rng.integers(0, 25, n).tolist(), "subs": rng.integers(0, 25, n).tolist(),
+            "del": rng.integers(0, 25, n).tolist(), "del_tag": tags.tolist(), "merge": rng.integers(0, 25, n).tolist()}
+
+
+def _pair(tpl, reads, sum_product, score_diff=12.5, params=None):
+    params = params or PARAMS2
+    g = GpuQuiver(tpl, params, score_diff=score_diff, sum_product=sum_product)
+    o = O.QuiverScorer(tpl, params, score_diff=score_diff, sum_product=sum_product)
+    for r in reads:
+        a = g.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"])
+        b = o.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"])
+        assert bool(a) == bool(b)
+    return g, o
+
+
+def _zmw(seed, length, passes):
+    from pbccs_amd import synth
+    z = synth.make_zmws(1, length, passes, seed=seed)[0]
+    rng = np.random.default_rng(seed)
+    reads = [dict(r, features=_features(rng, r["seq"])) for r in z["reads"]]
+    return z["draft"], reads
+
+
+@pytest.mark.parametrize("sum_product", [False, True])
+@pytest.mark.parametrize("seed,length,passes", [(101, 80, 3), (102, 200, 5)])
+def test_quiver_scores_match_oracle(sum_product, seed, length, passes):
+    tpl, reads = _zmw(seed, length, passes)
+    g, o = _pair(tpl, reads, sum_product)
+    assert g.s.BaselineScores() == [o.read_info(k)["score"] for k in range(len(reads)) if o.read_info(k)["active"]]
+    # NumFlipFlops of a read whose scorer construction threw is undefined in the reference (null scorer)
+    active = [k for k in range(len(reads)) if o.read_info(k)["active"]]
+    assert [g.s.NumFlipFlops()[k] for k in active] == [o.read_info(k)["flipflops"] for k in active]
+    assert [g.s.ReadInfo(k)["active"] for k in range(len(reads))] == [o.read_info(k)["active"] for k in range(len(reads))]
+    muts = O.unique_mutations(tpl)
+    vals = g.s.ScoreMany([g.P.Mutation(t, s, b) for (t, s, b) in muts])
+    fast = g.s.ScoreMany([g.P.Mutation(t, s, b) for (t, s, b) in muts], fast=True)
+    for (t, s, b), v, f in zip(muts, vals, fast):
+        assert v == o.score(t, s, b), (t, s, b)
+        assert f == o.score(t, s, b, fast=True), (t, s, b)
+
+
+@pytest.mark.parametrize("sum_product", [False, True])
+def test_quiver_refine_and_qvs_match_oracle(sum_product):
+    tpl, reads = _zmw(111, 150, 5)
+    g, o = _pair(tpl, reads, sum_product)
+    import pbccs_amd as P
+    conv, nt, na = P.RefineConsensus(g.s)
+    ref = o.refine()
+    assert (conv, nt, na) == (ref["converged"], ref["n_tested"], ref["n_applied"])
+    assert g.template() == o.template()
+    assert P.ConsensusQVs(g.s) == o.qvs()
+
+
+def test_quiver_add_threshold_memory_gate():
+    """AddRead's AllocatedEntries gate (MultiReadMutationScorer.cpp:263-276) reproduces the oracle's
+    libstdc++ capacity accounting."""
+    tpl, reads = _zmw(121, 120, 4)
+    g = GpuQuiver(tpl, PARAMS2, score_diff=12.5)
+    o = O.QuiverScorer(tpl, PARAMS2, score_diff=12.5)
+    for r in reads:
+        for thr in (0.05, 0.2):
+            a = g.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"], threshold=thr)
+            b = o.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"], threshold=thr)
+            assert bool(a) == bool(b), (thr, a, b)
+    for k in range(g.s.NumReads()):
+        info = o.read_info(k)
+        if info["active"]:
+            assert g.s.AllocatedEntries(k) == info["allocated"]
