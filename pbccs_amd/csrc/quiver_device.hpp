@@ -191,7 +191,9 @@ struct QBand {
     __device__ __forceinline__ float Get(int i, int j) const
     {
         const int2 r = range[j];
-        return (i >= r.x && i < r.y) ? val[off[j] + (i - r.x)] : kNegInf;
+        if (i < r.x || i >= r.y) return kNegInf;
+        const long long k = (long long)off[j] + (i - r.x);
+        return k < cap ? val[k] : kNegInf;   // past the arena only in overflow (count-only) mode
     }
     __device__ __forceinline__ bool Empty(int j) const { const int2 r = range[j]; return r.x >= r.y; }
 };
