@@ -32,7 +32,8 @@ constexpr int kFillBandHeight = 28;            // fill scratch values per column
 constexpr double kFillScratchBudget = 24.0 * (1ull << 30);
 constexpr int kCoopNarrowRows = 64;           // LDS column rows of the 16-lane fill path
 constexpr int kCoopTallRows = 1024;           // LDS column rows of the first 64-lane fill path
-constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill block (hard limit 64 KB)
+constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill block
+constexpr size_t kCoopTallLdsBytes = 150 * 1024;   // the 16-lane tall path's block (gfx950: 160 KB per CU)
 constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
 
 template <class T>
@@ -505,8 +506,19 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         return (int)(reads_[r].seq.size() + 7) / 8 + (reads_[r].te - reads_[r].ts + 8) / 8;
     };
     // rows a column buffer of path p gets for reads with these sizes (0: does not fit in LDS)
+    // Path 1 (tall bands) runs 16 lanes per read by default, with column buffers of up to 1024 rows in a
+    // block of up to 150 KB of LDS: the serial insertion chain then costs G = 16 wave-instructions per 16
+    // rows of four reads instead of 64 per 64 rows of one read -- 4x fewer VALU issue slots for the few
+    // reads per ZMW whose first band explodes (~36% of all fill work with 64 lanes).  Measured slower end to
+    // end (1290 vs 2480 ZMWs/s): the tall reads are each round's critical path and 16-row chunks pay the
+    // per-chunk band logic 4x as often, so it is opt-in (PBCCS_TALL16=1); the default is 64 lanes.
+    static const bool tall16 = std::getenv("PBCCS_TALL16") && std::strcmp(std::getenv("PBCCS_TALL16"), "1") == 0;
     auto rows_for = [&](int p, int maxI, int w) -> int {
         if (p == 0) return 4 * coop_group_bytes(kCoopNarrowRows, w, 0) <= kCoopLdsBytes ? kCoopNarrowRows : 0;
+        if (p == 1 && tall16) {
+            const int want = std::min<int>(kCoopTallRows, (maxI + 16) / 16 * 16);
+            return 4 * coop_group_bytes(want, w, 0) <= kCoopTallLdsBytes ? want : 0;
+        }
         const long long room = ((long long)kCoopLdsBytes - (long long)coop_group_bytes(0, w, 0)) / 16 / 64 * 64;
         const long long full = (maxI + 64) / 64 * 64;   // a column never exceeds I + 1 rows
         const long long want = p == 1 ? std::min<long long>(kCoopTallRows, full) : full;
@@ -572,7 +584,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             // Jacobi sweeps cut a tall chunk's latency but not its instruction count: use them when the
             // launch is latency-bound (few tall reads, e.g. a batch's convergence tail), serial steps when
             // the tall fills compete for issue slots with a full device.
-            static const int jacobiMax = std::getenv("PBCCS_JACOBI_MAX") ? std::atoi(std::getenv("PBCCS_JACOBI_MAX")) : 64;
+            static const int jacobiMax = std::getenv("PBCCS_JACOBI_MAX") ? std::atoi(std::getenv("PBCCS_JACOBI_MAX")) : 0;
             F.jacobi = chainMode ? std::strcmp(chainMode, "jacobi") == 0 : (p > 0 && n <= jacobiMax);
             F.prio = !(prioEnv && std::strcmp(prioEnv, "0") == 0);
             if (chainStats && p > 0) {
@@ -585,7 +597,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             }
             const int* lp = dList_.ptr + off;
             const hipStream_t st = (p > 0) ? stream2_ : stream_;
-            Timed(kKFill, [&] { launch_fill_coop(p == 0 ? 16 : 64, B, F, lp, n, st); }, st);
+            Timed(kKFill, [&] { launch_fill_coop((p == 0 || (p == 1 && tall16)) ? 16 : 64, B, F, lp, n, st); }, st);
             PBCCS_HIP(hipGetLastError());
             counters_.fillLaunches += 1;
             off += n;

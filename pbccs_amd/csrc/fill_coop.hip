@@ -692,7 +692,13 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     if (n <= 0) return;
     const int per = 64 / G;
     const size_t lds = (size_t)per * F.groupBytes;
-    if (lds > 64 * 1024) throw std::runtime_error("fill block needs more than 64 KB of LDS");
+    if (lds > 160 * 1024) throw std::runtime_error("fill block needs more than 160 KB of LDS");
+    static bool attrSet = false;   // dynamic LDS beyond 64 KB must be enabled per kernel
+    if (!attrSet) {
+        (void)hipFuncSetAttribute((const void*)k_fill_coop<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_fill_coop<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attrSet = true;
+    }
     const dim3 grid((n + per - 1) / per);
     if (G == 16) hipLaunchKernelGGL(k_fill_coop<16>, grid, dim3(64), lds, s, B, F, reads, n);
     else hipLaunchKernelGGL(k_fill_coop<64>, grid, dim3(64), lds, s, B, F, reads, n);
