@@ -91,6 +91,10 @@ class Engine:
         """Workspace slots = batches polished at the same time by polish_many (set before creating batches)."""
         _lib_mod.check(load().pbccs_engine_set_concurrency(self._h, int(batches_in_flight)))
 
+    def reserve_pool(self, bytes_per_slot):
+        """Map each workspace slot's band pool now (a one-time cost a long run pays once)."""
+        _lib_mod.check(load().pbccs_engine_reserve_pool(self._h, int(bytes_per_slot)))
+
     def set_profiling(self, on=True):
         _lib_mod.check(load().pbccs_engine_set_profiling(self._h, 1 if on else 0))
 

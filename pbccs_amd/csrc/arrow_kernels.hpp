@@ -58,6 +58,16 @@ struct CoopFill {
     unsigned long long* chainStats = nullptr;   // diagnostics (PBCCS_CHAIN_STATS): [chunks, sweeps, cycles, stops]
     bool jacobi = false;     // G = 64 chain by Jacobi sweeps (see fill_coop.hip)
     bool prio = true;        // G = 64 waves at raised issue priority
+    // In-kernel band growth: a read whose alpha/beta region overflows takes a larger region pair from
+    // the pool's free top (valBump, in values; mapped up to valLimit), copies what it must keep, and
+    // carries on -- no count-only pass and no relaunch.  The new region is written back to the
+    // descriptor arrays (aliases of DevBatch::rValA/rValB/rValCap).  Only when the mapped headroom runs
+    // out does the read fall back to count-only mode (kFillOverflow).
+    unsigned long long* valBump = nullptr;
+    long long valLimit = 0;
+    long long* rValA = nullptr;
+    long long* rValB = nullptr;
+    long long* rValCap = nullptr;
 };
 size_t coop_group_bytes(int hcap, int readWords, int tplWords);
 void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* reads, int n, hipStream_t s);

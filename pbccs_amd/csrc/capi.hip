@@ -571,6 +571,17 @@ int pbccs_engine_set_concurrency(pbccs_engine* eng, int batches_in_flight)
     return PBCCS_OK;
 }
 
+int pbccs_engine_reserve_pool(pbccs_engine* eng, size_t bytes_per_slot)
+{
+    if (!eng) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        if (hipSetDevice(eng->device) != hipSuccess) return fail(PBCCS_EDEVICE, "hipSetDevice failed");
+        for (int s = 0; s < std::max(1, eng->concurrency); ++s)
+            eng->Slot(s)->val.reserve(std::max<size_t>(bytes_per_slot / sizeof(double), 1), true);
+        return PBCCS_OK;
+    });
+}
+
 int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
                        pbccs_zmw_output* out)
 {

@@ -129,8 +129,10 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared)
     PBCCS_HIP(hipSetDevice(device_));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
+    PBCCS_HIP(hipStreamCreateWithFlags(&stream3_, hipStreamNonBlocking));
     PBCCS_HIP(hipEventCreateWithFlags(&evFork_, hipEventDisableTiming));
     PBCCS_HIP(hipEventCreateWithFlags(&evJoin_, hipEventDisableTiming));
+    PBCCS_HIP(hipEventCreateWithFlags(&evJoin3_, hipEventDisableTiming));
     dScratch_.reserve(kInitialScratch, false);
     dScratchTop_.reserve(1, false);
     dScratchOverflow_.reserve(1, false);
@@ -146,9 +148,12 @@ ArrowBatch::~ArrowBatch()
         }
         for (hipEvent_t e : eventPool_) (void)hipEventDestroy(e);
         (void)hipStreamSynchronize(stream2_);
+        (void)hipStreamSynchronize(stream3_);
         (void)hipEventDestroy(evFork_);
         (void)hipEventDestroy(evJoin_);
+        (void)hipEventDestroy(evJoin3_);
         (void)hipStreamDestroy(stream2_);
+        (void)hipStreamDestroy(stream3_);
         (void)hipStreamDestroy(stream_);
     }
 }
@@ -558,9 +563,31 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         // is then the slower of the two, not their sum.  Fork before the first launch (after the list
         // upload), so the tall fills do not wait for the 16-lane fill.
         const bool forked = !todo[1].empty() || !todo[2].empty();
+        // Headroom for in-kernel band growth (CoopFill::valBump): reads on the tall paths grow to a few
+        // percent of their full (I+1)(J+1) matrix; budgeted against the device's free memory.  Growth
+        // beyond the mapped headroom falls back to count-only + relaunch below.
+        const bool grow = ws_->val.allowVmm;
+        long long headroom = 0;
+        if (grow) {
+            long long want = 1ll << 24;   // 128 MB for the occasional 16-lane overflow
+            for (int p = 1; p < kPaths; ++p)
+                for (int r : todo[p]) {   // tall bands use ~2-22% of the full matrix (mean ~11%)
+                    const long long I = (long long)reads_[r].seq.size(), J = reads_[r].te - reads_[r].ts;
+                    want += 2 * std::max<long long>(0, (I + 1) * (J + 1) / 7 - reads_[r].valCap);
+                }
+            size_t freeB = 0, totalB = 0;
+            PBCCS_HIP(hipMemGetInfo(&freeB, &totalB));
+            headroom = std::min<long long>(want, (long long)(freeB / 4 / sizeof(double)));
+            dVal_.reserve((size_t)std::max<long long>(valTop_ + headroom, 1), true);
+            dBump_.reserve(1, false);
+            const unsigned long long top = (unsigned long long)valTop_;
+            PBCCS_HIP(hipMemcpyAsync(dBump_.ptr, &top, sizeof(top), hipMemcpyHostToDevice, stream_));
+        }
+        const long long valLimit = grow ? (long long)dVal_.cap : 0;
         if (forked) {
             PBCCS_HIP(hipEventRecord(evFork_, stream_));
             PBCCS_HIP(hipStreamWaitEvent(stream2_, evFork_, 0));
+            PBCCS_HIP(hipStreamWaitEvent(stream3_, evFork_, 0));
         }
         for (int p = 0; p < kPaths; ++p) {
             const int n = (int)todo[p].size();
@@ -577,6 +604,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.tplWords = (maxJ + 8) / 8;
             F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
             hcapOf[p] = F.hcap;
+            const int G = (p == 0 || (p == 1 && tall16)) ? 16 : 64;
             F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);
             static const bool chainStats = std::getenv("PBCCS_CHAIN_STATS") != nullptr;
             static const char* chainMode = std::getenv("PBCCS_CHAIN_MODE");   // "serial" | "jacobi"
@@ -587,6 +615,13 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             static const int jacobiMax = std::getenv("PBCCS_JACOBI_MAX") ? std::atoi(std::getenv("PBCCS_JACOBI_MAX")) : 0;
             F.jacobi = chainMode ? std::strcmp(chainMode, "jacobi") == 0 : (p > 0 && n <= jacobiMax);
             F.prio = !(prioEnv && std::strcmp(prioEnv, "0") == 0);
+            if (grow) {
+                F.valBump = dBump_.ptr;
+                F.valLimit = valLimit;
+                F.rValA = dRValA_.ptr;
+                F.rValB = dRValB_.ptr;
+                F.rValCap = dRValCap_.ptr;
+            }
             if (chainStats && p > 0) {
                 dChain_.reserve(4, false);
                 if (!chainInit_) {
@@ -596,8 +631,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 F.chainStats = dChain_.ptr;
             }
             const int* lp = dList_.ptr + off;
-            const hipStream_t st = (p > 0) ? stream2_ : stream_;
-            Timed(kKFill, [&] { launch_fill_coop((p == 0 || (p == 1 && tall16)) ? 16 : 64, B, F, lp, n, st); }, st);
+            const hipStream_t st = p == 0 ? stream_ : p == 1 ? stream2_ : stream3_;
+            Timed(kKFill, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
             PBCCS_HIP(hipGetLastError());
             counters_.fillLaunches += 1;
             off += n;
@@ -605,6 +640,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         if (forked) {
             PBCCS_HIP(hipEventRecord(evJoin_, stream2_));
             PBCCS_HIP(hipStreamWaitEvent(stream_, evJoin_, 0));
+            PBCCS_HIP(hipEventRecord(evJoin3_, stream3_));
+            PBCCS_HIP(hipStreamWaitEvent(stream_, evJoin3_, 0));
         }
         std::vector<int> st, fl, ua, ub;
         std::vector<double> bl;
@@ -613,7 +650,25 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         download(bl, dRBaseline_, R, stream_);
         download(ua, dUsedA_, R, stream_);
         download(ub, dUsedB_, R, stream_);
+        unsigned long long bump = (unsigned long long)valTop_;
+        if (grow) PBCCS_HIP(hipMemcpyAsync(&bump, dBump_.ptr, sizeof(bump), hipMemcpyDeviceToHost, stream_));
         PBCCS_HIP(hipStreamSynchronize(stream_));
+        if (grow && bump != (unsigned long long)valTop_) {
+            // some reads moved to larger regions: adopt the device's descriptors (host mirrors stay exact)
+            std::vector<long long> va, vb, vc;
+            download(va, dRValA_, R, stream_);
+            download(vb, dRValB_, R, stream_);
+            download(vc, dRValCap_, R, stream_);
+            PBCCS_HIP(hipStreamSynchronize(stream_));
+            for (auto& v : todo)
+                for (int r : v) {
+                    reads_[r].valA = va[r];
+                    reads_[r].valB = vb[r];
+                    reads_[r].valCap = vc[r];
+                }
+            valTop_ = (long long)std::min<unsigned long long>(bump, (unsigned long long)valLimit);
+            counters_.bandGrowths += 1;
+        }
         std::vector<int> next[kPaths];
         for (int p = 0; p < kPaths; ++p) {
             for (int r : todo[p]) {

@@ -105,6 +105,7 @@ struct Counters {   // work counters for the roofline report (bench.py)
     long long fillCells = 0, fillLaunches = 0;
     long long scoreTasks = 0, scoreLaunches = 0;
     long long mutations = 0;
+    long long bandGrowths = 0;   // fill launch sets in which some read grew its band region in-kernel
 };
 
 enum KernelKind { kKFill = 0, kKSuffix, kKEnumerate, kKScore, kKReduce, kKQv, kKSelect, kKCompact, kKernelKinds };
@@ -244,7 +245,9 @@ private:
     int device_ = 0;
     hipStream_t stream_ = nullptr;
     hipStream_t stream2_ = nullptr;      // second stream for the tall-band fill path
-    hipEvent_t evFork_ = nullptr, evJoin_ = nullptr;
+    hipStream_t stream3_ = nullptr;      // third stream: the all-rows 64-lane path, beside the second
+    hipEvent_t evFork_ = nullptr, evJoin_ = nullptr, evJoin3_ = nullptr;
+    DevVec<unsigned long long> dBump_;   // in-kernel band growth: the value pool's free top
     std::unique_ptr<Workspace> ownWs_;
     Workspace* ws_;
     std::vector<HZmw> zmws_;

@@ -165,6 +165,14 @@ struct Task {
     unsigned long long* dbg;   // chain diagnostics (nullptr: off)
     bool jacobi;               // G = 64: Jacobi sweeps instead of 64 serial DPP steps
     double prNot, prThird, sdn;
+    // in-kernel band growth (CoopFill::valBump): pool, bump pointer, mapped limit, descriptor arrays
+    int r;
+    double* pool;
+    unsigned long long* bump;
+    long long limit;
+    long long* gA;
+    long long* gB;
+    long long* gCap;
 
     __device__ __forceinline__ int TBase(int idx) const { return nib(tpW, idx); }
     __device__ __forceinline__ int TCtx(int idx) const
@@ -181,10 +189,63 @@ struct PassOut {
     bool changed;     // some column's [begin, end) differs from the previous pass of this matrix
 };
 
+// ---- band growth ---------------------------------------------------------------------------------
+template <int G>
+__device__ __forceinline__ void copy_vals(int lane, double* __restrict__ dst, const double* __restrict__ src, long long n)
+{
+    long long k = lane;
+    for (; k + 3 * G < n; k += 4 * G) {
+        const double x0 = src[k], x1 = src[k + G], x2 = src[k + 2 * G], x3 = src[k + 3 * G];
+        dst[k] = x0;
+        dst[k + G] = x1;
+        dst[k + 2 * G] = x2;
+        dst[k + 3 * G] = x3;
+    }
+    for (; k < n; k += G) dst[k] = src[k];
+}
+
+// Move the read's alpha/beta region pair to a larger one taken from the pool's free top.  `m` is the
+// matrix being filled (keep its first keepM values: the columns of the running pass), `o` the other
+// one (keep its first keepO values: its last complete pass).  The new capacity is the larger of twice
+// the old one and 1.25x the projected need; `done`/`total` columns give the projection.  Returns
+// false when the mapped headroom is exhausted (the caller then falls back to count-only mode).
+template <int G>
+__device__ bool grow_bands(const Task<G>& T, Band& m, Band& o, bool mIsAlpha, long long need, long long keepM,
+                           long long keepO, int done, int total)
+{
+    if (!T.bump) return false;
+    const long long full = (long long)(T.I + 1) * (T.J + 1) + 1;
+    const long long proj = need * (long long)total / (long long)max(done, 1);
+    long long cap = max(2 * m.cap, proj + proj / 4 + 64);
+    cap = max(min(cap, full), need);
+    unsigned long long base = 0;
+    if (T.g.lane == 0) base = atomicAdd(T.bump, (unsigned long long)(2 * cap));
+    base = (unsigned long long)__shfl((long long)base, 0, G);
+    if (base + 2 * (unsigned long long)cap > (unsigned long long)T.limit) return false;
+    __threadfence();   // the group's earlier band stores are visible to every lane's loads below
+    double* na = T.pool + base;          // alpha region first, beta region after it
+    double* nb = na + cap;
+    double* nm = mIsAlpha ? na : nb;
+    double* no = mIsAlpha ? nb : na;
+    copy_vals<G>(T.g.lane, nm, m.val, keepM);
+    copy_vals<G>(T.g.lane, no, o.val, keepO);
+    m.val = nm;
+    o.val = no;
+    m.cap = cap;
+    o.cap = cap;
+    if (T.g.lane == 0) {
+        T.gA[T.r] = (long long)base;
+        T.gB[T.r] = (long long)base + cap;
+        T.gCap[T.r] = cap;
+    }
+    return true;
+}
+
 // ---- FillAlpha (SimpleRecursor.cpp:60-181) --------------------------------------------------------
 template <int G>
-__device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide, bool selfValid, bool& ovf)
+__device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO)
 {
+    const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
     PassOut out{0, 0.0, 0.0, false, !selfValid};
     if (a.cap < 1) ovf = true;
@@ -276,6 +337,9 @@ __device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide
                 carry = T.g.bcast(x, G - 1);
             }
         }
+        if (!ovf && used + (e - b) + 1 > a.cap &&
+            !grow_bands<G>(T, a, o, true, used + (e - b) + 1, used, keepO, j + 1, J + 1))
+            ovf = true;
         // ScaledMatrix::FinishEditingColumn (ScaledMatrix-inl.hpp:35-60) + the next begin hint (:166)
         const double thrF = mx / T.sdn;
         const bool scale = (mx != 0.0 && mx != 1.0);
@@ -323,6 +387,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide
     const double c = (0.0 < lik) ? lik : 0.0;
     double v = lik, ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = lik / c; ls = log(c); }
+    if (!ovf && used + 1 > a.cap && !grow_bands<G>(T, a, o, true, used + 1, used, keepO, J + 1, J + 1)) ovf = true;
     if (used + 1 > a.cap) ovf = true;
     if (lane == 0) {
         if (!ovf) a.V(used) = v;
@@ -338,8 +403,9 @@ __device__ PassOut coop_alpha(const Task<G>& T, const Band& a, const Band* guide
 
 // ---- FillBeta (SimpleRecursor.cpp:183-296); rows run bottom-up, stored bottom-up --------------------
 template <int G>
-__device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide, bool selfValid, bool& ovf)
+__device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO)
 {
+    const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
     PassOut out{0, 0.0, 0.0, false, !selfValid};
     if (bm.cap < 1) ovf = true;
@@ -428,6 +494,9 @@ __device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide
                 carry = T.g.bcast(x, G - 1);
             }
         }
+        if (!ovf && used + (e - b) + 1 > bm.cap &&
+            !grow_bands<G>(T, bm, o, false, used + (e - b) + 1, used, keepO, J - j + 1, J + 1))
+            ovf = true;
         const double thrF = mx / T.sdn;
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhe = b;
@@ -470,6 +539,7 @@ __device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide
     const double c = (0.0 < raw) ? raw : 0.0;
     double v = raw, ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = raw / c; ls = log(c); }
+    if (!ovf && used + 1 > bm.cap && !grow_bands<G>(T, bm, o, false, used + 1, used, keepO, J + 1, J + 1)) ovf = true;
     if (used + 1 > bm.cap) ovf = true;
     double s = 0.0;
     if (lane == 0) {
@@ -481,12 +551,12 @@ __device__ PassOut coop_beta(const Task<G>& T, const Band& bm, const Band* guide
         // (loads batched 32 at a time so the serial adds, not the load latency, set the pace)
         s = s + ls;
         int k = 1;
-        for (; k + 31 <= J; k += 32) {
-            double v[32];
+        for (; k + 7 <= J; k += 8) {
+            double v[8];
 #pragma unroll
-            for (int q = 0; q < 32; ++q) v[q] = bm.L(k + q);
+            for (int q = 0; q < 8; ++q) v[q] = bm.L(k + q);
 #pragma unroll
-            for (int q = 0; q < 32; ++q) s = s + v[q];
+            for (int q = 0; q < 8; ++q) s = s + v[q];
         }
         for (; k <= J; ++k) s = s + bm.L(k);
     }
@@ -578,6 +648,13 @@ __global__ void __launch_bounds__(64) k_fill_coop(DevBatch B, CoopFill F, const 
     T.prNot = B.prNot;
     T.prThird = B.prThird;
     T.sdn = B.sdn;
+    T.r = r;
+    T.pool = B.valPool;
+    T.bump = F.valBump;
+    T.limit = F.valLimit;
+    T.gA = F.rValA;
+    T.gB = F.rValB;
+    T.gCap = F.rValCap;
 
     const long long cb = B.rColBase[r];
     Band a, bm;
@@ -599,68 +676,64 @@ __global__ void __launch_bounds__(64) k_fill_coop(DevBatch B, CoopFill F, const 
     auto fail_tall = [&]() {
         if (lane == 0) B.rStatus[r] = kFillTall;
     };
-    // MutationScorer ctor -> FillAlphaBeta (SimpleRecursor.cpp:642-691)
-    PassOut pa = coop_alpha<G>(T, a, nullptr, false, ovf);
-    if (pa.tall) return fail_tall();
-    PassOut pb = coop_beta<G>(T, bm, &a, false, ovf);
-    if (pb.tall) return fail_tall();
-    needA = max(needA, pa.used);
-    needB = max(needB, pb.used);
-    cells += pa.used + pb.used;
-    passes += 2;
-    long long ua = pa.used, ub = pb.used;
-    const int maxSize = (int)(0.5 + kRebandFrac * (I + 1) * (J + 1));
-    if (ua >= maxSize || ub >= maxSize) {
-        PassOut a1 = coop_alpha<G>(T, a, &bm, true, ovf);
-        if (a1.tall) return fail_tall();
-        pb = coop_beta<G>(T, bm, &a, true, ovf);
-        if (pb.tall) return fail_tall();
-        pa = coop_alpha<G>(T, a, &bm, true, ovf);
-        if (pa.tall) return fail_tall();
-        needA = max(needA, max(a1.used, pa.used));
-        needB = max(needB, pb.used);
-        cells += a1.used + pb.used + pa.used;
-        passes += 3;
-        flips += 3;
-        ua = pa.used;
-        ub = pb.used;
-    }
-    double av = log(pa.last) + pa.sumL;
-    double bv = log(pb.last) + pb.sumL;
-    // NB: alphaV / betaV are not re-evaluated inside the loop (SimpleRecursor.cpp:667-679)
-    const bool mismatched = fabs(av - bv) > kAlphaBetaTol;
+    // MutationScorer ctor -> FillAlphaBeta (SimpleRecursor.cpp:642-691), as a pass sequencer with one
+    // call site per matrix (every inlined pass costs registers and instruction cache):
+    //   step 0: alpha(Null guide); step 1: beta(alpha guide); if either used >= 4% of the matrix, the
+    //   reband steps 2..4 alpha(beta), beta(alpha), alpha(beta) (flip-flops += 3); then the flip-flop loop.
+    // NB: alphaV / betaV are evaluated once, after the reband (SimpleRecursor.cpp:667-679).
     // Flip-flop fixed point: a pass depends only on the band ranges of the other matrix (guide) and of
     // its own previous pass (hint), never on previous values.  Once an alpha pass and the beta pass after
     // it both reproduce their predecessors' ranges, every later pass repeats them bit for bit, so the
     // remaining flip-flops are skipped and only the count the reference reports is kept.
+    PassOut pa{0, 0.0, 0.0, false, false}, pb{0, 0.0, 0.0, false, false};
+    long long ua = 0, ub = 0;
+    const int maxSize = (int)(0.5 + kRebandFrac * (I + 1) * (J + 1));
+    bool mismatched = false;
     int unchanged = 0;
-    while (mismatched && flips <= kMaxFlipFlops) {
-        bool changed;
-        if (flips % 2 == 0) {
-            pa = coop_alpha<G>(T, a, &bm, true, ovf);
-            if (pa.tall) return fail_tall();
-            needA = max(needA, pa.used);
-            cells += pa.used;
-            ua = pa.used;
-            changed = pa.changed;
-        } else {
-            pb = coop_beta<G>(T, bm, &a, true, ovf);
-            if (pb.tall) return fail_tall();
-            needB = max(needB, pb.used);
-            cells += pb.used;
-            ub = pb.used;
-            changed = pb.changed;
+    for (int step = 0;; ++step) {
+        bool doAlpha;
+        if (step < 2) doAlpha = step == 0;
+        else if (step == 2 && !(ua >= maxSize || ub >= maxSize)) {
+            step = 5;   // no reband
+            doAlpha = true;
+        } else doAlpha = step == 2 || step == 4;
+        if (step == 5) {
+            if (flips == 0 || flips == 3) {   // first entry into the flip-flop loop
+                mismatched = fabs((log(pa.last) + pa.sumL) - (log(pb.last) + pb.sumL)) > kAlphaBetaTol;
+            }
         }
+        if (step >= 5) {
+            if (!(mismatched && flips <= kMaxFlipFlops)) break;
+            doAlpha = flips % 2 == 0;
+        }
+        const bool guided = step > 0, self = step > 1;
+        PassOut o;
+        if (doAlpha) o = coop_alpha<G>(T, a, bm, guided, self, ovf, ub);
+        else o = coop_beta<G>(T, bm, a, guided, self, ovf, ua);
+        if (o.tall) return fail_tall();
+        cells += o.used;
         passes += 1;
-        ++flips;
-        unchanged = changed ? 0 : unchanged + 1;
-        if (unchanged >= 2) {
-            flips = kMaxFlipFlops + 1;
-            break;
+        if (doAlpha) {
+            pa = o;
+            ua = o.used;
+            needA = max(needA, o.used);
+        } else {
+            pb = o;
+            ub = o.used;
+            needB = max(needB, o.used);
+        }
+        if (step >= 2 && step <= 4) ++flips;
+        if (step >= 5) {
+            ++flips;
+            unchanged = o.changed ? 0 : unchanged + 1;
+            if (unchanged >= 2) {
+                flips = kMaxFlipFlops + 1;
+                break;
+            }
         }
     }
-    av = log(pa.last) + pa.sumL;
-    bv = log(pb.last) + pb.sumL;
+    const double av = log(pa.last) + pa.sumL;
+    const double bv = log(pb.last) + pb.sumL;
     const double mism = fabs(1.0 - av / bv);
     if (lane == 0) {
         if (ovf) {

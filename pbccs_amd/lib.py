@@ -117,6 +117,7 @@ SIGNATURES = {
     "pbccs_batch_destroy": (None, [P]),
     "pbccs_batch_polish_many": (I, [ctypes.POINTER(P), I, ctypes.POINTER(ctypes.POINTER(CZmwOutput))]),
     "pbccs_engine_set_concurrency": (I, [P, I]),
+    "pbccs_engine_reserve_pool": (I, [P, ctypes.c_size_t]),
     "pbccs_engine_set_profiling": (I, [P, I]),
     "pbccs_engine_kernel_stats": (I, [P, ctypes.POINTER(CKernelStat), I, PI, I]),
     # Quiver family
