@@ -27,7 +27,6 @@ const char* const kKernelNames[kKernelKinds] = {"k_fill", "k_suffix", "k_enumera
 
 namespace {
 
-constexpr int kInitialBandHeight = 16;         // compact band values per column, first estimate
 constexpr int kFillBandHeight = 28;            // fill scratch values per column (doubled on overflow)
 constexpr double kFillScratchBudget = 24.0 * (1ull << 30);
 constexpr int kCoopNarrowRows = 64;           // LDS column rows of the 16-lane fill path
@@ -127,6 +126,9 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared)
       dScratchTop_(ws_->scratchTop), dScratchOverflow_(ws_->scratchOverflow)
 {
     PBCCS_HIP(hipSetDevice(device_));
+    // first value-region estimate per read (PBCCS_INITIAL_BAND_HEIGHT overrides it: tests use a tiny one
+    // to force in-kernel band growth on every read)
+    if (const char* e = std::getenv("PBCCS_INITIAL_BAND_HEIGHT")) initialBandHeight_ = std::max(1, std::atoi(e));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream3_, hipStreamNonBlocking));
@@ -331,7 +333,7 @@ int ArrowBatch::AppendRead(int z, const std::string& seq, int strand, int ts, in
     r.colCap = J + J / 4 + 66;
     r.colBase = colTop_;
     colTop_ += r.colCap;
-    r.valCap = (long long)r.colCap * kInitialBandHeight;
+    r.valCap = (long long)r.colCap * initialBandHeight_;
     r.valA = valTop_;
     r.valB = valTop_ + r.valCap;
     valTop_ += 2 * r.valCap;
@@ -366,8 +368,8 @@ void ArrowBatch::EnsureCapacity(int ri)
         r.colCap = J + J / 4 + 66;
         r.colBase = colTop_;
         colTop_ += r.colCap;
-        if ((long long)r.colCap * kInitialBandHeight > r.valCap) {
-            r.valCap = (long long)r.colCap * kInitialBandHeight;
+        if ((long long)r.colCap * initialBandHeight_ > r.valCap) {
+            r.valCap = (long long)r.colCap * initialBandHeight_;
             r.valA = valTop_;
             r.valB = valTop_ + r.valCap;
             valTop_ += 2 * r.valCap;

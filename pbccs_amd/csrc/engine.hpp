@@ -253,6 +253,7 @@ private:
     std::vector<HZmw> zmws_;
     std::vector<HRead> reads_;
     long long tplTop_ = 0, seqTop_ = 0, colTop_ = 0, valTop_ = 0;
+    int initialBandHeight_ = 16;   // compact band values per column, first estimate
     bool descDirty_ = true;
     size_t seqUploaded_ = 0;
 

@@ -21,6 +21,7 @@
 #include "arrow_device.hpp"
 #include "arrow_kernels.hpp"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace pbccs {
@@ -573,8 +574,8 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 // LDS per group: 2 column buffers (hcap doubles each), the ZMW's transition table, nibble-packed read
 // and template window.
 // ------------------------------------------------------------------------------------------------
-template <int G>
-__global__ void __launch_bounds__(64) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
+template <int G, int MINW>
+__global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     // tall reads are the latency-critical path of every refine round: issue ahead of the 16-lane fills
@@ -766,15 +767,19 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     const int per = 64 / G;
     const size_t lds = (size_t)per * F.groupBytes;
     if (lds > 160 * 1024) throw std::runtime_error("fill block needs more than 160 KB of LDS");
-    static bool attrSet = false;   // dynamic LDS beyond 64 KB must be enabled per kernel
-    if (!attrSet) {
-        (void)hipFuncSetAttribute((const void*)k_fill_coop<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_fill_coop<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attrSet = true;
+    // waves per SIMD the register allocator must allow (PBCCS_FILL_OCC: 2 = no spills, 3, 4 = spills)
+    static const int occ = std::getenv("PBCCS_FILL_OCC") ? std::atoi(std::getenv("PBCCS_FILL_OCC")) : 2;
+    auto pick = [&](auto k2, auto k3, auto k4) { return occ >= 4 ? k4 : occ == 3 ? k3 : k2; };
+    using K = void (*)(DevBatch, CoopFill, const int*, int);
+    const K k = G == 16 ? pick((K)k_fill_coop<16, 2>, (K)k_fill_coop<16, 3>, (K)k_fill_coop<16, 4>)
+                        : pick((K)k_fill_coop<64, 2>, (K)k_fill_coop<64, 3>, (K)k_fill_coop<64, 4>);
+    static bool attrSet[2] = {false, false};   // dynamic LDS beyond 64 KB must be enabled per kernel
+    if (!attrSet[G == 64]) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attrSet[G == 64] = true;
     }
     const dim3 grid((n + per - 1) / per);
-    if (G == 16) hipLaunchKernelGGL(k_fill_coop<16>, grid, dim3(64), lds, s, B, F, reads, n);
-    else hipLaunchKernelGGL(k_fill_coop<64>, grid, dim3(64), lds, s, B, F, reads, n);
+    hipLaunchKernelGGL(k, grid, dim3(64), lds, s, B, F, reads, n);
 }
 
 }  // namespace pbccs

@@ -202,6 +202,49 @@ def test_polish_2kb_batch_matches_oracle(P):
         assert max(abs(a - b) for a, b in zip(r["qvs"], e["qvs"])) <= 1
 
 
+def test_fills_10kb_match_oracle(P):
+    """configs[2] reads (10 kb insert, 8 passes): wide bands and long windows, including reads whose
+    columns outgrow the 1024-row LDS buffer (the all-rows 64-lane path) -- per-read LL and flip-flops."""
+    from pbccs_amd import synth
+    zs = synth.make_zmws(2, 10000, 8, seed=81)
+    for z in zs:
+        g, o, rg, ro = _scorers(P, z["draft"], z["reads"])
+        assert rg == ro
+        assert g.NumFlipFlops() == [o.read_info(k)["flipflops"] for k in range(len(z["reads"]))]
+        for x, y in zip(g.BaselineScores(), [o.read_info(k)["ll"] for k in range(len(z["reads"]))]):
+            assert _close(x, y, 1e-12, 1e-12)
+
+
+def test_polish_mixed_batch_matches_oracle(P):
+    """configs[3]-style batch (divergence stress): per-ZMW insert length, pass count and SNR all differ
+    within one batch (lengths scaled down to 0.3-1.5 kb so the oracle stays fast)."""
+    from pbccs_amd import synth
+    zs = synth.make_zmws(8, None, None, seed=91, length_range=(300, 1500), passes_range=(3, 30), random_snr=True)
+    res = P.polish_zmws(zs)
+    for z, r in zip(zs, res):
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+        assert r["add_read_results"] == e["add_read_results"]
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        if e["converged"]:
+            assert r["consensus"] == e["template"]
+            assert max(abs(a - b) for a, b in zip(r["qvs"], e["qvs"])) <= 1
+
+
+def test_band_growth_in_kernel_matches_oracle(P, monkeypatch):
+    """Every read starts with a 2-row-per-column value region, so nearly every fill outgrows it and moves
+    to a larger region inside the kernel (CoopFill::valBump) -- results must not change."""
+    from pbccs_amd import synth
+    monkeypatch.setenv("PBCCS_INITIAL_BAND_HEIGHT", "2")
+    zs = synth.make_zmws(4, 600, 6, seed=95)
+    res = P.polish_zmws(zs)
+    for z, r in zip(zs, res):
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+        assert r["add_read_results"] == e["add_read_results"]
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        if e["converged"]:
+            assert r["consensus"] == e["template"]
+
+
 # configs[1] ZMWs (seed 1, the bench's first step) that the reference loop leaves NonConvergent: their
 # templates oscillate until MaximumIterations, which the engine replays instead of re-running
 # (engine.hip, Refine: cycle replay).  Found with tools/find_nonconvergent.py 2000 2000 10 1.
