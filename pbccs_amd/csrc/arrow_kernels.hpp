@@ -68,6 +68,9 @@ struct CoopFill {
     long long* rValA = nullptr;
     long long* rValB = nullptr;
     long long* rValCap = nullptr;
+    // All-rows path for columns taller than LDS holds: 2 * hcap doubles per launch slot (64-lane groups
+    // only).  nullptr: the column buffers are in LDS.
+    double* colScratch = nullptr;
 };
 size_t coop_group_bytes(int hcap, int readWords, int tplWords);
 void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* reads, int n, hipStream_t s);

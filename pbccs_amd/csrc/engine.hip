@@ -501,7 +501,9 @@ DevBatch ArrowBatch::View() const
 // the kernel reported.  Bands land directly in the compact layout; k_suffix adds the log-scale sums.
 void ArrowBatch::FillReads(const std::vector<int>& readsIn)
 {
-    constexpr int kPaths = 3;   // 0: 16 lanes / 64 rows; 1: 64 lanes / 1024 rows; 2: 64 lanes / all rows
+    // 0: 16 lanes / 64 rows; 1: 64 lanes / 1024 rows; 2: 64 lanes / as many rows as LDS holds;
+    // 3: 64 lanes / all rows, column buffers in global memory (CoopFill::colScratch)
+    constexpr int kPaths = 4;
     for (int r : readsIn) EnsureCapacity(r);
     std::vector<int> todo[kPaths], serial, done;
     for (int r : readsIn) {
@@ -521,6 +523,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     // per-chunk band logic 4x as often, so it is opt-in (PBCCS_TALL16=1); the default is 64 lanes.
     static const bool tall16 = std::getenv("PBCCS_TALL16") && std::strcmp(std::getenv("PBCCS_TALL16"), "1") == 0;
     auto rows_for = [&](int p, int maxI, int w) -> int {
+        if (p == 3) return coop_group_bytes(0, w, 0) <= kCoopLdsBytes ? (maxI + 64) / 64 * 64 : 0;
         if (p == 0) return 4 * coop_group_bytes(kCoopNarrowRows, w, 0) <= kCoopLdsBytes ? kCoopNarrowRows : 0;
         if (p == 1 && tall16) {
             const int want = std::min<int>(kCoopTallRows, (maxI + 16) / 16 * 16);
@@ -545,7 +548,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             }
             todo[p].swap(keep);
         }
-        if (todo[0].empty() && todo[1].empty() && todo[2].empty()) break;
+        if (todo[0].empty() && todo[1].empty() && todo[2].empty() && todo[3].empty()) break;
         if (attempt > 8) throw DeviceError("band storage keeps overflowing");
         for (auto& v : todo)   // similar lengths share a launch (LDS is sized by the longest)
             std::stable_sort(v.begin(), v.end(), [&](int x, int y) {
@@ -560,11 +563,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         upload(dList_, list, stream_);
         const DevBatch B = View();
         size_t off = 0;
-        int hcapOf[kPaths] = {0, 0, 0};
+        int hcapOf[kPaths] = {0, 0, 0, 0};
         // the 64-lane (tall) launches run on a second stream beside the 16-lane one: a round's latency
         // is then the slower of the two, not their sum.  Fork before the first launch (after the list
         // upload), so the tall fills do not wait for the 16-lane fill.
-        const bool forked = !todo[1].empty() || !todo[2].empty();
+        const bool forked = !todo[1].empty() || !todo[2].empty() || !todo[3].empty();
         // Headroom for in-kernel band growth (CoopFill::valBump): reads on the tall paths grow to a few
         // percent of their full (I+1)(J+1) matrix; budgeted against the device's free memory.  Growth
         // beyond the mapped headroom falls back to count-only + relaunch below.
@@ -607,7 +610,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
             hcapOf[p] = F.hcap;
             const int G = (p == 0 || (p == 1 && tall16)) ? 16 : 64;
-            F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);
+            F.groupBytes = coop_group_bytes(p == 3 ? 0 : F.hcap, F.readWords, F.tplWords);
+            if (p == 3) {   // two column buffers of hcap rows per read, in global memory
+                dColScratch_.reserve((size_t)n * 2 * F.hcap, false);
+                F.colScratch = dColScratch_.ptr;
+            }
             static const bool chainStats = std::getenv("PBCCS_CHAIN_STATS") != nullptr;
             static const char* chainMode = std::getenv("PBCCS_CHAIN_MODE");   // "serial" | "jacobi"
             static const char* prioEnv = std::getenv("PBCCS_TALL_PRIO");      // "0" disables

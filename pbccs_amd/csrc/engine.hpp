@@ -221,7 +221,7 @@ private:
         double baseline = 0.0;
         int flips = 0;
         int status = 0;
-        int fillPath = 0;   // 0: k_fill_coop G=16, 1: k_fill_coop G=64, 2: lane-serial k_fill
+        int fillPath = 0;   // 0-3: k_fill_coop paths (FillReads), 4: lane-serial k_fill
         long long seqOff = 0;
         long long colBase = 0;
         int colCap = 0;
@@ -247,6 +247,7 @@ private:
     hipStream_t stream2_ = nullptr;      // second stream for the tall-band fill path
     hipStream_t stream3_ = nullptr;      // third stream: the all-rows 64-lane path, beside the second
     hipEvent_t evFork_ = nullptr, evJoin_ = nullptr, evJoin3_ = nullptr;
+    DevVec<double> dColScratch_;          // column buffers of the global-memory fill path
     DevVec<unsigned long long> dBump_;   // in-kernel band growth: the value pool's free top
     std::unique_ptr<Workspace> ownWs_;
     Workspace* ws_;

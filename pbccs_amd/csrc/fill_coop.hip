@@ -162,7 +162,8 @@ struct Task {
     const double* ctx;     // 9 x kCtxStride transition parameters
     double* col0;
     double* col1;
-    int hcap;              // rows per LDS column buffer
+    int hcap;              // rows per column buffer
+    bool gcol;             // column buffers live in global memory (CoopFill::colScratch), not LDS
     unsigned long long* dbg;   // chain diagnostics (nullptr: off)
     bool jacobi;               // G = 64: Jacobi sweeps instead of 64 serial DPP steps
     double prNot, prThird, sdn;
@@ -189,6 +190,16 @@ struct PassOut {
     bool tall;        // a column exceeded the LDS buffer
     bool changed;     // some column's [begin, end) differs from the previous pass of this matrix
 };
+
+// Column buffers in global memory (the all-rows path for columns taller than LDS holds): a column's
+// rows are written by one lane and read by its neighbours in the next column, so the group's stores must
+// have completed before the next column's loads.  One workgroup-scope fence per column (the group is one
+// wavefront on one CU, whose L1 its loads and stores share).  LDS columns need nothing: a wavefront's LDS
+// operations complete in order.
+__device__ __forceinline__ void col_fence(bool gcol)
+{
+    if (gcol) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+}
 
 // ---- band growth ---------------------------------------------------------------------------------
 template <int G>
@@ -259,6 +270,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     double* prev = T.col0;
     double* cur = T.col1;
     if (lane == 0) prev[0] = 1.0;
+    col_fence(T.gcol);
     int pb = 0, pe = 1;
     long long used = 1;
     int hb = 1, he = 1;
@@ -371,6 +383,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         }
         s = s + lsj;
         used += e - b;
+        col_fence(T.gcol);   // the next column's lanes read rows this column's lanes wrote
         double* t = prev;
         prev = cur;
         cur = t;
@@ -420,6 +433,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     double* nxt = T.col0;
     double* cur = T.col1;
     if (lane == 0) nxt[0] = 1.0;
+    col_fence(T.gcol);
     int pb = I, pe = I + 1;
     long long used = 1;
     int hb = I, he = I;
@@ -526,6 +540,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
             bm.L(j) = lsj;
         }
         used += e - b;
+        col_fence(T.gcol);
         double* t = nxt;
         nxt = cur;
         cur = t;
@@ -574,7 +589,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 // LDS per group: 2 column buffers (hcap doubles each), the ZMW's transition table, nibble-packed read
 // and template window.
 // ------------------------------------------------------------------------------------------------
-template <int G, int MINW>
+template <int G, int MINW, bool GC>
 __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
 {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -585,8 +600,9 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     const int t = blockIdx.x * (64 / G) + grp;
     const int lane = threadIdx.x & (G - 1);
     unsigned char* gbase = smem + (size_t)grp * F.groupBytes;
-    double* col = reinterpret_cast<double*>(gbase);
-    double* ctx = col + 2 * F.hcap;
+    // GC: the two column buffers are this slot's part of F.colScratch; LDS holds only ctx, read, template
+    double* col = GC ? F.colScratch + (size_t)t * 2 * F.hcap : reinterpret_cast<double*>(gbase);
+    double* ctx = GC ? reinterpret_cast<double*>(gbase) : col + 2 * F.hcap;
     unsigned* rdW = reinterpret_cast<unsigned*>(ctx + kCtxDoubles + 1);
     unsigned* tpW = rdW + F.readWords;
 
@@ -644,6 +660,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     T.col0 = col;
     T.col1 = col + F.hcap;
     T.hcap = F.hcap;
+    T.gcol = GC;
     T.dbg = F.chainStats;
     T.jacobi = F.jacobi;
     T.prNot = B.prNot;
@@ -771,12 +788,16 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     static const int occ = std::getenv("PBCCS_FILL_OCC") ? std::atoi(std::getenv("PBCCS_FILL_OCC")) : 2;
     auto pick = [&](auto k2, auto k3, auto k4) { return occ >= 4 ? k4 : occ == 3 ? k3 : k2; };
     using K = void (*)(DevBatch, CoopFill, const int*, int);
-    const K k = G == 16 ? pick((K)k_fill_coop<16, 2>, (K)k_fill_coop<16, 3>, (K)k_fill_coop<16, 4>)
-                        : pick((K)k_fill_coop<64, 2>, (K)k_fill_coop<64, 3>, (K)k_fill_coop<64, 4>);
-    static bool attrSet[2] = {false, false};   // dynamic LDS beyond 64 KB must be enabled per kernel
-    if (!attrSet[G == 64]) {
+    const bool gc = F.colScratch != nullptr;
+    if (gc && G != 64) throw std::runtime_error("global column buffers need 64-lane groups");
+    const K k = gc ? (K)k_fill_coop<64, 2, true>
+              : G == 16 ? pick((K)k_fill_coop<16, 2, false>, (K)k_fill_coop<16, 3, false>, (K)k_fill_coop<16, 4, false>)
+                        : pick((K)k_fill_coop<64, 2, false>, (K)k_fill_coop<64, 3, false>, (K)k_fill_coop<64, 4, false>);
+    static bool attrSet[3] = {false, false, false};   // dynamic LDS beyond 64 KB must be enabled per kernel
+    const int ak = gc ? 2 : (G == 64);
+    if (!attrSet[ak]) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attrSet[G == 64] = true;
+        attrSet[ak] = true;
     }
     const dim3 grid((n + per - 1) / per);
     hipLaunchKernelGGL(k, grid, dim3(64), lds, s, B, F, reads, n);
