@@ -54,6 +54,12 @@ void download(std::vector<T>& h, const DevVec<T>& d, size_t n, hipStream_t s)
 // ------------------------------------------------------------------------------------------------
 // VmPool
 // ------------------------------------------------------------------------------------------------
+void VmPool::try_reserve(size_t n)
+{
+    if (!vmm_ || n <= cap) return;
+    map_to(n, true);
+}
+
 void VmPool::reserve(size_t n, bool keep)
 {
     if (n <= cap) return;
@@ -70,8 +76,16 @@ void VmPool::reserve(size_t n, bool keep)
         cap = fallback_.cap;
         return;
     }
-    const size_t want = n * sizeof(double);
-    if (want > kVaBytes) throw DeviceError("band pool exceeds its address reservation");
+    map_to(n, false);
+}
+
+void VmPool::map_to(size_t n, bool soft)
+{
+    size_t want = n * sizeof(double);
+    if (want > kVaBytes) {
+        if (!soft) throw DeviceError("band pool exceeds its address reservation");
+        want = kVaBytes;
+    }
     int dev = 0;
     PBCCS_HIP(hipGetDevice(&dev));
     hipMemAllocationProp prop = {};
@@ -84,7 +98,11 @@ void VmPool::reserve(size_t n, bool keep)
     while (mappedBytes_ < want) {
         const size_t bytes = std::min(kChunkBytes, kVaBytes - mappedBytes_);
         hipMemGenericAllocationHandle_t h;
-        if (hipMemCreate(&h, bytes, &prop, 0) != hipSuccess) throw DeviceError("hipMemCreate failed (device memory)");
+        if (hipMemCreate(&h, bytes, &prop, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            if (soft) break;
+            throw DeviceError("hipMemCreate failed (device memory)");
+        }
         char* at = reinterpret_cast<char*>(ptr) + mappedBytes_;
         if (hipMemMap(at, bytes, 0, h, 0) != hipSuccess) {
             (void)hipMemRelease(h);
@@ -583,7 +601,10 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             size_t freeB = 0, totalB = 0;
             PBCCS_HIP(hipMemGetInfo(&freeB, &totalB));
             headroom = std::min<long long>(want, (long long)(freeB / 4 / sizeof(double)));
-            dVal_.reserve((size_t)std::max<long long>(valTop_ + headroom, 1), true);
+            // the reads' own regions must be mapped; the growth headroom only as far as device memory
+            // allows (several batches grow at once): the kernel's limit is what actually got mapped
+            dVal_.reserve((size_t)std::max<long long>(valTop_, 1), true);
+            dVal_.try_reserve((size_t)std::max<long long>(valTop_ + headroom, 1));
             dBump_.reserve(1, false);
             const unsigned long long top = (unsigned long long)valTop_;
             PBCCS_HIP(hipMemcpyAsync(dBump_.ptr, &top, sizeof(top), hipMemcpyHostToDevice, stream_));

@@ -87,11 +87,15 @@ struct VmPool {
     size_t cap = 0;   // doubles mapped
     bool allowVmm = false;   // only long-lived engine workspaces map 1 GB granules; scorers use hipMalloc
     void reserve(size_t n, bool keep);
+    // Best effort: map granules towards n doubles until the device runs out of memory (no throw).
+    // Only meaningful on the VMM path (the hipMalloc fallback would have to copy): there it is a no-op.
+    void try_reserve(size_t n);
     ~VmPool();
     VmPool() = default;
     VmPool(const VmPool&) = delete;
     VmPool& operator=(const VmPool&) = delete;
 private:
+    void map_to(size_t n, bool soft);
     static constexpr size_t kVaBytes = 1ull << 39;      // 512 GB of address space
     static constexpr size_t kChunkBytes = 1ull << 30;   // mapping granule
     bool tried_ = false, vmm_ = false;
