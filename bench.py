@@ -27,6 +27,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+TRAFFIC_PROFILE = "r1e_traffic_fill.json"   # PMC HBM bytes of the roofline kernel (tools/gpu_traffic.sh)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
 
 
@@ -171,8 +172,21 @@ def main():
     avg_ms = dom["device_ms"] / launches
     bytes_per_launch = dom["bytes"] / launches
     achieved = (bytes_per_launch / (avg_ms / 1e3)) / 1e9 if avg_ms > 0 else 0.0
+    # HBM traffic per launch: PMC counters cannot be read from inside this process, so `traffic` comes from
+    # the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same default command
+    # (tools/gpu_traffic.sh -> tools/pmc_traffic.py, gfx950 correction 2*FETCH_SIZE + WRITE_SIZE) when
+    # they were taken on this kernel family and workload; null otherwise.
+    traffic, traffic_src = None, None
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", TRAFFIC_PROFILE)
+    workload = (f"configs[1]: synthetic {args.length} bp insert, {args.passes} full passes, "
+                f"{args.zmws_per_step * args.steps} ZMWs per GPU ({args.steps} steps x {args.zmws_per_step})")
+    if os.path.exists(tpath):
+        t = json.load(open(tpath))
+        if t.get("kernel") == dom_name and t.get("workload") == workload:
+            traffic = t["traffic_bytes_per_launch"]
+            traffic_src = f"profiles/{TRAFFIC_PROFILE} (rocprofv3 --pmc, {t['dispatches_fetch_pass']} dispatches)"
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": dom_name, "avg_launch_ms": round(avg_ms, 4), "launches": dom["launches"],
                 "bytes_per_launch": bytes_per_launch, "cells_per_launch": dom["cells"] / launches}
 
@@ -189,9 +203,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY.md §8(d): truth iid ACGT; subreads 7%/4%/1% ins/del/sub; draft 0.5/0.5/0.2%)",
-        "config": {"workload": f"configs[1]: synthetic {args.length} bp insert, {args.passes} full passes, "
-                               f"{args.zmws_per_step * args.steps} ZMWs per GPU "
-                               f"({args.steps} steps x {args.zmws_per_step})",
+        "config": {"workload": workload,
                    "zmws_per_step": args.zmws_per_step, "insert_bp": args.length, "passes": args.passes,
                    "streams": streams,
                    "parallelism": f"zmw-shard x{world}"},
