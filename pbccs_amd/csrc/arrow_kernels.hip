@@ -958,11 +958,14 @@ __global__ void __launch_bounds__(256) k_score(DevBatch B, ScoreWork W, ScoreScr
     }
     const int z = waveLive ? W.zmw[k] : 0;
     const int M = waveLive ? W.nMut[k] : 0;
-    const int chunks = max(1, (M + 63) >> 6);
+    // mutations this phase scores: all of the item's, or its surviving ones (W.sel)
+    const int Mc = (waveLive && W.sel) ? W.nSel[k] : M;
+    const int chunks = max(1, (Mc + 63) >> 6);
     const long long local = waveLive ? wave - W.waveStart[k] : 0;
-    const int rr = (int)(local / chunks);
-    const int m = (int)(local % chunks) * 64 + lane;
-    const bool valid = waveLive && m < M;
+    const int rr = W.readLo + (int)(local / chunks);
+    const int mc = (int)(local % chunks) * 64 + lane;
+    const bool valid = waveLive && mc < Mc;
+    const int m = (valid && W.sel) ? (int)(W.sel[W.selBase[k] + mc] - W.mutStart[k]) : mc;
     const int r = waveLive ? B.zReadBegin[z] + rr : 0;
 
     // classify this lane's task
@@ -1122,6 +1125,60 @@ __global__ void __launch_bounds__(256) k_reduce(DevBatch B, ScoreWork W, double 
     fav[W.mutBase[k] + m] = (sum > 0.04) ? 1 : 0;   // MIN_FAVORABLE_SCOREDIFF, MultiReadMutationScorer.cpp:56
 }
 
+// The reduction's ordered prefix over the first readHi reads only (same sums, same break).
+__global__ void __launch_bounds__(256) k_alive(DevBatch B, ScoreWork W, double fastThr, int readHi,
+                                               unsigned char* __restrict__ alive)
+{
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= W.mutStart[W.nWork]) return;
+    int lo = 0, hi = W.nWork;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (W.mutStart[mid] <= g) lo = mid; else hi = mid;
+    }
+    const int k = lo;
+    const int z = W.zmw[k];
+    const int M = W.nMut[k];
+    const int m = (int)(g - W.mutStart[k]);
+    const int code = W.codes[W.mutBase[k] + m];
+    const int type = mut_type(code), pos = mut_pos(code);
+    const int me = (type == kIns) ? pos : pos + 1;
+    const int rb = B.zReadBegin[z], nr = min(B.zNReads[z], readHi);
+    const double* d = W.delta + W.deltaBase[k] + m;
+    double sum = 0.0;
+    bool live = true;
+    for (int rr = 0; rr < nr; ++rr) {
+        const int r = rb + rr;
+        if (B.rActive[r] && read_scores(B.rTs[r], B.rTe[r], type, pos, me)) sum += d[(long long)rr * M];
+        if (sum < fastThr) {
+            live = false;
+            break;
+        }
+    }
+    alive[g] = live ? 1 : 0;
+}
+
+// selBase[k] / nSel[k]: the entries of the ascending selected list that fall in item k's mutation range.
+__global__ void __launch_bounds__(256) k_sel_ranges(ScoreWork W, const long long* __restrict__ sel,
+                                                    const long long* __restrict__ count, long long* __restrict__ selBase,
+                                                    int* __restrict__ nSel)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= W.nWork) return;
+    const long long n = *count;
+    auto lower = [&](long long v) {
+        long long lo = 0, hi = n;
+        while (lo < hi) {
+            const long long mid = (lo + hi) >> 1;
+            if (sel[mid] < v) lo = mid + 1; else hi = mid;
+        }
+        return lo;
+    };
+    const long long b = lower(W.mutStart[k]), e = lower(W.mutStart[k + 1]);
+    selBase[k] = b;
+    nSel[k] = (int)(e - b);
+}
+
 // ConsensusQVs + ProbabilityToQV (Consensus-inl.hpp:130-138, 274-295).
 __global__ void __launch_bounds__(256) k_qv(DevBatch B, ScoreWork W, const long long* __restrict__ posBase,
                                             const int* __restrict__ posOff, const double* __restrict__ score,
@@ -1190,6 +1247,20 @@ void launch_reduce(const DevBatch& B, const ScoreWork& W, long long nMut, double
 {
     if (nMut <= 0) return;
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)((nMut + 255) / 256)), dim3(256), 0, s, B, W, fastThr, score, fav);
+}
+
+void launch_alive(const DevBatch& B, const ScoreWork& W, long long nMut, double fastThr, int readHi,
+                  unsigned char* alive, hipStream_t s)
+{
+    if (nMut <= 0) return;
+    hipLaunchKernelGGL(k_alive, dim3((unsigned)((nMut + 255) / 256)), dim3(256), 0, s, B, W, fastThr, readHi, alive);
+}
+
+void launch_sel_ranges(const ScoreWork& W, const long long* sel, const long long* count, long long* selBase,
+                       int* nSel, hipStream_t s)
+{
+    if (W.nWork <= 0) return;
+    hipLaunchKernelGGL(k_sel_ranges, dim3((W.nWork + 255) / 256), dim3(256), 0, s, W, sel, count, selBase, nSel);
 }
 
 void launch_qv(const DevBatch& B, const ScoreWork& W, long long nPos, const long long* posBase, const int* posOff,

@@ -23,6 +23,15 @@ struct ScoreWork {
     int* edgeList = nullptr;   // [edgeCap][3] = (work item, read, mutation)
     int* edgeCount = nullptr;
     int edgeCap = 0;
+    // Phased scoring (ArrowBatch::RunRound): a phase scores reads [readLo, readHi) of every item, and after
+    // the first phase only the mutations whose ordered fast-score prefix has not broken yet (sel: their
+    // global indices, ascending; item k owns sel[selBase[k] .. selBase[k] + nSel[k])).  waveStart then
+    // counts (reads in the phase) x ceil(nSel / 64) waves per item.
+    int readLo = 0;
+    int readHi = 1 << 30;
+    const long long* sel = nullptr;
+    const long long* selBase = nullptr;
+    const int* nSel = nullptr;
 };
 
 // Bump-allocated scratch for the rare whole-window refill case (tiny windows).
@@ -81,6 +90,12 @@ void launch_suffix(const DevBatch& B, const int* reads, int n, hipStream_t s, bo
 void launch_enumerate(const DevBatch& B, const int* zmws, int n, const long long* mutBase, const long long* posBase,
                       int* codes, int* posOff, hipStream_t s);
 void launch_score(const DevBatch& B, const ScoreWork& W, long long nWaves, const ScoreScratch& scratch, hipStream_t s);
+// Phased scoring helpers: alive[g] = the ordered fast-score sum of mutation g over reads [0, readHi) never
+// fell below fastThr (k_reduce's break has not happened yet); per-item ranges of the selected list.
+void launch_alive(const DevBatch& B, const ScoreWork& W, long long nMut, double fastThr, int readHi,
+                  unsigned char* alive, hipStream_t s);
+void launch_sel_ranges(const ScoreWork& W, const long long* sel, const long long* count, long long* selBase,
+                       int* nSel, hipStream_t s);
 void launch_reduce(const DevBatch& B, const ScoreWork& W, long long nMut, double fastThr, double* score,
                    unsigned char* fav, hipStream_t s);
 void launch_qv(const DevBatch& B, const ScoreWork& W, long long nPos, const long long* posBase, const int* posOff,

@@ -33,6 +33,7 @@ constexpr int kCoopNarrowRows = 64;           // LDS column rows of the 16-lane 
 constexpr int kCoopTallRows = 1024;           // LDS column rows of the first 64-lane fill path
 constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill block
 constexpr size_t kCoopTallLdsBytes = 150 * 1024;   // the 16-lane tall path's block (gfx950: 160 KB per CU)
+constexpr long long kPhasedMinTasks = 1 << 21;   // (mutation, read) tasks from which a round scores in phases
 constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
 
 template <class T>
@@ -936,7 +937,7 @@ void ArrowBatch::ZScores(int zi, double* zg, double* za, std::vector<double>* zs
 // scoring rounds
 // ------------------------------------------------------------------------------------------------
 void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vector<int>>* codes, double fastThr,
-                          bool needPositions)
+                          bool needPositions, bool phased)
 {
     UploadDescriptors();
     const int n = (int)zl.size();
@@ -1008,34 +1009,102 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
     W.edgeList = dEdge_.ptr;
     W.edgeCount = dEdgeCount_.ptr;
     W.edgeCap = (int)edgeCap;
-    for (int attempt = 0;; ++attempt) {
-        PBCCS_HIP(hipMemsetAsync(dEdgeCount_.ptr, 0, sizeof(int), stream_));
-        PBCCS_HIP(hipMemsetAsync(dScratchTop_.ptr, 0, sizeof(unsigned long long), stream_));
-        PBCCS_HIP(hipMemsetAsync(dScratchOverflow_.ptr, 0, sizeof(int), stream_));
-        ScoreScratch sc;
-        sc.pool = dScratch_.ptr;
-        sc.top = dScratchTop_.ptr;
-        sc.cap = dScratch_.cap;
-        sc.overflow = dScratchOverflow_.ptr;
-        Timed(kKScore, [&] { launch_score(B, W, waveStart[n], sc, stream_); });
-        PBCCS_HIP(hipGetLastError());
-        int ovf = 0;
-        PBCCS_HIP(hipMemcpyAsync(&ovf, dScratchOverflow_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
-        PBCCS_HIP(hipStreamSynchronize(stream_));
-        if (!ovf) break;
-        if (attempt > 8) throw DeviceError("scratch overflow");
-        if (ovf & 1) dScratch_.reserve(dScratch_.cap * 4, false);
-        if (ovf & 2) {
-            edgeCap *= 4;
-            dEdge_.reserve(3 * edgeCap, false);
-            W.edgeList = dEdge_.ptr;
-            W.edgeCap = (int)std::min<long long>(edgeCap, INT_MAX / 4);
+    // one scoring launch (k_score + k_score_edge) over W's current phase; re-run on scratch overflow
+    auto score_launch = [&](long long nWaves) {
+        for (int attempt = 0;; ++attempt) {
+            PBCCS_HIP(hipMemsetAsync(dEdgeCount_.ptr, 0, sizeof(int), stream_));
+            PBCCS_HIP(hipMemsetAsync(dScratchTop_.ptr, 0, sizeof(unsigned long long), stream_));
+            PBCCS_HIP(hipMemsetAsync(dScratchOverflow_.ptr, 0, sizeof(int), stream_));
+            ScoreScratch sc;
+            sc.pool = dScratch_.ptr;
+            sc.top = dScratchTop_.ptr;
+            sc.cap = dScratch_.cap;
+            sc.overflow = dScratchOverflow_.ptr;
+            Timed(kKScore, [&] { launch_score(B, W, nWaves, sc, stream_); });
+            PBCCS_HIP(hipGetLastError());
+            int ovf = 0;
+            PBCCS_HIP(hipMemcpyAsync(&ovf, dScratchOverflow_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
+            PBCCS_HIP(hipStreamSynchronize(stream_));
+            if (!ovf) break;
+            if (attempt > 8) throw DeviceError("scratch overflow");
+            if (ovf & 1) dScratch_.reserve(dScratch_.cap * 4, false);
+            if (ovf & 2) {
+                edgeCap *= 4;
+                dEdge_.reserve(3 * edgeCap, false);
+                W.edgeList = dEdge_.ptr;
+                W.edgeCap = (int)std::min<long long>(edgeCap, INT_MAX / 4);
+            }
         }
+    };
+    // Phased scoring (refine rounds only; fast-score threshold set, no per-read output wanted;
+    // PBCCS_PHASED_MIN_TASKS=-1 turns it off).  The
+    // reduction sums a mutation's reads in order and stops as soon as the sum falls below the fast-score
+    // threshold (MultiReadMutationScorer.cpp:352-362), so the deltas of the reads after that break are never
+    // read.  At configs[1] the break comes after 4.5 of 10 reads on average.  Phase 0 scores reads [0, 3)
+    // of every mutation; each later phase first evaluates the ordered prefix over the reads scored so far
+    // (k_alive: the same sums and break as k_reduce), keeps the mutations that have not broken (hipCUB
+    // select, kept in list order), and scores the next reads of those only.  k_reduce then runs unchanged
+    // over all reads: it breaks exactly where k_alive did and never touches an unscored delta.
+    // PBCCS_PHASED_MIN_TASKS overrides the size from which a round is phased (tests: 0 = every round)
+    const char* minEnv = std::getenv("PBCCS_PHASED_MIN_TASKS");
+    const long long minTasks = minEnv ? std::atoll(minEnv) : kPhasedMinTasks;
+    long long tasks = rTotalDelta_;
+    if (phased && minTasks >= 0 && rTotalDelta_ >= minTasks && rTotalMut_ <= INT_MAX) {
+        const int bounds[] = {0, 3, 5, 1 << 30};
+        std::vector<std::vector<long long>> ws(3);
+        std::vector<int> nSel;
+        ws_->sel.reserve(std::max<long long>(rTotalMut_, 1), false);
+        ws_->selCount.reserve(2, false);
+        dSelBase_.reserve(std::max(n, 1), false);
+        dNSel_.reserve(std::max(n, 1), false);
+        tasks = 0;
+        for (int ph = 0; ph < 3; ++ph) {
+            const int lo = bounds[ph], hi = bounds[ph + 1];
+            if (ph > 0) {
+                Timed(kKReduce, [&] { launch_alive(B, W, rTotalMut_, fastThr, lo, dFav_.ptr, stream_); });
+                size_t tb = 0;
+                hipcub::CountingInputIterator<long long> it(0);
+                PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, it, dFav_.ptr, ws_->sel.ptr, ws_->selCount.ptr,
+                                                        (int)rTotalMut_, stream_));
+                ws_->selTmp.reserve(std::max<size_t>(tb, 1), false);
+                PBCCS_HIP(hipcub::DeviceSelect::Flagged(ws_->selTmp.ptr, tb, it, dFav_.ptr, ws_->sel.ptr,
+                                                        ws_->selCount.ptr, (int)rTotalMut_, stream_));
+                launch_sel_ranges(W, ws_->sel.ptr, ws_->selCount.ptr, dSelBase_.ptr, dNSel_.ptr, stream_);
+                PBCCS_HIP(hipGetLastError());
+                download(nSel, dNSel_, n, stream_);
+                PBCCS_HIP(hipStreamSynchronize(stream_));
+                W.sel = ws_->sel.ptr;
+                W.selBase = dSelBase_.ptr;
+                W.nSel = dNSel_.ptr;
+            }
+            std::vector<long long>& wsv = ws[ph];
+            wsv.assign(n + 1, 0);
+            for (int k = 0; k < n; ++k) {
+                const int nr = zmws_[zl[k]].nReads;
+                const long long reads = std::max(0, std::min(hi, nr) - lo);
+                const long long mc = ph == 0 ? rNMut_[k] : nSel[k];
+                wsv[k + 1] = wsv[k] + reads * ((mc + 63) / 64);
+                tasks += reads * mc;
+            }
+            if (wsv[n] == 0) break;
+            W.readLo = lo;
+            W.readHi = hi;
+            upload(dWWaveStart_, wsv, stream_);
+            W.waveStart = dWWaveStart_.ptr;
+            score_launch(wsv[n]);
+        }
+        W.sel = nullptr;
+        W.selBase = nullptr;
+        W.nSel = nullptr;
+        W.readLo = 0;
+        W.readHi = 1 << 30;
+    } else {
+        score_launch(waveStart[n]);
     }
     Timed(kKReduce, [&] { launch_reduce(B, W, rTotalMut_, fastThr, dScore_.ptr, dFav_.ptr, stream_); });
     PBCCS_HIP(hipGetLastError());
     counters_.scoreLaunches += 1;
-    counters_.scoreTasks += rTotalDelta_;
+    counters_.scoreTasks += tasks;
     counters_.mutations += rTotalMut_;
 }
 
@@ -1277,12 +1346,12 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
         if (act.empty()) break;
         std::vector<std::vector<int>> lists;
         if (round == 0) {
-            RunRound(act, nullptr, fastThr, false);
+            RunRound(act, nullptr, fastThr, false, true);
         } else {
             lists.resize(act.size());
             for (size_t a = 0; a < act.size(); ++a)
                 nearby_mutations(zmws_[act[a]].tpl, centers[idx[a]], ro.mutationNeighborhood, &lists[a]);
-            RunRound(act, &lists, fastThr, false);
+            RunRound(act, &lists, fastThr, false, true);
         }
         for (size_t a = 0; a < act.size(); ++a) (*nTested)[idx[a]] += rNMut_[a];
         const Clock::time_point t1 = Clock::now();

@@ -244,13 +244,15 @@ private:
     void ResolveEvents();
     // one scoring round on the device; codes==nullptr => device enumeration of all mutations
     void RunRound(const std::vector<int>& zmws, const std::vector<std::vector<int>>* codes, double fastThr,
-                  bool needPositions);
+                  bool needPositions, bool phased = false);
 
     int device_ = 0;
     hipStream_t stream_ = nullptr;
     hipStream_t stream2_ = nullptr;      // second stream for the tall-band fill path
     hipStream_t stream3_ = nullptr;      // third stream: the all-rows 64-lane path, beside the second
     hipEvent_t evFork_ = nullptr, evJoin_ = nullptr, evJoin3_ = nullptr;
+    DevVec<long long> dSelBase_;          // phased scoring: per-item ranges of the surviving mutations
+    DevVec<int> dNSel_;
     DevVec<double> dColScratch_;          // column buffers of the global-memory fill path
     DevVec<unsigned long long> dBump_;   // in-kernel band growth: the value pool's free top
     std::unique_ptr<Workspace> ownWs_;

@@ -283,3 +283,24 @@ def test_nonconvergent_cycle_final_state_matches_oracle(P):
         ref = o.refine(max_iter=odd)
         assert (conv, nt, na) == (ref["converged"], ref["n_tested"], ref["n_applied"])
         assert g.Template() == o.template()
+
+
+def test_phased_scoring_matches_oracle(P, monkeypatch):
+    """Every refine round scored in phases (reads [0,3), then [3,5) and [5,n) of the mutations whose ordered
+    fast-score prefix has not broken yet; engine.hip RunRound): consensus, nTested/nApplied, AddRead results
+    and QVs as the oracle -- including a mixed batch where some ZMWs have fewer reads than a phase boundary
+    and the NonConvergent 2 kb ZMWs (their replayed iterations consume the phased rounds' favourable lists)."""
+    from pbccs_amd import synth
+    monkeypatch.setenv("PBCCS_PHASED_MIN_TASKS", "0")
+    seed, idx = NONCONVERGENT_2KB
+    allz = synth.make_zmws(max(idx) + 1, 2000, 10, seed=seed)
+    zs = [allz[i] for i in idx[:2]] + synth.make_zmws(2, 2000, 10, seed=72)
+    zs += synth.make_zmws(6, None, None, seed=93, length_range=(300, 1200), passes_range=(3, 12), random_snr=True)
+    res = P.polish_zmws(zs)
+    for z, r in zip(zs, res):
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+        assert r["add_read_results"] == e["add_read_results"]
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        if e["converged"]:
+            assert r["consensus"] == e["template"]
+            assert max(abs(a - b) for a, b in zip(r["qvs"], e["qvs"])) <= 1
