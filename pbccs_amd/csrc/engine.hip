@@ -33,6 +33,7 @@ constexpr int kCoopNarrowRows = 64;           // LDS column rows of the 16-lane 
 constexpr int kCoopTallRows = 1024;           // LDS column rows of the first 64-lane fill path
 constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill block
 constexpr size_t kCoopTallLdsBytes = 150 * 1024;   // the 16-lane tall path's block (gfx950: 160 KB per CU)
+constexpr size_t kHeadroomMargin = 24ull << 30;   // device bytes band-growth headroom leaves free
 constexpr long long kPhasedMinTasks = 1 << 21;   // (mutation, read) tasks from which a round scores in phases
 constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
 
@@ -102,7 +103,11 @@ void VmPool::map_to(size_t n, bool soft)
         if (hipMemCreate(&h, bytes, &prop, 0) != hipSuccess) {
             (void)hipGetLastError();
             if (soft) break;
-            throw DeviceError("hipMemCreate failed (device memory)");
+            size_t fr = 0, tot = 0;
+            (void)hipMemGetInfo(&fr, &tot);
+            throw DeviceError("hipMemCreate failed (device memory): band pool at " + std::to_string(mappedBytes_ >> 30) +
+                              " GB, needs " + std::to_string(want >> 30) + " GB, " + std::to_string(fr >> 20) +
+                              " MB free");
         }
         char* at = reinterpret_cast<char*>(ptr) + mappedBytes_;
         if (hipMemMap(at, bytes, 0, h, 0) != hipSuccess) {
@@ -601,7 +606,10 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 }
             size_t freeB = 0, totalB = 0;
             PBCCS_HIP(hipMemGetInfo(&freeB, &totalB));
-            headroom = std::min<long long>(want, (long long)(freeB / 4 / sizeof(double)));
+            // a quarter of what is free beyond a margin kept for the score buffers and the other slots'
+            // hipMalloc growth: speculative headroom must never be what runs the device out of memory
+            const long long spare = std::max<long long>(0, (long long)freeB - (long long)kHeadroomMargin);
+            headroom = std::min<long long>(want, spare / 4 / (long long)sizeof(double));
             // the reads' own regions must be mapped; the growth headroom only as far as device memory
             // allows (several batches grow at once): the kernel's limit is what actually got mapped
             dVal_.reserve((size_t)std::max<long long>(valTop_, 1), true);

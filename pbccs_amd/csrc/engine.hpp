@@ -13,6 +13,7 @@
 #include <limits>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "arrow_device.hpp"
@@ -38,9 +39,10 @@ enum AddReadResult { kSuccess = 0, kAlphaBetaMismatch = 1, kMemFail = 2, kPoorZS
 class DeviceError : public std::exception {
 public:
     explicit DeviceError(const char* what) : what_(what) {}
-    const char* what() const noexcept override { return what_; }
+    explicit DeviceError(std::string what) : what_(std::move(what)) {}
+    const char* what() const noexcept override { return what_.c_str(); }
 private:
-    const char* what_;
+    std::string what_;
 };
 
 // Device buffer with geometric growth (contents optionally preserved).
@@ -53,7 +55,13 @@ struct DevVec {
         if (n <= cap) return;
         const size_t nc = std::max(n, cap + cap / 2 + 256);
         T* p = nullptr;
-        if (hipMalloc(&p, nc * sizeof(T)) != hipSuccess) throw DeviceError("hipMalloc failed (device memory)");
+        if (hipMalloc(&p, nc * sizeof(T)) != hipSuccess) {
+            (void)hipGetLastError();
+            size_t fr = 0, tot = 0;
+            (void)hipMemGetInfo(&fr, &tot);
+            throw DeviceError("hipMalloc failed (device memory): " + std::to_string(nc * sizeof(T) >> 20) +
+                              " MB requested, " + std::to_string(fr >> 20) + " MB free");
+        }
         if (keep && ptr && cap) {
             if (hipDeviceSynchronize() != hipSuccess ||
                 hipMemcpy(p, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice) != hipSuccess)

@@ -304,3 +304,27 @@ def test_phased_scoring_matches_oracle(P, monkeypatch):
         if e["converged"]:
             assert r["consensus"] == e["template"]
             assert max(abs(a - b) for a, b in zip(r["qvs"], e["qvs"])) <= 1
+
+
+def test_polish_10kb_batch_matches_oracle(P):
+    """configs[2] ZMWs (10 kb insert, 8 passes) through the batch entry point: wide bands and long windows
+    (reads on the all-rows global-column fill path included) -- bit-exact consensus, nTested/nApplied and
+    AddRead results; QVs within +-1.  The oracle needs ~2.5 CPU-minutes for these two ZMWs, so its outputs
+    are a committed fixture (tests/golden/make_polish_fixtures.py); the inputs are regenerated and checked
+    against the fixture's digest."""
+    import sys
+    from pbccs_amd import synth
+    sys.path.insert(0, GOLD)
+    from make_polish_fixtures import digest
+    fx = json.load(open(os.path.join(GOLD, "polish_10kb.json")))
+    zs = synth.make_zmws(2, 10000, 8, seed=82)
+    res = P.polish_zmws(zs)
+    for z, r, e in zip(zs, res, fx["zmws"]):
+        assert digest(z) == e["digest"]
+        assert r["add_read_results"] == e["add_read_results"]
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        assert e["converged"]
+        assert r["consensus"] == e["consensus"]
+        got = [min(max(q, 0), 93) for q in r["qvs"]]
+        exp = [ord(c) - 33 for c in e["qvs"]]
+        assert len(got) == len(exp) and max(abs(a - b) for a, b in zip(got, exp)) <= 1

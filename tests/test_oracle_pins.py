@@ -87,3 +87,18 @@ def test_zmw6251_polish_matches_reference_record():
     assert r["n_applied"] == e["n_applied"]
     assert len(r["template"]) == e["final_length"]
     assert abs(r["pred_acc"] - e["pred_acc"]) < tol["pred_acc"]
+
+
+def test_polish_fixture_inputs_regenerate():
+    """tests/golden/polish_10kb.json was made from synth.make_zmws(2, 10000, 8, seed=82): the inputs the GPU
+    test regenerates must still hash to the fixture's digests (guards synth drift)."""
+    import json
+    import os
+    import sys
+    from pbccs_amd import synth
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    sys.path.insert(0, gold)
+    from make_polish_fixtures import digest
+    fx = json.load(open(os.path.join(gold, "polish_10kb.json")))
+    zs = synth.make_zmws(2, 10000, 8, seed=82)
+    assert [digest(z) for z in zs] == [e["digest"] for e in fx["zmws"]]
