@@ -37,7 +37,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--zmws-per-step", type=int, default=2000)
-    ap.add_argument("--warmup-zmws", type=int, default=200)
+    ap.add_argument("--warmup-zmws", type=int, default=0,
+                    help="ZMWs per warmup step (0 = --zmws-per-step: a warmup step is a full-size step, so the "
+                         "engine's score and selection buffers reach their steady-state size before timing)")
     ap.add_argument("--length", type=int, default=2000)
     ap.add_argument("--passes", type=int, default=10)
     ap.add_argument("--seed", type=int, default=1)
@@ -110,6 +112,8 @@ def main():
     seed0 = args.seed + 7919 * rank
 
     # ---- warmup (untimed) -------------------------------------------------------------------
+    if args.warmup_zmws <= 0:
+        args.warmup_zmws = args.zmws_per_step
     for w in range(args.warmup):
         zs = synth.make_zmws(args.warmup_zmws, args.length, args.passes, seed=seed0 + 1000 + w)
         b = pbccs_amd.PreparedBatch(zs, settings, eng)

@@ -928,10 +928,13 @@ __device__ __forceinline__ int wave_max(int v)
 
 // LDS stage of one wave: the alpha columns sc-1 and beta columns bc its 64 lanes read (contiguous in
 // HBM because fills append columns in order) and the read bases under their rows.
+#ifndef PBCCS_SCORE_STAGE
+#define PBCCS_SCORE_STAGE 512
+#endif
 constexpr int kScoreWaves = 4;
-constexpr int kStageA = 512;
-constexpr int kStageB = 512;
-constexpr int kStageR = 1024;
+constexpr int kStageA = PBCCS_SCORE_STAGE;
+constexpr int kStageB = PBCCS_SCORE_STAGE;
+constexpr int kStageR = 2 * PBCCS_SCORE_STAGE;
 struct WaveStage {
     double a[kStageA];
     double b[kStageB];

@@ -3,7 +3,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libpbccs_amd.so")
+# PBCCS_LIB: load another in-tree build of the same library (A/B experiments, tools/gpu_ab.sh)
+LIB_PATH = os.environ.get("PBCCS_LIB") or os.path.join(HERE, "_lib", "libpbccs_amd.so")
 
 PBCCS_OK = 0
 ERRORS = {-1: "EINVAL", -2: "EOOM", -3: "EDEVICE", -4: "ESTATE", -5: "ERANGE"}
