@@ -114,12 +114,17 @@ def main():
     # ---- warmup (untimed) -------------------------------------------------------------------
     if args.warmup_zmws <= 0:
         args.warmup_zmws = args.zmws_per_step
+    # a warmup step polishes one batch per workspace slot, concurrently like the timed steps, so every
+    # slot's score/selection buffers and band pool reach steady-state size (their growth would otherwise
+    # allocate -- and synchronise the device -- inside the timed region)
     for w in range(args.warmup):
-        zs = synth.make_zmws(args.warmup_zmws, args.length, args.passes, seed=seed0 + 1000 + w)
-        b = pbccs_amd.PreparedBatch(zs, settings, eng)
-        b.polish()
-        b.close()
-    log(rank, f"[bench] warmup done ({args.warmup} x {args.warmup_zmws} ZMWs)")
+        wb = [pbccs_amd.PreparedBatch(synth.make_zmws(args.warmup_zmws, args.length, args.passes,
+                                                      seed=seed0 + 1000 + 37 * w + s), settings, eng)
+              for s in range(streams)]
+        pbccs_amd.polish_many(wb)
+        for b in wb:
+            b.close()
+    log(rank, f"[bench] warmup done ({args.warmup} x {streams} x {args.warmup_zmws} ZMWs)")
 
     # ---- engine pools mapped before the timed region (a long run maps them once and reuses them) ----
     if torch.cuda.is_available():

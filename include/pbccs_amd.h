@@ -192,7 +192,8 @@ int pbccs_engine_set_concurrency(pbccs_engine* eng, int batches_in_flight);
 
 /* Map `bytes_per_slot` of band-value pool for every workspace slot now, instead of on first use.  Pool
  * memory stays mapped for the engine's lifetime and is reused by every batch the slot polishes, so a
- * long run pays the mapping once; this moves that one-time cost out of a timed region.  Optional. */
+ * long run pays the mapping once; this moves that one-time cost out of a timed region.  The mapped
+ * memory is also written once (zeroed), so call it while no batch is polishing.  Optional. */
 int pbccs_engine_reserve_pool(pbccs_engine* eng, size_t bytes_per_slot);
 
 /* Work counters of the engine since the last reset (for roofline accounting). */

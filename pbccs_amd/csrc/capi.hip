@@ -576,8 +576,15 @@ int pbccs_engine_reserve_pool(pbccs_engine* eng, size_t bytes_per_slot)
     if (!eng) return fail(PBCCS_EINVAL, "bad argument");
     return guarded([&] {
         if (hipSetDevice(eng->device) != hipSuccess) return fail(PBCCS_EDEVICE, "hipSetDevice failed");
-        for (int s = 0; s < std::max(1, eng->concurrency); ++s)
-            eng->Slot(s)->val.reserve(std::max<size_t>(bytes_per_slot / sizeof(double), 1), true);
+        for (int s = 0; s < std::max(1, eng->concurrency); ++s) {
+            VmPool& v = eng->Slot(s)->val;
+            v.reserve(std::max<size_t>(bytes_per_slot / sizeof(double), 1), true);
+            // touch the mapped memory once here, so first-use costs of fresh device pages are not paid by
+            // the first fills that land on them
+            if (hipMemsetAsync(v.ptr, 0, v.cap * sizeof(double), nullptr) != hipSuccess)
+                return fail(PBCCS_EDEVICE, "hipMemset of the band pool failed");
+        }
+        if (hipDeviceSynchronize() != hipSuccess) return fail(PBCCS_EDEVICE, "device synchronisation failed");
         return PBCCS_OK;
     });
 }

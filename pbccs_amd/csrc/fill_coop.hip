@@ -84,8 +84,25 @@ struct Group {
         if constexpr (G == 64) return m;
         else return (m >> base) & ((1ull << G) - 1);
     }
-    __device__ __forceinline__ double bcast(double x, int src) const { return __shfl(x, src, G); }
-    __device__ __forceinline__ int bcast(int x, int src) const { return __shfl(x, src, G); }
+    // value of group lane `src` (uniform across the group).  G = 64: the group is the wavefront and src is
+    // wave-uniform at every call site (a loop counter, a ballot's first set bit, a constant), so the value
+    // moves through an SGPR (v_readlane, a few cycles) instead of an LDS permute (ds_bpermute) -- this sits
+    // on the insertion chain's critical path once per 64-row chunk.
+    __device__ __forceinline__ double bcast(double x, int src) const
+    {
+        if constexpr (G == 64) {
+            const int lo = __builtin_amdgcn_readlane(__double2loint(x), src);
+            const int hi = __builtin_amdgcn_readlane(__double2hiint(x), src);
+            return __hiloint2double(hi, lo);
+        } else {
+            return __shfl(x, src, G);
+        }
+    }
+    __device__ __forceinline__ int bcast(int x, int src) const
+    {
+        if constexpr (G == 64) return __builtin_amdgcn_readlane(x, src);
+        else return __shfl(x, src, G);
+    }
 };
 
 // The in-column insertion chain x_i = (m_i + x_{i-1} k_i) + d_i over the G rows of a chunk (lane l = row
