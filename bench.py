@@ -43,7 +43,13 @@ def parse():
     ap.add_argument("--length", type=int, default=2000)
     ap.add_argument("--passes", type=int, default=10)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-sample", type=int, default=192, help="ZMWs polished by the CPU baseline (0 = skip)")
+    ap.add_argument("--workload", choices=["2kb", "10kb", "mixed"], default="2kb",
+                    help="2kb: configs[1], the headline line (pre-created batches, inputs resident in HBM). "
+                         "10kb / mixed: configs[2] / configs[3] through the ZMW work queue (polish_stream: "
+                         "length/pass buckets, memory-sized batches, largest first); the timed region then "
+                         "includes the host->device copy of the reads")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="ZMWs polished by the CPU baseline (0 = skip; default 192 for 2kb, 0 otherwise)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--streams", type=int, default=0,
                     help="batches polished concurrently (0 = min(steps, 8)); each has its own HIP stream")
@@ -67,20 +73,68 @@ def cpu_baseline(args, rank):
     n = args.cpu_sample
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
     threads = max(1, min(threads, n))
-    zmws = synth.make_zmws(n, args.length, args.passes, seed=args.seed + 99991)
+    zmws = synth.make_zmws(n, seed=args.seed + 99991, **workload_kw(args))
     O.lib()
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=threads) as ex:
         list(ex.map(lambda z: O.polish_zmw(z["draft"], z["reads"], z["snr"]), zmws))
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "ZMWs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} synthetic ZMWs of the same config ({args.length} bp, {args.passes} passes), "
+            "sample": f"{n} synthetic ZMWs of the same config ({args.workload}), "
                       f"oracle/arrow_oracle.cpp polish (AddRead, RefineConsensus, ConsensusQVs) on {threads} "
                       f"host threads, {dt:.1f} s wall"}
 
 
+def workload_kw(args):
+    """synth.make_zmws keywords of the workload (SURVEY.md §8(d) configs #2-#4)."""
+    if args.workload == "10kb":
+        return dict(length=10000, passes=8)
+    if args.workload == "mixed":
+        return dict(length=None, passes=None, length_range=(500, 20000), passes_range=(3, 30), random_snr=True)
+    return dict(length=args.length, passes=args.passes)
+
+
+def queue_workload(args, rank, world, eng, settings, seed0):
+    """configs[2] / configs[3] through the work queue; returns (job_time, local_time, results, workload)."""
+    import pbccs_amd
+    import torch
+    import torch.distributed as dist
+    from pbccs_amd import synth
+    n = args.steps * args.zmws_per_step
+    kw = workload_kw(args)
+    if args.workload == "10kb":
+        desc = f"configs[2]: synthetic 10000 bp insert, 8 full passes, {n} ZMWs per GPU"
+    else:
+        desc = f"configs[3]: synthetic 0.5-20 kb inserts, 3-30 passes, per-ZMW SNR U[4,20], {n} ZMWs per GPU"
+    for w in range(args.warmup):
+        pbccs_amd.polish_stream(synth.make_zmws(max(1, args.warmup_zmws), seed=seed0 + 1000 + w, **kw), settings, eng)
+    log(rank, "[bench] warmup done")
+    zs = synth.make_zmws(n, seed=seed0, **kw)
+    eng.kernel_stats(reset=True)
+    eng.counters(reset=True)
+    if world > 1:
+        dist.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = pbccs_amd.polish_stream(zs, settings, eng)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    local_time = time.perf_counter() - t0
+    job_time = local_time
+    if world > 1:
+        t = torch.tensor([local_time], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        job_time = float(t.item())
+    return job_time, local_time, res, desc + " (work queue; timed region includes the read upload)"
+
+
 def main():
     args = parse()
+    if args.cpu_sample is None:
+        args.cpu_sample = 192 if args.workload == "2kb" else 0
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -110,6 +164,10 @@ def main():
         eng.set_profiling(True)   # HIP events on the engine stream + in-kernel algorithmic counters
     settings = pbccs_amd.ConsensusSettings()
     seed0 = args.seed + 7919 * rank
+
+    if args.workload != "2kb":
+        job_time, local_time, res, workload = queue_workload(args, rank, world, eng, settings, seed0)
+        return report(args, rank, world, eng, streams, job_time, local_time, res, workload)
 
     # ---- warmup (untimed) -------------------------------------------------------------------
     if args.warmup_zmws <= 0:
@@ -160,15 +218,22 @@ def main():
     else:
         job_time = local_time
 
+    res = [r for b in batches for r in b.results()]
+    for b in batches:
+        b.close()
+    workload = (f"configs[1]: synthetic {args.length} bp insert, {args.passes} full passes, "
+                f"{args.zmws_per_step * args.steps} ZMWs per GPU ({args.steps} steps x {args.zmws_per_step})")
+    report(args, rank, world, eng, streams, job_time, local_time, res, workload)
+
+
+def report(args, rank, world, eng, streams, job_time, local_time, res, workload):
+    import torch.distributed as dist
     stats = eng.kernel_stats(reset=True)
     counters = eng.counters(reset=True)
-    res = [r for b in batches for r in b.results()]
     n_local = len(res)
     statuses = {}
     for r in res:
         statuses[r["status"]] = statuses.get(r["status"], 0) + 1
-    for b in batches:
-        b.close()
 
     total_zmws = n_local * world
     value = total_zmws / job_time
@@ -187,8 +252,6 @@ def main():
     # they were taken on this kernel family and workload; null otherwise.
     traffic, traffic_src = None, None
     tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", TRAFFIC_PROFILE)
-    workload = (f"configs[1]: synthetic {args.length} bp insert, {args.passes} full passes, "
-                f"{args.zmws_per_step * args.steps} ZMWs per GPU ({args.steps} steps x {args.zmws_per_step})")
     if os.path.exists(tpath):
         t = json.load(open(tpath))
         if t.get("kernel") == dom_name and t.get("workload") == workload:
@@ -213,7 +276,10 @@ def main():
         "dtype": "f64",
         "data": "synthetic (SURVEY.md §8(d): truth iid ACGT; subreads 7%/4%/1% ins/del/sub; draft 0.5/0.5/0.2%)",
         "config": {"workload": workload,
-                   "zmws_per_step": args.zmws_per_step, "insert_bp": args.length, "passes": args.passes,
+                   "zmws_per_step": args.zmws_per_step,
+                   "insert_bp": args.length if args.workload == "2kb" else
+                   (10000 if args.workload == "10kb" else "500-20000"),
+                   "passes": args.passes if args.workload == "2kb" else (8 if args.workload == "10kb" else "3-30"),
                    "streams": streams,
                    "parallelism": f"zmw-shard x{world}"},
         "gcups": round(gcups_local * world, 3),

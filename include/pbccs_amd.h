@@ -167,9 +167,23 @@ typedef struct {
 } pbccs_zmw_output;
 
 void pbccs_polish_options_default(pbccs_polish_options* o);
-/* One call: upload, polish and download n ZMWs (chunked by opts->zmws_per_batch / memory budget). */
+/* One call: upload, polish and download n ZMWs -- the ZMW work queue of ccs (src/main/ccs.cpp:222-262,
+ * WorkQueue.h:64-167) for a stream of heterogeneous ZMWs.  With opts->zmws_per_batch == 0 the ZMWs are
+ * bucketed by template length and pass count into device batches sized to the free device memory
+ * (pbccs_plan_batches), and the engine's workspace slots pull batches largest-first from a shared queue;
+ * otherwise consecutive chunks of zmws_per_batch.  Outputs land in input order either way. */
 int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
                        pbccs_zmw_output* out);
+
+/* Host-only batch plan behind pbccs_polish_batch (no device needed).  ZMWs are ordered by (draft length,
+ * read count); a batch closes when it holds max_per_batch ZMWs, when its estimated FP64 band footprint
+ * would pass budget_bytes, or when a draft is more than max_len_ratio times the batch's first draft
+ * (length buckets limit divergence inside a launch).  A ZMW whose own estimate exceeds the budget gets a
+ * batch of its own.  order[n] receives the ZMW permutation, batch_start[n + 1] the batch offsets into it
+ * (batch b is order[batch_start[b] .. batch_start[b + 1])), est_bytes[n] (may be NULL) each ZMW's
+ * estimate; *n_batches the batch count.  Batches are listed largest estimate first. */
+int pbccs_plan_batches(const pbccs_zmw_input* in, int n, double budget_bytes, int max_per_batch,
+                       double max_len_ratio, int* order, int* batch_start, double* est_bytes, int* n_batches);
 
 /* The same in two phases, so that inputs can be made resident in HBM ahead of time:
  * pbccs_batch_create copies the ZMWs to the device; pbccs_batch_polish runs the hot path (AddRead fills,

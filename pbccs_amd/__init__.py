@@ -251,13 +251,14 @@ def QVsToASCII(qvs):
     return "".join(chr(min(max(0, q), 93) + 33) for q in qvs)
 
 
-from .polish import ConsensusSettings, PreparedBatch, polish_many, polish_zmws  # noqa: E402  (batched ccs driver)
+from .polish import (ConsensusSettings, PreparedBatch, plan_batches, polish_many, polish_stream,  # noqa: E402
+                     polish_zmws)  # batched ccs driver
 from . import quiver as _quiver  # noqa: E402
 from .quiver import (QvModelParams, QuiverConfig, QuiverConfigTable,  # noqa: E402,F401
                      QuiverMultiReadMutationScorer, ALL_MOVES, BASIC_MOVES)
 
 __all__ = [
     "ArrowConfig", "ArrowMultiReadMutationScorer", "ConsensusQVs", "ConsensusSettings", "Engine", "Mutation",
-    "PbccsError", "QVsToASCII", "RefineConsensus", "polish_many", "polish_zmws", "INSERTION", "DELETION", "SUBSTITUTION",
+    "PbccsError", "QVsToASCII", "RefineConsensus", "polish_many", "polish_zmws", "polish_stream", "plan_batches", "INSERTION", "DELETION", "SUBSTITUTION",
     "FORWARD_STRAND", "REVERSE_STRAND",
 ]

@@ -4,10 +4,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <limits>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -17,6 +19,12 @@
 #include "engine.hpp"
 
 using namespace pbccs;
+
+// ZMW work queue (pbccs_polish_batch): device memory left free beside the batches' band pools (score
+// buffers, selection scratch, in-kernel growth headroom), and the largest batch (the best 2 kb batch
+// shape measured).
+constexpr double kQueueMargin = 24.0 * (1ull << 30);
+constexpr int kQueueMaxZmws = 2000;
 
 struct pbccs_engine {
     int device = 0;
@@ -385,8 +393,9 @@ static void merge_engine_stats(pbccs_engine* eng, ArrowBatch& B)
     B.CollectProfile(eng->stats);
 }
 
-int pbccs_batch_create(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
-                       pbccs_batch** out)
+// A batch on an explicit workspace slot (slot < 0: the next slot round-robin).
+static int create_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
+                        int slot, pbccs_batch** out)
 {
     if (!eng || n < 0 || (n > 0 && !in) || !out) return fail(PBCCS_EINVAL, "bad argument");
     return guarded([&] {
@@ -396,7 +405,7 @@ int pbccs_batch_create(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
         pbccs_polish_options_default(&b->o);
         if (opts) b->o = *opts;
         b->n = n;
-        b->slot = eng->nextSlot++ % std::max(1, eng->concurrency);
+        b->slot = slot >= 0 ? slot : eng->nextSlot++ % std::max(1, eng->concurrency);
         b->B.reset(new ArrowBatch(eng->device, eng->Slot(b->slot)));
         b->B->SetProfiling(eng->profiling);
         ArrowOptions ao;
@@ -428,6 +437,12 @@ int pbccs_batch_create(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
         *out = b.release();
         return PBCCS_OK;
     });
+}
+
+int pbccs_batch_create(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
+                       pbccs_batch** out)
+{
+    return create_batch(eng, in, n, opts, -1, out);
 }
 
 void pbccs_batch_destroy(pbccs_batch* b) { delete b; }
@@ -589,44 +604,141 @@ int pbccs_engine_reserve_pool(pbccs_engine* eng, size_t bytes_per_slot)
     });
 }
 
+// ---- ZMW work queue ------------------------------------------------------------------------------
+// Estimated FP64 band footprint of one ZMW at its high-water mark.  Per read: two band regions of ~32 rows
+// x window plus column metadata and score deltas (the typical band), plus the expected share of reads
+// whose first band explodes (the tall-band paths hold ~2-22% of the (I+1)(J+1) matrix).  Fitted to the
+// measured pools: ~13.5 MB per 2 kb / 10-pass ZMW, ~1.1 GB per 10 kb / 8-pass ZMW;
+// the fit overestimates the 2 kb case about 2x, which only shortens its batches.
+static double zmw_est_bytes(const pbccs_zmw_input& z)
+{
+    double b = 0.0;
+    for (int k = 0; k < z.n_reads; ++k) {
+        const double J = std::max(1, z.tends ? z.tends[k] - (z.tstarts ? z.tstarts[k] : 0) : z.draft_len);
+        const double I = z.lens ? std::max(0, z.lens[k]) : J;
+        const double typical = J * (2 * 32 * 8 * 1.25 + 80 + 8 * 8);
+        const double tall = std::min(0.22 * 8.0 * (I + 1) * (J + 1), 1.33e8 * std::pow(J / 1e4, 3.0));
+        b += typical + tall;
+    }
+    return std::max(b, 4096.0);
+}
+
+int pbccs_plan_batches(const pbccs_zmw_input* in, int n, double budget_bytes, int max_per_batch,
+                       double max_len_ratio, int* order, int* batch_start, double* est_bytes, int* n_batches)
+{
+    if (n < 0 || (n > 0 && (!in || !order || !batch_start)) || !n_batches || max_per_batch < 1 ||
+        !(budget_bytes > 0) || !(max_len_ratio >= 1.0))
+        return fail(PBCCS_EINVAL, "bad argument");
+    std::vector<double> est(n);
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; ++i) {
+        est[i] = zmw_est_bytes(in[i]);
+        idx[i] = i;
+        if (est_bytes) est_bytes[i] = est[i];
+    }
+    // length buckets (then pass count): similar windows share launches, whose LDS and band heights are
+    // sized by their longest read; the input index breaks ties so the plan is deterministic
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) {
+        if (in[a].draft_len != in[b].draft_len) return in[a].draft_len < in[b].draft_len;
+        return in[a].n_reads < in[b].n_reads;
+    });
+    struct Span { int b, e; double bytes; };
+    std::vector<Span> spans;
+    for (int k = 0; k < n;) {
+        Span s{k, k, 0.0};
+        const double first = std::max(1, in[idx[k]].draft_len);
+        while (s.e < n) {
+            const int z = idx[s.e];
+            const bool room = s.e - s.b < max_per_batch && s.bytes + est[z] <= budget_bytes &&
+                              in[z].draft_len <= max_len_ratio * first;
+            if (!room && s.e > s.b) break;   // a ZMW over budget on its own still gets a batch
+            s.bytes += est[z];
+            ++s.e;
+        }
+        spans.push_back(s);
+        k = s.e;
+    }
+    // largest first: the queue's tail is then made of short batches (LPT)
+    std::stable_sort(spans.begin(), spans.end(), [](const Span& a, const Span& b) { return a.bytes > b.bytes; });
+    int o = 0;
+    for (size_t b = 0; b < spans.size(); ++b) {
+        batch_start[b] = o;
+        for (int k = spans[b].b; k < spans[b].e; ++k) order[o++] = idx[k];
+    }
+    batch_start[spans.size()] = o;
+    *n_batches = (int)spans.size();
+    return PBCCS_OK;
+}
+
 int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
                        pbccs_zmw_output* out)
 {
     if (!eng || n < 0 || (n > 0 && (!in || !out))) return fail(PBCCS_EINVAL, "bad argument");
+    if (n == 0) return PBCCS_OK;
     pbccs_polish_options o;
     pbccs_polish_options_default(&o);
     if (opts) o = *opts;
-    int per = o.zmws_per_batch;
-    if (per <= 0) {
-        // memory budget: two band regions of 32 rows x window per read, column metadata and the largest
-        // round's (read x mutation) deltas
-        const double budget = 96.0 * (1ull << 30);
-        double bytes = 0.0;
-        for (int i = 0; i < n; ++i)
-            for (int k = 0; k < in[i].n_reads; ++k) bytes += (double)in[i].draft_len * (2 * 32 * 8 * 1.25 + 80 + 8 * 8);
-        const double perZmw = n > 0 ? bytes / n : 1.0;
-        per = (int)std::max(1.0, std::min((double)n, budget / std::max(perZmw, 1.0)));
-    }
-    // split so that every workspace slot gets work, then polish `concurrency` chunks at a time
     const int slots = std::max(1, eng->concurrency);
-    if (n >= 64 * slots) per = std::min(per, (n + slots - 1) / slots);
-    for (int b0 = 0; b0 < n;) {
-        std::vector<pbccs_batch*> wave;
-        std::vector<pbccs_zmw_output*> outs;
-        int rc = PBCCS_OK;
-        for (int k = 0; k < slots && b0 < n; ++k) {
-            const int m = std::min(per, n - b0);
-            pbccs_batch* h = nullptr;
-            rc = pbccs_batch_create(eng, in + b0, m, &o, &h);
-            if (rc != PBCCS_OK) break;
-            wave.push_back(h);
-            outs.push_back(out + b0);
-            b0 += m;
-        }
-        if (rc == PBCCS_OK) rc = pbccs_batch_polish_many(wave.data(), (int)wave.size(), outs.data());
-        for (pbccs_batch* h : wave) pbccs_batch_destroy(h);
+    std::vector<int> order(n), start(n + 1);
+    int nb = 0;
+    if (o.zmws_per_batch > 0) {   // caller-sized consecutive chunks
+        for (int i = 0; i < n; ++i) order[i] = i;
+        for (int b0 = 0; b0 < n; b0 += o.zmws_per_batch) start[nb++] = b0;
+        start[nb] = n;
+    } else {
+        size_t freeB = 0, totalB = 0;
+        if (hipSetDevice(eng->device) != hipSuccess || hipMemGetInfo(&freeB, &totalB) != hipSuccess)
+            return fail(PBCCS_EDEVICE, "hipMemGetInfo failed");
+        // every slot polishes at once: split what is free beyond the growth margin between them
+        const double spare = std::max(0.0, (double)freeB - (double)kQueueMargin);
+        const double budget = std::max(1.0 * (1 << 30), 0.9 * spare / slots);
+        const int rc = pbccs_plan_batches(in, n, budget, kQueueMaxZmws, 1.5, order.data(), start.data(), nullptr, &nb);
         if (rc != PBCCS_OK) return rc;
     }
+    // the workspace slots exist before the workers start (Slot() grows a shared vector)
+    for (int s = 0; s < slots; ++s) eng->Slot(s);
+    std::atomic<int> next{0};
+    std::atomic<bool> stop{false};
+    std::vector<int> rc(slots, PBCCS_OK);
+    std::vector<std::string> err(slots);
+    std::mutex statsMu;
+    auto worker = [&](int slot) {
+        std::vector<pbccs_zmw_input> bin;
+        std::vector<pbccs_zmw_output> bout;
+        for (;;) {
+            const int b = next.fetch_add(1);
+            if (b >= nb || stop.load()) return;
+            const int m = start[b + 1] - start[b];
+            bin.resize(m);
+            bout.resize(m);
+            for (int k = 0; k < m; ++k) {   // output structs point at the caller's buffers
+                bin[k] = in[order[start[b] + k]];
+                bout[k] = out[order[start[b] + k]];
+            }
+            pbccs_batch* h = nullptr;
+            int r = create_batch(eng, bin.data(), m, &o, slot, &h);
+            if (r == PBCCS_OK) r = polish_one(h, bout.data());
+            if (h) {
+                if (h->B) {
+                    std::lock_guard<std::mutex> lk(statsMu);
+                    merge_engine_stats(eng, *h->B);
+                }
+                pbccs_batch_destroy(h);
+            }
+            if (r != PBCCS_OK) {
+                rc[slot] = r;
+                err[slot] = g_lastError;
+                stop.store(true);
+                return;
+            }
+            for (int k = 0; k < m; ++k) out[order[start[b] + k]] = bout[k];
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int s = 0; s < std::min(slots, nb); ++s) pool.emplace_back(worker, s);
+    for (std::thread& t : pool) t.join();
+    for (int s = 0; s < slots; ++s)
+        if (rc[s] != PBCCS_OK) return fail(rc[s], err[s].c_str());
     return PBCCS_OK;
 }
 

@@ -113,6 +113,7 @@ SIGNATURES = {
     "pbccs_polish_options_default": (None, [ctypes.POINTER(CPolishOptions)]),
     "pbccs_polish_batch": (I, [P, ctypes.POINTER(CZmwInput), I, ctypes.POINTER(CPolishOptions),
                                ctypes.POINTER(CZmwOutput)]),
+    "pbccs_plan_batches": (I, [ctypes.POINTER(CZmwInput), I, D, I, D, PI, PI, PD, PI]),
     "pbccs_batch_create": (I, [P, ctypes.POINTER(CZmwInput), I, ctypes.POINTER(CPolishOptions), ctypes.POINTER(P)]),
     "pbccs_batch_polish": (I, [P, ctypes.POINTER(CZmwOutput)]),
     "pbccs_batch_destroy": (None, [P]),

@@ -40,16 +40,12 @@ class ConsensusSettings:
         return o
 
 
-class PreparedBatch:
-    """ZMWs copied to HBM (pbccs_batch_create); polish() runs the hot path once (pbccs_batch_polish)."""
+class _Marshalled:
+    """pbccs_zmw_input / pbccs_zmw_output arrays for a list of ZMW dicts; the output buffers stay owned here."""
 
-    def __init__(self, zmws, settings=None, engine=None):
-        from . import default_engine
-        self._lib = L.load()
-        self.engine = engine or default_engine()
-        self.settings = settings or ConsensusSettings()
-        self.zmws = zmws
+    def __init__(self, zmws):
         n = len(zmws)
+        self.zmws = zmws
         self._ins = (L.CZmwInput * max(1, n))()
         self._outs = (L.CZmwOutput * max(1, n))()
         self._keep = []
@@ -85,13 +81,6 @@ class PreparedBatch:
             self._outs[i].qvs = qv
             self._outs[i].add_read_results = arr
             self._outs[i].zscores = zs
-        self._opts = self.settings._c()
-        h = ctypes.c_void_p()
-        L.check(L.load().pbccs_batch_create(self.engine._h, self._ins, n, ctypes.byref(self._opts), ctypes.byref(h)))
-        self._h = h
-
-    def polish(self):
-        L.check(L.load().pbccs_batch_polish(self._h, self._outs))
 
     def results(self):
         from . import ZMW_STATUS
@@ -111,6 +100,25 @@ class PreparedBatch:
                 "n_applied": o.n_applied, "n_passes": o.n_passes, "status_counts": list(o.status_counts),
             })
         return res
+
+
+class PreparedBatch(_Marshalled):
+    """ZMWs copied to HBM (pbccs_batch_create); polish() runs the hot path once (pbccs_batch_polish)."""
+
+    def __init__(self, zmws, settings=None, engine=None):
+        from . import default_engine
+        self._lib = L.load()
+        self.engine = engine or default_engine()
+        self.settings = settings or ConsensusSettings()
+        super().__init__(zmws)
+        n = len(zmws)
+        self._opts = self.settings._c()
+        h = ctypes.c_void_p()
+        L.check(L.load().pbccs_batch_create(self.engine._h, self._ins, n, ctypes.byref(self._opts), ctypes.byref(h)))
+        self._h = h
+
+    def polish(self):
+        L.check(L.load().pbccs_batch_polish(self._h, self._outs))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -144,3 +152,33 @@ def polish_zmws(zmws, settings=None, engine=None):
         return b.results()
     finally:
         b.close()
+
+
+def plan_batches(zmws, budget_bytes, max_per_batch=2000, max_len_ratio=1.5):
+    """The work queue's batch plan (pbccs_plan_batches; host only, no device).
+
+    Returns (batches, est): batches = lists of ZMW indices, largest estimated band footprint first;
+    est = per-ZMW estimated FP64 band bytes.
+    """
+    m = _Marshalled(zmws)
+    n = len(zmws)
+    order = (ctypes.c_int * max(1, n))()
+    start = (ctypes.c_int * (n + 1))()
+    est = (ctypes.c_double * max(1, n))()
+    nb = ctypes.c_int()
+    L.check(L.load().pbccs_plan_batches(m._ins, n, float(budget_bytes), int(max_per_batch), float(max_len_ratio),
+                                        order, start, est, ctypes.byref(nb)))
+    return [list(order[start[b]:start[b + 1]]) for b in range(nb.value)], list(est[:n])
+
+
+def polish_stream(zmws, settings=None, engine=None):
+    """Polish a stream of heterogeneous ZMWs (pbccs_polish_batch): bucketed by length and pass count into
+    memory-sized device batches that the engine's workspace slots pull largest-first from one queue, like
+    ccs's ZMW work queue (src/main/ccs.cpp:222-262).  Results in input order, as polish_zmws()."""
+    from . import default_engine
+    engine = engine or default_engine()
+    settings = settings or ConsensusSettings()
+    m = _Marshalled(zmws)
+    opts = settings._c()
+    L.check(L.load().pbccs_polish_batch(engine._h, m._ins, len(zmws), ctypes.byref(opts), m._outs))
+    return m.results()

@@ -1,0 +1,82 @@
+"""ZMW work queue (pbccs_polish_batch / pbccs_plan_batches): the host-side batch plan on CPU, and on the
+GPU the queue's results against the oracle and against one-batch polish (a ZMW's result must not depend on
+which batch, slot or bucket it lands in)."""
+import math
+
+import pytest
+
+from pbccs_amd import synth
+
+
+def _mixed(n, seed, lo=500, hi=20000):
+    return synth.make_zmws(n, None, None, seed=seed, length_range=(lo, hi), passes_range=(3, 30), random_snr=True)
+
+
+@pytest.mark.parametrize("budget,cap,ratio", [(30e9, 2000, 1.5), (2e9, 3, 1.5), (1e12, 2000, 1e9), (1.0, 5, 1.0)])
+def test_plan_is_a_bucketed_partition(budget, cap, ratio):
+    import pbccs_amd
+    zs = _mixed(60, seed=5)
+    batches, est = pbccs_amd.plan_batches(zs, budget, cap, ratio)
+    flat = [i for b in batches for i in b]
+    assert sorted(flat) == list(range(len(zs)))
+    sizes = []
+    for b in batches:
+        assert 1 <= len(b) <= cap
+        lens = [len(zs[i]["draft"]) for i in b]
+        assert lens == sorted(lens)
+        assert max(lens) <= ratio * min(lens) + 1e-9
+        bytes_ = sum(est[i] for i in b)
+        assert len(b) == 1 or bytes_ <= budget
+        sizes.append(bytes_)
+    assert sizes == sorted(sizes, reverse=True)   # largest first
+    assert (batches, est) == pbccs_amd.plan_batches(zs, budget, cap, ratio)   # deterministic
+
+
+def test_plan_estimates_grow_with_length_and_passes():
+    import pbccs_amd
+    a = synth.make_zmws(1, 2000, 10, seed=1)[0]
+    b = synth.make_zmws(1, 10000, 8, seed=1)[0]
+    c = synth.make_zmws(1, 2000, 20, seed=1)[0]
+    _, est = pbccs_amd.plan_batches([a, b, c], 1e12)
+    assert est[1] > 20 * est[0] and 1.8 * est[0] < est[2] < 2.2 * est[0]
+    # the one-batch budget of a 2 kb / 10-pass ZMW is within ~2x of the measured 13.5 MB
+    assert 13.5e6 <= est[0] <= 30e6
+
+
+def test_plan_rejects_bad_arguments():
+    import pbccs_amd
+    zs = _mixed(3, seed=1)
+    for args in [(0.0, 10, 1.5), (1e9, 0, 1.5), (1e9, 10, 0.5)]:
+        with pytest.raises(pbccs_amd.PbccsError):
+            pbccs_amd.plan_batches(zs, *args)
+    assert pbccs_amd.plan_batches([], 1e9) == ([], [])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("per_batch", [0, 2])
+def test_work_queue_matches_oracle_and_single_batch(per_batch):
+    """Mixed lengths (0.3-1.5 kb so the oracle stays fast), passes and SNRs through the queue: buckets of
+    different sizes on different workspace slots; zmws_per_batch=2 exercises the caller-sized chunks."""
+    import pbccs_amd
+    from oracle import oracle as O
+    zs = _mixed(10, seed=97, lo=300, hi=1500)
+    eng = pbccs_amd.Engine(0)
+    eng.set_concurrency(3)
+    got = pbccs_amd.polish_stream(zs, pbccs_amd.ConsensusSettings(zmws_per_batch=per_batch), eng)
+    one = pbccs_amd.polish_zmws(zs, engine=eng)
+    def same(a, b):   # NaN z-scores (ZMWs gated before ZScores) compare equal
+        return a == b or (isinstance(a, float) and isinstance(b, float) and math.isnan(a) and math.isnan(b))
+
+    for z, r, s in zip(zs, got, one):
+        assert r.keys() == s.keys()
+        for k in r:
+            if isinstance(r[k], list):
+                assert len(r[k]) == len(s[k]) and all(same(x, y) for x, y in zip(r[k], s[k])), k
+            else:
+                assert same(r[k], s[k]), k
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+        assert r["add_read_results"] == e["add_read_results"]
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        if e["converged"]:
+            assert r["consensus"] == e["template"]
+            assert max(abs(a - b) for a, b in zip(r["qvs"], e["qvs"])) <= 1
