@@ -275,11 +275,23 @@ __global__ void __launch_bounds__(256) k_compact(DevBatch B, FillScratch F, cons
 
 // ------------------------------------------------------------------------------------------------
 // k_suffix: bSuf[k] = accumulate(bLs[k..J], 0.0) for k in [0, J+1] (bSuf[J+1] = 0), and with
-// withPrefix the alpha prefixes aPre (the cooperative fill leaves them to this kernel).  Each lane sums
-// its own suffix left to right, reading the shared log-scale column from LDS (broadcast-friendly:
-// lanes k, k+1, ... read consecutive words at every step).
+// withPrefix the alpha prefixes aPre (the cooperative fill leaves them to this kernel).  Every lane sums
+// its own k left to right (the reference's order, so no sharing between k is exact).  A wave owns 64
+// consecutive k and walks the log-scale column in wave-uniform order: each LDS read is a broadcast, the
+// 64 columns next to the wave's own k are added under a per-lane predicate (the lane's first add is
+// 0.0 + ls[k], as in the reference), and every other column is added by all lanes with 8 reads in flight.
 // ------------------------------------------------------------------------------------------------
 constexpr int kSuffixTile = 2048;
+
+__device__ __forceinline__ double add8(double s, const double* __restrict__ t)
+{
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = t[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s = s + v[i];
+    return s;
+}
 
 __global__ void __launch_bounds__(256) k_suffix(DevBatch B, const int* __restrict__ reads, int n, int withPrefix)
 {
@@ -291,18 +303,25 @@ __global__ void __launch_bounds__(256) k_suffix(DevBatch B, const int* __restric
     const double* ls = B.bLs + cb;
     double* suf = B.bSuf + cb;
     const int ncol = J + 1;
+    const int lane = threadIdx.x & 63;
+    const int wbase = threadIdx.x & ~63;
     for (int k0 = 0; k0 <= ncol; k0 += blockDim.x) {
-        const int k = k0 + threadIdx.x;
+        const int kb = k0 + wbase;   // the wave's first k
+        const int k = kb + lane;
         double s = 0.0;
-        // walk the columns [k, ncol) in tiles staged through LDS
         for (int c0 = k0; c0 < ncol; c0 += kSuffixTile) {
             __syncthreads();
             for (int q = threadIdx.x; q < kSuffixTile && c0 + q < ncol; q += blockDim.x) tile[q] = ls[c0 + q];
             __syncthreads();
-            const int lo = max(k, c0) - c0;
             const int hi = min(ncol - c0, kSuffixTile);
-            if (k <= ncol)
-                for (int q = lo; q < hi; ++q) s = s + tile[q];
+            int q = max(kb - c0, 0);
+            const int headEnd = min(hi, kb + 64 - c0);   // columns [kb, kb + 64): lane k starts at k
+            for (; q < headEnd; ++q) {
+                const double v = tile[q];
+                if (c0 + q >= k) s = s + v;
+            }
+            for (; q + 8 <= hi; q += 8) s = add8(s, tile + q);
+            for (; q < hi; ++q) s = s + tile[q];
         }
         if (k <= ncol) suf[k] = s;
     }
@@ -311,16 +330,23 @@ __global__ void __launch_bounds__(256) k_suffix(DevBatch B, const int* __restric
     const double* als = B.aLs + cb;
     double* pre = B.aPre + cb;
     for (int k0 = 0; k0 <= ncol; k0 += blockDim.x) {
-        const int k = k0 + threadIdx.x;
+        const int kb = k0 + wbase;
+        const int k = kb + lane;
         double s = 0.0;
-        const int cend = min(ncol, k0 + (int)blockDim.x);
+        const int cend = min(ncol, k0 + (int)blockDim.x);   // block-uniform: the columns any lane needs
         for (int c0 = 0; c0 < cend; c0 += kSuffixTile) {
             __syncthreads();
             for (int q = threadIdx.x; q < kSuffixTile && c0 + q < ncol; q += blockDim.x) tile[q] = als[c0 + q];
             __syncthreads();
-            const int hi = min(min(k, ncol) - c0, kSuffixTile);
-            if (k <= ncol)
-                for (int q = 0; q < hi; ++q) s = s + tile[q];
+            const int hi = min(min(cend, kb + 64) - c0, kSuffixTile);
+            const int bodyEnd = min(hi, kb - c0);   // columns < kb: every lane of the wave adds them
+            int q = 0;
+            for (; q + 8 <= bodyEnd; q += 8) s = add8(s, tile + q);
+            for (; q < bodyEnd; ++q) s = s + tile[q];
+            for (; q < hi; ++q) {
+                const double v = tile[q];
+                if (c0 + q < k) s = s + v;
+            }
         }
         if (k <= ncol) pre[k] = s;
     }

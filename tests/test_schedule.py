@@ -80,3 +80,16 @@ def test_work_queue_matches_oracle_and_single_batch(per_batch):
         if e["converged"]:
             assert r["consensus"] == e["template"]
             assert max(abs(a - b) for a, b in zip(r["qvs"], e["qvs"])) <= 1
+
+
+def test_queue_fails_loudly_without_engine():
+    """pbccs_polish_batch never throws across the ABI: a null engine is EINVAL, not a crash or a CPU fallback."""
+    import ctypes
+    from pbccs_amd import lib as L
+    n = 2
+    ins = (L.CZmwInput * n)()
+    outs = (L.CZmwOutput * n)()
+    opts = L.CPolishOptions()
+    L.load().pbccs_polish_options_default(ctypes.byref(opts))
+    rc = L.load().pbccs_polish_batch(None, ins, n, ctypes.byref(opts), outs)
+    assert L.ERRORS[rc] == "EINVAL"
