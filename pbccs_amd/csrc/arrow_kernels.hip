@@ -955,7 +955,7 @@ __device__ __forceinline__ int wave_max(int v)
 // LDS stage of one wave: the alpha columns sc-1 and beta columns bc its 64 lanes read (contiguous in
 // HBM because fills append columns in order) and the read bases under their rows.
 #ifndef PBCCS_SCORE_STAGE
-#define PBCCS_SCORE_STAGE 512
+#define PBCCS_SCORE_STAGE 384
 #endif
 constexpr int kScoreWaves = 4;
 constexpr int kStageA = PBCCS_SCORE_STAGE;
@@ -969,7 +969,17 @@ struct WaveStage {
 
 // One wave per (work item, read, 64-mutation chunk): the lanes take consecutive mutations of one read,
 // i.e. adjacent template positions, so the wave shares a handful of band columns.
-__global__ void __launch_bounds__(256) k_score(DevBatch B, ScoreWork W, ScoreScratch scratch)
+// Occupancy: at 100 VGPRs and 4 x 9 KB of stage per block, k_score ran 4 waves per SIMD.  A 384-entry
+// stage (27 KB per block) and a 5-wave register budget (96 VGPRs, a few spills) give 5.
+#ifndef PBCCS_SCORE_WAVES
+#define PBCCS_SCORE_WAVES 5
+#endif
+#if PBCCS_SCORE_WAVES > 0
+#define PBCCS_SCORE_OCC __attribute__((amdgpu_waves_per_eu(PBCCS_SCORE_WAVES)))
+#else
+#define PBCCS_SCORE_OCC
+#endif
+__global__ void __launch_bounds__(256) PBCCS_SCORE_OCC k_score(DevBatch B, ScoreWork W, ScoreScratch scratch)
 {
     __shared__ WaveStage stage[kScoreWaves];
     const int wid = threadIdx.x >> 6;
