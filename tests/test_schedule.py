@@ -93,3 +93,23 @@ def test_queue_fails_loudly_without_engine():
     L.load().pbccs_polish_options_default(ctypes.byref(opts))
     rc = L.load().pbccs_polish_batch(None, ins, n, ctypes.byref(opts), outs)
     assert L.ERRORS[rc] == "EINVAL"
+
+
+@pytest.mark.gpu
+def test_work_queue_gated_zmws_keep_input_order():
+    """ZMWs rejected before the device (no subreads, draft shorter than MinLength) mixed into the queue, one
+    of them alone in its length bucket: statuses land at their input positions and the rest still polish."""
+    import pbccs_amd
+    from oracle import oracle as O
+    zs = _mixed(4, seed=98, lo=300, hi=600)
+    empty = {"draft": "ACGTACGTACGTACGT", "snr": [10.0, 7.0, 5.0, 11.0], "reads": []}
+    short = {"draft": "ACGTAC", "snr": [10.0, 7.0, 5.0, 11.0], "reads": [{"seq": "ACGTAC", "strand": 0}] * 3}
+    batch = [zs[0], empty, zs[1], short, zs[2], zs[3]]
+    got = pbccs_amd.polish_stream(batch, engine=pbccs_amd.Engine(0))
+    assert got[1]["status"] == "NoSubreads" and got[3]["status"] == "TooShort"
+    for z, r in zip(zs, [got[0], got[2], got[4], got[5]]):
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+        assert r["add_read_results"] == e["add_read_results"]
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        if e["converged"]:
+            assert r["consensus"] == e["template"]
