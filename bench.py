@@ -27,7 +27,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-TRAFFIC_PROFILE = "r1e_traffic_fill.json"   # PMC HBM bytes of the roofline kernel (tools/gpu_traffic.sh)
+TRAFFIC_PROFILE = "r1i_traffic_fill.json"   # PMC HBM bytes of the roofline kernel (tools/gpu_traffic.sh)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
 
 
