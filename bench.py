@@ -117,7 +117,20 @@ def queue_workload(args, rank, world, eng, settings, seed0):
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res = pbccs_amd.polish_stream(zs, settings, eng)
+    # one native call polishes the whole stream; a heartbeat on stderr shows it is alive (ctypes drops the GIL)
+    import threading
+    done = threading.Event()
+
+    def heartbeat():
+        while not done.wait(30.0):
+            log(rank, f"[bench] work queue running t={time.perf_counter() - t0:.0f}s")
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    try:
+        res = pbccs_amd.polish_stream(zs, settings, eng)
+    finally:
+        done.set()
+        hb.join()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     if world > 1:
