@@ -955,7 +955,7 @@ __device__ __forceinline__ int wave_max(int v)
 // LDS stage of one wave: the alpha columns sc-1 and beta columns bc its 64 lanes read (contiguous in
 // HBM because fills append columns in order) and the read bases under their rows.
 #ifndef PBCCS_SCORE_STAGE
-#define PBCCS_SCORE_STAGE 384
+#define PBCCS_SCORE_STAGE 512
 #endif
 constexpr int kScoreWaves = 4;
 constexpr int kStageA = PBCCS_SCORE_STAGE;
@@ -969,10 +969,12 @@ struct WaveStage {
 
 // One wave per (work item, read, 64-mutation chunk): the lanes take consecutive mutations of one read,
 // i.e. adjacent template positions, so the wave shares a handful of band columns.
-// Occupancy: at 100 VGPRs and 4 x 9 KB of stage per block, k_score ran 4 waves per SIMD.  A 384-entry
-// stage (27 KB per block) and a 5-wave register budget (96 VGPRs, a few spills) give 5.
+// Occupancy experiment switch (off): a 384-entry stage with PBCCS_SCORE_WAVES=5 runs 5 waves per SIMD but
+// spills 12 VGPRs, and a kernel with a private segment needs scratch allocated at dispatch -- which fails
+// (HSA_STATUS_ERROR_OUT_OF_RESOURCES, process abort) when the band pools have taken the device memory.
+// The default build keeps k_score spill-free (100 VGPRs, 4 waves per SIMD).
 #ifndef PBCCS_SCORE_WAVES
-#define PBCCS_SCORE_WAVES 5
+#define PBCCS_SCORE_WAVES 0
 #endif
 #if PBCCS_SCORE_WAVES > 0
 #define PBCCS_SCORE_OCC __attribute__((amdgpu_waves_per_eu(PBCCS_SCORE_WAVES)))

@@ -80,6 +80,8 @@ int guarded(F&& f)
 {
     try {
         return f();
+    } catch (const DeviceOom& e) {
+        return fail(PBCCS_EOOM, e.what());
     } catch (const DeviceError& e) {
         return fail(PBCCS_EDEVICE, e.what());
     } catch (const std::bad_alloc&) {
@@ -702,36 +704,48 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
     std::vector<int> rc(slots, PBCCS_OK);
     std::vector<std::string> err(slots);
     std::mutex statsMu;
+    // a span [b, e) of `order` on one slot; outputs scattered back to input order on success
+    auto run_span = [&](int slot, int b, int e) {
+        const int m = e - b;
+        std::vector<pbccs_zmw_input> bin(m);
+        std::vector<pbccs_zmw_output> bout(m);
+        for (int k = 0; k < m; ++k) {   // output structs point at the caller's buffers
+            bin[k] = in[order[b + k]];
+            bout[k] = out[order[b + k]];
+        }
+        pbccs_batch* h = nullptr;
+        int r = create_batch(eng, bin.data(), m, &o, slot, &h);
+        if (r == PBCCS_OK) r = polish_one(h, bout.data());
+        if (h) {
+            if (h->B) {
+                std::lock_guard<std::mutex> lk(statsMu);
+                merge_engine_stats(eng, *h->B);
+            }
+            pbccs_batch_destroy(h);
+        }
+        if (r == PBCCS_OK)
+            for (int k = 0; k < m; ++k) out[order[b + k]] = bout[k];
+        return r;
+    };
+    // Batches that ran the device out of memory while the other slots held theirs are deferred, and run
+    // one at a time once every slot's pool is unmapped (halved while they still do not fit).  A ZMW's
+    // result does not depend on its batch, so the retry changes nothing but the schedule.
+    std::mutex deferMu;
+    std::vector<std::pair<int, int>> deferred;
     auto worker = [&](int slot) {
-        std::vector<pbccs_zmw_input> bin;
-        std::vector<pbccs_zmw_output> bout;
         for (;;) {
             const int b = next.fetch_add(1);
             if (b >= nb || stop.load()) return;
-            const int m = start[b + 1] - start[b];
-            bin.resize(m);
-            bout.resize(m);
-            for (int k = 0; k < m; ++k) {   // output structs point at the caller's buffers
-                bin[k] = in[order[start[b] + k]];
-                bout[k] = out[order[start[b] + k]];
-            }
-            pbccs_batch* h = nullptr;
-            int r = create_batch(eng, bin.data(), m, &o, slot, &h);
-            if (r == PBCCS_OK) r = polish_one(h, bout.data());
-            if (h) {
-                if (h->B) {
-                    std::lock_guard<std::mutex> lk(statsMu);
-                    merge_engine_stats(eng, *h->B);
-                }
-                pbccs_batch_destroy(h);
-            }
-            if (r != PBCCS_OK) {
+            const int r = run_span(slot, start[b], start[b + 1]);
+            if (r == PBCCS_EOOM) {
+                std::lock_guard<std::mutex> lk(deferMu);
+                deferred.emplace_back(start[b], start[b + 1]);
+            } else if (r != PBCCS_OK) {
                 rc[slot] = r;
                 err[slot] = g_lastError;
                 stop.store(true);
                 return;
             }
-            for (int k = 0; k < m; ++k) out[order[start[b] + k]] = bout[k];
         }
     };
     std::vector<std::thread> pool;
@@ -739,6 +753,21 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
     for (std::thread& t : pool) t.join();
     for (int s = 0; s < slots; ++s)
         if (rc[s] != PBCCS_OK) return fail(rc[s], err[s].c_str());
+    if (!deferred.empty()) {
+        for (int s = 0; s < slots; ++s) eng->Slot(s)->val.unmap_all();
+        std::sort(deferred.begin(), deferred.end());
+        while (!deferred.empty()) {
+            const std::pair<int, int> span = deferred.back();
+            deferred.pop_back();
+            const int r = run_span(0, span.first, span.second);
+            if (r == PBCCS_OK) continue;
+            if (r != PBCCS_EOOM || span.second - span.first < 2) return r;
+            eng->Slot(0)->val.unmap_all();
+            const int mid = span.first + (span.second - span.first) / 2;
+            deferred.emplace_back(mid, span.second);
+            deferred.emplace_back(span.first, mid);
+        }
+    }
     return PBCCS_OK;
 }
 

@@ -105,7 +105,7 @@ void VmPool::map_to(size_t n, bool soft)
             if (soft) break;
             size_t fr = 0, tot = 0;
             (void)hipMemGetInfo(&fr, &tot);
-            throw DeviceError("hipMemCreate failed (device memory): band pool at " + std::to_string(mappedBytes_ >> 30) +
+            throw DeviceOom("hipMemCreate failed (device memory): band pool at " + std::to_string(mappedBytes_ >> 30) +
                               " GB, needs " + std::to_string(want >> 30) + " GB, " + std::to_string(fr >> 20) +
                               " MB free");
         }
@@ -124,6 +124,27 @@ void VmPool::map_to(size_t n, bool soft)
         mappedBytes_ += bytes;
     }
     cap = mappedBytes_ / sizeof(double);
+}
+
+void VmPool::unmap_all()
+{
+    if (!vmm_) {
+        fallback_.release();
+        ptr = nullptr;
+        cap = 0;
+        return;
+    }
+    (void)hipDeviceSynchronize();
+    size_t off = 0;
+    for (size_t k = 0; k < handles_.size(); ++k) {
+        (void)hipMemUnmap(reinterpret_cast<char*>(ptr) + off, sizes_[k]);
+        (void)hipMemRelease(handles_[k]);
+        off += sizes_[k];
+    }
+    handles_.clear();
+    sizes_.clear();
+    mappedBytes_ = 0;
+    cap = 0;
 }
 
 VmPool::~VmPool()

@@ -45,6 +45,13 @@ private:
     std::string what_;
 };
 
+// Device memory exhausted (hipMalloc / hipMemCreate): PBCCS_EOOM at the C ABI, so the work queue can
+// retry the batch once the other slots' pools are unmapped.
+class DeviceOom : public DeviceError {
+public:
+    explicit DeviceOom(std::string what) : DeviceError(std::move(what)) {}
+};
+
 // Device buffer with geometric growth (contents optionally preserved).
 template <class T>
 struct DevVec {
@@ -59,7 +66,7 @@ struct DevVec {
             (void)hipGetLastError();
             size_t fr = 0, tot = 0;
             (void)hipMemGetInfo(&fr, &tot);
-            throw DeviceError("hipMalloc failed (device memory): " + std::to_string(nc * sizeof(T) >> 20) +
+            throw DeviceOom("hipMalloc failed (device memory): " + std::to_string(nc * sizeof(T) >> 20) +
                               " MB requested, " + std::to_string(fr >> 20) + " MB free");
         }
         if (keep && ptr && cap) {
@@ -98,6 +105,8 @@ struct VmPool {
     // Best effort: map granules towards n doubles until the device runs out of memory (no throw).
     // Only meaningful on the VMM path (the hipMalloc fallback would have to copy): there it is a no-op.
     void try_reserve(size_t n);
+    // Unmap every granule (the address reservation stays); the next reserve maps afresh.  Synchronises.
+    void unmap_all();
     ~VmPool();
     VmPool() = default;
     VmPool(const VmPool&) = delete;
