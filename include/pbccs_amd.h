@@ -171,7 +171,9 @@ void pbccs_polish_options_default(pbccs_polish_options* o);
  * WorkQueue.h:64-167) for a stream of heterogeneous ZMWs.  With opts->zmws_per_batch == 0 the ZMWs are
  * bucketed by template length and pass count into device batches sized to the free device memory
  * (pbccs_plan_batches), and the engine's workspace slots pull batches largest-first from a shared queue;
- * otherwise consecutive chunks of zmws_per_batch.  Outputs land in input order either way. */
+ * otherwise consecutive chunks of zmws_per_batch.  Outputs land in input order either way.  A batch that
+ * runs the device out of memory (PBCCS_EOOM) while the other slots hold theirs is rerun alone after the
+ * slots' band pools are unmapped, halved while it still does not fit. */
 int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, const pbccs_polish_options* opts,
                        pbccs_zmw_output* out);
 
