@@ -1,20 +1,25 @@
 #!/usr/bin/env python3
 """CCS polish throughput on MI355X (BASELINE.json metric: CCS ZMWs/sec and GCUPS).
 
-A step polishes one batch of synthetic ZMWs (2 kb insert, 10 full passes)
-end to end on the GPU: AddRead fills + z-score gates, RefineConsensus, ConsensusQVs -- the per-ZMW
-polish that pbccs' Consensus.h runs after the POA.  Inputs are copied to HBM before the timed region
+A step polishes one batch of synthetic ZMWs (2 kb insert, 10 full passes, 2000
+ZMWs per batch) end to end on the GPU: AddRead fills + z-score gates, RefineConsensus, ConsensusQVs -- the
+per-ZMW polish that pbccs' Consensus.h runs after the POA.  Inputs are copied to HBM before the timed region
 (pbccs_batch_create); the timed region is exactly K steps, bracketed by a barrier and
-torch.cuda.synchronize() on both sides; the job time is the max over ranks.  The K steps are pipelined
-(pbccs_batch_polish_many: one host thread + HIP stream per batch in flight), so one batch's convergence
-tail -- the last refine rounds of its few slow ZMWs -- overlaps the others' work, the way ccs's ZMW thread
-pool overlaps ZMWs.  Default: 5 steps x 2000 ZMWs = the 10k-ZMW workload of configs[1].  Multi-GPU: each rank polishes its own shard (weak scaling,
-no data-path collective).  rank 0 prints one JSON line.
+torch.cuda.synchronize() on both sides; the job time is the max over ranks.  The K steps are pipelined over
+S workspace slots (pbccs_batch_polish_many: one host thread + HIP stream per slot), so one batch's
+convergence tail -- the last refine rounds of its few slow ZMWs -- overlaps the others' work, the way ccs's
+ZMW thread pool overlaps ZMWs.  S is the measured best split (5) capped by what fits in HBM.
+
+Multi-GPU: `--gpus N` without a launcher spawns N ranks itself (one process per GPU, RANK/LOCAL_RANK/
+WORLD_SIZE set before any HIP call; the parent never touches the GPU); under torch.distributed.run the
+launcher's ranks are used.  Each rank polishes its own K steps (weak scaling, no data-path collective);
+rank 0 prints one JSON line.
 """
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,8 +32,11 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-TRAFFIC_PROFILE = "r1i_traffic_fill.json"   # PMC HBM bytes of the roofline kernel (tools/gpu_traffic.sh)
+TRAFFIC_PROFILE = "r2_traffic_fill.json"   # PMC HBM bytes of the roofline kernel (tools/gpu_traffic.sh)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
+BEST_SLOTS = 5                 # measured best split of 2 kb batches
+SLOT_BYTES_PER_ZMW = 18 << 20  # measured band + score high-water per 2 kb / 10-pass ZMW in a slot
+HBM_MARGIN = 24 << 30          # device memory left to scratch, selection buffers and the runtime
 
 
 def parse():
@@ -37,24 +45,21 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--zmws-per-step", type=int, default=2000)
-    ap.add_argument("--warmup-zmws", type=int, default=0,
-                    help="ZMWs per warmup step (0 = --zmws-per-step: a warmup step is a full-size step, so the "
-                         "engine's score and selection buffers reach their steady-state size before timing)")
     ap.add_argument("--length", type=int, default=2000)
     ap.add_argument("--passes", type=int, default=10)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--workload", choices=["2kb", "10kb", "mixed"], default="2kb",
+    ap.add_argument("--workload", choices=["2kb", "10kb", "mixed", "smrtcell"], default="2kb",
                     help="2kb: configs[1], the headline line (pre-created batches, inputs resident in HBM). "
                          "10kb / mixed: configs[2] / configs[3] through the ZMW work queue (polish_stream: "
-                         "length/pass buckets, memory-sized batches, largest first); the timed region then "
-                         "includes the host->device copy of the reads")
+                         "length/pass buckets, memory-sized batches, largest first); smrtcell: configs[4], a mix "
+                         "of the three (steps x zmws-per-step ZMWs in total, strong scaling) pulled by the ranks "
+                         "from a dynamic queue.  For the queue workloads the timed region includes the read upload")
     ap.add_argument("--cpu-sample", type=int, default=None,
-                    help="ZMWs polished by the CPU baseline (0 = skip; default 192 for 2kb, 0 otherwise)")
+                    help="ZMWs polished by the CPU baseline (0 = skip; default 256 for 2kb, 0 otherwise)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--streams", type=int, default=0,
-                    help="batches polished concurrently (0 = min(steps, 8)); each has its own HIP stream")
+                    help="workspace slots = batches polished concurrently (0 = min(steps, 5), capped by HBM)")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
 
@@ -63,26 +68,66 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(args, rank):
-    """The oracle (bit-faithful CPU restatement, test infrastructure) on host cores, one ZMW per task on a
-    thread pool like `ccs --numThreads` (src/main/ccs.cpp:222-230)."""
+# ---------------------------------------------------------------------------------------------------------
+# self-launch of N ranks (the parent never initialises HIP)
+# ---------------------------------------------------------------------------------------------------------
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    return rc
+
+
+# ---------------------------------------------------------------------------------------------------------
+# CPU baseline
+# ---------------------------------------------------------------------------------------------------------
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args):
+    """The oracle (bit-faithful CPU restatement of the reference's polish, test infrastructure) on host
+    cores, one ZMW per task on a thread pool like `ccs --numThreads` (src/main/ccs.cpp:222-230).  The thread
+    count is this process's CPU share: the GPU boxes give one GPU's job 16 cores of a larger machine
+    (OMP_NUM_THREADS), so hardware_concurrency() would oversubscribe."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
     from pbccs_amd import synth
 
     n = args.cpu_sample
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    threads = args.cpu_threads or max(1, min(share, os.cpu_count() or 1))
     threads = max(1, min(threads, n))
     zmws = synth.make_zmws(n, seed=args.seed + 99991, **workload_kw(args))
     O.lib()
     t0 = time.perf_counter()
-    with ThreadPoolExecutor(max_workers=threads) as ex:
+    with ThreadPoolExecutor(max_workers=threads) as ex:   # ctypes releases the GIL: native threads in parallel
         list(ex.map(lambda z: O.polish_zmw(z["draft"], z["reads"], z["snr"]), zmws))
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "ZMWs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} synthetic ZMWs of the same config ({args.workload}), "
-                      f"oracle/arrow_oracle.cpp polish (AddRead, RefineConsensus, ConsensusQVs) on {threads} "
-                      f"host threads, {dt:.1f} s wall"}
+    return {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port",
+            "cpu": cpu_model(), "nproc": os.cpu_count(),
+            "sample": f"{n} synthetic ZMWs of the same config ({args.workload}, seed {args.seed + 99991}), "
+                      f"oracle/arrow_oracle.cpp polish (AddRead, RefineConsensus, ConsensusQVs) one ZMW per task "
+                      f"on {threads} host threads, {dt:.1f} s wall"}
 
 
 def workload_kw(args):
@@ -94,22 +139,45 @@ def workload_kw(args):
     return dict(length=args.length, passes=args.passes)
 
 
+# ---------------------------------------------------------------------------------------------------------
+# queue workloads (configs[2], [3], [4])
+# ---------------------------------------------------------------------------------------------------------
+def heartbeat(rank, t0):
+    import threading
+    done = threading.Event()
+
+    def beat():
+        while not done.wait(30.0):
+            log(rank, f"[bench] work queue running t={time.perf_counter() - t0:.0f}s")
+    threading.Thread(target=beat, daemon=True).start()
+    return done
+
+
 def queue_workload(args, rank, world, eng, settings, seed0):
-    """configs[2] / configs[3] through the work queue; returns (job_time, local_time, results, workload)."""
+    """configs[2] / [3] through the work queue, configs[4] through the ranks' dynamic queue; returns
+    (job_time, local_time, results, workload, scaling)."""
     import pbccs_amd
     import torch
     import torch.distributed as dist
-    from pbccs_amd import synth
+    from pbccs_amd import shard, synth
     n = args.steps * args.zmws_per_step
-    kw = workload_kw(args)
-    if args.workload == "10kb":
-        desc = f"configs[2]: synthetic 10000 bp insert, 8 full passes, {n} ZMWs per GPU"
+    if args.workload == "smrtcell":
+        desc = (f"configs[4]: SMRT-cell mix of configs[1]-[3] (2 kb x 10, 10 kb x 8, 0.5-20 kb x 3-30 passes; "
+                f"one third each), {n} ZMWs in total over {world} GPU(s), dynamic pull queue")
+        kw = None
     else:
-        desc = f"configs[3]: synthetic 0.5-20 kb inserts, 3-30 passes, per-ZMW SNR U[4,20], {n} ZMWs per GPU"
+        kw = workload_kw(args)
+        desc = (f"configs[2]: synthetic 10000 bp insert, 8 full passes, {n} ZMWs per GPU" if args.workload == "10kb"
+                else f"configs[3]: synthetic 0.5-20 kb inserts, 3-30 passes, per-ZMW SNR U[4,20], {n} ZMWs per GPU")
     for w in range(args.warmup):
-        pbccs_amd.polish_stream(synth.make_zmws(max(1, args.warmup_zmws), seed=seed0 + 1000 + w, **kw), settings, eng)
+        wz = synth.make_smrtcell(4, seed=seed0 + 1000 + w) if kw is None else \
+            synth.make_zmws(4, seed=seed0 + 1000 + w, **kw)
+        pbccs_amd.polish_stream(wz, settings, eng)
     log(rank, "[bench] warmup done")
-    zs = synth.make_zmws(n, seed=seed0, **kw)
+    if kw is None:
+        zs = synth.make_smrtcell(n, seed=args.seed + 3)   # the same cell on every rank; the queue splits it
+    else:
+        zs = synth.make_zmws(n, seed=seed0, **kw)
     eng.kernel_stats(reset=True)
     eng.counters(reset=True)
     if world > 1:
@@ -117,47 +185,68 @@ def queue_workload(args, rank, world, eng, settings, seed0):
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # one native call polishes the whole stream; a heartbeat on stderr shows it is alive (ctypes drops the GIL)
-    import threading
-    done = threading.Event()
-
-    def heartbeat():
-        while not done.wait(30.0):
-            log(rank, f"[bench] work queue running t={time.perf_counter() - t0:.0f}s")
-    hb = threading.Thread(target=heartbeat, daemon=True)
-    hb.start()
+    done = heartbeat(rank, t0)
     try:
-        res = pbccs_amd.polish_stream(zs, settings, eng)
+        if kw is None:
+            res = shard.polish_dynamic(zs, settings, eng, rank, world, chunk=max(1, args.zmws_per_step // 4))
+        else:
+            res = pbccs_amd.polish_stream(zs, settings, eng)
     finally:
         done.set()
-        hb.join()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     local_time = time.perf_counter() - t0
-    job_time = local_time
-    if world > 1:
-        t = torch.tensor([local_time], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        job_time = float(t.item())
-    return job_time, local_time, res, desc + " (work queue; timed region includes the read upload)"
+    job_time = max_over_ranks(local_time, world)
+    if kw is None:   # rank 0 holds the whole cell's records; the count is the cell
+        return job_time, local_time, (res or []), desc, "strong", n
+    return job_time, local_time, res, desc + " (work queue; timed region includes the read upload)", "weak", \
+        n * world
+
+
+def max_over_ranks(t, world):
+    if world == 1:
+        return t
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor([t], dtype=torch.float64)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    return float(v.item())
+
+
+# ---------------------------------------------------------------------------------------------------------
+def choose_slots(args, local):
+    """Workspace slots: the measured best split, capped by the steps and by the HBM the slots' band pools
+    need at their high-water mark (a 2 kb / 10-pass batch of 2000 ZMWs peaks near 36 GB)."""
+    import torch
+    want = args.streams or max(1, min(args.steps, BEST_SLOTS))
+    if not torch.cuda.is_available():
+        return want
+    free_b, _ = torch.cuda.mem_get_info(local)
+    per_slot = max(1, args.zmws_per_step) * SLOT_BYTES_PER_ZMW
+    fit = max(1, int((free_b - HBM_MARGIN) // per_slot))
+    return max(1, min(want, fit))
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     if args.cpu_sample is None:
-        args.cpu_sample = 192 if args.workload == "2kb" else 0
+        args.cpu_sample = 256 if args.workload == "2kb" else 0
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(rank, f"[bench] note: --gpus {args.gpus} but the launcher started {world} rank(s); using {world}")
     # torch first: the engine then binds to the same HIP runtime instance (both carry soname libamdhip64.so.7)
     import torch
     import torch.distributed as dist
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group(backend="gloo")   # barrier + max-time only: the polish path has no collective
+        dist.init_process_group(backend="gloo")   # barrier + max-time + the queue's counter: no device collective
 
     import pbccs_amd
     from pbccs_amd import synth
@@ -171,38 +260,32 @@ def main():
             torch.cuda.synchronize()
 
     eng = pbccs_amd.Engine(local)
-    streams = args.streams or max(1, min(args.steps, 8))
-    eng.set_concurrency(streams)
+    slots = choose_slots(args, local)
+    eng.set_concurrency(slots)
     if not args.no_profile:
-        eng.set_profiling(True)   # HIP events on the engine stream + in-kernel algorithmic counters
+        eng.set_profiling(True)   # HIP events on the launch streams + in-kernel algorithmic counters
     settings = pbccs_amd.ConsensusSettings()
     seed0 = args.seed + 7919 * rank
 
     if args.workload != "2kb":
-        job_time, local_time, res, workload = queue_workload(args, rank, world, eng, settings, seed0)
-        return report(args, rank, world, eng, streams, job_time, local_time, res, workload)
+        job_time, local_time, res, workload, scaling, total = queue_workload(args, rank, world, eng, settings, seed0)
+        return report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total)
 
-    # ---- warmup (untimed) -------------------------------------------------------------------
-    if args.warmup_zmws <= 0:
-        args.warmup_zmws = args.zmws_per_step
-    # a warmup step polishes one batch per workspace slot, concurrently like the timed steps, so every
-    # slot's score/selection buffers and band pool reach steady-state size (their growth would otherwise
-    # allocate -- and synchronise the device -- inside the timed region)
-    for w in range(args.warmup):
-        wb = [pbccs_amd.PreparedBatch(synth.make_zmws(args.warmup_zmws, args.length, args.passes,
-                                                      seed=seed0 + 1000 + 37 * w + s), settings, eng)
-              for s in range(streams)]
-        pbccs_amd.polish_many(wb)
-        for b in wb:
-            b.close()
-    log(rank, f"[bench] warmup done ({args.warmup} x {streams} x {args.warmup_zmws} ZMWs)")
+    # ---- warmup (untimed): W steps, concurrently over the slots like the timed ones ------------------
+    wb = [pbccs_amd.PreparedBatch(synth.make_zmws(args.zmws_per_step, args.length, args.passes,
+                                                  seed=seed0 + 1000 + w), settings, eng)
+          for w in range(args.warmup)]
+    pbccs_amd.polish_many(wb)
+    for b in wb:
+        b.close()
+    log(rank, f"[bench] warmup done ({args.warmup} x {args.zmws_per_step} ZMWs over {slots} slots)")
 
     # ---- engine pools mapped before the timed region (a long run maps them once and reuses them) ----
     if torch.cuda.is_available():
         free_b, _ = torch.cuda.mem_get_info(local)
-        per_slot = int(min(0.6 * free_b / streams, 48 << 30))
+        per_slot = int(min(0.6 * free_b / slots, 36 << 30))
         eng.reserve_pool(per_slot)
-        log(rank, f"[bench] mapped {per_slot / 2**30:.1f} GB of band pool per slot x {streams}")
+        log(rank, f"[bench] band pools: {per_slot / 2**30:.1f} GB mapped per slot x {slots}")
 
     # ---- inputs resident in HBM before the timed region ------------------------------------------
     t_prep = time.perf_counter()
@@ -210,7 +293,7 @@ def main():
     for k in range(args.steps):
         zs = synth.make_zmws(args.zmws_per_step, args.length, args.passes, seed=seed0 + k)
         batches.append(pbccs_amd.PreparedBatch(zs, settings, eng))
-        log(rank, f"[bench] prepared step {k} ({args.zmws_per_step} ZMWs) t={time.perf_counter() - t_prep:.1f}s")
+    log(rank, f"[bench] prepared {args.steps} steps x {args.zmws_per_step} ZMWs in {time.perf_counter() - t_prep:.1f}s")
     eng.kernel_stats(reset=True)
     eng.counters(reset=True)
 
@@ -218,40 +301,38 @@ def main():
     barrier()
     sync()
     t0 = time.perf_counter()
-    pbccs_amd.polish_many(batches)   # the K steps, pipelined over `streams` HIP streams / host threads
-    log(rank, f"[bench] {args.steps} steps done t={time.perf_counter() - t0:.2f}s")
+    pbccs_amd.polish_many(batches)   # the K steps, pipelined over the slots' HIP streams / host threads
     sync()
     barrier()
-    t1 = time.perf_counter()
-    local_time = t1 - t0
-    if world > 1:
-        t = torch.tensor([local_time], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        job_time = float(t.item())
-    else:
-        job_time = local_time
+    local_time = time.perf_counter() - t0
+    log(rank, f"[bench] {args.steps} steps done t={local_time:.2f}s")
+    job_time = max_over_ranks(local_time, world)
 
     res = [r for b in batches for r in b.results()]
     for b in batches:
         b.close()
     workload = (f"configs[1]: synthetic {args.length} bp insert, {args.passes} full passes, "
-                f"{args.zmws_per_step * args.steps} ZMWs per GPU ({args.steps} steps x {args.zmws_per_step})")
-    report(args, rank, world, eng, streams, job_time, local_time, res, workload)
+                f"{args.zmws_per_step} ZMWs per step")
+    report(args, rank, world, eng, slots, job_time, local_time, res, workload, "weak", len(res) * world)
 
 
-def report(args, rank, world, eng, streams, job_time, local_time, res, workload):
+def report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total_zmws):
     import torch.distributed as dist
     stats = eng.kernel_stats(reset=True)
     counters = eng.counters(reset=True)
-    n_local = len(res)
     statuses = {}
     for r in res:
         statuses[r["status"]] = statuses.get(r["status"], 0) + 1
 
-    total_zmws = n_local * world
     value = total_zmws / job_time
     cells = sum(s["cells"] for s in stats.values())
     gcups_local = cells / local_time / 1e9 if local_time > 0 else 0.0
+    gcups = gcups_local * world
+    if world > 1:   # sum of the ranks' cells over the job time
+        import torch
+        t = torch.tensor([cells], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        gcups = float(t.item()) / job_time / 1e9
 
     # dominant kernel (by device time) -> roofline: algorithmic band bytes / its device time
     dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["device_ms"])
@@ -264,7 +345,7 @@ def report(args, rank, world, eng, streams, job_time, local_time, res, workload)
     # (tools/gpu_traffic.sh -> tools/pmc_traffic.py, gfx950 correction 2*FETCH_SIZE + WRITE_SIZE) when
     # they were taken on this kernel family and workload; null otherwise.
     traffic, traffic_src = None, None
-    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", TRAFFIC_PROFILE)
+    tpath = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE)
     if os.path.exists(tpath):
         t = json.load(open(tpath))
         if t.get("kernel") == dom_name and t.get("workload") == workload:
@@ -284,18 +365,20 @@ def report(args, rank, world, eng, streams, job_time, local_time, res, workload)
         "warmup": args.warmup,
         "ms_per_step": round(job_time / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY.md §8(d): truth iid ACGT; subreads 7%/4%/1% ins/del/sub; draft 0.5/0.5/0.2%)",
         "config": {"workload": workload,
                    "zmws_per_step": args.zmws_per_step,
+                   "zmws_total": total_zmws,
                    "insert_bp": args.length if args.workload == "2kb" else
-                   (10000 if args.workload == "10kb" else "500-20000"),
-                   "passes": args.passes if args.workload == "2kb" else (8 if args.workload == "10kb" else "3-30"),
-                   "streams": streams,
+                   {"10kb": 10000, "mixed": "500-20000", "smrtcell": "mix"}[args.workload],
+                   "passes": args.passes if args.workload == "2kb" else
+                   {"10kb": 8, "mixed": "3-30", "smrtcell": "mix"}[args.workload],
+                   "slots": slots,
                    "parallelism": f"zmw-shard x{world}"},
-        "gcups": round(gcups_local * world, 3),
+        "gcups": round(gcups, 3),
         "zmw_status": statuses,
         "roofline": roofline,
         "kernels": {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
@@ -303,9 +386,12 @@ def report(args, rank, world, eng, streams, job_time, local_time, res, workload)
                     for k, v in stats.items()},
         "score_tasks": counters["score_tasks"],
         "mutations_scored": counters["mutations"],
+        "band_memory_gb": {k: round(counters[k] / 2**30, 3) for k in
+                           ("band_top_bytes", "band_region_bytes", "band_used_bytes", "pool_mapped_bytes")},
+        "oom_retries": counters["oom_retries"],
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline(args, rank)
+        out["cpu_baseline"] = cpu_baseline(args)
         out["vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -199,7 +199,10 @@ void pbccs_batch_destroy(pbccs_batch* b);
 /* Polish several batches of one engine concurrently: one host thread and one HIP stream per workspace
  * slot, so that one batch's convergence tail (the last refine rounds of a few ZMWs) overlaps the other
  * batches' work.  The analogue of ccs's ZMW thread pool (src/main/ccs.cpp:222-230, WorkQueue.h).
- * outs[i] receives batch i's outputs.  Returns the first failure. */
+ * outs[i] receives batch i's outputs.  A batch that runs the device out of memory (PBCCS_EOOM) while the
+ * others hold their band pools is rebuilt from its inputs (the batch keeps a host copy) and rerun alone once
+ * every slot's pool is unmapped, halved while it still does not fit; pbccs_batch_polish does the same for
+ * a single batch.  Returns the first failure. */
 int pbccs_batch_polish_many(pbccs_batch* const* batches, int n, pbccs_zmw_output* const* outs);
 
 /* Number of workspace slots = batches that may polish at the same time (default 4).  Set it before
@@ -215,6 +218,11 @@ int pbccs_engine_reserve_pool(pbccs_engine* eng, size_t bytes_per_slot);
 /* Work counters of the engine since the last reset (for roofline accounting). */
 typedef struct {
     long long fill_launches, score_launches, score_tasks, mutations;
+    long long band_top_bytes;    /* max over batches: band value pool handed out (the bump top) */
+    long long band_region_bytes; /* max over batches: the reads' current band regions (2 x capacity each) */
+    long long band_used_bytes;   /* max over batches: band cells the reads' last fills stored */
+    long long pool_mapped_bytes; /* device memory the workspace slots' band pools hold mapped now */
+    long long oom_retries;       /* device batches rerun after running the device out of memory */
 } pbccs_counters;
 int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset);
 

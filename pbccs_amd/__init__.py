@@ -108,8 +108,7 @@ class Engine:
     def counters(self, reset=False):
         c = _lib_mod.CCounters()
         _lib_mod.check(load().pbccs_engine_counters(self._h, ctypes.byref(c), 1 if reset else 0))
-        return {"fill_launches": c.fill_launches, "score_launches": c.score_launches, "score_tasks": c.score_tasks,
-                "mutations": c.mutations}
+        return {k: getattr(c, k) for k, _ in _lib_mod.CCounters._fields_}
 
 
 _default_engine = None

@@ -35,6 +35,8 @@ struct pbccs_engine {
     // share a slot never polish at the same time (pbccs_batch_polish_many runs one slot per thread).
     int concurrency = 4;
     int nextSlot = 0;
+    std::mutex statsMu;        // counters / stats are merged from the slots' worker threads
+    long long oomRetries = 0;   // device batches rerun after PBCCS_EOOM
     std::vector<std::unique_ptr<Workspace>> slots;
     Workspace* Slot(int s)
     {
@@ -43,7 +45,57 @@ struct pbccs_engine {
     }
 };
 
+// Owned host copy of a batch's inputs: a batch that ran the device out of memory is rebuilt from it.
+struct HostInputs {
+    struct Zmw {
+        std::string draft;
+        std::vector<std::string> seqs;
+        std::vector<const char*> seqPtr;
+        std::vector<int> lens, strands, ts, te;
+        std::vector<unsigned char> full;
+    };
+    std::vector<Zmw> z;
+    std::vector<pbccs_zmw_input> in;   // views into z
+    void assign(const pbccs_zmw_input* src, int n)
+    {
+        z.assign(n, Zmw());
+        in.assign(n, pbccs_zmw_input());
+        for (int i = 0; i < n; ++i) {
+            const pbccs_zmw_input& s = src[i];
+            Zmw& d = z[i];
+            const int nr = std::max(0, s.n_reads);
+            d.draft.assign(s.draft ? s.draft : "", s.draft ? std::max(0, s.draft_len) : 0);
+            d.seqs.resize(nr);
+            d.lens.assign(nr, 0);
+            d.strands.assign(nr, 0);
+            d.ts.assign(nr, 0);
+            d.te.assign(nr, 0);
+            d.full.assign(nr, 1);
+            for (int k = 0; k < nr; ++k) {
+                d.lens[k] = s.lens[k];
+                d.seqs[k].assign(s.seqs[k], std::max(0, s.lens[k]));
+                d.strands[k] = s.strands[k];
+                d.ts[k] = s.tstarts[k];
+                d.te[k] = s.tends[k];
+                if (s.full_pass) d.full[k] = s.full_pass[k];
+            }
+            d.seqPtr.resize(nr);
+            for (int k = 0; k < nr; ++k) d.seqPtr[k] = d.seqs[k].c_str();
+            pbccs_zmw_input& v = in[i];
+            v = s;
+            v.draft = d.draft.c_str();
+            v.seqs = d.seqPtr.data();
+            v.lens = d.lens.data();
+            v.strands = d.strands.data();
+            v.tstarts = d.ts.data();
+            v.tends = d.te.data();
+            v.full_pass = d.full.data();
+        }
+    }
+};
+
 struct pbccs_batch {
+    HostInputs inputs;
     pbccs_engine* eng = nullptr;
     int slot = 0;
     std::unique_ptr<ArrowBatch> B;
@@ -164,7 +216,17 @@ int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset)
     out->score_launches = eng->counters.scoreLaunches;
     out->score_tasks = eng->counters.scoreTasks;
     out->mutations = eng->counters.mutations;
-    if (reset) eng->counters = Counters();
+    out->band_top_bytes = eng->counters.bandTopBytes;
+    out->band_region_bytes = eng->counters.bandRegionBytes;
+    out->band_used_bytes = eng->counters.bandUsedBytes;
+    long long mapped = 0;
+    for (const auto& s : eng->slots) mapped += (long long)s->val.mapped_bytes();
+    out->pool_mapped_bytes = mapped;
+    out->oom_retries = eng->oomRetries;
+    if (reset) {
+        eng->counters = Counters();
+        eng->oomRetries = 0;
+    }
     return PBCCS_OK;
 }
 
@@ -384,15 +446,25 @@ void pbccs_polish_options_default(pbccs_polish_options* o)
     o->zmws_per_batch = 0;
 }
 
+// Merge a batch's counters and profile into its engine.  Never throws: it runs in worker threads and on
+// the way out of the C ABI (a device error while resolving events only loses that batch's timings).
 static void merge_engine_stats(pbccs_engine* eng, ArrowBatch& B)
 {
-    const Counters& c = B.counters();
-    eng->counters.fillLaunches += c.fillLaunches;
-    eng->counters.scoreLaunches += c.scoreLaunches;
-    eng->counters.scoreTasks += c.scoreTasks;
-    eng->counters.mutations += c.mutations;
-    B.ResetCounters();
-    B.CollectProfile(eng->stats);
+    std::lock_guard<std::mutex> lk(eng->statsMu);
+    try {
+        const Counters& c = B.counters();
+        eng->counters.fillLaunches += c.fillLaunches;
+        eng->counters.scoreLaunches += c.scoreLaunches;
+        eng->counters.scoreTasks += c.scoreTasks;
+        eng->counters.mutations += c.mutations;
+        eng->counters.bandTopBytes = std::max(eng->counters.bandTopBytes, c.bandTopBytes);
+        eng->counters.bandRegionBytes = std::max(eng->counters.bandRegionBytes, c.bandRegionBytes);
+        eng->counters.bandUsedBytes = std::max(eng->counters.bandUsedBytes, c.bandUsedBytes);
+        B.ResetCounters();
+        B.CollectProfile(eng->stats);
+    } catch (...) {
+        (void)hipGetLastError();
+    }
 }
 
 // A batch on an explicit workspace slot (slot < 0: the next slot round-robin).
@@ -408,6 +480,7 @@ static int create_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, con
         if (opts) b->o = *opts;
         b->n = n;
         b->slot = slot >= 0 ? slot : eng->nextSlot++ % std::max(1, eng->concurrency);
+        b->inputs.assign(in, n);
         b->B.reset(new ArrowBatch(eng->device, eng->Slot(b->slot)));
         b->B->SetProfiling(eng->profiling);
         ArrowOptions ao;
@@ -453,6 +526,7 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
 {
     if (!b || (b->n > 0 && !out)) return fail(PBCCS_EINVAL, "bad argument");
     if (b->polished) return fail(PBCCS_ESTATE, "a batch polishes once");
+    if (!b->B) return fail(PBCCS_ESTATE, "the batch's device state was released");
     return guarded([&] {
         if (hipSetDevice(b->eng->device) != hipSuccess) return fail(PBCCS_EDEVICE, "hipSetDevice failed");
         b->polished = true;
@@ -539,10 +613,55 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
     });
 }
 
+// Create, polish, account and destroy one device batch of m ZMWs on `slot`.
+static int polish_span(pbccs_engine* eng, int slot, const pbccs_zmw_input* in, int m, const pbccs_polish_options* o,
+                       pbccs_zmw_output* out)
+{
+    pbccs_batch* h = nullptr;
+    int r = create_batch(eng, in, m, o, slot, &h);
+    if (r == PBCCS_OK) r = polish_one(h, out);
+    if (h) {
+        if (h->B) merge_engine_stats(eng, *h->B);
+        pbccs_batch_destroy(h);
+    }
+    return r;
+}
+
+// Rerun ZMWs whose batch ran the device out of memory, alone on `slot` once the other slots have drained
+// and every slot's band pool is unmapped; a span that still does not fit is halved.  A ZMW's result does
+// not depend on the batch it polishes in (the engine's only cross-ZMW state is the launch grouping), so
+// the retry changes the schedule and nothing else.  Outputs land in out[0..n) in input order.
+static int polish_retry(pbccs_engine* eng, int slot, const pbccs_zmw_input* in, int n, const pbccs_polish_options* o,
+                        pbccs_zmw_output* out)
+{
+    std::vector<std::pair<int, int>> todo{{0, n}};
+    while (!todo.empty()) {
+        const std::pair<int, int> span = todo.back();
+        todo.pop_back();
+        {
+            std::lock_guard<std::mutex> lk(eng->statsMu);
+            eng->oomRetries += 1;
+        }
+        const int r = polish_span(eng, slot, in + span.first, span.second - span.first, o, out + span.first);
+        if (r == PBCCS_OK) continue;
+        if (r != PBCCS_EOOM || span.second - span.first < 2) return r;
+        eng->Slot(slot)->val.unmap_all();
+        const int mid = span.first + (span.second - span.first) / 2;
+        todo.emplace_back(mid, span.second);
+        todo.emplace_back(span.first, mid);
+    }
+    return PBCCS_OK;
+}
+
 int pbccs_batch_polish(pbccs_batch* b, pbccs_zmw_output* out)
 {
-    const int rc = polish_one(b, out);
+    int rc = polish_one(b, out);
     if (b && b->B) merge_engine_stats(b->eng, *b->B);
+    if (rc == PBCCS_EOOM && b) {   // alone on the device already: free this slot's pool and rerun, halving
+        b->B.reset();
+        b->eng->Slot(b->slot)->val.unmap_all();
+        rc = polish_retry(b->eng, b->slot, b->inputs.in.data(), b->n, &b->o, out);
+    }
     return rc;
 }
 
@@ -567,15 +686,29 @@ int pbccs_batch_polish_many(pbccs_batch* const* batches, int n, pbccs_zmw_output
     for (const std::vector<int>& list : bySlot) {
         if (list.empty()) continue;
         pool.emplace_back([&, list] {
-            for (int i : list) {
+            for (int i : list) {   // polish_one and merge_engine_stats never throw
                 rc[i] = polish_one(batches[i], outs[i]);
                 if (rc[i] != PBCCS_OK) err[i] = g_lastError;
+                if (batches[i]->B) merge_engine_stats(eng, *batches[i]->B);
             }
         });
     }
     for (std::thread& t : pool) t.join();
+    // Batches that ran the device out of memory while the other slots held their pools are rebuilt from
+    // their inputs and rerun one at a time, after every slot's pool is unmapped (halved while they still do
+    // not fit).
+    std::vector<int> deferred;
     for (int i = 0; i < n; ++i)
-        if (batches[i]->B) merge_engine_stats(eng, *batches[i]->B);
+        if (rc[i] == PBCCS_EOOM) deferred.push_back(i);
+    if (!deferred.empty()) {
+        for (int i : deferred) batches[i]->B.reset();
+        for (size_t s = 0; s < eng->slots.size(); ++s) eng->slots[s]->val.unmap_all();
+        for (int i : deferred) {
+            pbccs_batch* b = batches[i];
+            rc[i] = polish_retry(eng, b->slot, b->inputs.in.data(), b->n, &b->o, outs[i]);
+            if (rc[i] != PBCCS_OK) err[i] = g_lastError;
+        }
+    }
     for (int i = 0; i < n; ++i)
         if (rc[i] != PBCCS_OK) return fail(rc[i], err[i].c_str());
     return PBCCS_OK;
@@ -703,44 +836,42 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
     std::atomic<bool> stop{false};
     std::vector<int> rc(slots, PBCCS_OK);
     std::vector<std::string> err(slots);
-    std::mutex statsMu;
-    // a span [b, e) of `order` on one slot; outputs scattered back to input order on success
-    auto run_span = [&](int slot, int b, int e) {
-        const int m = e - b;
-        std::vector<pbccs_zmw_input> bin(m);
-        std::vector<pbccs_zmw_output> bout(m);
-        for (int k = 0; k < m; ++k) {   // output structs point at the caller's buffers
-            bin[k] = in[order[b + k]];
-            bout[k] = out[order[b + k]];
+    // a span [b, e) of `order`: inputs gathered, outputs scattered back to input order (also on failure:
+    // the output structs only point at the caller's buffers)
+    auto gather = [&](int b, int e, std::vector<pbccs_zmw_input>* bin, std::vector<pbccs_zmw_output>* bout) {
+        bin->resize(e - b);
+        bout->resize(e - b);
+        for (int k = 0; k < e - b; ++k) {
+            (*bin)[k] = in[order[b + k]];
+            (*bout)[k] = out[order[b + k]];
         }
-        pbccs_batch* h = nullptr;
-        int r = create_batch(eng, bin.data(), m, &o, slot, &h);
-        if (r == PBCCS_OK) r = polish_one(h, bout.data());
-        if (h) {
-            if (h->B) {
-                std::lock_guard<std::mutex> lk(statsMu);
-                merge_engine_stats(eng, *h->B);
-            }
-            pbccs_batch_destroy(h);
-        }
-        if (r == PBCCS_OK)
-            for (int k = 0; k < m; ++k) out[order[b + k]] = bout[k];
-        return r;
     };
-    // Batches that ran the device out of memory while the other slots held theirs are deferred, and run
-    // one at a time once every slot's pool is unmapped (halved while they still do not fit).  A ZMW's
-    // result does not depend on its batch, so the retry changes nothing but the schedule.
+    auto scatter = [&](int b, int e, const std::vector<pbccs_zmw_output>& bout) {
+        for (int k = 0; k < e - b; ++k) out[order[b + k]] = bout[k];
+    };
+    // Batches that ran the device out of memory while the other slots held theirs are deferred and rerun
+    // one at a time once every slot's pool is unmapped (polish_retry).
     std::mutex deferMu;
     std::vector<std::pair<int, int>> deferred;
     auto worker = [&](int slot) {
+        std::vector<pbccs_zmw_input> bin;
+        std::vector<pbccs_zmw_output> bout;
         for (;;) {
             const int b = next.fetch_add(1);
             if (b >= nb || stop.load()) return;
-            const int r = run_span(slot, start[b], start[b + 1]);
-            if (r == PBCCS_EOOM) {
+            int r = PBCCS_OK;
+            try {
+                gather(start[b], start[b + 1], &bin, &bout);
+            } catch (...) {
+                r = fail(PBCCS_EOOM, "out of host memory");
+            }
+            if (r == PBCCS_OK) r = polish_span(eng, slot, bin.data(), start[b + 1] - start[b], &o, bout.data());
+            if (r == PBCCS_OK) {
+                scatter(start[b], start[b + 1], bout);
+            } else if (r == PBCCS_EOOM) {
                 std::lock_guard<std::mutex> lk(deferMu);
                 deferred.emplace_back(start[b], start[b + 1]);
-            } else if (r != PBCCS_OK) {
+            } else {
                 rc[slot] = r;
                 err[slot] = g_lastError;
                 stop.store(true);
@@ -756,17 +887,17 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
     if (!deferred.empty()) {
         for (int s = 0; s < slots; ++s) eng->Slot(s)->val.unmap_all();
         std::sort(deferred.begin(), deferred.end());
-        while (!deferred.empty()) {
-            const std::pair<int, int> span = deferred.back();
-            deferred.pop_back();
-            const int r = run_span(0, span.first, span.second);
-            if (r == PBCCS_OK) continue;
-            if (r != PBCCS_EOOM || span.second - span.first < 2) return r;
-            eng->Slot(0)->val.unmap_all();
-            const int mid = span.first + (span.second - span.first) / 2;
-            deferred.emplace_back(mid, span.second);
-            deferred.emplace_back(span.first, mid);
-        }
+        return guarded([&] {
+            std::vector<pbccs_zmw_input> bin;
+            std::vector<pbccs_zmw_output> bout;
+            for (const std::pair<int, int>& span : deferred) {
+                gather(span.first, span.second, &bin, &bout);
+                const int r = polish_retry(eng, 0, bin.data(), span.second - span.first, &o, bout.data());
+                if (r != PBCCS_OK) return r;
+                scatter(span.first, span.second, bout);
+            }
+            return PBCCS_OK;
+        });
     }
     return PBCCS_OK;
 }

@@ -88,6 +88,19 @@ void VmPool::map_to(size_t n, bool soft)
         if (!soft) throw DeviceError("band pool exceeds its address reservation");
         want = kVaBytes;
     }
+    // Test hook: PBCCS_POOL_CAP_MB caps what one pool may map, so a batch runs out of device memory on
+    // purpose and the EOOM defer/rerun paths can be checked (read on every call: tests set it at run time).
+    size_t capBytes = kVaBytes;
+    if (const char* e = std::getenv("PBCCS_POOL_CAP_MB")) {
+        const long long mb = std::atoll(e);
+        if (mb > 0) capBytes = std::min(kVaBytes, (size_t)mb << 20);
+    }
+    if (want > capBytes) {
+        if (!soft)
+            throw DeviceOom("band pool capped at " + std::to_string(capBytes >> 20) + " MB (PBCCS_POOL_CAP_MB), needs " +
+                            std::to_string(want >> 20) + " MB");
+        want = capBytes;
+    }
     int dev = 0;
     PBCCS_HIP(hipGetDevice(&dev));
     hipMemAllocationProp prop = {};
@@ -98,7 +111,8 @@ void VmPool::map_to(size_t n, bool soft)
     desc.location = prop.location;
     desc.flags = hipMemAccessFlagsProtReadWrite;
     while (mappedBytes_ < want) {
-        const size_t bytes = std::min(kChunkBytes, kVaBytes - mappedBytes_);
+        const size_t bytes = std::min(std::min(kChunkBytes, capBytes), kVaBytes - mappedBytes_);
+        if (mappedBytes_ + bytes > capBytes) break;
         hipMemGenericAllocationHandle_t h;
         if (hipMemCreate(&h, bytes, &prop, 0) != hipSuccess) {
             (void)hipGetLastError();
@@ -124,6 +138,9 @@ void VmPool::map_to(size_t n, bool soft)
         mappedBytes_ += bytes;
     }
     cap = mappedBytes_ / sizeof(double);
+    if (!soft && mappedBytes_ < want)
+        throw DeviceOom("band pool capped at " + std::to_string(capBytes >> 20) + " MB (PBCCS_POOL_CAP_MB), needs " +
+                        std::to_string(want >> 20) + " MB");
 }
 
 void VmPool::unmap_all()
@@ -244,15 +261,32 @@ void ArrowBatch::Timed(KernelKind k, F&& launch, hipStream_t st)
 void ArrowBatch::ResolveEvents()
 {
     if (pending_.empty()) return;
+    // events sit on all three streams (the tall fills run on stream2_/stream3_); a batch that failed after
+    // the fork may not have joined them back into stream_, so wait for each
     PBCCS_HIP(hipStreamSynchronize(stream_));
+    PBCCS_HIP(hipStreamSynchronize(stream2_));
+    PBCCS_HIP(hipStreamSynchronize(stream3_));
     for (const Pending& p : pending_) {
         float ms = 0.0f;
-        PBCCS_HIP(hipEventElapsedTime(&ms, p.a, p.b));
-        stats_[p.kind].ms += ms;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) stats_[p.kind].ms += ms;
+        else (void)hipGetLastError();   // a launch that never ran (failed batch): no time to add
         eventPool_.push_back(p.a);
         eventPool_.push_back(p.b);
     }
     pending_.clear();
+}
+
+const Counters& ArrowBatch::counters()
+{
+    long long region = 0, used = 0;
+    for (const HRead& r : reads_) {
+        region += 2 * r.valCap;
+        used += r.usedA + r.usedB;
+    }
+    counters_.bandTopBytes = std::max(counters_.bandTopBytes, valTop_ * (long long)sizeof(double));
+    counters_.bandRegionBytes = std::max(counters_.bandRegionBytes, region * (long long)sizeof(double));
+    counters_.bandUsedBytes = std::max(counters_.bandUsedBytes, used * (long long)sizeof(double));
+    return counters_;
 }
 
 void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
@@ -756,6 +790,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 h.flips = fl[r];
                 h.baseline = bl[r];
                 h.filled = true;
+                h.usedA = ua[r];
+                h.usedB = ub[r];
                 if (st[r] == kFillOk || st[r] == kFillMismatch) done.push_back(r);
             }
         }
@@ -769,6 +805,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         PBCCS_HIP(hipStreamSynchronize(stream_));   // the list buffer is reused by the next step
     }
     if (!serial.empty()) FillReadsSerial(serial);
+    (void)counters();   // band footprint high-water marks
 }
 
 void ArrowBatch::FillReadsSerial(const std::vector<int>& readsIn)
@@ -840,6 +877,8 @@ void ArrowBatch::FillReadsSerial(const std::vector<int>& readsIn)
                 h.flips = fl[r];
                 h.baseline = bl[r];
                 h.filled = true;
+                h.usedA = ua[r];
+                h.usedB = ub[r];
                 if (st[r] == kFillOk || st[r] == kFillMismatch) {
                     const long long need = std::max(ua[r], ub[r]);
                     if (need > h.valCap) {   // move to a larger compact region

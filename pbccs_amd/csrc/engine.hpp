@@ -107,6 +107,7 @@ struct VmPool {
     void try_reserve(size_t n);
     // Unmap every granule (the address reservation stays); the next reserve maps afresh.  Synchronises.
     void unmap_all();
+    size_t mapped_bytes() const { return vmm_ ? mappedBytes_ : cap * sizeof(double); }
     ~VmPool();
     VmPool() = default;
     VmPool(const VmPool&) = delete;
@@ -127,6 +128,9 @@ struct Counters {   // work counters for the roofline report (bench.py)
     long long scoreTasks = 0, scoreLaunches = 0;
     long long mutations = 0;
     long long bandGrowths = 0;   // fill launch sets in which some read grew its band region in-kernel
+    // band value pool of the batch, bytes (maxima over the batches merged into an engine's counters):
+    // bump top (everything ever handed out), current regions (2 x capacity per read), cells in use
+    long long bandTopBytes = 0, bandRegionBytes = 0, bandUsedBytes = 0;
 };
 
 enum KernelKind { kKFill = 0, kKSuffix, kKEnumerate, kKScore, kKReduce, kKQv, kKSelect, kKCompact, kKernelKinds };
@@ -213,7 +217,8 @@ public:
     double BaselineScore(int z) const;
     void ZScores(int z, double* zg, double* za, std::vector<double>* zs) const;
     const ArrowOptions& Options(int z) const { return zmws_[z].opt; }
-    const Counters& counters() const { return counters_; }
+    // work counters + the band pool's current footprint (Counters::band*Bytes)
+    const Counters& counters();
     void ResetCounters() { counters_ = Counters(); }
     hipStream_t stream() const { return stream_; }
     // Upload everything and reserve the largest round's buffers (so a timed polish does no H2D of inputs).
@@ -247,6 +252,7 @@ private:
         long long colBase = 0;
         int colCap = 0;
         long long valA = 0, valB = 0, valCap = 0;
+        long long usedA = 0, usedB = 0;   // band cells of the last fill
     };
 
     void EnsureZmwUploaded();

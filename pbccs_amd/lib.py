@@ -62,7 +62,10 @@ class CKernelStat(ctypes.Structure):
 
 class CCounters(ctypes.Structure):
     _fields_ = [("fill_launches", ctypes.c_longlong), ("score_launches", ctypes.c_longlong),
-                ("score_tasks", ctypes.c_longlong), ("mutations", ctypes.c_longlong)]
+                ("score_tasks", ctypes.c_longlong), ("mutations", ctypes.c_longlong),
+                ("band_top_bytes", ctypes.c_longlong), ("band_region_bytes", ctypes.c_longlong),
+                ("band_used_bytes", ctypes.c_longlong), ("pool_mapped_bytes", ctypes.c_longlong),
+                ("oom_retries", ctypes.c_longlong)]
 
 
 class CQvModelParams(ctypes.Structure):

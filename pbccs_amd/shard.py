@@ -50,6 +50,53 @@ def gather_in_order(local_results, local_indices, n_total, rank, world, group=No
     return out
 
 
+_queue_calls = [0]
+
+
+def dynamic_chunks(zmws, chunk):
+    """The pull queue's work items: ZMW indices in decreasing cost, cut into chunks of `chunk` ZMWs (largest
+    first, so the ranks' last pulls are the cheap chunks)."""
+    order = sorted(range(len(zmws)), key=lambda i: (-zmw_cost(zmws[i]), i))
+    return [order[k:k + chunk] for k in range(0, len(order), chunk)]
+
+
+def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chunk=256, polish_fn=None, store=None,
+                   group=None):
+    """Polish `zmws` across ranks through a dynamic pull queue: every rank takes the next
+    chunk index from one shared counter -- an atomic fetch-add on the rank-0 key-value store, host-side, not a
+    device collective -- until the queue is empty, so a rank that drew slow ZMWs (tall bands, long templates)
+    simply pulls fewer chunks.  Rank 0 returns every ZMW's result in input order (one ordered gather, as
+    WorkQueue.h:128-167); the other ranks return None."""
+    import torch.distributed as dist
+    if rank is None:
+        rank = dist.get_rank() if dist.is_initialized() else 0
+    if world is None:
+        world = dist.get_world_size() if dist.is_initialized() else 1
+    chunks = dynamic_chunks(zmws, chunk)
+    if polish_fn is None:
+        from . import polish_stream
+
+        def polish_fn(zs):
+            return polish_stream(zs, settings, engine)
+    _queue_calls[0] += 1
+    key = f"pbccs_queue_{_queue_calls[0]}"
+    if world > 1 and store is None:
+        store = dist.distributed_c10d._get_default_store()
+    mine, local = [], []
+    serial = 0
+    while True:
+        if world > 1:
+            c = store.add(key, 1) - 1
+        else:
+            c, serial = serial, serial + 1
+        if c >= len(chunks):
+            break
+        idx = chunks[c]
+        local.extend(polish_fn([zmws[i] for i in idx]))
+        mine.extend(idx)
+    return gather_in_order(local, mine, len(zmws), rank, world, group)
+
+
 def polish_sharded(zmws, settings=None, engine=None, rank=None, world=None, polish_fn=None, group=None):
     """Polish `zmws` across the ranks of the default process group; rank 0 returns every ZMW's result in
     input order, the other ranks return None.  `polish_fn(list_of_zmws) -> list_of_results` defaults to this

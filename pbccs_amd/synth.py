@@ -63,6 +63,26 @@ def make_zmws(n, length, passes, seed, snr=(10.0, 7.0, 5.0, 11.0), length_range=
     return out
 
 
+def make_smrtcell(n, seed=4):
+    """configs[4]: a SMRT cell's mix of the configs #2-#4 shapes, one third each, the
+    shape of every ZMW drawn from the seeded stream (so any prefix of the cell is the same mix)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = []
+    for _ in range(n):
+        kind = int(rng.integers(0, 3))
+        if kind == 0:
+            z = make_zmw(rng, 2000, 10)
+        elif kind == 1:
+            z = make_zmw(rng, 10000, 8)
+        else:
+            L = int(rng.integers(500, 20001))
+            P = int(rng.integers(3, 31))
+            z = make_zmw(rng, L, P, tuple(float(x) for x in rng.uniform(4.0, 20.0, size=4)))
+        z["kind"] = ("2kb", "10kb", "mixed")[kind]
+        out.append(z)
+    return out
+
+
 CONFIGS = {
     # name: (n_zmws, insert length, passes, seed) -- BASELINE.json configs[1..3]
     "2kb_10pass": dict(length=2000, passes=10, seed=1),

@@ -113,3 +113,56 @@ def test_work_queue_gated_zmws_keep_input_order():
         assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
         if e["converged"]:
             assert r["consensus"] == e["template"]
+
+
+def _same_records(got, ref):
+    def same(a, b):   # NaN z-scores (ZMWs gated before ZScores) compare equal
+        return a == b or (isinstance(a, float) and isinstance(b, float) and math.isnan(a) and math.isnan(b))
+    for r, s in zip(got, ref):
+        assert r.keys() == s.keys()
+        for k in r:
+            if isinstance(r[k], list):
+                assert len(r[k]) == len(s[k]) and all(same(x, y) for x, y in zip(r[k], s[k])), k
+            else:
+                assert same(r[k], s[k]), k
+
+
+@pytest.mark.gpu
+def test_out_of_memory_batches_are_rerun_with_identical_results(monkeypatch):
+    """PBCCS_POOL_CAP_MB caps every band pool, so a 24-ZMW 2 kb batch runs the pool out of memory mid-polish
+    (PBCCS_EOOM inside the engine).  Each entry point rebuilds the batch from its inputs and reruns it,
+    halved until it fits -- pbccs_batch_polish, pbccs_batch_polish_many beside a batch that fits, and the
+    work queue -- and every ZMW's record equals the uncapped polish."""
+    import pbccs_amd
+    zs = synth.make_zmws(24, 2000, 10, seed=31)
+    small = synth.make_zmws(2, 600, 6, seed=32)
+    ref = pbccs_amd.polish_zmws(zs, engine=pbccs_amd.Engine(0))
+    ref_small = pbccs_amd.polish_zmws(small, engine=pbccs_amd.Engine(0))
+
+    eng = pbccs_amd.Engine(0)
+    eng.set_concurrency(2)
+    batch = pbccs_amd.PreparedBatch(zs, engine=eng)    # created uncapped (its inputs fit)
+    monkeypatch.setenv("PBCCS_POOL_CAP_MB", "256")
+    batch.polish()
+    _same_records(batch.results(), ref)
+    assert eng.counters()["oom_retries"] >= 2          # the whole batch, then its halves
+    batch.close()
+
+    eng = pbccs_amd.Engine(0)
+    eng.set_concurrency(2)
+    monkeypatch.delenv("PBCCS_POOL_CAP_MB")
+    b1 = pbccs_amd.PreparedBatch(zs, engine=eng)
+    b2 = pbccs_amd.PreparedBatch(small, engine=eng)
+    monkeypatch.setenv("PBCCS_POOL_CAP_MB", "256")
+    pbccs_amd.polish_many([b1, b2])
+    _same_records(b1.results(), ref)
+    _same_records(b2.results(), ref_small)
+    assert eng.counters()["oom_retries"] >= 1
+    b1.close()
+    b2.close()
+
+    eng = pbccs_amd.Engine(0)
+    eng.set_concurrency(2)
+    got = pbccs_amd.polish_stream(zs + small, pbccs_amd.ConsensusSettings(zmws_per_batch=24), eng)
+    _same_records(got, ref + ref_small)
+    assert eng.counters()["oom_retries"] >= 1
