@@ -129,7 +129,8 @@ def _same_records(got, ref):
 
 @pytest.mark.gpu
 def test_out_of_memory_batches_are_rerun_with_identical_results(monkeypatch):
-    """PBCCS_POOL_CAP_MB caps every band pool, so a 24-ZMW 2 kb batch runs the pool out of memory mid-polish
+    """PBCCS_POOL_CAP_MB caps every band pool, so a 24-ZMW 2 kb batch (~340 MB of bands at its high-water
+    mark) runs the pool out of memory mid-polish
     (PBCCS_EOOM inside the engine).  Each entry point rebuilds the batch from its inputs and reruns it,
     halved until it fits -- pbccs_batch_polish, pbccs_batch_polish_many beside a batch that fits, and the
     work queue -- and every ZMW's record equals the uncapped polish."""
@@ -139,10 +140,12 @@ def test_out_of_memory_batches_are_rerun_with_identical_results(monkeypatch):
     ref = pbccs_amd.polish_zmws(zs, engine=pbccs_amd.Engine(0))
     ref_small = pbccs_amd.polish_zmws(small, engine=pbccs_amd.Engine(0))
 
+    # the cap is set before the batches are created: a pool maps in granules of min(1 GB, cap), and an
+    # uncapped creation would map a whole 1 GB granule that the 24 ZMWs then fit in
+    monkeypatch.setenv("PBCCS_POOL_CAP_MB", "200")
     eng = pbccs_amd.Engine(0)
     eng.set_concurrency(2)
-    batch = pbccs_amd.PreparedBatch(zs, engine=eng)    # created uncapped (its inputs fit)
-    monkeypatch.setenv("PBCCS_POOL_CAP_MB", "256")
+    batch = pbccs_amd.PreparedBatch(zs, engine=eng)    # its initial band regions (~160 MB) fit the cap
     batch.polish()
     _same_records(batch.results(), ref)
     assert eng.counters()["oom_retries"] >= 2          # the whole batch, then its halves
@@ -150,10 +153,8 @@ def test_out_of_memory_batches_are_rerun_with_identical_results(monkeypatch):
 
     eng = pbccs_amd.Engine(0)
     eng.set_concurrency(2)
-    monkeypatch.delenv("PBCCS_POOL_CAP_MB")
     b1 = pbccs_amd.PreparedBatch(zs, engine=eng)
     b2 = pbccs_amd.PreparedBatch(small, engine=eng)
-    monkeypatch.setenv("PBCCS_POOL_CAP_MB", "256")
     pbccs_amd.polish_many([b1, b2])
     _same_records(b1.results(), ref)
     _same_records(b2.results(), ref_small)
