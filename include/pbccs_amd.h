@@ -132,7 +132,9 @@ typedef struct {
     int draft_len;
     double snr[4];
     int n_reads;
-    const char* const* seqs;   /* read bases as passed to MappedArrowRead (already extent-clipped) */
+    const char* const* seqs;   /* read bases as passed to MappedArrowRead (already extent-clipped); NULL: a
+                                * read the driver did not add (POA key -1 or ExtractMappedRead none,
+                                * Consensus.h:448-451) -- counted in the drop fraction's denominator only */
     const int* lens;
     const int* strands;
     const int* tstarts;        /* mapped window on the draft [tstart, tend) */

@@ -25,6 +25,9 @@ using namespace pbccs;
 // shape measured).
 constexpr double kQueueMargin = 24.0 * (1ull << 30);
 constexpr int kQueueMaxZmws = 2000;
+// readOf entry of a read the caller did not add (NULL sequence): counted in the drop fraction's
+// denominator only, as the reads Consensus.h:441-471 skips (POA rejected it, or ExtractMappedRead did)
+constexpr int kSkippedRead = -2;
 
 struct pbccs_engine {
     int device = 0;
@@ -73,14 +76,14 @@ struct HostInputs {
             d.full.assign(nr, 1);
             for (int k = 0; k < nr; ++k) {
                 d.lens[k] = s.lens[k];
-                d.seqs[k].assign(s.seqs[k], std::max(0, s.lens[k]));
+                if (s.seqs[k]) d.seqs[k].assign(s.seqs[k], std::max(0, s.lens[k]));
                 d.strands[k] = s.strands[k];
                 d.ts[k] = s.tstarts[k];
                 d.te[k] = s.tends[k];
                 if (s.full_pass) d.full[k] = s.full_pass[k];
             }
             d.seqPtr.resize(nr);
-            for (int k = 0; k < nr; ++k) d.seqPtr[k] = d.seqs[k].c_str();
+            for (int k = 0; k < nr; ++k) d.seqPtr[k] = s.seqs[k] ? d.seqs[k].c_str() : nullptr;
             pbccs_zmw_input& v = in[i];
             v = s;
             v.draft = d.draft.c_str();
@@ -500,7 +503,8 @@ static int create_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, con
             b->zOf[i] = b->B->AddZmw(draft, z.snr, ao);
             for (int k = 0; k < z.n_reads; ++k) {
                 int r = -1;
-                if (z.tstarts[k] >= 0 && z.tends[k] <= z.draft_len && z.tstarts[k] < z.tends[k] && z.lens[k] > 0)
+                if (!z.seqs[k]) r = kSkippedRead;   // not added (Consensus.h:448-451): denominator only
+                else if (z.tstarts[k] >= 0 && z.tends[k] <= z.draft_len && z.tstarts[k] < z.tends[k] && z.lens[k] > 0)
                     r = b->B->AppendRead(b->zOf[i], std::string(z.seqs[k], z.lens[k]), z.strands[k] ? 1 : 0,
                                          z.tstarts[k], z.tends[k]);
                 b->readOf[i].push_back(r);
@@ -555,6 +559,7 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
             int nPasses = 0, nDropped = 0;
             for (int k = 0; k < b->nReads[i]; ++k) {
                 const int r = b->readOf[i][k];
+                if (r == kSkippedRead) continue;
                 const int st = (r >= 0) ? B.FinishAddRead(r, o.min_zscore) : PBCCS_ADD_OTHER;
                 if (q.add_read_results) q.add_read_results[k] = st;
                 q.status_counts[st] += 1;

@@ -1,0 +1,126 @@
+"""Per-ZMW driver steps on the host side of the boundary: FilterReads, the POA
+step's bookkeeping and ExtractMappedRead of include/pacbio/ccs/Consensus.h, turning one ZMW's raw
+subreads into the pbccs_zmw_input the GPU polish takes.
+
+    chunk (subreads + SNR) --FilterReads--> ordered reads --POA--> draft + per-read extents
+        --ExtractMappedRead--> mapped, extent-clipped reads --> polish boundary (pbccs_batch_*)
+
+The POA itself is pluggable (`poa`: a callable with the SparsePoa contract, below).  The boundary keeps
+the reference's bookkeeping: reads the POA did not take and reads ExtractMappedRead rejected are passed as
+placeholders (no sequence), so they count in the drop fraction's denominator exactly as Consensus.h's
+`nReads = readKeys.size()` does (:441-482).
+
+Parity: no reference test exercises FilterReads / ExtractMappedRead directly; this restatement follows
+the cited lines (float32 arithmetic where the reference uses float) and is checked by tests/test_driver.py
+against hand-derived expectations -- parity unpinned by reference fixtures.
+"""
+import numpy as np
+
+ADAPTER_BEFORE = 1
+ADAPTER_AFTER = 2
+FULL_PASS = ADAPTER_BEFORE | ADAPTER_AFTER
+
+
+def _full(read):
+    f = read.get("flags", FULL_PASS)
+    return bool(f & ADAPTER_BEFORE) and bool(f & ADAPTER_AFTER)
+
+
+def _median(lengths):
+    """Median<size_t> (Consensus.h:213-221): the middle element, or 0.5 * (sum of the two middle ones) as
+    double, returned as float."""
+    v = sorted(lengths)
+    n = len(v)
+    if n % 2 == 1:
+        return np.float32(v[n // 2])
+    return np.float32(0.5 * (v[n // 2 - 1] + v[n // 2]))
+
+
+def filter_reads(reads, min_length):
+    """FilterReads (include/pacbio/ccs/Consensus.h:223-292).
+
+    reads: dicts with "seq" and "flags" (LocalContextFlags; default a full pass).  Returns the reads in the
+    reference's priority order -- full passes first by closeness of their length to the median full-pass
+    length, then the others by the same closeness -- with None for reads of at least twice the median
+    length, which sort last.  An empty list when no read can be used (median shorter than min_length)."""
+    if not reads:
+        return []
+    longest = 0
+    lengths = []
+    for r in reads:
+        longest = max(longest, len(r["seq"]))
+        if _full(r):
+            lengths.append(len(r["seq"]))
+    median = np.float32(longest) if not lengths else _median(lengths)
+    max_len = 2 * int(median)                 # 2 * static_cast<size_t>(median)
+    if median < np.float32(min_length):
+        return []
+    results = [r if len(r["seq"]) < max_len else None for r in reads]
+
+    def lex(r):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            l = np.float32(len(r["seq"]))
+            v = min(l / median, median / l)   # float arithmetic (:271-272)
+        return (v, np.float32(0.0)) if _full(r) else (np.float32(0.0), v)
+
+    # std::stable_sort with "lhs > rhs", nullptr last (:281-289): non-null reads by descending key, ties
+    # in input order; Python's sort is stable, so sort on the negated key
+    kept = [r for r in results if r is not None]
+    kept.sort(key=lambda r: tuple(-x for x in lex(r)))
+    return kept + [None] * (len(results) - len(kept))
+
+
+def extract_mapped_read(read, summary, min_length):
+    """ExtractMappedRead (Consensus.h:294-325).  summary: {"rc": bool, "read": (l, r), "tpl": (l, r)}
+    (PoaAlignmentSummary: ReverseComplementedRead, ExtentOnRead, ExtentOnConsensus).  Returns the mapped
+    read as the polish boundary takes it, or None when the extent on the read is shorter than min_length.
+    Quirk: the substring is taken from the read as given, even when the POA
+    added it reverse-complemented and the extent is in the reverse complement's coordinates."""
+    rs, re_ = summary["read"]
+    ts, te = summary["tpl"]
+    if rs > re_ or re_ - rs < min_length:
+        return None
+    return {"seq": read["seq"][rs:re_], "strand": 1 if summary["rc"] else 0, "ts": int(ts), "te": int(te),
+            "full_pass": _full(read)}
+
+
+def poa_inputs(reads, poa, max_poa_coverage=None):
+    """PoaConsensus (Consensus.h:352-390): feed the filtered reads to the POA in order (None -> key -1) until
+    max_poa_coverage reads were added, then take the consensus with minCoverage = 1 below 5 reads, else
+    (cov + 1) / 2 - 1.
+
+    poa: an object with the SparsePoa surface -- orient_and_add_read(seq) -> key (>= 0, or -1 when the read
+    could not be added) and find_consensus(min_coverage) -> (sequence, summaries by key).
+    Returns (draft, read_keys, summaries)."""
+    keys = []
+    cov = 0
+    for r in reads:
+        key = -1 if r is None else poa.orient_and_add_read(r["seq"])
+        keys.append(key)
+        if key >= 0:
+            cov += 1
+            if max_poa_coverage is not None and cov >= max_poa_coverage:
+                break
+    min_cov = 1 if cov < 5 else (cov + 1) // 2 - 1
+    draft, summaries = poa.find_consensus(min_cov)
+    return draft, keys, summaries
+
+
+def zmw_input(chunk, poa, min_length=10, max_poa_coverage=None):
+    """One ZMW's subreads -> the polish boundary's ZMW dict, or (status, None) when the ZMW ends before the
+    scorer: NoSubreads (Consensus.h:414-420) or TooShort (:427-434).
+
+    chunk: {"snr": 4 floats, "reads": [{"seq", "flags"}]}.  Returns (None, zmw) on success, where zmw is
+    {"draft", "snr", "reads"} and reads holds one entry per POA key in order: the mapped read, or a
+    placeholder {"seq": None} for a read the POA or ExtractMappedRead skipped."""
+    reads = filter_reads(chunk["reads"], min_length)
+    if not reads or all(r is None for r in reads):
+        return "NoSubreads", None
+    draft, keys, summaries = poa_inputs(reads, poa, max_poa_coverage)
+    if len(draft) < min_length:
+        return "TooShort", None
+    out = []
+    for i, key in enumerate(keys):
+        mr = extract_mapped_read(reads[i], summaries[key], min_length) if key >= 0 else None
+        out.append(mr if mr is not None else {"seq": None, "strand": 0, "ts": 0, "te": 0, "full_pass": False})
+    return None, {"draft": draft, "snr": list(chunk["snr"]), "reads": out}

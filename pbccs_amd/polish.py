@@ -1,8 +1,8 @@
 """Batched ccs polish driver: pbccs' Consensus<>() from the scorer setup on (Consensus.h:436-552).
 
-The POA draft, FilterReads and ExtractMappedRead (Consensus.h:223-325, 352-390) stay with the caller: the
-boundary takes a draft plus mapped, extent-clipped reads per ZMW, exactly what Consensus.h hands to
-ArrowMultiReadMutationScorer.  Thousands of ZMWs go to the GPU per call; results come back in input order.
+The POA draft, FilterReads and ExtractMappedRead (Consensus.h:223-325, 352-390) run before the boundary
+(pbccs_amd.driver): it takes a draft plus mapped, extent-clipped reads per ZMW, exactly what Consensus.h
+hands to ArrowMultiReadMutationScorer.  Thousands of ZMWs go to the GPU per call; results come back in input order.
 """
 import ctypes
 import math
@@ -53,8 +53,10 @@ class _Marshalled:
             reads = z["reads"]
             nr = len(reads)
             draft = z["draft"].encode()
-            seqs = (ctypes.c_char_p * max(1, nr))(*[r["seq"].encode() for r in reads])
-            lens = (ctypes.c_int * max(1, nr))(*[len(r["seq"]) for r in reads])
+            # a read with no sequence is a placeholder the driver skipped (pbccs_amd.driver): not added, counted
+            # in the drop fraction's denominator only
+            seqs = (ctypes.c_char_p * max(1, nr))(*[None if r["seq"] is None else r["seq"].encode() for r in reads])
+            lens = (ctypes.c_int * max(1, nr))(*[0 if r["seq"] is None else len(r["seq"]) for r in reads])
             strands = (ctypes.c_int * max(1, nr))(*[int(r.get("strand", 0)) for r in reads])
             ts = (ctypes.c_int * max(1, nr))(*[int(r.get("ts", 0)) for r in reads])
             te = (ctypes.c_int * max(1, nr))(*[int(r.get("te", len(z["draft"]))) for r in reads])
