@@ -580,9 +580,12 @@ DevBatch ArrowBatch::View() const
 // the kernel reported.  Bands land directly in the compact layout; k_suffix adds the log-scale sums.
 void ArrowBatch::FillReads(const std::vector<int>& readsIn)
 {
-    // 0: 16 lanes / 64 rows; 1: 64 lanes / 1024 rows; 2: 64 lanes / as many rows as LDS holds;
-    // 3: 64 lanes / all rows, column buffers in global memory (CoopFill::colScratch)
-    constexpr int kPaths = 4;
+    // 0: one lane per read, columns of up to kFillLaneRows rows in an LDS ring (fill_lane.hip);
+    // cooperative (fill_coop.hip): 1: 16 lanes / 64 rows; 2: 64 lanes / 1024 rows; 3: 64 lanes / as many
+    // rows as LDS holds; 4: 64 lanes / all rows, column buffers in global memory (CoopFill::colScratch)
+    constexpr int kPaths = 5;
+    // PBCCS_FILL_LANE=0 starts every read on the cooperative paths (A/B against the lane fill)
+    static const bool laneFill = !(std::getenv("PBCCS_FILL_LANE") && std::strcmp(std::getenv("PBCCS_FILL_LANE"), "0") == 0);
     for (int r : readsIn) EnsureCapacity(r);
     std::vector<int> todo[kPaths], serial, done;
     for (int r : readsIn) {
@@ -602,16 +605,17 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     // per-chunk band logic 4x as often, so it is opt-in (PBCCS_TALL16=1); the default is 64 lanes.
     static const bool tall16 = std::getenv("PBCCS_TALL16") && std::strcmp(std::getenv("PBCCS_TALL16"), "1") == 0;
     auto rows_for = [&](int p, int maxI, int w) -> int {
-        if (p == 3) return coop_group_bytes(0, w, 0) <= kCoopLdsBytes ? (maxI + 64) / 64 * 64 : 0;
-        if (p == 0) return 4 * coop_group_bytes(kCoopNarrowRows, w, 0) <= kCoopLdsBytes ? kCoopNarrowRows : 0;
-        if (p == 1 && tall16) {
+        if (p == 0) return laneFill ? kFillLaneRows : 0;
+        if (p == 4) return coop_group_bytes(0, w, 0) <= kCoopLdsBytes ? (maxI + 64) / 64 * 64 : 0;
+        if (p == 1) return 4 * coop_group_bytes(kCoopNarrowRows, w, 0) <= kCoopLdsBytes ? kCoopNarrowRows : 0;
+        if (p == 2 && tall16) {
             const int want = std::min<int>(kCoopTallRows, (maxI + 16) / 16 * 16);
             return 4 * coop_group_bytes(want, w, 0) <= kCoopTallLdsBytes ? want : 0;
         }
         const long long room = ((long long)kCoopLdsBytes - (long long)coop_group_bytes(0, w, 0)) / 16 / 64 * 64;
         const long long full = (maxI + 64) / 64 * 64;   // a column never exceeds I + 1 rows
-        const long long want = p == 1 ? std::min<long long>(kCoopTallRows, full) : full;
-        return room >= want ? (int)want : (p == 2 && room >= 64 ? (int)room : 0);
+        const long long want = p == 2 ? std::min<long long>(kCoopTallRows, full) : full;
+        return room >= want ? (int)want : (p == 3 && room >= 64 ? (int)room : 0);
     };
     for (int attempt = 0;; ++attempt) {
         // route reads whose buffers do not fit this path's LDS budget to the next path
@@ -627,7 +631,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             }
             todo[p].swap(keep);
         }
-        if (todo[0].empty() && todo[1].empty() && todo[2].empty() && todo[3].empty()) break;
+        if (std::all_of(todo, todo + kPaths, [](const std::vector<int>& v) { return v.empty(); })) break;
         if (attempt > 8) throw DeviceError("band storage keeps overflowing");
         for (auto& v : todo)   // similar lengths share a launch (LDS is sized by the longest)
             std::stable_sort(v.begin(), v.end(), [&](int x, int y) {
@@ -642,11 +646,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         upload(dList_, list, stream_);
         const DevBatch B = View();
         size_t off = 0;
-        int hcapOf[kPaths] = {0, 0, 0, 0};
+        int hcapOf[kPaths] = {0, 0, 0, 0, 0};
         // the 64-lane (tall) launches run on a second stream beside the 16-lane one: a round's latency
         // is then the slower of the two, not their sum.  Fork before the first launch (after the list
         // upload), so the tall fills do not wait for the 16-lane fill.
-        const bool forked = !todo[1].empty() || !todo[2].empty() || !todo[3].empty();
+        const bool forked = !todo[2].empty() || !todo[3].empty() || !todo[4].empty();
         // Headroom for in-kernel band growth (CoopFill::valBump): reads on the tall paths grow to a few
         // percent of their full (I+1)(J+1) matrix; budgeted against the device's free memory.  Growth
         // beyond the mapped headroom falls back to count-only + relaunch below.
@@ -654,7 +658,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         long long headroom = 0;
         if (grow) {
             long long want = 1ll << 24;   // 128 MB for the occasional 16-lane overflow
-            for (int p = 1; p < kPaths; ++p)
+            for (int p = 2; p < kPaths; ++p)
                 for (int r : todo[p]) {   // tall bands use ~2-22% of the full matrix (mean ~11%)
                     const long long I = (long long)reads_[r].seq.size(), J = reads_[r].te - reads_[r].ts;
                     want += 2 * std::max<long long>(0, (I + 1) * (J + 1) / 7 - reads_[r].valCap);
@@ -694,9 +698,9 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.tplWords = (maxJ + 8) / 8;
             F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
             hcapOf[p] = F.hcap;
-            const int G = (p == 0 || (p == 1 && tall16)) ? 16 : 64;
-            F.groupBytes = coop_group_bytes(p == 3 ? 0 : F.hcap, F.readWords, F.tplWords);
-            if (p == 3) {   // two column buffers of hcap rows per read, in global memory
+            const int G = (p == 1 || (p == 2 && tall16)) ? 16 : 64;
+            F.groupBytes = coop_group_bytes(p == 4 ? 0 : F.hcap, F.readWords, F.tplWords);
+            if (p == 4) {   // two column buffers of hcap rows per read, in global memory
                 dColScratch_.reserve((size_t)n * 2 * F.hcap, false);
                 F.colScratch = dColScratch_.ptr;
             }
@@ -707,7 +711,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             // launch is latency-bound (few tall reads, e.g. a batch's convergence tail), serial steps when
             // the tall fills compete for issue slots with a full device.
             static const int jacobiMax = std::getenv("PBCCS_JACOBI_MAX") ? std::atoi(std::getenv("PBCCS_JACOBI_MAX")) : 0;
-            F.jacobi = chainMode ? std::strcmp(chainMode, "jacobi") == 0 : (p > 0 && n <= jacobiMax);
+            F.jacobi = chainMode ? std::strcmp(chainMode, "jacobi") == 0 : (p > 1 && n <= jacobiMax);
             F.prio = !(prioEnv && std::strcmp(prioEnv, "0") == 0);
             if (grow) {
                 F.valBump = dBump_.ptr;
@@ -716,7 +720,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 F.rValB = dRValB_.ptr;
                 F.rValCap = dRValCap_.ptr;
             }
-            if (chainStats && p > 0) {
+            if (chainStats && p > 1) {
                 dChain_.reserve(4, false);
                 if (!chainInit_) {
                     PBCCS_HIP(hipMemsetAsync(dChain_.ptr, 0, 4 * sizeof(unsigned long long), stream_));
@@ -725,8 +729,9 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 F.chainStats = dChain_.ptr;
             }
             const int* lp = dList_.ptr + off;
-            const hipStream_t st = p == 0 ? stream_ : p == 1 ? stream2_ : stream3_;
-            Timed(kKFill, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
+            const hipStream_t st = p <= 1 ? stream_ : p == 2 ? stream2_ : stream3_;
+            if (p == 0) Timed(kKFill, [&] { launch_fill_lane(B, F, lp, n, st); }, st);
+            else Timed(kKFill, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
             PBCCS_HIP(hipGetLastError());
             counters_.fillLaunches += 1;
             off += n;
@@ -770,7 +775,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 if (st[r] == kFillTall) {
                     // skip a path whose buffer would be no taller than the one that just failed
                     int q = p + 1;
-                    if (q == 2 && hcapOf[1] > 0 && rows_for(2, (int)h.seq.size(), words(r)) <= hcapOf[1]) ++q;
+                    if (q == 3 && hcapOf[2] > 0 && rows_for(3, (int)h.seq.size(), words(r)) <= hcapOf[2]) ++q;
                     h.fillPath = q;
                     if (q >= kPaths) serial.push_back(r);
                     else next[q].push_back(r);

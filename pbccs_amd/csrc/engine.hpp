@@ -247,7 +247,7 @@ private:
         double baseline = 0.0;
         int flips = 0;
         int status = 0;
-        int fillPath = 0;   // 0-3: k_fill_coop paths (FillReads), 4: lane-serial k_fill
+        int fillPath = 0;   // 0: k_fill_lane, 1-4: k_fill_coop paths (FillReads), 5: lane-serial k_fill
         long long seqOff = 0;
         long long colBase = 0;
         int colCap = 0;
