@@ -72,6 +72,23 @@ __device__ __forceinline__ double& slot(const LaneTask& T, int row)
     return T.ring[(row & (H - 1)) * 64];
 }
 
+constexpr int kLaneChunk = 4;
+
+// The previous column's values (0 outside its rows [pb, pe)) and the read bases rd[row + baseOff] of the
+// kLaneChunk rows r0, r0 + dir, ... (dir = +1 for alpha's top-down rows, -1 for beta's bottom-up rows).
+template <int H>
+__device__ __forceinline__ void fetch_rows(const LaneTask& T, int r0, int baseOff, int pb, int pe, double* lf,
+                                           char* rb, int dir = 1)
+{
+#pragma unroll
+    for (int q = 0; q < kLaneChunk; ++q) {
+        const int row = r0 + dir * q;
+        const double x = slot<H>(T, row);
+        lf[q] = (row >= pb && row < pe) ? x : 0.0;
+        rb[q] = T.rd[min(max(row + baseOff, 0), T.I - 1)];
+    }
+}
+
 // Move the read's alpha/beta region pair to a larger one taken from the pool's free top (as
 // fill_coop.hip grow_bands, one lane): keep the running pass's first keepM values and the other matrix's
 // last complete pass (keepO values).  False when the mapped headroom is exhausted.
@@ -122,18 +139,22 @@ __device__ __forceinline__ LanePass lane_alpha(const LaneTask& T, Band& a, Band&
     int curCtx;
     T.tv.At(0, curBase, curCtx);
     double s = 0.0;   // 0.0 + L(0)
+    // column metadata of the next column, loaded one column ahead (the guide's and this matrix's previous
+    // ranges of column j + 1 are read before column j + 1 overwrites them)
+    int2 gNext = make_int2(0, 0), sNext = make_int2(0, 0);
+    if (J > 1) {
+        if (guided) gNext = o.R(1);
+        if (selfValid) sNext = a.R(1);
+    }
     for (int j = 1; j < J; ++j) {
-        if (guided) {   // RangeGuide (SimpleRecursor.cpp:728-757)
-            const int2 g = o.R(j);
-            if (g.x < g.y) { hb = min(g.x, hb); he = max(g.y, he); }
+        const int2 gR = gNext, sR = sNext;
+        if (j + 1 < J) {
+            if (guided) gNext = o.R(j + 1);
+            if (selfValid) sNext = a.R(j + 1);
         }
-        int sx = 0, sy = 0;
-        if (selfValid) {
-            const int2 sr = a.R(j);
-            sx = sr.x;
-            sy = sr.y;
-            if (sx < sy) { hb = min(sx, hb); he = max(sy, he); }
-        }
+        if (guided && gR.x < gR.y) { hb = min(gR.x, hb); he = max(gR.y, he); }   // RangeGuide (:728-757)
+        const int sx = sR.x, sy = sR.y;
+        if (selfValid && sx < sy) { hb = min(sx, hb); he = max(sy, he); }
         const int reqEnd = min(I, he);
         char nextBase;
         int nextCtx;
@@ -149,26 +170,42 @@ __device__ __forceinline__ LanePass lane_alpha(const LaneTask& T, Band& a, Band&
         bool thrOk = true;   // thr == mx / sdn (computed lazily: only the loop's continue test past reqEnd reads it)
         int i = b;
         bool go = i < I;
+        // rows in chunks of kLaneChunk: the previous column's values and the read bases of the next chunk are
+        // loaded while this one computes (its ring slots are distinct mod H, and a row more than H below b
+        // aborts as tall before its slot could alias one this column wrote)
+        double lf[kLaneChunk];
+        char rbs[kLaneChunk];
+        fetch_rows<H>(T, i, -1, pb, pe, lf, rbs);
         while (go) {
-            if (i - b >= H) { out.tall = true; return out; }
-            const double left = (i >= pb && i < pe) ? slot<H>(T, i) : 0.0;
-            const char rb = T.rd[min(max(i - 1, 0), I - 1)];
-            const double mpe = diag * (rb == curBase ? T.prNot : T.prThird);
-            double move = 0.0;
-            if (i == 1 && j == 1) move = mpe;
-            else if (i != 1 && j != 1) move = mpe * pMatch;
-            double score = 0.0 + move;
-            if (i > 1) score = score + up * (rb == nextBase ? cBranch : cStick3);
-            if (j > 1) score = score + left * pDel;
-            slot<H>(T, i) = score;
-            if (score > mx) { mx = score; thrOk = false; }
-            up = score;
-            diag = left;
-            ++i;
-            go = i < I;
-            if (go && i >= reqEnd) {
-                if (!thrOk) { thr = mx / T.sdn; thrOk = true; }
-                go = score >= thr;
+            double lfN[kLaneChunk];
+            char rbN[kLaneChunk];
+            fetch_rows<H>(T, i + kLaneChunk, -1, pb, pe, lfN, rbN);
+#pragma unroll
+            for (int q = 0; q < kLaneChunk; ++q) {
+                if (i - b >= H) { out.tall = true; return out; }
+                const double left = lf[q];
+                const char rb = rbs[q];
+                const double mpe = diag * (rb == curBase ? T.prNot : T.prThird);
+                // 0.0 + move == move: every term is a product of non-negative probabilities
+                double score = (i == 1 && j == 1) ? mpe : ((i != 1 && j != 1) ? mpe * pMatch : 0.0);
+                if (i > 1) score = score + up * (rb == nextBase ? cBranch : cStick3);
+                if (j > 1) score = score + left * pDel;
+                slot<H>(T, i) = score;
+                if (score > mx) { mx = score; thrOk = false; }
+                up = score;
+                diag = left;
+                ++i;
+                go = i < I;
+                if (go && i >= reqEnd) {
+                    if (!thrOk) { thr = mx / T.sdn; thrOk = true; }
+                    go = score >= thr;
+                }
+                if (!go) break;
+            }
+#pragma unroll
+            for (int q = 0; q < kLaneChunk; ++q) {
+                lf[q] = lfN[q];
+                rbs[q] = rbN[q];
             }
         }
         const int e = i;
@@ -181,6 +218,7 @@ __device__ __forceinline__ LanePass lane_alpha(const LaneTask& T, Band& a, Band&
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhb = e;
         const bool store = !ovf && used + (e - b) <= a.cap;
+#pragma unroll 4
         for (int k = b; k < e; ++k) {
             double& c = slot<H>(T, k);
             const double v = scale ? c / mx : c;
@@ -241,21 +279,23 @@ __device__ __forceinline__ LanePass lane_beta(const LaneTask& T, Band& bm, Band&
     char nextBase;
     int nextCtx;
     T.tv.At(J - 1, nextBase, nextCtx);
+    int2 gNext = make_int2(0, 0), sNext = make_int2(0, 0);
+    if (J > 1) {
+        if (guided) gNext = o.R(J - 1);
+        if (selfValid) sNext = bm.R(J - 1);
+    }
     for (int j = J - 1; j > 0; --j) {
+        const int2 gR = gNext, sR = sNext;
+        if (j - 1 > 0) {
+            if (guided) gNext = o.R(j - 1);
+            if (selfValid) sNext = bm.R(j - 1);
+        }
         char curBase;
         int curCtx;
         T.tv.At(j - 1, curBase, curCtx);
-        if (guided) {
-            const int2 g = o.R(j);
-            if (g.x < g.y) { hb = min(g.x, hb); he = max(g.y, he); }
-        }
-        int sx = 0, sy = 0;
-        if (selfValid) {
-            const int2 sr = bm.R(j);
-            sx = sr.x;
-            sy = sr.y;
-            if (sx < sy) { hb = min(sx, hb); he = max(sy, he); }
-        }
+        if (guided && gR.x < gR.y) { hb = min(gR.x, hb); he = max(gR.y, he); }
+        const int sx = sR.x, sy = sR.y;
+        if (selfValid && sx < sy) { hb = min(sx, hb); he = max(sy, he); }
         const int reqBegin = max(0, hb);
         const double* cp = T.ctx + curCtx * kCtxStride;
         const double cMatch = cp[kM], cDel = cp[kD], cBranch = cp[kB], cStick3 = cp[kS3];
@@ -266,26 +306,41 @@ __device__ __forceinline__ LanePass lane_beta(const LaneTask& T, Band& bm, Band&
         double mx = 0.0, thr = 0.0, up = 0.0;
         bool thrOk = true;
         bool go = i > 0;
+        double lf[kLaneChunk];
+        char nbs[kLaneChunk];
+        fetch_rows<H>(T, i, 0, pb, pe, lf, nbs, -1);
         while (go) {
-            if (e - 1 - i >= H) { out.tall = true; return out; }
-            const double left = (i >= pb && i < pe) ? slot<H>(T, i) : 0.0;
-            const char nb = T.rd[min(max(i, 0), I - 1)];
-            const bool same = nb == nextBase;
-            const double mpe = diag * (same ? T.prNot : T.prThird);
-            double score = 0.0;
-            if (i < I - 1) score = 0.0 + mpe * cMatch;
-            else if (i == I - 1 && j == J - 1) score = 0.0 + mpe;
-            if (i < I - 1 && i > 0) score = score + up * (same ? cBranch : cStick3);
-            if (j < J - 1 && j > 0) score = score + left * cDel;
-            slot<H>(T, i) = score;
-            if (score > mx) { mx = score; thrOk = false; }
-            up = score;
-            diag = left;
-            --i;
-            go = i > 0;
-            if (go && i < reqBegin) {
-                if (!thrOk) { thr = mx / T.sdn; thrOk = true; }
-                go = score >= thr;
+            double lfN[kLaneChunk];
+            char nbN[kLaneChunk];
+            fetch_rows<H>(T, i - kLaneChunk, 0, pb, pe, lfN, nbN, -1);
+#pragma unroll
+            for (int q = 0; q < kLaneChunk; ++q) {
+                if (e - 1 - i >= H) { out.tall = true; return out; }
+                const double left = lf[q];
+                const char nb = nbs[q];
+                const bool same = nb == nextBase;
+                const double mpe = diag * (same ? T.prNot : T.prThird);
+                double score = 0.0;
+                if (i < I - 1) score = mpe * cMatch;   // 0.0 + x == x for the non-negative products
+                else if (i == I - 1 && j == J - 1) score = mpe;
+                if (i < I - 1 && i > 0) score = score + up * (same ? cBranch : cStick3);
+                if (j < J - 1 && j > 0) score = score + left * cDel;
+                slot<H>(T, i) = score;
+                if (score > mx) { mx = score; thrOk = false; }
+                up = score;
+                diag = left;
+                --i;
+                go = i > 0;
+                if (go && i < reqBegin) {
+                    if (!thrOk) { thr = mx / T.sdn; thrOk = true; }
+                    go = score >= thr;
+                }
+                if (!go) break;
+            }
+#pragma unroll
+            for (int q = 0; q < kLaneChunk; ++q) {
+                lf[q] = lfN[q];
+                nbs[q] = nbN[q];
             }
         }
         const int b = i + 1;
@@ -298,6 +353,7 @@ __device__ __forceinline__ LanePass lane_beta(const LaneTask& T, Band& bm, Band&
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhe = b;
         const bool store = !ovf && used + (e - b) <= bm.cap;
+#pragma unroll 4
         for (int k = e - 1; k >= b; --k) {
             double& c = slot<H>(T, k);
             const double v = scale ? c / mx : c;
