@@ -199,6 +199,9 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared)
     PBCCS_HIP(hipEventCreateWithFlags(&evJoin3_, hipEventDisableTiming));
     dScratch_.reserve(kInitialScratch, false);
     dScratchTop_.reserve(1, false);
+    // the read pool starts with 16 bytes of padding (see UploadDescriptors: word loads of read bases)
+    hSeq_.assign(16, '\0');
+    seqTop_ = 16;
     dScratchOverflow_.reserve(1, false);
 }
 
@@ -507,7 +510,9 @@ void ArrowBatch::UploadDescriptors()
     upload(dRZmw_, rz, stream_);
     // pools (templates re-uploaded whole: they change every refine round)
     upload(dTpl_, hTpl_, stream_);
-    dSeq_.reserve(std::max<size_t>(hSeq_.size(), 1), true);
+    // 32 bytes of slack at the end: the lane fill loads read bases 8 at a time (two aligned words), and
+    // its prefetch of the rows past a band may reach 24 bytes beyond a read
+    dSeq_.reserve(hSeq_.size() + 32, true);
     if (hSeq_.size() > seqUploaded_) {
         PBCCS_HIP(hipMemcpyAsync(dSeq_.ptr + seqUploaded_, hSeq_.data() + seqUploaded_, hSeq_.size() - seqUploaded_,
                                  hipMemcpyHostToDevice, stream_));
