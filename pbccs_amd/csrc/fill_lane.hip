@@ -160,6 +160,9 @@ __device__ __forceinline__ LanePass lane_alpha(const LaneTask& T, Band& a, Band&
     char curBase;
     int curCtx;
     T.tv.At(0, curBase, curCtx);
+    char nbNext = 0;   // template base / context of the next column, loaded one column ahead
+    int ncNext = kCtxZero;
+    if (J > 1) T.tv.At(1, nbNext, ncNext);
     double s = 0.0;   // 0.0 + L(0)
     // column metadata of the next column, loaded one column ahead (the guide's and this matrix's previous
     // ranges of column j + 1 are read before column j + 1 overwrites them)
@@ -178,9 +181,9 @@ __device__ __forceinline__ LanePass lane_alpha(const LaneTask& T, Band& a, Band&
         const int sx = sR.x, sy = sR.y;
         if (selfValid && sx < sy) { hb = min(sx, hb); he = max(sy, he); }
         const int reqEnd = min(I, he);
-        char nextBase;
-        int nextCtx;
-        T.tv.At(j, nextBase, nextCtx);
+        const char nextBase = nbNext;
+        const int nextCtx = ncNext;
+        if (j + 1 < J) T.tv.At(j + 1, nbNext, ncNext);
         const double* cp = T.ctx + curCtx * kCtxStride;
         const double* pp = T.ctx + prevCtx * kCtxStride;
         const double pMatch = pp[kM], pDel = pp[kD];
@@ -238,13 +241,21 @@ __device__ __forceinline__ LanePass lane_alpha(const LaneTask& T, Band& a, Band&
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhb = e;
         const bool store = !ovf && used + (e - b) <= a.cap;
-#pragma unroll 4
-        for (int k = b; k < e; ++k) {
-            double& c = slot<H>(T, k);
-            const double v = scale ? c / mx : c;
-            c = v;
-            if (store) a.V(used + (k - b)) = v;
-            if (nhb == e && !(v < thr)) nhb = k;
+        // in chunks: the chunk's slots are read first, so its divisions are independent and overlap
+        for (int k0 = b; k0 < e; k0 += kLaneChunk) {
+            double x[kLaneChunk];
+#pragma unroll
+            for (int q = 0; q < kLaneChunk; ++q) x[q] = slot<H>(T, k0 + q);
+#pragma unroll
+            for (int q = 0; q < kLaneChunk; ++q) {
+                const int k = k0 + q;
+                if (k < e) {
+                    const double v = scale ? x[q] / mx : x[q];
+                    slot<H>(T, k) = v;
+                    if (store) a.V(used + (k - b)) = v;
+                    if (nhb == e && !(v < thr)) nhb = k;
+                }
+            }
         }
         if (!store) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
@@ -299,6 +310,9 @@ __device__ __forceinline__ LanePass lane_beta(const LaneTask& T, Band& bm, Band&
     char nextBase;
     int nextCtx;
     T.tv.At(J - 1, nextBase, nextCtx);
+    char cbNext = 0;   // template base / context of the next column (j - 2 of column j), loaded ahead
+    int ccNext = kCtxZero;
+    if (J > 1) T.tv.At(J - 2, cbNext, ccNext);
     int2 gNext = make_int2(0, 0), sNext = make_int2(0, 0);
     if (J > 1) {
         if (guided) gNext = o.R(J - 1);
@@ -310,9 +324,9 @@ __device__ __forceinline__ LanePass lane_beta(const LaneTask& T, Band& bm, Band&
             if (guided) gNext = o.R(j - 1);
             if (selfValid) sNext = bm.R(j - 1);
         }
-        char curBase;
-        int curCtx;
-        T.tv.At(j - 1, curBase, curCtx);
+        const char curBase = cbNext;
+        const int curCtx = ccNext;
+        if (j - 2 >= 0) T.tv.At(j - 2, cbNext, ccNext);
         if (guided && gR.x < gR.y) { hb = min(gR.x, hb); he = max(gR.y, he); }
         const int sx = sR.x, sy = sR.y;
         if (selfValid && sx < sy) { hb = min(sx, hb); he = max(sy, he); }
@@ -371,13 +385,20 @@ __device__ __forceinline__ LanePass lane_beta(const LaneTask& T, Band& bm, Band&
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhe = b;
         const bool store = !ovf && used + (e - b) <= bm.cap;
-#pragma unroll 4
-        for (int k = e - 1; k >= b; --k) {
-            double& c = slot<H>(T, k);
-            const double v = scale ? c / mx : c;
-            c = v;
-            if (store) bm.V(used + (e - 1 - k)) = v;
-            if (nhe == b && !(v < thr)) nhe = k + 1;
+        for (int k0 = e - 1; k0 >= b; k0 -= kLaneChunk) {
+            double x[kLaneChunk];
+#pragma unroll
+            for (int q = 0; q < kLaneChunk; ++q) x[q] = slot<H>(T, k0 - q);
+#pragma unroll
+            for (int q = 0; q < kLaneChunk; ++q) {
+                const int k = k0 - q;
+                if (k >= b) {
+                    const double v = scale ? x[q] / mx : x[q];
+                    slot<H>(T, k) = v;
+                    if (store) bm.V(used + (e - 1 - k)) = v;
+                    if (nhe == b && !(v < thr)) nhe = k + 1;
+                }
+            }
         }
         if (!store) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
