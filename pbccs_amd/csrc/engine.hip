@@ -589,8 +589,13 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     // cooperative (fill_coop.hip): 1: 16 lanes / 64 rows; 2: 64 lanes / 1024 rows; 3: 64 lanes / as many
     // rows as LDS holds; 4: 64 lanes / all rows, column buffers in global memory (CoopFill::colScratch)
     constexpr int kPaths = 5;
-    // PBCCS_FILL_LANE=0 starts every read on the cooperative paths (A/B against the lane fill)
-    static const bool laneFill = !(std::getenv("PBCCS_FILL_LANE") && std::strcmp(std::getenv("PBCCS_FILL_LANE"), "0") == 0);
+    // The lane fill is opt-in (PBCCS_FILL_LANE=1).  It issues ~2x fewer VALU instructions for the band cells it
+    // takes (rocprofv3: 142 G + 149 G for the reads it passes on, against 510 G on k_fill_coop<16>), but one
+    // read's fill is a single lane's serial loop -- ~3x the latency of the 16-lane group -- and a batch's refine
+    // rounds wait on their slowest fill: measured 2965-3095 ZMWs/s against 3194-3263 without it
+    // (profiles/r2_lane_fill_ab.txt).  Lanes idle once their read's passes end (a wave runs its slowest read's
+    // flip-flops), which is where most of the remaining instructions go.
+    static const bool laneFill = std::getenv("PBCCS_FILL_LANE") && std::strcmp(std::getenv("PBCCS_FILL_LANE"), "1") == 0;
     for (int r : readsIn) EnsureCapacity(r);
     std::vector<int> todo[kPaths], serial, done;
     for (int r : readsIn) {

@@ -5,6 +5,10 @@ holds only the input digest and the oracle's outputs:
 
   tests/golden/polish_10kb.json -- synth.make_zmws(2, 10000, 8, seed=82) (configs[2] shape), polished by
   oracle/arrow_oracle.cpp (AddRead, RefineConsensus, ConsensusQVs).
+  tests/golden/polish_mixed_long.json -- mixed_long_zmws() (configs[3] shape: a 15.2 kb insert with 21
+  passes beside a 0.7 kb / 3-pass and a 4.8 kb / 14-pass ZMW at random SNRs), the same records.
+
+Usage: make_polish_fixtures.py [10kb|mixed_long]  (default: both; the 15 kb ZMW takes ~10 CPU-minutes)
 
 The oracle is test infrastructure (CPU restatement of the reference path, oracle/ header); the GPU test
 compares the engine's batch polish against these records.
@@ -13,6 +17,9 @@ import hashlib
 import json
 import os
 import sys
+from concurrent.futures import ProcessPoolExecutor
+
+import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", ".."))
@@ -29,23 +36,44 @@ def digest(z):
     return h.hexdigest()
 
 
+def mixed_long_zmws():
+    """configs[3] shapes for the GPU test: one ZMW of at least 15 kb with at least 20 passes (SNR as
+    configs[1], so its reads pass the z-score gate), one short few-pass ZMW and one mid-size one at
+    per-ZMW random SNRs."""
+    rng = np.random.Generator(np.random.PCG64(303))
+    return [synth.make_zmw(rng, 15200, 21),
+            synth.make_zmw(rng, 700, 3, tuple(float(x) for x in rng.uniform(6.0, 14.0, size=4))),
+            synth.make_zmw(rng, 4800, 14, tuple(float(x) for x in rng.uniform(6.0, 14.0, size=4)))]
+
+
+def record(z):
+    e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+    return {
+        "digest": digest(z),
+        "converged": bool(e["converged"]),
+        "n_tested": e["n_tested"],
+        "n_applied": e["n_applied"],
+        "add_read_results": e["add_read_results"],
+        "consensus": e["template"],
+        "qvs": "".join(chr(33 + min(max(q, 0), 93)) for q in e.get("qvs", [])),
+        "qvs_raw_max": max(e["qvs"]) if e.get("qvs") else None,
+    }
+
+
+def write(name, inputs, zs):
+    with ProcessPoolExecutor(max_workers=len(zs)) as ex:   # one ZMW per process: the oracle is serial
+        recs = list(ex.map(record, zs))
+    for r in recs:
+        print(name, r["n_tested"], r["n_applied"], r["converged"], flush=True)
+    json.dump({"inputs": inputs, "zmws": recs}, open(os.path.join(HERE, name), "w"))
+
+
 def main():
-    zs = synth.make_zmws(2, 10000, 8, seed=82)
-    out = {"inputs": "synth.make_zmws(2, 10000, 8, seed=82)", "zmws": []}
-    for z in zs:
-        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
-        out["zmws"].append({
-            "digest": digest(z),
-            "converged": bool(e["converged"]),
-            "n_tested": e["n_tested"],
-            "n_applied": e["n_applied"],
-            "add_read_results": e["add_read_results"],
-            "consensus": e["template"],
-            "qvs": "".join(chr(33 + min(max(q, 0), 93)) for q in e["qvs"]),
-            "qvs_raw_max": max(e["qvs"]),
-        })
-        print(len(out["zmws"]), e["n_tested"], e["n_applied"], flush=True)
-    json.dump(out, open(os.path.join(HERE, "polish_10kb.json"), "w"))
+    which = sys.argv[1:] or ["10kb", "mixed_long"]
+    if "10kb" in which:
+        write("polish_10kb.json", "synth.make_zmws(2, 10000, 8, seed=82)", synth.make_zmws(2, 10000, 8, seed=82))
+    if "mixed_long" in which:
+        write("polish_mixed_long.json", "make_polish_fixtures.mixed_long_zmws()", mixed_long_zmws())
 
 
 if __name__ == "__main__":
