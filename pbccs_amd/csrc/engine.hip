@@ -595,7 +595,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     // rounds wait on their slowest fill: measured 2965-3095 ZMWs/s against 3194-3263 without it
     // (profiles/r2_lane_fill_ab.txt).  Lanes idle once their read's passes end (a wave runs its slowest read's
     // flip-flops), which is where most of the remaining instructions go.
-    static const bool laneFill = std::getenv("PBCCS_FILL_LANE") && std::strcmp(std::getenv("PBCCS_FILL_LANE"), "1") == 0;
+    const char* laneEnv = std::getenv("PBCCS_FILL_LANE");   // read per call: a test switches it at run time
+    const bool laneFill = laneEnv && std::strcmp(laneEnv, "1") == 0;
     for (int r : readsIn) EnsureCapacity(r);
     std::vector<int> todo[kPaths], serial, done;
     for (int r : readsIn) {

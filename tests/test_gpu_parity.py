@@ -188,6 +188,26 @@ def test_fills_2kb_match_oracle(P):
             assert _close(x, y, 1e-12, 1e-12)
 
 
+def test_lane_fill_matches_oracle(P, monkeypatch):
+    """The opt-in lane fill (PBCCS_FILL_LANE=1, fill_lane.hip): configs[1] fills (per-read LL, flip-flops;
+    the reads whose columns outgrow its 32-row ring move on to the cooperative paths) and a batch polish."""
+    from pbccs_amd import synth
+    monkeypatch.setenv("PBCCS_FILL_LANE", "1")
+    for z in synth.make_zmws(2, 2000, 10, seed=62):
+        g, o, rg, ro = _scorers(P, z["draft"], z["reads"])
+        assert rg == ro
+        assert g.NumFlipFlops() == [o.read_info(k)["flipflops"] for k in range(len(z["reads"]))]
+        for x, y in zip(g.BaselineScores(), [o.read_info(k)["ll"] for k in range(len(z["reads"]))]):
+            assert _close(x, y, 1e-12, 1e-12)
+    zs = synth.make_zmws(6, 700, 8, seed=63)
+    for z, r in zip(zs, P.polish_zmws(zs)):
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+        assert r["add_read_results"] == e["add_read_results"]
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        if e["converged"]:
+            assert r["consensus"] == e["template"]
+
+
 def test_polish_2kb_batch_matches_oracle(P):
     """configs[1] ZMWs (2 kb insert, 10 passes) through the batch entry point: bit-exact consensus,
     nTested/nApplied and AddRead results; QVs within +-1."""
@@ -328,3 +348,34 @@ def test_polish_10kb_batch_matches_oracle(P):
         got = [min(max(q, 0), 93) for q in r["qvs"]]
         exp = [ord(c) - 33 for c in e["qvs"]]
         assert len(got) == len(exp) and max(abs(a - b) for a, b in zip(got, exp)) <= 1
+
+
+def test_polish_mixed_long_matches_fixture(P):
+    """configs[3] shapes at full size: a 15.2 kb insert with 21 passes beside a 0.7 kb / 3-pass and a
+    4.8 kb / 14-pass ZMW at random SNRs, through the work queue (polish_stream: length buckets, memory-sized
+    batches).  The oracle needs ~10 CPU-minutes for the long ZMW, so its records are a committed fixture
+    (tests/golden/make_polish_fixtures.py mixed_long); inputs are regenerated and checked by digest."""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_polish_fixtures import digest, mixed_long_zmws
+    fx = json.load(open(os.path.join(GOLD, "polish_mixed_long.json")))
+    zs = mixed_long_zmws()
+    assert len(zs[0]["draft"]) >= 15000 and len(zs[0]["reads"]) >= 20
+    res = P.polish_stream(zs)
+    for z, r, e in zip(zs, res, fx["zmws"]):
+        assert digest(z) == e["digest"]
+        assert r["add_read_results"] == e["add_read_results"]
+        # the oracle record is the scorer's polish; the batch applies Consensus.h's gates first (:473-490)
+        st = e["add_read_results"]
+        if sum(1 for s in st if s == 0) < 3:
+            assert r["status"] == "TooFewPasses"
+            continue
+        if sum(1 for s in st if s != 0) / len(st) > 0.34:
+            assert r["status"] == "TooManyUnusable"
+            continue
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        if e["converged"]:
+            assert r["consensus"] == e["consensus"]
+            got = [min(max(q, 0), 93) for q in r["qvs"]]
+            exp = [ord(c) - 33 for c in e["qvs"]]
+            assert len(got) == len(exp) and max(abs(a - b) for a, b in zip(got, exp)) <= 1
