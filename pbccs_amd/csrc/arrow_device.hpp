@@ -120,7 +120,7 @@ struct TaskStat {
 struct VirtualMut {
     int mpos = kNoMutation;
     int moff = 0;
-    char mb0 = '0', mb1 = '0';
+    int mb0 = '0', mb1 = '0';   // base chars (int: byte-sized members of a by-value struct were kept in scratch)
     int mc0 = kCtxZero, mc1 = kCtxZero;
 };
 

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Build check: no kernel of the library may need a private (scratch) segment or spill VGPRs.
+
+A dispatch that needs scratch must get it from the runtime at launch, and under a full HBM that allocation
+fails (HSA_STATUS_ERROR_OUT_OF_RESOURCES aborted a 12-slot run in round 1, profiles/r1i_mixed240_s12_abort.err.txt).
+Reads the `-Rpass-analysis=kernel-resource-usage` remarks hipcc wrote for each object (*.res) and exits 1
+naming every offending kernel.
+Usage: check_resources.py FILE.res...
+"""
+import re
+import sys
+
+
+def main(paths):
+    bad = []
+    kernels = 0
+    for p in paths:
+        name = None
+        for line in open(p, errors="replace"):
+            m = re.search(r"Function Name: (\S+)", line)
+            if m:
+                name = m.group(1)
+                kernels += 1
+                continue
+            m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
+            if m and int(m.group(1)) > 0:
+                bad.append(f"{p}: {name}: private segment {m.group(1)} bytes/lane")
+            m = re.search(r"VGPRs Spill: (\d+)", line)
+            if m and int(m.group(1)) > 0:
+                bad.append(f"{p}: {name}: {m.group(1)} VGPRs spilled")
+    if bad:
+        print("kernel resource check failed:\n  " + "\n  ".join(bad), file=sys.stderr)
+        return 1
+    print(f"kernel resource check: {kernels} kernels, no scratch, no VGPR spills")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))

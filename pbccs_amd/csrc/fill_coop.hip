@@ -801,15 +801,12 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     const int per = 64 / G;
     const size_t lds = (size_t)per * F.groupBytes;
     if (lds > 160 * 1024) throw std::runtime_error("fill block needs more than 160 KB of LDS");
-    // waves per SIMD the register allocator must allow (PBCCS_FILL_OCC: 2 = no spills, 3, 4 = spills)
-    static const int occ = std::getenv("PBCCS_FILL_OCC") ? std::atoi(std::getenv("PBCCS_FILL_OCC")) : 2;
-    auto pick = [&](auto k2, auto k3, auto k4) { return occ >= 4 ? k4 : occ == 3 ? k3 : k2; };
     using K = void (*)(DevBatch, CoopFill, const int*, int);
     const bool gc = F.colScratch != nullptr;
     if (gc && G != 64) throw std::runtime_error("global column buffers need 64-lane groups");
-    const K k = gc ? (K)k_fill_coop<64, 2, true>
-              : G == 16 ? pick((K)k_fill_coop<16, 2, false>, (K)k_fill_coop<16, 3, false>, (K)k_fill_coop<16, 4, false>)
-                        : pick((K)k_fill_coop<64, 2, false>, (K)k_fill_coop<64, 3, false>, (K)k_fill_coop<64, 4, false>);
+    // two waves per SIMD: the register budget that leaves these kernels without spills (higher occupancy
+    // was measured slower and needs a private segment, which the resource check in the Makefile forbids)
+    const K k = gc ? (K)k_fill_coop<64, 2, true> : G == 16 ? (K)k_fill_coop<16, 2, false> : (K)k_fill_coop<64, 2, false>;
     static bool attrSet[3] = {false, false, false};   // dynamic LDS beyond 64 KB must be enabled per kernel
     const int ak = gc ? 2 : (G == 64);
     if (!attrSet[ak]) {

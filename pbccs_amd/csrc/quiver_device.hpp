@@ -138,13 +138,13 @@ struct QTpl {
     int len;             // length of the (possibly edited) template
     int editPos = -1;    // position of the edit in the unedited template (-1: none)
     int editType = 0;    // 0 insertion, 1 deletion, 2 substitution (single base)
-    char editBase = 0;
+    int editBase = 0;    // a char (int: byte-sized members of a by-value struct were kept in scratch)
     __device__ __forceinline__ char at(int j) const   // std::string semantics: '\0' at j == len
     {
         if (j >= len) return '\0';
         if (editPos < 0 || j < editPos) return base[j];
-        if (editType == 2) return j == editPos ? editBase : base[j];
-        if (editType == 0) return j == editPos ? editBase : base[j - 1];
+        if (editType == 2) return j == editPos ? (char)editBase : base[j];
+        if (editType == 0) return j == editPos ? (char)editBase : base[j - 1];
         return base[j + 1];
     }
 };
@@ -152,30 +152,30 @@ struct QTpl {
 __device__ __forceinline__ int tpl_code(char b) { return b == 'A' ? 0 : b == 'C' ? 1 : b == 'G' ? 2 : 3; }
 
 struct QEval {
-    const QRead* r;
+    QRead r;   // by value: a pointer to a kernel-local QRead would keep it in scratch
     const QParams* p;
     QTpl t;
-    __device__ __forceinline__ int I() const { return r->I; }
+    __device__ __forceinline__ int I() const { return r.I; }
     __device__ __forceinline__ int J() const { return t.len; }
     __device__ __forceinline__ float Inc(int i, int j) const
     {
-        return (r->seq[i] == t.at(j)) ? p->Match : p->Mismatch + p->MismatchS * r->subs[i];
+        return (r.seq[i] == t.at(j)) ? p->Match : p->Mismatch + p->MismatchS * r.subs[i];
     }
     __device__ __forceinline__ float Del(int i, int j) const   // pinStart = pinEnd = true
     {
         const float tb = (float)t.at(j);
-        return (i < r->I && tb == r->tag[i]) ? p->DeletionWithTag + p->DeletionWithTagS * r->del[i] : p->DeletionN;
+        return (i < r.I && tb == r.tag[i]) ? p->DeletionWithTag + p->DeletionWithTagS * r.del[i] : p->DeletionN;
     }
     __device__ __forceinline__ float Extra(int i, int j) const
     {
-        return (j < t.len && r->seq[i] == t.at(j)) ? p->Branch + p->BranchS * r->ins[i] : p->Nce + p->NceS * r->ins[i];
+        return (j < t.len && r.seq[i] == t.at(j)) ? p->Branch + p->BranchS * r.ins[i] : p->Nce + p->NceS * r.ins[i];
     }
     __device__ __forceinline__ float Merge(int i, int j) const
     {
-        const char a = t.at(j), b = t.at(j + 1), s = r->seq[i];
+        const char a = t.at(j), b = t.at(j + 1), s = r.seq[i];
         if (!(s == a && s == b)) return kNegInf;
         const int k = tpl_code(a);
-        return p->Merge[k] + p->MergeS[k] * r->merge[i];
+        return p->Merge[k] + p->MergeS[k] * r.merge[i];
     }
 };
 

@@ -15,7 +15,7 @@ namespace quiver {
 namespace {
 
 // ---- RangeGuide / RowRange (detail/RecursorBase-inl.hpp:49-114) ----------------------------------------
-__device__ void row_range(const QBand& m, int j, float scoreDiff, int* ob, int* oe)
+__device__ __forceinline__ void row_range(const QBand& m, int j, float scoreDiff, int* ob, int* oe)
 {
     int b = m.range[j].x, e = m.range[j].y;
     int maxRow = b;
@@ -33,7 +33,7 @@ __device__ void row_range(const QBand& m, int j, float scoreDiff, int* ob, int* 
     *oe = i + 1;
 }
 
-__device__ void range_guide(int j, const QBand* guide, const QBand* self, float scoreDiff, int* hb, int* he)
+__device__ __forceinline__ void range_guide(int j, const QBand* guide, const QBand* self, float scoreDiff, int* hb, int* he)
 {
     const bool useG = guide && !guide->Empty(j);
     const bool useS = self && !self->Empty(j);
@@ -54,7 +54,7 @@ __device__ __forceinline__ void put(const QBand& m, long long k, float v, bool& 
 // ---- SseRecursor::FillAlpha (SseRecursor.cpp:73-213) -----------------------------------------------------
 // `prev`: this matrix's previous pass (RangeGuide's self hint); `out`: the arena written now.  Rows come
 // top-down, so column j's cells are appended at `used` as they are produced.
-__device__ long long fill_alpha(const QEval& e, const QBand* guide, const QBand* prev, const QBand& out,
+__device__ __forceinline__ long long fill_alpha(const QEval& e, const QBand* guide, const QBand* prev, const QBand& out,
                                 QAlloc* alloc, bool allocExists, bool& ovf)
 {
     const int I = e.I(), J = e.J();
@@ -123,7 +123,7 @@ __device__ long long fill_alpha(const QEval& e, const QBand* guide, const QBand*
 // ---- SseRecursor::FillBeta (SseRecursor.cpp:216-353) -----------------------------------------------------
 // Rows come bottom-up and the column's first row is known only at its end: cells go to the read's column
 // buffer (indexed by row) and are copied top-down into the arena when the column is finished.
-__device__ long long fill_beta(const QEval& e, const QBand* guide, const QBand* prev, const QBand& out,
+__device__ __forceinline__ long long fill_beta(const QEval& e, const QBand* guide, const QBand* prev, const QBand& out,
                                float* colbuf, QAlloc* alloc, bool allocExists, bool& ovf)
 {
     const int I = e.I(), J = e.J();
@@ -196,7 +196,7 @@ __device__ long long fill_beta(const QEval& e, const QBand* guide, const QBand* 
 }
 
 // ---- SseRecursor::ExtendAlpha (SseRecursor.cpp:433-551) --------------------------------------------------
-__device__ void extend_alpha(const QEval& e, const QBand& a, int beginColumn, const QBand& ext, int numExt, bool& ovf)
+__device__ __forceinline__ void extend_alpha(const QEval& e, const QBand& a, int beginColumn, const QBand& ext, int numExt, bool& ovf)
 {
     const bool sp = e.p->sumProduct != 0;
     const bool merge = (e.p->moves & kMerge) != 0;
@@ -246,7 +246,7 @@ __device__ void extend_alpha(const QEval& e, const QBand& a, int beginColumn, co
 }
 
 // ---- SimpleRecursor::ExtendBeta (Quiver/SimpleRecursor.cpp:407-495) ---------------------------------------
-__device__ void extend_beta(const QEval& e, const QBand& b, int lastColumn, const QBand& ext, int numExt,
+__device__ __forceinline__ void extend_beta(const QEval& e, const QBand& b, int lastColumn, const QBand& ext, int numExt,
                             int lengthDiff, bool& ovf)
 {
     const bool sp = e.p->sumProduct != 0;
@@ -284,7 +284,7 @@ __device__ void extend_beta(const QEval& e, const QBand& b, int lastColumn, cons
 }
 
 // ---- SseRecursor::LinkAlphaBeta (SseRecursor.cpp:355-431) ------------------------------------------------
-__device__ float link_alpha_beta(const QEval& e, const QBand& a, int ac, const QBand& b, int bc, int absc)
+__device__ __forceinline__ float link_alpha_beta(const QEval& e, const QBand& a, int ac, const QBand& b, int bc, int absc)
 {
     const bool sp = e.p->sumProduct != 0;
     const bool merge = (e.p->moves & kMerge) != 0;
@@ -321,59 +321,72 @@ __device__ float link_alpha_beta(const QEval& e, const QBand& a, int ac, const Q
 }
 
 // ---- per-read views -----------------------------------------------------------------------------------
+// A read's four pass arenas (alpha 0, alpha 1, beta 0, beta 1) are computed on demand from their bases: an
+// array of QBand indexed by a run-time arena number would live in scratch.
 struct ReadView {
-    QRead rd;
     QEval ev;
-    QBand arena[4];   // alpha 0, alpha 1, beta 0, beta 1
+    int2* range0;
+    int* off0;
+    float* val0;
+    long long colCap, valCap;
+    int cols;
     QAlloc* allocA;
     QAlloc* allocB;
     float* colbuf;
 };
 
-__device__ ReadView read_view(const QBatch& B, int r)
+__device__ __forceinline__ QBand arena(const ReadView& v, int k)
+{
+    QBand m;
+    m.range = v.range0 + (long long)k * v.colCap;
+    m.off = v.off0 + (long long)k * v.colCap;
+    m.val = v.val0 + (long long)k * v.valCap;
+    m.cap = v.valCap;
+    m.cols = v.cols;
+    return m;
+}
+
+__device__ __forceinline__ ReadView read_view(const QBatch& B, int r)
 {
     ReadView v;
     const int z = B.rZmw[r];
     const int I = B.rLen[r];
     const long long so = B.rSeq[r];
-    v.rd.seq = B.seqPool + so;
+    v.ev.r.seq = B.seqPool + so;
     const float* f = B.featPool + 5 * so;
-    v.rd.ins = f;
-    v.rd.subs = f + I;
-    v.rd.del = f + 2 * I;
-    v.rd.tag = f + 3 * I;
-    v.rd.merge = f + 4 * I;
-    v.rd.I = I;
+    v.ev.r.ins = f;
+    v.ev.r.subs = f + I;
+    v.ev.r.del = f + 2 * I;
+    v.ev.r.tag = f + 3 * I;
+    v.ev.r.merge = f + 4 * I;
+    v.ev.r.I = I;
     const int ts = B.rTs[r], te = B.rTe[r], L = B.zLen[z];
-    v.ev.r = &v.rd;
     v.ev.p = B.params + B.rParam[r];
     v.ev.t.base = B.tplPool + (B.rStrand[r] == 0 ? B.zFwd[z] + ts : B.zRev[z] + (L - te));
     v.ev.t.len = te - ts;
     v.ev.t.editPos = -1;
     const long long cb = B.rColBase[r];
     const int cc = B.rColCap[r];
-    const long long vb = B.rValBase[r], vc = B.rValCap[r];
-    for (int k = 0; k < 4; ++k) {
-        v.arena[k].range = B.range + cb + (long long)k * cc;
-        v.arena[k].off = B.off + cb + (long long)k * cc;
-        v.arena[k].val = B.valPool + vb + (long long)k * vc;
-        v.arena[k].cap = vc;
-        v.arena[k].cols = te - ts + 1;
-    }
+    v.range0 = B.range + cb;
+    v.off0 = B.off + cb;
+    v.val0 = B.valPool + B.rValBase[r];
+    v.colCap = cc;
+    v.valCap = B.rValCap[r];
+    v.cols = te - ts + 1;
     v.allocA = B.alloc + cb / 2;   // 2 x colCap alloc slots per read (colBase advances by 4 x colCap)
     v.allocB = v.allocA + cc;
     v.colbuf = B.valPool + B.rColBuf[r];
     return v;
 }
 
-__device__ long long used_entries(const QBand& m)
+__device__ __forceinline__ long long used_entries(const QBand& m)
 {
     long long s = 0;
     for (int j = 0; j < m.cols; ++j) s += max(0, m.range[j].y - m.range[j].x);
     return s;
 }
 
-__device__ long long allocated_entries(const QAlloc* a, int cols)
+__device__ __forceinline__ long long allocated_entries(const QAlloc* a, int cols)
 {
     long long s = 0;
     for (int j = 0; j < cols; ++j) s += a[j].capacity;
@@ -388,24 +401,25 @@ __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ 
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const int r = reads[t];
-    ReadView v = read_view(B, r);
-    v.ev.r = &v.rd;
+    const ReadView v = read_view(B, r);
     const QEval& e = v.ev;
     const int I = e.I(), J = e.J();
     if (I < 1 || J < 1 || J + 1 > B.rColCap[r]) {
         B.rStatus[r] = kQBad;
         return;
     }
-    for (int k = 0; k < 4; ++k)
-        for (int j = 0; j <= J; ++j) v.arena[k].range[j] = make_int2(0, 0);
+    for (int k = 0; k < 4; ++k) {
+        const QBand m = arena(v, k);
+        for (int j = 0; j <= J; ++j) m.range[j] = make_int2(0, 0);
+    }
     bool ovf = false;
     long long needA = 0, needB = 0;
     int curA = 0, curB = 2;   // arena index of the latest alpha / beta pass
     bool aPassed = false, bPassed = false;
     auto passA = [&](bool guided) {
         const int nxt = aPassed ? (curA ^ 1) : 0;
-        const long long u = fill_alpha(e, guided ? &v.arena[curB] : nullptr, aPassed ? &v.arena[curA] : nullptr,
-                                       v.arena[nxt], v.allocA, aPassed, ovf);
+        const QBand g = arena(v, curB), self = arena(v, curA), out = arena(v, nxt);
+        const long long u = fill_alpha(e, guided ? &g : nullptr, aPassed ? &self : nullptr, out, v.allocA, aPassed, ovf);
         needA = max(needA, u);
         curA = nxt;
         aPassed = true;
@@ -413,8 +427,8 @@ __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ 
     };
     auto passB = [&]() {
         const int nxt = bPassed ? (curB ^ 1) : 2;
-        const long long u = fill_beta(e, &v.arena[curA], bPassed ? &v.arena[curB] : nullptr, v.arena[nxt], v.colbuf,
-                                      v.allocB, bPassed, ovf);
+        const QBand g = arena(v, curA), self = arena(v, curB), out = arena(v, nxt);
+        const long long u = fill_beta(e, &g, bPassed ? &self : nullptr, out, v.colbuf, v.allocB, bPassed, ovf);
         needB = max(needB, u);
         curB = nxt;
         bPassed = true;
@@ -431,8 +445,8 @@ __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ 
         passA(true);
         flips += 3;
     }
-    auto a_end = [&]() { return v.arena[curA].Get(I, J); };
-    auto b_start = [&]() { return v.arena[curB].Get(0, 0); };
+    auto a_end = [&]() { return arena(v, curA).Get(I, J); };
+    auto b_start = [&]() { return arena(v, curB).Get(0, 0); };
     // fabs(a(I, J) - b(0, 0)) > ALPHA_BETA_MISMATCH_TOLERANCE: a float difference against the double 0.2
     while (!ovf && (double)fabsf(a_end() - b_start()) > 0.2 && flips <= kMaxFlipFlops) {
         if (flips % 2 == 0) passA(true);
@@ -470,17 +484,16 @@ __global__ void __launch_bounds__(64) k_qscore(QBatch B, QScoreWork W)
         return;
     }
     ReadView v = read_view(B, r);
-    v.ev.r = &v.rd;
     QEval& e = v.ev;
-    const char kB[4] = {'A', 'C', 'G', 'T'};
+    const char* kB = "ACGT";
     // OrientedMutation (:79-120), single-base mutations
     int os, oe;
     char ob;
     if (W.raw) { os = ms; oe = me; ob = kB[base]; }
     else if (B.rStrand[r] == 0) { os = ms - ts; oe = me - ts; ob = kB[base]; }
     else { os = te - me; oe = te - ms; ob = kB[3 - base]; }
-    const QBand& a = v.arena[B.rCurA[r]];
-    const QBand& b = v.arena[2 + B.rCurB[r]];
+    const QBand a = arena(v, B.rCurA[r]);
+    const QBand b = arena(v, 2 + B.rCurB[r]);
     const int J = e.J();   // unmutated window length
     const int lengthDiff = (type == 0) ? 1 : (type == 1) ? -1 : 0;
     // MutationScorer::ScoreMutation (Quiver/MutationScorer.cpp:113-226)
@@ -493,9 +506,12 @@ __global__ void __launch_bounds__(64) k_qscore(QBatch B, QScoreWork W)
     e.t.editBase = ob;
     e.t.len = J + lengthDiff;
     const int newLen = e.t.len;
-    // extend buffer: at most 8 columns (EXTEND_BUFFER_COLUMNS), values bump-allocated from the pool
-    int2 xr[8];
-    int xo[8];
+    // extend buffer: at most 8 columns (EXTEND_BUFFER_COLUMNS), values bump-allocated from the pool; the
+    // per-column ranges and offsets sit in LDS (a per-lane local array would be scratch)
+    __shared__ int2 sxr[64][8];
+    __shared__ int sxo[64][8];
+    int2* xr = sxr[threadIdx.x];
+    int* xo = sxo[threadIdx.x];
     QBand ext;
     ext.range = xr;
     ext.off = xo;
