@@ -790,6 +790,20 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                     h.fillPath = q;
                     if (q >= kPaths) serial.push_back(r);
                     else next[q].push_back(r);
+                    // A read that moves to the tall paths gets a region of its expected tall size now: exploded
+                    // bands hold ~8% of the (I+1)(J+1) matrix per pass at 2 kb (oracle, 400 reads), so growing
+                    // from the typical region inside the kernel would copy and abandon two or three regions.
+                    if (q >= 2 && q < kPaths) {
+                        const long long I = (long long)h.seq.size(), J = h.te - h.ts;
+                        const long long want = (I + 1) * (J + 1) / 10 + 64;
+                        if (want > h.valCap) {
+                            h.valCap = want;
+                            h.valA = valTop_;
+                            h.valB = valTop_ + h.valCap;
+                            valTop_ += 2 * h.valCap;
+                            descDirty_ = true;
+                        }
+                    }
                     continue;
                 }
                 if (st[r] == kFillOverflow) {
