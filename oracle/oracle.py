@@ -53,6 +53,10 @@ def lib():
         L.orc_enum_nearby.argtypes = [c_s, c_i, I, c_i, I, I, c_s, c_i]
         L.orc_apply_mutations.argtypes = [c_s, c_i, I, I, I, c_s, c_s, c_i, I, c_i]
         L.orc_context_params.argtypes = [D, D]
+        L.orc_poa_consensus.argtypes = [ctypes.POINTER(c_s), c_i, c_i, c_i, c_s, c_i, c_s, c_i, c_i]
+        L.orc_sparse_poa.argtypes = [ctypes.POINTER(c_s), c_i, c_i, ctypes.c_long, I, I, I, I, c_s, c_i]
+        L.orc_poa_kat_reads.restype = ctypes.c_long
+        L.orc_poa_kat_reads.argtypes = [c_i, c_s, ctypes.c_long, I]
         _lib = L
     return _lib
 
@@ -367,3 +371,60 @@ class QuiverScorer:
 
 def quiver_log_add(a, b):
     return _qlib().qorc_log_add(a, b)
+
+
+# ---------------------------------------------------------------- POA (oracle/poa_oracle.cpp)
+POA_GLOBAL, POA_SEMIGLOBAL, POA_LOCAL = 0, 1, 2
+INT_MAX = 2**31 - 1
+
+
+def _cstrs(seqs):
+    arr = (ctypes.c_char_p * max(1, len(seqs)))()
+    for k, s in enumerate(seqs):
+        arr[k] = None if s is None else s.encode()
+    return arr
+
+
+def poa_consensus(reads, mode=POA_GLOBAL, min_coverage=-INT_MAX, graphviz_flags=None):
+    """PoaConsensus::FindConsensus(reads, mode, minCoverage): the consensus, plus ToGraphViz(flags) when
+    graphviz_flags is given (1 = COLOR_NODES, 2 = VERBOSE_NODES)."""
+    cap = sum(len(r) for r in reads) + 16
+    seq = ctypes.create_string_buffer(cap)
+    dot = ctypes.create_string_buffer(512 * (cap + 8) + 4096) if graphviz_flags is not None else None
+    n = lib().orc_poa_consensus(_cstrs(reads), len(reads), mode, min_coverage, seq, cap, dot,
+                                len(dot) if dot is not None else 0, graphviz_flags or 0)
+    if n < 0:
+        raise ValueError("Input sequences must have nonzero length.")
+    return (seq.value.decode(), dot.value.decode()) if dot is not None else seq.value.decode()
+
+
+def sparse_poa(reads, min_coverage=None, max_coverage=None):
+    """SparsePoa driven as Consensus.h's PoaConsensus does (None reads get key -1).  Returns
+    {"consensus", "keys" (per input read; -2 = not reached), "summaries" (per POA key: rc, read, tpl)}."""
+    n = len(reads)
+    keys = (ctypes.c_int * max(1, n))()
+    nk = ctypes.c_int()
+    rc = (ctypes.c_int * max(1, n))()
+    ext = (ctypes.c_int * max(4, 4 * n))()
+    cap = sum(len(r) for r in reads if r) + 16
+    seq = ctypes.create_string_buffer(cap)
+    lib().orc_sparse_poa(_cstrs(reads), n, -1 if min_coverage is None else min_coverage,
+                         2**62 if max_coverage is None else max_coverage, keys, ctypes.byref(nk), rc, ext, seq, cap)
+    summ = [{"rc": bool(rc[k]), "read": (ext[4 * k], ext[4 * k + 1]), "tpl": (ext[4 * k + 2], ext[4 * k + 3])}
+            for k in range(nk.value)]
+    return {"consensus": seq.value.decode(), "keys": list(keys[:n]), "summaries": summ}
+
+
+def poa_kat_reads(kind):
+    """The 100 seeded sequences of TestSparsePoa.cpp's SingleReadx100 (kind 0) / SingleAndHalfx100 (kind 1)."""
+    cap = 100 * 20001
+    buf = ctypes.create_string_buffer(cap)
+    lens = (ctypes.c_int * 100)()
+    total = lib().orc_poa_kat_reads(kind, buf, cap, lens)
+    assert total > 0
+    raw = buf.raw[:total].decode()
+    out, o = [], 0
+    for L in lens:
+        out.append(raw[o:o + L])
+        o += L
+    return out

@@ -8,8 +8,12 @@ Reads data that the reference's own tests and demos hold (never its code):
   * SURVEY.md §0 item 4 / Appendix C -- the reference's recorded polish outputs on that ZMW
     (draft = subread 2, reads 1..8 mapped over the full draft, odd index REVERSE,
      SNR (10,7,5,11), MinZScore -5).
+  * ConsensusCore/src/Tests/TestPoaConsensus.cpp and tests/TestSparsePoa.cpp -- the POA known answers
+    (read sets, alignment modes, expected graph dumps, consensus sequences and per-read extents), parsed
+    out of the test sources' string literals and EXPECT lines.
 Writes:
-  tests/golden/arrow_kats.json, tests/golden/zmw6251.json
+  tests/golden/arrow_kats.json, tests/golden/zmw6251.json, tests/golden/quiver_kats.json,
+  tests/golden/poa_kats.json
 Only this script touches /root/reference; the fixtures travel, the reference does not.
 """
 import json
@@ -181,6 +185,122 @@ def make_quiver_kats():
     return {"params": P, "tolerance_abs": 0.0, "kats": kats}
 
 
+def _cpp_statements(body):
+    """Split C++ test code into statements; each is (text with literals replaced by @k, [literals]).
+    Adjacent literals are concatenated (C++ translation phase 6); comments are dropped."""
+    out, text, lits, i = [], "", [], 0
+    while i < len(body):
+        c = body[i]
+        if body.startswith("//", i):
+            i = body.index("\n", i)
+            continue
+        if body.startswith("/*", i):
+            i = body.index("*/", i) + 2
+            continue
+        if c == '"':
+            j, buf = i + 1, ""
+            while body[j] != '"':
+                if body[j] == "\\":
+                    buf += body[j + 1]
+                    j += 2
+                else:
+                    buf += body[j]
+                    j += 1
+            i = j + 1
+            if text.rstrip().endswith("@%d" % (len(lits) - 1)) and lits:
+                lits[-1] += buf
+            else:
+                text += "@%d" % len(lits)
+                lits.append(buf)
+            continue
+        if c in ";{}":
+            if text.strip():
+                out.append((" ".join(text.split()), lits))
+            text, lits = "", []
+            i += 1
+            continue
+        text += c
+        i += 1
+    return out
+
+
+def _tests(src):
+    """TEST(Suite, Name) bodies of a gtest source, skipping #if 0 regions."""
+    src = re.sub(r"#if 0.*?#endif", "", src, flags=re.S)
+    tests = {}
+    for m in re.finditer(r"TEST\((\w+), (\w+)\)\s*\{", src):
+        depth, j = 1, m.end()
+        while depth:
+            depth += {"{": 1, "}": -1}.get(src[j], 0)
+            j += 1
+        tests[m.group(1) + "." + m.group(2)] = src[m.end():j - 1]
+    return tests
+
+
+def make_poa_kats():
+    modes = {"GLOBAL": 0, "SEMIGLOBAL": 1, "LOCAL": 2}
+    path = "ConsensusCore/src/Tests/TestPoaConsensus.cpp"
+    cases = []
+    for name, body in _tests(open(os.path.join(REF, path)).read()).items():
+        cur = None
+        for text, lits in _cpp_statements(body):
+            if text.startswith("vector<std::string> reads") or text.startswith("std::vector<std::string> reads"):
+                cur = {"test": name, "source": path, "reads": [], "mode": 0, "min_coverage": None,
+                       "expected_dot": None, "graphviz_flags": 0, "expected": None}
+            elif text.startswith("reads +="):
+                cur["reads"] += lits
+            elif "FindConsensus(reads" in text:
+                m = re.search(r"FindConsensus\(reads, (\w+)(?:, (\d+))?\)", text)
+                cur["mode"] = modes[m.group(1)]
+                cur["min_coverage"] = int(m.group(2)) if m.group(2) else None
+            elif text.startswith("string expectedDot"):
+                cur["expected_dot"] = lits[0]
+            elif "ToGraphViz(PoaGraph::COLOR_NODES | PoaGraph::VERBOSE_NODES" in text:
+                cur["graphviz_flags"] = 3
+            elif text.startswith("EXPECT_EQ(@0, pc->Sequence"):
+                cur["expected"] = lits[0]
+            elif text.startswith("delete pc") and "run" not in name.lower() and cur and cur not in cases:
+                cases.append(cur)
+            elif text.startswith("ASSERT_EQ(1, answers.size())"):
+                cur["deterministic_only"] = True
+    sp_path = "tests/TestSparsePoa.cpp"
+    sparse = []
+    for name, body in _tests(open(os.path.join(REF, sp_path)).read()).items():
+        stmts = _cpp_statements(body)
+        case = {"test": name, "source": sp_path, "reads": [], "summaries": {}}
+        brace_init = False
+        for text, lits in stmts:
+            if text.startswith("reads +=") or brace_init:
+                case["reads"] += lits
+            brace_init = text.startswith("vector<std::string> reads =")
+            m = re.search(r"FindConsensus\((\d+), &summaries\)", text)
+            if m:
+                case["min_coverage"] = int(m.group(1))
+            if text.startswith("EXPECT_EQ(@0, consensusSeq"):
+                case["expected"] = lits[0]
+            m = re.match(r"EXPECT_EQ\(Interval\( ?(\d+), ?(\d+)\), summaries\[(\d+)\]\.ExtentOn(Read|Consensus)", text)
+            if m:
+                d = case["summaries"].setdefault(m.group(3), {})
+                d["read" if m.group(4) == "Read" else "tpl"] = [int(m.group(1)), int(m.group(2))]
+            m = re.match(r"EXPECT_(TRUE|FALSE) ?\(summaries\[(\d+)\]\.ReverseComplementedRead", text)
+            if m and name in ("SparsePoaTest.TestLocalStaggered", "SparsePoaTest.TestOrientation"):
+                case["summaries"].setdefault(m.group(2), {})["rc"] = m.group(1) == "TRUE"
+        sparse.append(case)
+    fasta = open(os.path.join(REF, "tests/data/m140905_042212_sidney_c100564852550000001823085912221377_s1_X0.fasta")).read()
+    zmw = [ "".join(rec.split("\n")[1:]) for rec in fasta.split(">")[1:]]
+    for c in sparse:
+        if c["test"] == "SparsePoaTest.TestZmw6251":
+            c["reads"] = zmw
+            # EXPECTs (:169-194): 10 reads in the graph; summaries[0] is forward, summaries[1] reverse;
+            # extent of read 0 covers [300, 595) and read 1 covers [5, 595) on the ~600 bp consensus.
+            c["num_reads"] = 10
+            c["covers"] = {"0": [300, 595], "1": [5, 595]}
+            c["summaries"] = {"0": {"rc": False}, "1": {"rc": True}}
+        if c["test"] in ("SparsePoaTest.SingleReadx100", "SparsePoaTest.SingleAndHalfx100"):
+            c["generated"] = "orc_poa_kat_reads (std::mt19937(42) stream of the test)"
+    return {"poa_consensus": cases, "sparse_poa": sparse}
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference tree not present; fixtures are committed, nothing to regenerate")
@@ -190,7 +310,9 @@ def main():
         json.dump(make_zmw6251(), f, indent=1)
     with open(os.path.join(HERE, "quiver_kats.json"), "w") as f:
         json.dump(make_quiver_kats(), f, indent=1)
-    print("wrote arrow_kats.json, zmw6251.json, quiver_kats.json")
+    with open(os.path.join(HERE, "poa_kats.json"), "w") as f:
+        json.dump(make_poa_kats(), f, indent=1)
+    print("wrote arrow_kats.json, zmw6251.json, quiver_kats.json, poa_kats.json")
 
 
 if __name__ == "__main__":
