@@ -299,6 +299,66 @@ int pbccs_quiver_refine_consensus(pbccs_quiver_scorer* s, const pbccs_refine_opt
                                   long long* n_applied, int* converged);
 int pbccs_quiver_consensus_qvs(pbccs_quiver_scorer* s, int* qvs, int cap, int* n);
 
+/* ---- POA draft (pbccs src/SparsePoa.cpp, ConsensusCore/src/C++/Poa) ---------------------------------
+ * The read-vs-graph DP and its traceback run on the device (k_poa_fill / k_poa_trace); the graph lives on
+ * the host.  Scores use DefaultPoaConfig (match 3, mismatch -5, insert -4, delete -4). */
+#define PBCCS_POA_GLOBAL 0
+#define PBCCS_POA_SEMIGLOBAL 1
+#define PBCCS_POA_LOCAL 2
+
+/* One ZMW's subreads in FilterReads order (include/pacbio/ccs/Consensus.h:223-292); a NULL sequence is a
+ * read FilterReads dropped (key -1, as Consensus.h:378 passes nullptr reads). */
+typedef struct {
+    const char* const* seqs;
+    const int* lens;
+    int n_reads;
+} pbccs_poa_input;
+
+typedef struct {
+    char* consensus;   /* caller buffer of cap bytes (not NUL-terminated); len = consensus length */
+    int cap;
+    int len;
+    int* keys;         /* n_reads: SparsePoa::ReadKey per read; -1 not added; -2 not reached (maxPoaCov) */
+    int* rc;           /* n_reads, by key: PoaAlignmentSummary::ReverseComplementedRead */
+    int* extents;      /* 4 * n_reads, by key: ExtentOnRead begin/end, ExtentOnConsensus begin/end */
+    int n_keys;
+} pbccs_poa_output;
+
+/* Consensus.h's PoaConsensus (:352-390) for n ZMWs at once: SparsePoa::OrientAndAddRead per read until
+ * max_coverage reads were added, then FindConsensus(min_coverage) with the per-read summaries.
+ * min_coverage < 0 uses Consensus.h's rule ((cov < 5) ? 1 : (cov + 1) / 2 - 1).  A consensus longer
+ * than its buffer sets that output's len and makes the call return PBCCS_ERANGE after all outputs are
+ * written. */
+int pbccs_poa_batch(pbccs_engine* eng, const pbccs_poa_input* in, int n, long long max_coverage, int min_coverage,
+                    pbccs_poa_output* out);
+
+/* SparsePoa (include/pacbio/ccs/SparsePoa.h:94-131), one graph per handle */
+typedef struct pbccs_sparse_poa pbccs_sparse_poa;
+int pbccs_sparse_poa_create(pbccs_engine* eng, pbccs_sparse_poa** out);
+void pbccs_sparse_poa_destroy(pbccs_sparse_poa* p);
+/* ReadKey OrientAndAddRead(seq, alnOptions, minScoreToAdd)                       (src/SparsePoa.cpp:95-138) */
+int pbccs_sparse_poa_orient_and_add_read(pbccs_sparse_poa* p, const char* seq, int len, float min_score_to_add,
+                                         int* key);
+/* FindConsensus(minCoverage, &summaries)                                          (src/SparsePoa.cpp:140-201)
+ * rc / extents as in pbccs_poa_output, one entry per key. */
+int pbccs_sparse_poa_find_consensus(pbccs_sparse_poa* p, int min_coverage, char* out, int cap, int* len, int* rc,
+                                    int* extents, int* n_keys);
+/* ToGraphViz(flags, pc) with pc = FindConsensus(min_coverage)'s consensus; flags: COLOR_NODES 1, VERBOSE_NODES 2 */
+int pbccs_sparse_poa_graphviz(pbccs_sparse_poa* p, int flags, int min_coverage, char* out, int cap, int* len);
+
+/* PoaConsensus::FindConsensus(reads, mode, minCoverage) (ConsensusCore PoaConsensus.cpp:86-115): every read
+ * added with AddRead in the given mode (no orientation choice).  dot (optional) receives
+ * pc->Graph.ToGraphViz(flags, pc).  PBCCS_EINVAL for an empty read (InvalidInputError). */
+int pbccs_poa_consensus(pbccs_engine* eng, const char* const* reads, const int* lens, int n, int mode,
+                        int min_coverage, char* out, int cap, int* len, int flags, char* dot, int dot_cap,
+                        int* dot_len);
+/* POA work counters since the last reset: alignments, DP cells, fill/trace device ms (profiling on) */
+typedef struct {
+    long long alignments, cells, launches, trace_steps;
+    double fill_ms, trace_ms, bytes;
+} pbccs_poa_stats;
+int pbccs_poa_stats_get(pbccs_engine* eng, pbccs_poa_stats* out, int reset);
+
 #ifdef __cplusplus
 }
 #endif

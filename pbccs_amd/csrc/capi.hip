@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "engine.hpp"
+#include "poa_engine.hpp"
 
 using namespace pbccs;
 
@@ -41,6 +42,14 @@ struct pbccs_engine {
     std::mutex statsMu;        // counters / stats are merged from the slots' worker threads
     long long oomRetries = 0;   // device batches rerun after PBCCS_EOOM
     std::vector<std::unique_ptr<Workspace>> slots;
+    std::unique_ptr<poa::PoaRunner> poa;   // the POA draft step's device state (made on first use)
+    std::mutex poaMu;
+    poa::PoaRunner& Poa()
+    {
+        if (!poa) poa.reset(new poa::PoaRunner(device));
+        poa->profiling = profiling;
+        return *poa;
+    }
     Workspace* Slot(int s)
     {
         while ((int)slots.size() <= s) slots.emplace_back(new Workspace(true));
@@ -1211,6 +1220,179 @@ int pbccs_quiver_consensus_qvs(pbccs_quiver_scorer* s, int* qvs, int cap, int* n
         *n = (int)q.size();
         if ((int)q.size() > cap || !qvs) return fail(PBCCS_ERANGE, "buffer too small");
         std::copy(q.begin(), q.end(), qvs);
+        return PBCCS_OK;
+    });
+}
+
+// ---------------------------------------------------------------- POA draft
+
+struct pbccs_sparse_poa {
+    pbccs_engine* eng;
+    poa::ZmwPoa z;
+};
+
+namespace {
+
+int put_text(const std::string& s, char* out, int cap, int* len)
+{
+    if (len) *len = (int)s.size();
+    if ((int)s.size() > cap || (!out && !s.empty())) return fail(PBCCS_ERANGE, "buffer too small");
+    if (!s.empty()) memcpy(out, s.data(), s.size());
+    return PBCCS_OK;
+}
+
+}  // namespace
+
+int pbccs_poa_batch(pbccs_engine* eng, const pbccs_poa_input* in, int n, long long max_coverage, int min_coverage,
+                    pbccs_poa_output* out)
+{
+    if (!eng || n < 0 || (n > 0 && (!in || !out)) || max_coverage < 1) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::vector<std::vector<std::string>> own(n);
+        std::vector<std::vector<const std::string*>> reads(n);
+        for (int z = 0; z < n; ++z) {
+            if (in[z].n_reads < 0 || (in[z].n_reads > 0 && (!in[z].seqs || !in[z].lens)))
+                return fail(PBCCS_EINVAL, "bad pbccs_poa_input");
+            own[z].resize(in[z].n_reads);
+            for (int r = 0; r < in[z].n_reads; ++r) {
+                if (in[z].seqs[r] && in[z].lens[r] <= 0) return fail(PBCCS_EINVAL, "empty read");
+                if (in[z].seqs[r]) own[z][r].assign(in[z].seqs[r], in[z].lens[r]);
+            }
+            for (int r = 0; r < in[z].n_reads; ++r) reads[z].push_back(in[z].seqs[r] ? &own[z][r] : nullptr);
+        }
+        std::vector<std::string> css;
+        std::vector<std::vector<int>> keys, ext;
+        std::vector<std::vector<char>> rc;
+        {
+            std::lock_guard<std::mutex> lk(eng->poaMu);
+            poa::PoaBatch(eng->Poa(), reads, max_coverage, min_coverage, &css, &keys, &rc, &ext);
+        }
+        bool range = false;
+        for (int z = 0; z < n; ++z) {
+            pbccs_poa_output& o = out[z];
+            o.len = (int)css[z].size();
+            o.n_keys = (int)rc[z].size();
+            if (o.consensus && o.len <= o.cap) memcpy(o.consensus, css[z].data(), css[z].size());
+            else range = true;
+            for (int r = 0; r < in[z].n_reads; ++r)
+                if (o.keys) o.keys[r] = keys[z][r];
+            for (int k = 0; k < o.n_keys; ++k) {
+                if (o.rc) o.rc[k] = rc[z][k];
+                if (o.extents)
+                    for (int e = 0; e < 4; ++e) o.extents[4 * k + e] = ext[z][4 * k + e];
+            }
+        }
+        return range ? fail(PBCCS_ERANGE, "consensus buffer too small") : PBCCS_OK;
+    });
+}
+
+int pbccs_sparse_poa_create(pbccs_engine* eng, pbccs_sparse_poa** out)
+{
+    if (!eng || !out) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        *out = new pbccs_sparse_poa{eng, poa::ZmwPoa()};
+        return PBCCS_OK;
+    });
+}
+
+void pbccs_sparse_poa_destroy(pbccs_sparse_poa* p) { delete p; }
+
+int pbccs_sparse_poa_orient_and_add_read(pbccs_sparse_poa* p, const char* seq, int len, float min_score_to_add,
+                                         int* key)
+{
+    if (!p || !seq || len <= 0 || !key) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        const std::string s(seq, len);
+        if (p->z.graph.NumReads() == 0) {
+            std::vector<int> path;
+            p->z.graph.AddFirstRead(s, &path);
+            p->z.readPaths.push_back(std::move(path));
+            p->z.rc.push_back(0);
+            *key = 0;
+            return PBCCS_OK;
+        }
+        std::vector<poa::AlignRequest> req{poa::AlignRequest{&p->z.graph, s, poa::kLocal, true, min_score_to_add}};
+        std::vector<poa::AlignResult> res;
+        {
+            std::lock_guard<std::mutex> lk(p->eng->poaMu);
+            p->eng->Poa().Align(req, &res);
+        }
+        if (res[0].chosen < 0) {
+            *key = -1;
+            return PBCCS_OK;
+        }
+        p->z.readPaths.push_back(std::move(res[0].path));
+        p->z.rc.push_back((char)res[0].chosen);
+        *key = (int)p->z.readPaths.size() - 1;
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_sparse_poa_find_consensus(pbccs_sparse_poa* p, int min_coverage, char* out, int cap, int* len, int* rc,
+                                    int* extents, int* n_keys)
+{
+    if (!p || !len) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::vector<int> ext;
+        const std::string css = p->z.readPaths.empty() ? std::string() : p->z.FindConsensus(min_coverage, &ext);
+        const int nk = (int)p->z.rc.size();
+        if (n_keys) *n_keys = nk;
+        for (int k = 0; k < nk; ++k) {
+            if (rc) rc[k] = p->z.rc[k];
+            if (extents)
+                for (int e = 0; e < 4; ++e) extents[4 * k + e] = ext[4 * k + e];
+        }
+        return put_text(css, out, cap, len);
+    });
+}
+
+int pbccs_sparse_poa_graphviz(pbccs_sparse_poa* p, int flags, int min_coverage, char* out, int cap, int* len)
+{
+    if (!p || !len) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::vector<int> path;
+        if (!p->z.readPaths.empty()) p->z.FindConsensus(min_coverage, nullptr, &path);
+        return put_text(p->z.graph.GraphViz(flags & 1, flags & 2, &path), out, cap, len);
+    });
+}
+
+int pbccs_poa_consensus(pbccs_engine* eng, const char* const* reads, const int* lens, int n, int mode,
+                        int min_coverage, char* out, int cap, int* len, int flags, char* dot, int dot_cap,
+                        int* dot_len)
+{
+    if (!eng || n < 0 || (n > 0 && (!reads || !lens)) || !len || mode < 0 || mode > 2)
+        return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        poa::PoaGraph g;
+        for (int r = 0; r < n; ++r) {
+            if (!reads[r] || lens[r] <= 0) return fail(PBCCS_EINVAL, "Input sequences must have nonzero length.");
+            const std::string s(reads[r], lens[r]);
+            if (g.NumReads() == 0) {
+                g.AddFirstRead(s, nullptr);
+                continue;
+            }
+            std::vector<poa::AlignRequest> req{poa::AlignRequest{&g, s, (poa::AlignMode)mode, false, 0.f}};
+            std::vector<poa::AlignResult> res;
+            std::lock_guard<std::mutex> lk(eng->poaMu);
+            eng->Poa().Align(req, &res);
+        }
+        const std::vector<int> path = g.ConsensusPath((poa::AlignMode)mode, min_coverage);
+        if (dot) {
+            const int rc = put_text(g.GraphViz(flags & 1, flags & 2, &path), dot, dot_cap, dot_len);
+            if (rc != PBCCS_OK) return rc;
+        }
+        return put_text(g.Sequence(path), out, cap, len);
+    });
+}
+
+int pbccs_poa_stats_get(pbccs_engine* eng, pbccs_poa_stats* out, int reset)
+{
+    if (!eng || !out) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::lock_guard<std::mutex> lk(eng->poaMu);
+        const poa::PoaStats& s = eng->Poa().stats;
+        *out = pbccs_poa_stats{s.alignments, s.cells, s.launches, s.traceSteps, s.fillMs, s.traceMs, s.bytes};
+        if (reset) eng->Poa().stats = poa::PoaStats();
         return PBCCS_OK;
     });
 }

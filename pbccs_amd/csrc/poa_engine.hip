@@ -1,0 +1,709 @@
+// pbccs_amd/csrc/poa_engine.hip -- the POA draft step: read-vs-graph DP and traceback kernels for
+// gfx950, and the host loop that threads reads into the graphs.
+//
+// Reference: ConsensusCore/src/C++/Poa/PoaGraphImpl.cpp:177-447 (alignment columns, TryAddRead,
+// CommitAdd), PoaGraphTraversals.cpp:227-369 (traceback), pbccs src/SparsePoa.cpp:95-201.
+//
+// The DP (makeAlignmentColumn, PoaGraphImpl.cpp:236-352) scores with DefaultPoaConfig's integers
+// (match 3, mismatch -5, insert -4, delete -4) in float; every cell is an integer far below 2^24, so
+// the float sums are exact and the device runs them in int32 -- the same values, bit for bit.  A cell
+//     S(v, i) = max( [LOCAL, i > 0] 0,
+//                    max over predecessors u:  S(u, i-1) + (read[i-1] == base(v) ? 3 : -5),  S(u, i) - 4,
+//                    S(v, i-1) - 4 )
+// is a column recurrence whose only serial term is the last one (the Extra move).  With
+// g(i) = ne(i) + 4 i, where ne is the max of the other terms, S(v, i) = max_{k <= i} g(k) - 4 i: a prefix
+// maximum, which the wavefront takes with DPP.  So one wavefront fills a column 1024 rows at a time
+// (16 contiguous rows per lane), columns in the graph's topological order.
+//
+// Layout in HBM: each alignment owns nCols x colStride score cells (colStride = rows padded to 1024),
+// row-major per column so a lane's 16 rows are one or two 16-byte accesses and a wave's are contiguous.
+// LOCAL scores are >= 0 and at most 3 * rows, so they are stored as uint16 when that fits (half the
+// traffic); other modes and longer reads use int32.  The traceback does not store moves: it recomputes
+// the reaching move of each visited cell from the scores with the reference's candidate order and strict
+// '>' ties, which is what tracebackAndThread reads from AlignmentColumn::ReachingMove / PreviousVertex.
+#include "poa_engine.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <climits>
+#include <cstring>
+#include <thread>
+
+namespace pbccs {
+namespace poa {
+
+namespace {
+
+constexpr int kMatchScore = 3, kMismatchScore = -5, kInsertScore = -4, kDeleteScore = -4;   // DefaultPoaConfig
+constexpr int kNeg = -(1 << 29);   // stands in for -FLT_MAX: every real candidate beats it
+
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_i(int old, int x)
+{
+    return __builtin_amdgcn_update_dpp(old, x, CTRL, ROWMASK, 0xF, false);
+}
+
+// inclusive prefix maximum over the wavefront's 64 lanes
+__device__ __forceinline__ int wave_prefix_max(int x)
+{
+    x = max(x, dpp_i<0x111, 0xF>(kNeg, x));   // row_shr:1
+    x = max(x, dpp_i<0x112, 0xF>(kNeg, x));   // row_shr:2
+    x = max(x, dpp_i<0x114, 0xF>(kNeg, x));   // row_shr:4
+    x = max(x, dpp_i<0x118, 0xF>(kNeg, x));   // row_shr:8
+    x = max(x, dpp_i<0x142, 0xA>(kNeg, x));   // row_bcast:15
+    x = max(x, dpp_i<0x143, 0xC>(kNeg, x));   // row_bcast:31
+    return x;
+}
+
+// (value, key) maximum over the wave: larger value, then smaller key
+__device__ __forceinline__ void wave_argmax(int& v, int& key)
+{
+    for (int off = 32; off > 0; off >>= 1) {
+        const int ov = __shfl_xor(v, off);
+        const int ok = __shfl_xor(key, off);
+        if (ov > v || (ov == v && ok < key)) {
+            v = ov;
+            key = ok;
+        }
+    }
+}
+
+template <class ST>
+struct Rows16;
+
+template <>
+struct Rows16<uint16_t> {
+    static __device__ __forceinline__ void load(const uint16_t* p, int* v)
+    {
+        const uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
+        const unsigned w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = (int)((w[r >> 1] >> ((r & 1) * 16)) & 0xFFFFu);
+    }
+    static __device__ __forceinline__ void store(uint16_t* p, const int* v)
+    {
+        unsigned w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = (unsigned)(v[2 * k] & 0xFFFF) | ((unsigned)v[2 * k + 1] << 16);
+        reinterpret_cast<uint4*>(p)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        reinterpret_cast<uint4*>(p)[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
+};
+
+template <>
+struct Rows16<int> {
+    static __device__ __forceinline__ void load(const int* p, int* v)
+    {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int4 a = reinterpret_cast<const int4*>(p)[k];
+            v[4 * k] = a.x;
+            v[4 * k + 1] = a.y;
+            v[4 * k + 2] = a.z;
+            v[4 * k + 3] = a.w;
+        }
+    }
+    static __device__ __forceinline__ void store(int* p, const int* v)
+    {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            reinterpret_cast<int4*>(p)[k] = make_int4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
+};
+
+// TryAddRead's alignment columns (PoaGraphImpl.cpp:384-435): one wavefront per job, columns in the
+// program's topological order.  Also the $ column (makeAlignmentColumnForExit, :177-233): its score
+// and the column it is reached from.
+template <class ST>
+__global__ __launch_bounds__(64) void k_poa_fill(const PoaJob* __restrict__ jobs, int jobBase, PoaPools P,
+                                                 ST* __restrict__ pool, int* __restrict__ outScore,
+                                                 int* __restrict__ outExitCol)
+{
+    const int j = jobBase + blockIdx.x;
+    const PoaJob J = jobs[j];
+    const int lane = threadIdx.x;
+    ST* S = pool + J.scoreOff;
+    const uint8_t* rb = P.rowBase + J.readOff;
+    const int I = J.I, stride = J.colStride, mode = J.mode;
+    const int* predStart = P.predStart + J.predStartOff;
+    int bestVal = kNeg, bestVid = INT_MAX, bestCol = 0;
+    for (int k = 0; k < J.nCols; ++k) {
+        const int base = P.base[J.progOff + k];
+        const int vid = P.vertexOfCol[J.progOff + k];
+        const int ps = predStart[k], pe = predStart[k + 1];
+        ST* col = S + (long long)k * stride;
+        int carry = kNeg, colBest = kNeg;
+        for (int c0 = 0; c0 <= I; c0 += kChunkRows) {
+            const int i0 = c0 + lane * 16;
+            const uint4 rw = *reinterpret_cast<const uint4*>(rb + i0);
+            const unsigned rbw[4] = {rw.x, rw.y, rw.z, rw.w};
+            int ne[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ne[r] = mode == kLocal ? 0 : kNeg;
+            // row 0: ^ has no reaching move (0); LOCAL/SEMIGLOBAL start there (0); GLOBAL deletes into it
+            if (i0 == 0) ne[0] = (ps == pe || mode != kGlobal) ? 0 : kNeg;
+            for (int p = ps; p < pe; ++p) {
+                const ST* q = S + (long long)P.predCol[p] * stride;
+                int qv[16];
+                Rows16<ST>::load(q + i0, qv);
+                int up = i0 > 0 ? (int)q[i0 - 1] : kNeg;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int b = (rbw[r >> 2] >> ((r & 3) * 8)) & 0xFF;
+                    const int diag = up + (b == base ? kMatchScore : kMismatchScore);
+                    ne[r] = max(ne[r], max(diag, qv[r] + kDeleteScore));
+                    up = qv[r];
+                }
+            }
+            // Extra moves: S(i) = max_{k<=i} (ne(k) - k * insert) + i * insert
+            int run = kNeg;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                run = max(run, ne[r] - (i0 + r) * kInsertScore);
+                ne[r] = run;
+            }
+            const int incl = wave_prefix_max(run);
+            const int excl = max(dpp_i<0x138, 0xF>(kNeg, incl), carry);   // wave_shr:1
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = i0 + r;
+                ne[r] = max(ne[r], excl) + i * kInsertScore;
+                if (i <= I && (mode == kLocal || (mode == kSemiGlobal && i == I))) colBest = max(colBest, ne[r]);
+            }
+            Rows16<ST>::store(col + i0, ne);
+            carry = __builtin_amdgcn_readlane(max(incl, carry), 63);
+        }
+        if (colBest > bestVal || (colBest == bestVal && vid < bestVid)) {
+            bestVal = colBest;
+            bestVid = vid;
+            bestCol = k;
+        }
+        // the next columns' lanes read rows this column's lanes wrote
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    }
+    if (mode == kGlobal) {
+        // regular predecessors of $ in in-edge order, strict '>' (PoaGraphImpl.cpp:214-227)
+        bestVal = kNeg;
+        bestCol = 0;
+        for (int e = 0; e < J.nExit; ++e) {
+            const int c = P.exitPred[J.exitOff + e];
+            const int v = (int)S[(long long)c * stride + I];
+            if (v > bestVal) {
+                bestVal = v;
+                bestCol = c;
+            }
+        }
+    } else {
+        int key = bestVid;
+        const int v0 = bestVal;
+        wave_argmax(bestVal, key);
+        // the lane holding the winner publishes its column
+        const unsigned long long m = __ballot(v0 == bestVal && bestVid == key);
+        bestCol = __shfl(bestCol, (int)__builtin_ctzll(m));
+    }
+    if (lane == 0) {
+        outScore[j] = bestVal;
+        outExitCol[j] = bestCol;
+    }
+}
+
+// tracebackAndThread's walk (PoaGraphTraversals.cpp:252-347) for the jobs whose reads are committed:
+// the End move into $, then each visited cell with the move that reached it, recomputed as
+// makeAlignmentColumn chose it (candidates in order Start, per predecessor Match/Mismatch then Delete,
+// then Extra; strict '>').
+template <class ST>
+__global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ jobs, const int* __restrict__ traceJobs,
+                                                  int traceBase, PoaPools P, const ST* __restrict__ pool,
+                                                  const int* __restrict__ exitCol, TraceStep* __restrict__ steps,
+                                                  int* __restrict__ nSteps)
+{
+    const int t = traceBase + blockIdx.x;
+    const int j = traceJobs[t];
+    const PoaJob J = jobs[j];
+    const int lane = threadIdx.x;
+    const ST* S = pool + J.scoreOff;
+    const int I = J.I, stride = J.colStride, mode = J.mode;
+    const int ec = exitCol[j];
+    const int* vtx = P.vertexOfCol + J.progOff;
+    // LOCAL: the End move comes from ArgMax of that column (first maximum, VectorL.hpp:66-69)
+    int prevRow = I;
+    if (mode == kLocal) {
+        int bv = kNeg, br = INT_MAX;
+        for (int i = lane; i <= I; i += 64) {
+            const int v = (int)S[(long long)ec * stride + i];
+            if (v > bv) {
+                bv = v;
+                br = i;
+            }
+        }
+        wave_argmax(bv, br);
+        prevRow = br;
+    }
+    if (lane != 0) return;
+    TraceStep* out = steps + J.stepOff;
+    const int cap = I + J.nCols + 2;
+    int n = 0;
+    out[n++] = TraceStep{kExit, vtx[ec], I, prevRow, kEnd};
+    int k = ec, i = mode == kLocal ? prevRow : I;
+    const uint8_t* rb = P.rowBase + J.readOff;
+    const int* predStart = P.predStart + J.predStartOff;
+    while (!(k == 0 && i == 0)) {
+        if (n >= cap) {
+            n = -1;
+            break;
+        }
+        const int ps = predStart[k], pe = predStart[k + 1];
+        int best, mv, pv;
+        if (i == 0) {
+            if (mode != kGlobal) {
+                mv = kStart;
+                pv = 0;
+            } else {
+                best = kNeg;
+                mv = kInvalid;
+                pv = -1;
+                for (int p = ps; p < pe; ++p) {
+                    const int c = P.predCol[p];
+                    const int cand = (int)S[(long long)c * stride] + kDeleteScore;
+                    if (cand > best) {
+                        best = cand;
+                        pv = c;
+                        mv = kDelete;
+                    }
+                }
+            }
+        } else {
+            if (mode == kLocal) {
+                best = 0;
+                mv = kStart;
+                pv = 0;
+            } else {
+                best = kNeg;
+                mv = kInvalid;
+                pv = -1;
+            }
+            const bool isMatch = rb[i] == P.base[J.progOff + k];
+            for (int p = ps; p < pe; ++p) {
+                const int c = P.predCol[p];
+                const ST* q = S + (long long)c * stride;
+                int cand = (int)q[i - 1] + (isMatch ? kMatchScore : kMismatchScore);
+                if (cand > best) {
+                    best = cand;
+                    pv = c;
+                    mv = isMatch ? kMatch : kMismatch;
+                }
+                cand = (int)q[i] + kDeleteScore;
+                if (cand > best) {
+                    best = cand;
+                    pv = c;
+                    mv = kDelete;
+                }
+            }
+            const int cand = (int)S[(long long)k * stride + i - 1] + kInsertScore;
+            if (cand > best) {
+                pv = k;
+                mv = kExtra;
+            }
+        }
+        if (mv == kInvalid) {
+            n = -1;
+            break;
+        }
+        out[n++] = TraceStep{vtx[k], vtx[pv], i, 0, mv};
+        if (mv == kStart) i = 0;
+        else if (mv != kDelete) i--;
+        k = pv;
+    }
+    nSteps[t] = n;
+}
+
+// ConsensusCore Sequence.cpp:44-105 (ComplementArray; note N <-> M)
+char complement(char c)
+{
+    switch (c) {
+        case 'A': return 'T'; case 'C': return 'G'; case 'G': return 'C'; case 'T': return 'A';
+        case 'a': return 't'; case 'c': return 'g'; case 'g': return 'c'; case 't': return 'a';
+        case 'N': return 'M'; case 'M': return 'N'; case 'n': return 'm'; case 'm': return 'n';
+        case '-': return '-';
+        case 0: return 3; case 1: return 2; case 2: return 1; case 3: return 0;
+    }
+    return (char)127;
+}
+
+std::string reverse_complement(const std::string& s)
+{
+    std::string r(s.size(), 0);
+    for (size_t k = 0; k < s.size(); ++k) r[s.size() - 1 - k] = complement(s[k]);
+    return r;
+}
+
+template <class F>
+void parallel_for(int threads, int n, F&& f)
+{
+    if (threads <= 1 || n < 2) {
+        for (int k = 0; k < n; ++k) f(k);
+        return;
+    }
+    std::atomic<int> next(0);
+    std::vector<std::thread> pool;
+    std::exception_ptr err;
+    std::atomic<bool> failed(false);
+    const int nt = std::min(threads, n);
+    for (int t = 0; t < nt; ++t)
+        pool.emplace_back([&] {
+            for (int k; (k = next.fetch_add(1)) < n;) {
+                if (failed.load()) return;
+                try {
+                    f(k);
+                } catch (...) {
+                    if (!failed.exchange(true)) err = std::current_exception();
+                    return;
+                }
+            }
+        });
+    for (auto& t : pool) t.join();
+    if (err) std::rethrow_exception(err);
+}
+
+void check(hipError_t e, const char* what)
+{
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        throw DeviceError(std::string("POA: ") + what + ": " + hipGetErrorString(e));
+    }
+}
+
+template <class T>
+void upload(DevVec<T>& d, const std::vector<T>& h, hipStream_t s)
+{
+    d.reserve(std::max<size_t>(h.size(), 1), false);
+    if (!h.empty()) check(hipMemcpyAsync(d.ptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s), "upload");
+}
+
+}  // namespace
+
+PoaRunner::PoaRunner(int device, int hostThreads) : device_(device)
+{
+    const int hw = (int)std::thread::hardware_concurrency();
+    threads_ = hostThreads > 0 ? hostThreads : std::max(1, std::min(16, hw));
+    check(hipSetDevice(device_), "hipSetDevice");
+    check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+    for (auto& e : ev_) check(hipEventCreate(&e), "hipEventCreate");
+}
+
+PoaRunner::~PoaRunner()
+{
+    (void)hipSetDevice(device_);
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto& e : ev_)
+        if (e) (void)hipEventDestroy(e);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>* out)
+{
+    check(hipSetDevice(device_), "hipSetDevice");
+    const int n = (int)reqs.size();
+    out->assign(n, AlignResult());
+    if (n == 0) return;
+
+    // ---- host: column programs and job layout
+    std::vector<ColumnProgram> prog(n);
+    std::vector<std::string> rcRead(n);
+    parallel_for(threads_, n, [&](int r) {
+        reqs[r].graph->Program(&prog[r]);
+        if (reqs[r].orient) rcRead[r] = reverse_complement(reqs[r].read);
+    });
+    std::vector<uint8_t> hBase, hRowBase;
+    std::vector<int> hVertex, hPredStart, hPredCol, hExit;
+    std::vector<PoaJob> jobs;
+    std::vector<int> jobReq, jobOri;
+    for (int r = 0; r < n; ++r) {
+        const ColumnProgram& C = prog[r];
+        const int nCols = (int)C.vertexOfCol.size();
+        const int progOff = (int)hBase.size(), psOff = (int)hPredStart.size(), exOff = (int)hExit.size();
+        const int predOff = (int)hPredCol.size();
+        hBase.insert(hBase.end(), C.base.begin(), C.base.end());
+        hVertex.insert(hVertex.end(), C.vertexOfCol.begin(), C.vertexOfCol.end());
+        for (int v : C.predStart) hPredStart.push_back(v + predOff);
+        hPredCol.insert(hPredCol.end(), C.predCol.begin(), C.predCol.end());
+        hExit.insert(hExit.end(), C.exitPredCol.begin(), C.exitPredCol.end());
+        for (int o = 0; o < (reqs[r].orient ? 2 : 1); ++o) {
+            const std::string& s = o ? rcRead[r] : reqs[r].read;
+            PoaJob J{};
+            J.nCols = nCols;
+            J.I = (int)s.size();
+            J.colStride = (J.I + 1 + kChunkRows - 1) / kChunkRows * kChunkRows;
+            J.mode = reqs[r].mode;
+            J.progOff = progOff;
+            J.predStartOff = psOff;
+            J.exitOff = exOff;
+            J.nExit = (int)C.exitPredCol.size();
+            J.readOff = (long long)hRowBase.size();
+            J.wide = !(J.mode == kLocal && 3LL * J.colStride < 65536);
+            hRowBase.resize(hRowBase.size() + J.colStride + 16, 0);
+            memcpy(hRowBase.data() + J.readOff + 1, s.data(), s.size());
+            jobs.push_back(J);
+            jobReq.push_back(r);
+            jobOri.push_back(o);
+        }
+    }
+    const int nJobs = (int)jobs.size();
+    upload(dBase_, hBase, stream_);
+    upload(dVertexOfCol_, hVertex, stream_);
+    upload(dPredStart_, hPredStart, stream_);
+    upload(dPredCol_, hPredCol, stream_);
+    upload(dExitPred_, hExit, stream_);
+    upload(dRowBase_, hRowBase, stream_);
+    const PoaPools pools{dBase_.ptr, dVertexOfCol_.ptr, dPredStart_.ptr, dPredCol_.ptr, dExitPred_.ptr, dRowBase_.ptr};
+
+    size_t budget = budget_;
+    if (budget == 0) {
+        size_t fr = 0, tot = 0;
+        check(hipMemGetInfo(&fr, &tot), "hipMemGetInfo");
+        budget = std::min<size_t>((size_t)(0.5 * (double)fr), 48ull << 30) + dPool_.cap;
+        budget = std::max<size_t>(budget, 64ull << 20);
+    }
+    auto jobBytes = [&](const PoaJob& J) {
+        return ((size_t)J.nCols * J.colStride * (J.wide ? 4 : 2) + 255) / 256 * 256;
+    };
+
+    // ---- launch groups: the requests whose jobs fit the score-pool budget together
+    std::vector<int> scoreH(nJobs), exitH(nJobs);
+    std::vector<std::vector<TraceStep>> stepsH(n);
+    std::vector<int> nStepsH(n, 0);
+    dScore_.reserve(nJobs, false);
+    dExitCol_.reserve(nJobs, false);
+    int j0 = 0;
+    while (j0 < nJobs) {
+        // group [j0, j1): whole requests
+        size_t bytes = 0;
+        int j1 = j0;
+        while (j1 < nJobs) {
+            int j2 = j1;
+            size_t b = 0;
+            while (j2 < nJobs && jobReq[j2] == jobReq[j1]) b += jobBytes(jobs[j2++]);
+            if (j1 > j0 && bytes + b > budget) break;
+            bytes += b;
+            j1 = j2;
+        }
+        // order the group's jobs: uint16 first, then int32 (each kernel instantiation gets a range)
+        std::vector<int> order;
+        for (int j = j0; j < j1; ++j)
+            if (!jobs[j].wide) order.push_back(j);
+        const int nNarrow = (int)order.size();
+        for (int j = j0; j < j1; ++j)
+            if (jobs[j].wide) order.push_back(j);
+        size_t off16 = 0;
+        for (int k = 0; k < nNarrow; ++k) {
+            jobs[order[k]].scoreOff = (long long)(off16 / 2);
+            off16 += jobBytes(jobs[order[k]]);
+        }
+        size_t off32 = 0;
+        for (int k = nNarrow; k < (int)order.size(); ++k) {
+            jobs[order[k]].scoreOff = (long long)(off32 / 4);
+            off32 += jobBytes(jobs[order[k]]);
+        }
+        dPool_.reserve(off16 + off32 + 256, false);
+        // the group's jobs, in launch order, with their trace step regions
+        std::vector<PoaJob> gj;
+        for (int j : order) gj.push_back(jobs[j]);
+        upload(dJobs_, gj, stream_);
+        const int gn = (int)gj.size();
+        uint16_t* pool16 = reinterpret_cast<uint16_t*>(dPool_.ptr);
+        int* pool32 = reinterpret_cast<int*>(dPool_.ptr + off16);
+        if (profiling) check(hipEventRecord(ev_[0], stream_), "event");
+        if (nNarrow > 0)
+            hipLaunchKernelGGL(k_poa_fill<uint16_t>, dim3(nNarrow), dim3(64), 0, stream_, dJobs_.ptr, 0, pools, pool16,
+                               dScore_.ptr, dExitCol_.ptr);
+        if (gn > nNarrow)
+            hipLaunchKernelGGL(k_poa_fill<int>, dim3(gn - nNarrow), dim3(64), 0, stream_, dJobs_.ptr, nNarrow, pools,
+                               pool32, dScore_.ptr, dExitCol_.ptr);
+        check(hipGetLastError(), "k_poa_fill launch");
+        if (profiling) check(hipEventRecord(ev_[1], stream_), "event");
+        std::vector<int> gScore(gn), gExit(gn);
+        check(hipMemcpyAsync(gScore.data(), dScore_.ptr, gn * sizeof(int), hipMemcpyDeviceToHost, stream_), "d2h");
+        check(hipMemcpyAsync(gExit.data(), dExitCol_.ptr, gn * sizeof(int), hipMemcpyDeviceToHost, stream_), "d2h");
+        check(hipStreamSynchronize(stream_), "k_poa_fill");
+        if (profiling) {
+            float ms = 0.f;
+            check(hipEventElapsedTime(&ms, ev_[0], ev_[1]), "event");
+            stats.fillMs += ms;
+        }
+        stats.launches += (nNarrow > 0) + (gn > nNarrow);
+        for (int k = 0; k < gn; ++k) {
+            const PoaJob& J = gj[k];
+            scoreH[order[k]] = gScore[k];
+            exitH[order[k]] = gExit[k];
+            stats.alignments++;
+            stats.cells += (long long)J.nCols * (J.I + 1);
+            stats.bytes += (double)J.nCols * (J.I + 1) * (J.wide ? 4 : 2);
+        }
+        // SparsePoa's choice (src/SparsePoa.cpp:112-131) / AddRead's unconditional commit
+        for (int k = 0; k < gn; ++k) {
+            const int j = order[k], r = jobReq[j];
+            AlignResult& R = (*out)[r];
+            R.score[jobOri[j]] = (float)scoreH[j];
+        }
+        for (int k = 0; k < gn; ++k) {
+            const int j = order[k], r = jobReq[j];
+            AlignResult& R = (*out)[r];
+            if (jobOri[j] != 0) continue;
+            if (!reqs[r].orient) R.chosen = 0;
+            else if (R.score[0] >= R.score[1] && R.score[0] >= reqs[r].minScore) R.chosen = 0;
+            else if (R.score[1] >= R.score[0] && R.score[1] >= reqs[r].minScore) R.chosen = 1;
+        }
+        long long stepTotal = 0;
+        std::vector<int> traceNarrow, traceWide;
+        for (int k = 0; k < gn; ++k) {
+            const int j = order[k], r = jobReq[j];
+            if ((*out)[r].chosen != jobOri[j]) continue;
+            (gj[k].wide ? traceWide : traceNarrow).push_back(k);
+        }
+        std::vector<int> traceJobs(traceNarrow);
+        traceJobs.insert(traceJobs.end(), traceWide.begin(), traceWide.end());
+        std::vector<long long> stepOff(traceJobs.size());
+        for (size_t t = 0; t < traceJobs.size(); ++t) {
+            PoaJob& J = gj[traceJobs[t]];
+            J.stepOff = stepTotal;
+            stepOff[t] = stepTotal;
+            stepTotal += J.I + J.nCols + 2;
+        }
+        if (!traceJobs.empty()) {
+            upload(dJobs_, gj, stream_);
+            upload(dTraceJobs_, traceJobs, stream_);
+            dSteps_.reserve(stepTotal, false);
+            dNSteps_.reserve(traceJobs.size(), false);
+            // exit columns were written at the jobs' group positions
+            if (profiling) check(hipEventRecord(ev_[2], stream_), "event");
+            const int tn = (int)traceNarrow.size(), tw = (int)traceWide.size();
+            if (tn > 0)
+                hipLaunchKernelGGL(k_poa_trace<uint16_t>, dim3(tn), dim3(64), 0, stream_, dJobs_.ptr, dTraceJobs_.ptr, 0,
+                                   pools, pool16, dExitCol_.ptr, dSteps_.ptr, dNSteps_.ptr);
+            if (tw > 0)
+                hipLaunchKernelGGL(k_poa_trace<int>, dim3(tw), dim3(64), 0, stream_, dJobs_.ptr, dTraceJobs_.ptr, tn,
+                                   pools, pool32, dExitCol_.ptr, dSteps_.ptr, dNSteps_.ptr);
+            check(hipGetLastError(), "k_poa_trace launch");
+            if (profiling) check(hipEventRecord(ev_[3], stream_), "event");
+            std::vector<int> ns(traceJobs.size());
+            std::vector<TraceStep> st(stepTotal);
+            check(hipMemcpyAsync(ns.data(), dNSteps_.ptr, ns.size() * sizeof(int), hipMemcpyDeviceToHost, stream_), "d2h");
+            check(hipMemcpyAsync(st.data(), dSteps_.ptr, st.size() * sizeof(TraceStep), hipMemcpyDeviceToHost, stream_),
+                  "d2h");
+            check(hipStreamSynchronize(stream_), "k_poa_trace");
+            if (profiling) {
+                float ms = 0.f;
+                check(hipEventElapsedTime(&ms, ev_[2], ev_[3]), "event");
+                stats.traceMs += ms;
+            }
+            for (size_t t = 0; t < traceJobs.size(); ++t) {
+                const int r = jobReq[order[traceJobs[t]]];
+                if (ns[t] < 1) throw DeviceError("POA traceback did not reach the start vertex");
+                stepsH[r].assign(st.begin() + stepOff[t], st.begin() + stepOff[t] + ns[t]);
+                nStepsH[r] = ns[t];
+                stats.traceSteps += ns[t];
+            }
+        }
+        j0 = j1;
+    }
+
+    // ---- host: thread the committed reads into their graphs (CommitAdd)
+    parallel_for(threads_, n, [&](int r) {
+        AlignResult& R = (*out)[r];
+        if (R.chosen < 0) return;
+        const std::string& s = R.chosen ? rcRead[r] : reqs[r].read;
+        reqs[r].graph->ThreadTraceback(s, reqs[r].mode, stepsH[r].data(), nStepsH[r], &R.path);
+    });
+}
+
+std::string ZmwPoa::FindConsensus(int minCoverage, std::vector<int>* extents, std::vector<int>* cssPath)
+{
+    const std::vector<int> path = graph.ConsensusPath(kLocal, minCoverage);
+    if (cssPath) *cssPath = path;
+    if (extents) {
+        std::vector<int> pos(graph.NumVertices(), -1);
+        for (size_t k = 0; k < path.size(); ++k) pos[path[k]] = (int)k;
+        extents->clear();
+        for (const std::vector<int>& rp : readPaths) {
+            int rs = 0, re = 0, cs = 0, ce = 0;
+            bool found = false;
+            for (size_t p = 0; p < rp.size(); ++p) {
+                const int x = pos[rp[p]];
+                if (x < 0) continue;
+                if (!found) {
+                    cs = x;
+                    rs = (int)p;
+                    found = true;
+                }
+                ce = x + 1;
+                re = (int)p + 1;
+            }
+            extents->insert(extents->end(), {rs, re, cs, ce});
+        }
+    }
+    return graph.Sequence(path);
+}
+
+void PoaBatch(PoaRunner& R, const std::vector<std::vector<const std::string*>>& reads, long long maxCov, int minCov,
+              std::vector<std::string>* consensus, std::vector<std::vector<int>>* keys,
+              std::vector<std::vector<char>>* rc, std::vector<std::vector<int>>* extents)
+{
+    const int nz = (int)reads.size();
+    std::vector<ZmwPoa> Z(nz);
+    std::vector<int> next(nz, 0);
+    std::vector<long long> cov(nz, 0);
+    std::vector<char> done(nz, 0);
+    keys->assign(nz, std::vector<int>());
+    for (int z = 0; z < nz; ++z) (*keys)[z].assign(reads[z].size(), -2);
+    auto record = [&](int z, int key) {
+        (*keys)[z][next[z]++] = key;
+        if (key >= 0 && ++cov[z] >= maxCov) done[z] = 1;
+        if (next[z] >= (int)reads[z].size()) done[z] = 1;
+    };
+    for (;;) {
+        std::vector<AlignRequest> reqs;
+        std::vector<int> reqZ;
+        for (int z = 0; z < nz; ++z) {
+            while (!done[z]) {
+                const std::string* s = reads[z][next[z]];
+                if (s == nullptr) {
+                    record(z, -1);
+                } else if (Z[z].graph.NumReads() == 0) {
+                    std::vector<int> path;
+                    Z[z].graph.AddFirstRead(*s, &path);
+                    Z[z].readPaths.push_back(std::move(path));
+                    Z[z].rc.push_back(0);
+                    record(z, 0);
+                } else {
+                    reqs.push_back(AlignRequest{&Z[z].graph, *s, kLocal, true, 0.0f});
+                    reqZ.push_back(z);
+                    break;
+                }
+            }
+        }
+        if (reqs.empty()) break;
+        std::vector<AlignResult> res;
+        R.Align(reqs, &res);
+        for (size_t q = 0; q < reqs.size(); ++q) {
+            const int z = reqZ[q];
+            if (res[q].chosen < 0) {
+                record(z, -1);
+                continue;
+            }
+            Z[z].readPaths.push_back(std::move(res[q].path));
+            Z[z].rc.push_back((char)res[q].chosen);
+            record(z, (int)Z[z].readPaths.size() - 1);
+        }
+    }
+    consensus->assign(nz, std::string());
+    rc->assign(nz, std::vector<char>());
+    extents->assign(nz, std::vector<int>());
+    parallel_for(R.HostThreads(), nz, [&](int z) {
+        const int mc = minCov >= 0 ? minCov : (cov[z] < 5 ? 1 : (int)((cov[z] + 1) / 2 - 1));
+        (*consensus)[z] = Z[z].readPaths.empty() ? std::string() : Z[z].FindConsensus(mc, &(*extents)[z]);
+        (*rc)[z] = Z[z].rc;
+    });
+}
+
+}  // namespace poa
+}  // namespace pbccs

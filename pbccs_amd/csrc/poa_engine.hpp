@@ -1,0 +1,112 @@
+// pbccs_amd/csrc/poa_engine.hpp -- POA draft step on the device.
+//
+// PoaRunner aligns reads against their ZMWs' partial-order graphs in batches: the host builds each
+// graph's column program (poa_graph.hpp), k_poa_fill fills the read-vs-graph DP of every (ZMW, read
+// orientation) pair at once -- one wavefront per pair -- and k_poa_trace walks the chosen orientation's
+// traceback, which the host then threads into the graph.  ZmwPoa drives SparsePoa's OrientAndAddRead /
+// FindConsensus (src/SparsePoa.cpp:95-201) for a whole batch of ZMWs in lock-step read rounds.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "engine.hpp"
+#include "poa_graph.hpp"
+
+namespace pbccs {
+namespace poa {
+
+constexpr int kChunkRows = 1024;   // rows per wave pass: 64 lanes x 16 rows
+
+// One read-vs-graph alignment on the device.
+struct PoaJob {
+    long long scoreOff;   // element offset of the alignment's score matrix (ST units), nCols x colStride
+    int nCols, colStride, I, mode;
+    int progOff;          // into base[] / vertexOfCol[]  (nCols entries)
+    int predStartOff;     // into predStart[]             (nCols + 1 entries, values index predCol[])
+    int exitOff, nExit;   // into exitPred[]              ($'s predecessor columns, GLOBAL end move)
+    long long readOff;    // into rowBase[]: byte i = read[i - 1] for rows 1..I, colStride bytes
+    long long stepOff;    // into the traceback step pool (I + nCols + 2 steps)
+    int wide;             // score matrix stored as int32 (else uint16)
+    int pad;
+};
+
+struct PoaPools {
+    const uint8_t* base;
+    const int* vertexOfCol;
+    const int* predStart;
+    const int* predCol;
+    const int* exitPred;
+    const uint8_t* rowBase;
+};
+
+struct AlignRequest {
+    PoaGraph* graph;
+    std::string read;   // forward orientation as given
+    AlignMode mode;
+    bool orient;        // SparsePoa::OrientAndAddRead (also try the reverse complement)
+    float minScore;     // minScoreToAdd
+};
+
+struct AlignResult {
+    int chosen = -1;    // 0 forward, 1 reverse complement, -1 not added
+    float score[2] = {0.f, 0.f};
+    std::vector<int> path;   // per read position, the vertex it was threaded through
+};
+
+struct PoaStats {
+    long long alignments = 0, cells = 0, launches = 0, traceSteps = 0;
+    double fillMs = 0.0, traceMs = 0.0;
+    double bytes = 0.0;   // algorithmic score-matrix bytes written by the fills
+};
+
+class PoaRunner {
+public:
+    explicit PoaRunner(int device, int hostThreads = 0);
+    ~PoaRunner();
+    PoaRunner(const PoaRunner&) = delete;
+    PoaRunner& operator=(const PoaRunner&) = delete;
+
+    // TryAddRead for every request (both orientations when orient), the SparsePoa choice, CommitAdd of
+    // the chosen orientation.  Graphs of different requests must be distinct.
+    void Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>* out);
+
+    void SetPoolBudget(size_t bytes) { budget_ = bytes; }
+    int HostThreads() const { return threads_; }
+    PoaStats stats;
+    bool profiling = false;
+
+private:
+    int device_;
+    int threads_;
+    size_t budget_ = 0;   // score-matrix bytes per launch group; 0 = from free memory
+    hipStream_t stream_ = nullptr;
+    hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+    DevVec<uint8_t> dBase_, dRowBase_, dPool_;
+    DevVec<int> dVertexOfCol_, dPredStart_, dPredCol_, dExitPred_, dScore_, dExitCol_, dNSteps_, dTraceJobs_;
+    DevVec<PoaJob> dJobs_;
+    DevVec<TraceStep> dSteps_;
+};
+
+// SparsePoa state of one ZMW (src/SparsePoa.cpp:60-201).
+struct ZmwPoa {
+    PoaGraph graph;
+    std::vector<std::vector<int>> readPaths;   // per key
+    std::vector<char> rc;                      // per key
+    // FindConsensus (src/SparsePoa.cpp:140-201): the consensus and, per key, the read extent and
+    // consensus extent (PoaAlignmentSummary); extents[4k..4k+3] = read begin, end, consensus begin, end.
+    std::string FindConsensus(int minCoverage, std::vector<int>* extents, std::vector<int>* cssPath = nullptr);
+};
+
+// Consensus.h's PoaConsensus (include/pacbio/ccs/Consensus.h:352-390) over a batch of ZMWs: reads
+// (nullptr = dropped by FilterReads, key -1) are added in order with OrientAndAddRead until maxCov were
+// taken; keys[z][r] = key, -2 past the coverage stop.  minCov < 0: (cov < 5) ? 1 : (cov + 1) / 2 - 1.
+void PoaBatch(PoaRunner& R, const std::vector<std::vector<const std::string*>>& reads, long long maxCov, int minCov,
+              std::vector<std::string>* consensus, std::vector<std::vector<int>>* keys,
+              std::vector<std::vector<char>>* rc, std::vector<std::vector<int>>* extents);
+
+}  // namespace poa
+}  // namespace pbccs

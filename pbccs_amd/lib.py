@@ -80,6 +80,23 @@ class CQuiverConfig(ctypes.Structure):
                 ("sum_product", ctypes.c_int)]
 
 
+class CPoaInput(ctypes.Structure):
+    _fields_ = [("seqs", ctypes.POINTER(ctypes.c_char_p)), ("lens", ctypes.POINTER(ctypes.c_int)),
+                ("n_reads", ctypes.c_int)]
+
+
+class CPoaOutput(ctypes.Structure):
+    _fields_ = [("consensus", ctypes.c_char_p), ("cap", ctypes.c_int), ("len", ctypes.c_int),
+                ("keys", ctypes.POINTER(ctypes.c_int)), ("rc", ctypes.POINTER(ctypes.c_int)),
+                ("extents", ctypes.POINTER(ctypes.c_int)), ("n_keys", ctypes.c_int)]
+
+
+class CPoaStats(ctypes.Structure):
+    _fields_ = [("alignments", ctypes.c_longlong), ("cells", ctypes.c_longlong), ("launches", ctypes.c_longlong),
+                ("trace_steps", ctypes.c_longlong), ("fill_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
+                ("bytes", ctypes.c_double)]
+
+
 # exported symbol -> (restype, argtypes); tests check that every symbol of include/pbccs_amd.h is exported
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -145,6 +162,16 @@ SIGNATURES = {
     "pbccs_quiver_scorer_allocated_entries": (I, [P, I, PLL, PLL]),
     "pbccs_quiver_refine_consensus": (I, [P, ctypes.POINTER(CRefineOptions), PLL, PLL, PI]),
     "pbccs_quiver_consensus_qvs": (I, [P, PI, I, PI]),
+    # POA draft
+    "pbccs_poa_batch": (I, [P, ctypes.POINTER(CPoaInput), I, ctypes.c_longlong, I, ctypes.POINTER(CPoaOutput)]),
+    "pbccs_sparse_poa_create": (I, [P, ctypes.POINTER(P)]),
+    "pbccs_sparse_poa_destroy": (None, [P]),
+    "pbccs_sparse_poa_orient_and_add_read": (I, [P, ctypes.c_char_p, I, ctypes.c_float, PI]),
+    "pbccs_sparse_poa_find_consensus": (I, [P, I, ctypes.c_char_p, I, PI, PI, PI, PI]),
+    "pbccs_sparse_poa_graphviz": (I, [P, I, I, ctypes.c_char_p, I, PI]),
+    "pbccs_poa_consensus": (I, [P, ctypes.POINTER(ctypes.c_char_p), PI, I, I, I, ctypes.c_char_p, I, PI, I,
+                                ctypes.c_char_p, I, PI]),
+    "pbccs_poa_stats_get": (I, [P, ctypes.POINTER(CPoaStats), I]),
 }
 
 

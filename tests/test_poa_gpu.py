@@ -1,0 +1,187 @@
+"""POA draft step on the GPU (pbccs_amd.poa over pbccs_poa_* / pbccs_sparse_poa_*) against the reference's own
+POA tests (tests/golden/poa_kats.json, parsed from ConsensusCore/src/Tests/TestPoaConsensus.cpp and
+tests/TestSparsePoa.cpp) and against the CPU restatement (oracle/poa_oracle.cpp) on seeded synthetic ZMWs.
+Bar: bit-exact (consensus strings, read keys, orientations, extents, graph dumps)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "poa_kats.json")))
+
+
+@pytest.fixture(scope="module")
+def P():
+    import pbccs_amd
+    from pbccs_amd import poa
+    eng = pbccs_amd.Engine(0)
+    poa.poa_stats(eng, reset=True)
+    return poa, eng
+
+
+def _rc(s):
+    return s[::-1].translate(str.maketrans("ACGT", "TGCA"))
+
+
+@pytest.mark.parametrize("case", GOLD["poa_consensus"], ids=lambda c: c["test"])
+def test_poa_consensus_kats(P, case):
+    poa, eng = P
+    mc = case["min_coverage"] if case["min_coverage"] is not None else -poa.INT_MAX
+    seq, dot = poa.poa_consensus(case["reads"], case["mode"], mc, graphviz_flags=case["graphviz_flags"], engine=eng)
+    if case["expected"] is not None:
+        assert seq == case["expected"]
+    if case["expected_dot"]:
+        assert dot.replace("\n", "") == case["expected_dot"]
+    exp_seq, exp_dot = O.poa_consensus(case["reads"], case["mode"], mc, graphviz_flags=case["graphviz_flags"])
+    assert (seq, dot) == (exp_seq, exp_dot)
+
+
+def _sparse(name):
+    return next(c for c in GOLD["sparse_poa"] if c["test"] == name)
+
+
+@pytest.mark.parametrize("name", ["SparsePoaTest.TestLocalStaggered", "SparsePoaTest.TestOrientation"])
+def test_sparse_poa_kats(P, name):
+    poa, eng = P
+    case = _sparse(name)
+    sp = poa.SparsePoa(eng)
+    keys = [sp.OrientAndAddRead(r) for r in case["reads"]]
+    assert all(k >= 0 for k in keys)
+    css, summ = sp.FindConsensus(case["min_coverage"])
+    assert css == case["expected"]
+    for k, exp in case["summaries"].items():
+        s = summ[int(k)]
+        if "rc" in exp:
+            assert s["rc"] == exp["rc"]
+        if "read" in exp:
+            assert list(s["read"]) == exp["read"] and list(s["tpl"]) == exp["tpl"]
+    # the batched form agrees
+    b = poa.poa_batch([case["reads"]], min_coverage=case["min_coverage"], engine=eng)[0]
+    assert b["consensus"] == css and b["summaries"] == summ
+
+
+def test_sparse_poa_zmw6251(P):
+    poa, eng = P
+    case = _sparse("SparsePoaTest.TestZmw6251")
+    sp = poa.SparsePoa(eng)
+    assert all(sp.OrientAndAddRead(r) >= 0 for r in case["reads"])
+    css, summ = sp.FindConsensus(case["min_coverage"])
+    assert len(summ) == case["num_reads"]
+    for k, exp in case["summaries"].items():
+        assert summ[int(k)]["rc"] == exp["rc"]
+    for k, (lo, hi) in case["covers"].items():
+        b, e = summ[int(k)]["tpl"]
+        assert b <= lo and hi <= e
+    exp = O.sparse_poa(case["reads"], case["min_coverage"])
+    assert css == exp["consensus"] and summ == exp["summaries"]
+    dot = sp.ToGraphViz(3, case["min_coverage"])
+    assert dot.startswith("digraph G {") and dot.count("->") > 1000
+
+
+def test_sparse_poa_single_read_x100(P):
+    """SparsePoaTest.SingleReadx100: 100 seeded 2-20 kb reads, one per graph (batched as 100 ZMWs)."""
+    poa, eng = P
+    seqs = O.poa_kat_reads(0)
+    res = poa.poa_batch([[s] for s in seqs], min_coverage=1, engine=eng)
+    for s, r in zip(seqs, res):
+        assert r["consensus"] == s and r["keys"] == [0]
+        assert r["summaries"] == [{"rc": False, "read": (0, len(s)), "tpl": (0, len(s))}]
+
+
+def test_sparse_poa_single_and_half_x100(P):
+    """SparsePoaTest.SingleAndHalfx100: a 1-5 kb read and the first third of its reverse complement."""
+    poa, eng = P
+    seqs = O.poa_kat_reads(1)
+    res = poa.poa_batch([[s, _rc(s)[:len(s) // 3]] for s in seqs], min_coverage=1, engine=eng)
+    for s, r in zip(seqs, res):
+        L = len(s)
+        assert r["consensus"] == s and r["keys"] == [0, 1]
+        assert r["summaries"][0] == {"rc": False, "read": (0, L), "tpl": (0, L)}
+        assert r["summaries"][1] == {"rc": True, "read": (0, L // 3), "tpl": (L - L // 3, L)}
+
+
+def _synthetic_subreads(n, length_range, passes_range, seed):
+    from pbccs_amd import synth
+    zs = synth.make_zmws(n, None, None, seed=seed, length_range=length_range, passes_range=passes_range)
+    return [[r["seq"] for r in z["reads"]] for z in zs]
+
+
+def test_poa_batch_matches_oracle_synthetic(P):
+    """Seeded ZMWs of 200-1500 bp with 2-12 passes; dropped reads (None) and a maxPoaCov stop included."""
+    poa, eng = P
+    zr = _synthetic_subreads(24, (200, 1500), (2, 12), seed=71)
+    rng = np.random.default_rng(5)
+    for reads in zr[:6]:
+        reads[int(rng.integers(0, len(reads)))] = None
+    res = poa.poa_batch(zr, max_coverage=None, engine=eng)
+    for reads, got in zip(zr, res):
+        exp = O.sparse_poa(reads)
+        assert got["consensus"] == exp["consensus"]
+        assert got["keys"] == exp["keys"] and got["summaries"] == exp["summaries"]
+    res = poa.poa_batch(zr[:8], max_coverage=3, engine=eng)
+    for reads, got in zip(zr[:8], res):
+        exp = O.sparse_poa(reads, max_coverage=3)
+        assert got["consensus"] == exp["consensus"] and got["keys"] == exp["keys"]
+        assert got["summaries"] == exp["summaries"]
+
+
+def test_poa_batch_matches_oracle_2kb(P):
+    """configs[1] shape: 2 kb insert, 10 passes (alternate passes reverse-complemented)."""
+    poa, eng = P
+    zr = _synthetic_subreads(4, (2000, 2000), (10, 10), seed=1)
+    res = poa.poa_batch(zr, engine=eng)
+    for reads, got in zip(zr, res):
+        exp = O.sparse_poa(reads)
+        assert got["consensus"] == exp["consensus"] and got["summaries"] == exp["summaries"]
+        assert [s["rc"] for s in got["summaries"]] == [False, True] * 5
+
+
+def test_poa_wide_scores_long_reads(P):
+    """Reads past 21.5 kb store int32 scores (3 * rows no longer fits uint16): a 21.6 kb, 2-pass ZMW, and
+    GLOBAL / SEMIGLOBAL graphs (always int32) over several 1024-row chunks."""
+    poa, eng = P
+    zr = _synthetic_subreads(1, (21600, 21600), (2, 2), seed=9)
+    got = poa.poa_batch(zr, engine=eng)[0]
+    exp = O.sparse_poa(zr[0])
+    assert got["consensus"] == exp["consensus"] and got["summaries"] == exp["summaries"]
+    reads = _synthetic_subreads(1, (1500, 1500), (4, 4), seed=10)[0]
+    reads = [r if k % 2 == 0 else _rc(r) for k, r in enumerate(reads)]   # one orientation for GLOBAL
+    for mode in (O.POA_GLOBAL, O.POA_SEMIGLOBAL, O.POA_LOCAL):
+        assert poa.poa_consensus(reads, mode, 2, graphviz_flags=3, engine=eng) == \
+            O.poa_consensus(reads, mode, 2, graphviz_flags=3)
+
+
+def test_driver_zmw_input_with_gpu_poa(P):
+    """driver.zmw_input (FilterReads -> POA -> ExtractMappedRead) with the GPU SparsePoa equals the same
+    driver with the oracle's POA."""
+    poa, eng = P
+    from pbccs_amd import driver
+
+    class OraclePoa:
+        def __init__(self):
+            self.reads = []
+
+        def orient_and_add_read(self, seq):
+            self.reads.append(seq)
+            return O.sparse_poa(self.reads)["keys"][-1]
+
+        def find_consensus(self, min_cov):
+            r = O.sparse_poa(self.reads, min_cov)
+            return r["consensus"], dict(enumerate(r["summaries"]))
+
+    for reads in _synthetic_subreads(3, (400, 900), (5, 9), seed=33):
+        chunk = {"snr": [10.0, 7.0, 5.0, 11.0], "reads": [{"seq": s} for s in reads]}
+        st_g, z_g = driver.zmw_input(chunk, poa.SparsePoa(eng))
+        st_o, z_o = driver.zmw_input(chunk, OraclePoa())
+        assert st_g == st_o and z_g == z_o
+
+
+def test_poa_stats_counted(P):
+    poa, eng = P
+    s = poa.poa_stats(eng)
+    assert s["alignments"] > 0 and s["cells"] > 0 and s["trace_steps"] > 0
