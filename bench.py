@@ -60,6 +60,10 @@ def parse():
     ap.add_argument("--streams", type=int, default=0,
                     help="workspace slots = batches polished concurrently (0 = min(steps, 5), capped by HBM)")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--stage", choices=["polish", "poa"], default="polish",
+                    help="polish: the headline line (Consensus.h's Arrow polish, from the draft on); poa: the POA "
+                         "draft step before it (SparsePoa over each ZMW's raw subreads, SURVEY.md §8(f) row 1) on "
+                         "the same configs[1] ZMWs")
     return ap.parse_args()
 
 
@@ -267,6 +271,8 @@ def main():
     settings = pbccs_amd.ConsensusSettings()
     seed0 = args.seed + 7919 * rank
 
+    if args.stage == "poa":
+        return poa_stage(args, rank, world, eng, barrier, sync, seed0)
     if args.workload != "2kb":
         job_time, local_time, res, workload, scaling, total = queue_workload(args, rank, world, eng, settings, seed0)
         return report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total)
@@ -314,6 +320,85 @@ def main():
     workload = (f"configs[1]: synthetic {args.length} bp insert, {args.passes} full passes, "
                 f"{args.zmws_per_step} ZMWs per step")
     report(args, rank, world, eng, slots, job_time, local_time, res, workload, "weak", len(res) * world)
+
+
+def poa_cpu_baseline(args, n):
+    """The POA restatement (oracle/poa_oracle.cpp, SparsePoa as Consensus.h drives it) one ZMW per task on the
+    host threads, like the polish baseline."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    from pbccs_amd import synth
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    threads = max(1, min(args.cpu_threads or share, os.cpu_count() or 1, n))
+    zr = [[r["seq"] for r in z["reads"]] for z in synth.make_zmws(n, args.length, args.passes, seed=args.seed + 99991)]
+    O.lib()
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(O.sparse_poa, zr))
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+            "nproc": os.cpu_count(),
+            "sample": f"{n} synthetic ZMWs of the same config (seed {args.seed + 99991}), oracle/poa_oracle.cpp "
+                      f"SparsePoa (OrientAndAddRead per subread, FindConsensus) one ZMW per task on {threads} host "
+                      f"threads, {dt:.1f} s wall"}
+
+
+def poa_stage(args, rank, world, eng, barrier, sync, seed0):
+    """The POA draft step of configs[1]: a step hands one batch of ZMWs' raw subreads (alternate passes
+    reverse-complemented, as sequenced) to pbccs_poa_batch, which adds every ZMW's next read in the same
+    device round (k_poa_fill over all (ZMW, orientation) alignments, k_poa_trace over the committed ones,
+    host threading of the graphs) and ends with FindConsensus + the per-read extents.  The graphs are host
+    state, so the timed region includes the host threading and the per-round uploads of the column
+    programs; the subreads themselves start in host memory, as the reference's do."""
+    from pbccs_amd import poa, synth
+
+    def subreads(n, seed):
+        return [[r["seq"] for r in z["reads"]] for z in synth.make_zmws(n, args.length, args.passes, seed=seed)]
+
+    poa.poa_batch(subreads(min(args.zmws_per_step, 256), seed0 + 1000), engine=eng)
+    steps_in = [subreads(args.zmws_per_step, seed0 + k) for k in range(args.steps)]
+    poa.poa_stats(eng, reset=True)
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    res = [poa.poa_batch(x, engine=eng) for x in steps_in]
+    sync()
+    barrier()
+    local_time = time.perf_counter() - t0
+    job_time = max_over_ranks(local_time, world)
+    st = poa.poa_stats(eng, reset=True)
+    total = args.steps * args.zmws_per_step * world
+    launches = max(1, st["launches"])
+    avg_ms = st["fill_ms"] / launches
+    bpl = st["bytes"] / launches
+    achieved = bpl / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
+    out = {
+        "metric": "POA draft ZMWs/sec (SparsePoa over raw subreads) on MI355X vs host-CPU",
+        "value": round(total / job_time, 3), "unit": "ZMWs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(job_time / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int32/uint16",
+        "data": "synthetic subreads (SURVEY.md §8(d): truth iid ACGT; 7%/4%/1% ins/del/sub; odd passes RC)",
+        "config": {"workload": f"configs[1] POA: {args.length} bp insert, {args.passes} subreads per ZMW, "
+                               f"{args.zmws_per_step} ZMWs per step", "zmws_per_step": args.zmws_per_step,
+                   "zmws_total": total, "parallelism": f"zmw-shard x{world}"},
+        "gcups": round(st["cells"] / local_time / 1e9, 3),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None, "kernel": "k_poa_fill",
+                     "avg_launch_ms": round(avg_ms, 4), "launches": st["launches"], "bytes_per_launch": bpl,
+                     "cells_per_launch": st["cells"] / launches},
+        "poa": {"alignments": st["alignments"], "gcells": round(st["cells"] / 1e9, 3),
+                "fill_ms": round(st["fill_ms"], 2), "trace_ms": round(st["trace_ms"], 2),
+                "trace_steps": st["trace_steps"],
+                "draft_len_mean": round(sum(len(r["consensus"]) for b in res for r in b) / max(1, total // world), 1)},
+    }
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        out["cpu_baseline"] = poa_cpu_baseline(args, min(args.cpu_sample, 48))
+        out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total_zmws):

@@ -295,6 +295,11 @@ int pbccs_quiver_scorer_baseline_scores(pbccs_quiver_scorer* s, float* out, int 
 int pbccs_quiver_scorer_num_flipflops(pbccs_quiver_scorer* s, int* out);
 /* AllocatedEntries of read i's alpha / beta (SparseMatrix-inl.hpp:275-284) */
 int pbccs_quiver_scorer_allocated_entries(pbccs_quiver_scorer* s, int i, long long* alpha, long long* beta);
+/* RecursorBase::Alignment(e, alpha) (Quiver/detail/RecursorBase.cpp:124-264) of read i on its template window:
+ * the Viterbi traceback through the read's alpha band, as PairwiseAlignment Target() / Query() (gapped,
+ * len characters each).  PBCCS_ESTATE for a sum-product scorer (the reference's ShouldNotReachHere) or a
+ * read without a scorer; PBCCS_ERANGE when cap < len. */
+int pbccs_quiver_scorer_alignment(pbccs_quiver_scorer* s, int i, char* target, char* query, int cap, int* len);
 int pbccs_quiver_refine_consensus(pbccs_quiver_scorer* s, const pbccs_refine_options* opts, long long* n_tested,
                                   long long* n_applied, int* converged);
 int pbccs_quiver_consensus_qvs(pbccs_quiver_scorer* s, int* qvs, int cap, int* n);

@@ -149,6 +149,17 @@ class Scorer:
         return {"converged": conv == 1, "error": conv < 0, "n_tested": nt.value, "n_applied": na.value,
                 "applied": applied}
 
+    def alignment(self, r):
+        """RecursorBase::Alignment of read r (Viterbi): (target, query); None for a sum-product scorer."""
+        cap = 1 << 20
+        t = ctypes.create_string_buffer(cap)
+        q = ctypes.create_string_buffer(cap)
+        n = _qlib().qorc_scorer_alignment(self._h, r, t, q, cap)
+        if n == -1:
+            return None
+        assert n >= 0
+        return t.value.decode(), q.value.decode()
+
     def qvs(self):
         L = len(self.template())
         out = (ctypes.c_int * max(1, L))()
@@ -257,6 +268,7 @@ def _qlib():
         L.qorc_scorer_apply.argtypes = [c_p, c_i, I, I, I, c_s]
         L.qorc_refine.argtypes = [c_p, c_i, c_i, c_i, Lg, Lg]
         L.qorc_qvs.argtypes = [c_p, I, c_i]
+        L.qorc_scorer_alignment.argtypes = [c_p, c_i, c_s, c_s, c_i]
         L._q_ready = True
     return L
 
@@ -361,6 +373,17 @@ class QuiverScorer:
         nt, na = ctypes.c_long(), ctypes.c_long()
         conv = _qlib().qorc_refine(self._h, max_iter, separation, neighborhood, ctypes.byref(nt), ctypes.byref(na))
         return {"converged": conv == 1, "error": conv < 0, "n_tested": nt.value, "n_applied": na.value}
+
+    def alignment(self, r):
+        """RecursorBase::Alignment of read r (Viterbi): (target, query); None for a sum-product scorer."""
+        cap = 1 << 20
+        t = ctypes.create_string_buffer(cap)
+        q = ctypes.create_string_buffer(cap)
+        n = _qlib().qorc_scorer_alignment(self._h, r, t, q, cap)
+        if n == -1:
+            return None
+        assert n >= 0
+        return t.value.decode(), q.value.decode()
 
     def qvs(self):
         L = len(self.template())

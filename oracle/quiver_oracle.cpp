@@ -648,6 +648,57 @@ struct MutationScorer {
     }
 };
 
+// ---------------------------------------------------------------- traceback (detail/RecursorBase.cpp:118-264)
+// RecursorBase::Alignment: the Viterbi path through a filled alpha matrix, moves tried in the order
+// Incorporate, Delete, Extra, Merge with strict '>' against lfloat(); then replayed into the gapped
+// target / query strings of the PairwiseAlignment.  Viterbi combiner only (ShouldNotReachHere otherwise).
+static bool Alignment(const Evaluator& e, const QMatrix& a, int moves, std::string* target, std::string* query)
+{
+    struct Spec { int type, dr, dt; };
+    const Spec inc{INCORPORATE, 1, 1}, del{DELETE, 0, 1}, extra{EXTRA, 1, 0}, merge{MERGE, 1, 2};
+    const int I = e.I(), J = e.J();
+    int i = I, j = J;
+    std::vector<Spec> path;
+    while (i > 0 || j > 0) {
+        Spec best{0, 0, 0};
+        float bestScore = -FLT_MAX;
+        if (i > 0 && j > 0) {
+            const float t = a.Get(i - 1, j - 1) + e.Inc(i - 1, j - 1);
+            if (t > bestScore) { best = inc; bestScore = t; }
+        }
+        if (j > 0) {
+            const bool freeDelete = (!e.pinEnd && i == I) || (!e.pinStart && i == 0);
+            const float t = a.Get(i, j - 1) + (freeDelete ? 0.0f : e.Del(i, j - 1));
+            if (t > bestScore) { best = del; bestScore = t; }
+        }
+        if (i > 0) {
+            const float t = a.Get(i - 1, j) + e.Extra(i - 1, j);
+            if (t > bestScore) { best = extra; bestScore = t; }
+        }
+        if ((moves & MERGE) && i > 0 && j > 1) {
+            const float t = a.Get(i - 1, j - 2) + e.Merge(i - 1, j - 2);
+            if (t > bestScore) { best = merge; bestScore = t; }
+        }
+        if (best.type == 0) return false;   // assert(bestMove.MoveType != INVALID_MOVE)
+        path.push_back(best);
+        i -= best.dr;
+        j -= best.dt;
+    }
+    std::reverse(path.begin(), path.end());
+    target->clear();
+    query->clear();
+    i = j = 0;
+    for (const Spec& m : path) {
+        if (m.type == INCORPORATE) { *target += e.tpl[j]; *query += e.r->seq[i]; }
+        else if (m.type == EXTRA) { *target += '-'; *query += e.r->seq[i]; }
+        else if (m.type == DELETE) { *target += e.tpl[j]; *query += '-'; }
+        else { *target += e.tpl[j]; *target += e.tpl[j + 1]; *query += '-'; *query += e.r->seq[i]; }
+        i += m.dr;
+        j += m.dt;
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------- multi-read scorer (Quiver/MultiReadMutationScorer.cpp)
 struct MappedRead {
     QvRead read;
@@ -876,6 +927,9 @@ using namespace qorc;
 extern "C" {
 
 float qorc_log_add(float a, float b) { return logAdd(a, b); }
+
+// RecursorBase::Alignment of read r's MutationScorer alpha (Viterbi only): 0 ok, -1 sum-product, -2 no path
+int qorc_scorer_alignment(void* h, int r, char* target, char* query, int cap);
 float qorc_exp_ps(float x) { return exp_ps1(x); }
 float qorc_log_ps(float x) { return log_ps1(x); }
 
@@ -1036,6 +1090,21 @@ int qorc_qvs(void* h, int* out, int cap)
     if ((int)q.size() > cap) return -(int)q.size();
     for (size_t k = 0; k < q.size(); ++k) out[k] = q[k];
     return (int)q.size();
+}
+
+int qorc_scorer_alignment(void* h, int r, char* target, char* query, int cap)
+{
+    MultiReadScorer* m = static_cast<MultiReadScorer*>(h);
+    const ReadState& rs = m->reads.at(r);
+    if (!rs.sc) return -2;
+    if (rs.sc->rec.Cb.sumProduct) return -1;
+    std::string t, q;
+    if (!Alignment(rs.sc->ev, rs.sc->alpha, rs.sc->rec.moves, &t, &q)) return -2;
+    const int n = (int)std::min<size_t>(t.size(), (size_t)std::max(cap - 1, 0));
+    memcpy(target, t.data(), n);
+    memcpy(query, q.data(), n);
+    target[n] = query[n] = 0;
+    return (int)t.size();
 }
 
 }  // extern "C"

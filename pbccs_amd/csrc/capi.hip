@@ -1194,6 +1194,21 @@ int pbccs_quiver_scorer_allocated_entries(pbccs_quiver_scorer* s, int i, long lo
     return PBCCS_OK;
 }
 
+int pbccs_quiver_scorer_alignment(pbccs_quiver_scorer* s, int i, char* target, char* query, int cap, int* len)
+{
+    if (!s || i < 0 || i >= s->batch->NumReads(s->z) || !len) return fail(PBCCS_EINVAL, "bad argument");
+    return guarded([&] {
+        std::string t, q;
+        if (!s->batch->Alignment(s->batch->ReadIndex(s->z, i), &t, &q))
+            return fail(PBCCS_ESTATE, "Alignment needs a Viterbi scorer and a read with a scorer");
+        *len = (int)t.size();
+        if ((int)t.size() > cap || !target || !query) return fail(PBCCS_ERANGE, "buffer too small");
+        memcpy(target, t.data(), t.size());
+        memcpy(query, q.data(), q.size());
+        return PBCCS_OK;
+    });
+}
+
 int pbccs_quiver_refine_consensus(pbccs_quiver_scorer* s, const pbccs_refine_options* opts, long long* n_tested,
                                   long long* n_applied, int* converged)
 {

@@ -214,8 +214,8 @@ __global__ __launch_bounds__(64) void k_poa_fill(const PoaJob* __restrict__ jobs
 template <class ST>
 __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ jobs, const int* __restrict__ traceJobs,
                                                   int traceBase, PoaPools P, const ST* __restrict__ pool,
-                                                  const int* __restrict__ exitCol, TraceStep* __restrict__ steps,
-                                                  int* __restrict__ nSteps)
+                                                  const int* __restrict__ exitCol, uint32_t* __restrict__ steps,
+                                                  TraceHeader* __restrict__ heads)
 {
     const int t = traceBase + blockIdx.x;
     const int j = traceJobs[t];
@@ -240,10 +240,10 @@ __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ job
         prevRow = br;
     }
     if (lane != 0) return;
-    TraceStep* out = steps + J.stepOff;
+    uint32_t* out = steps + J.stepOff;
     const int cap = I + J.nCols + 2;
     int n = 0;
-    out[n++] = TraceStep{kExit, vtx[ec], I, prevRow, kEnd};
+    out[n++] = pack_step(kExit, kEnd);
     int k = ec, i = mode == kLocal ? prevRow : I;
     const uint8_t* rb = P.rowBase + J.readOff;
     const int* predStart = P.predStart + J.predStartOff;
@@ -309,12 +309,12 @@ __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ job
             n = -1;
             break;
         }
-        out[n++] = TraceStep{vtx[k], vtx[pv], i, 0, mv};
+        out[n++] = pack_step(vtx[k], mv);
         if (mv == kStart) i = 0;
         else if (mv != kDelete) i--;
         k = pv;
     }
-    nSteps[t] = n;
+    heads[t] = TraceHeader{n, prevRow, vtx[ec], 0};
 }
 
 // ConsensusCore Sequence.cpp:44-105 (ComplementArray; note N <-> M)
@@ -407,54 +407,86 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
     out->assign(n, AlignResult());
     if (n == 0) return;
 
-    // ---- host: column programs and job layout
+    // ---- host: column programs, then the job layout (sizes -> prefix offsets -> parallel fill)
     std::vector<ColumnProgram> prog(n);
     std::vector<std::string> rcRead(n);
     parallel_for(threads_, n, [&](int r) {
         reqs[r].graph->Program(&prog[r]);
         if (reqs[r].orient) rcRead[r] = reverse_complement(reqs[r].read);
     });
-    std::vector<uint8_t> hBase, hRowBase;
-    std::vector<int> hVertex, hPredStart, hPredCol, hExit;
-    std::vector<PoaJob> jobs;
-    std::vector<int> jobReq, jobOri;
+    std::vector<int> firstJob(n + 1, 0);
+    for (int r = 0; r < n; ++r) firstJob[r + 1] = firstJob[r] + (reqs[r].orient ? 2 : 1);
+    const int nJobs = firstJob[n];
+    hJobs_.reserve(2 * (size_t)nJobs);   // [0, nJobs): by request; [nJobs, 2 nJobs): a group in launch order
+    PoaJob* jobs = hJobs_.ptr;
+    std::vector<int> jobReq(nJobs), jobOri(nJobs);
+    long long nBase = 0, nPredStart = 0, nPredCol = 0, nExit = 0, nRow = 0;
     for (int r = 0; r < n; ++r) {
         const ColumnProgram& C = prog[r];
         const int nCols = (int)C.vertexOfCol.size();
-        const int progOff = (int)hBase.size(), psOff = (int)hPredStart.size(), exOff = (int)hExit.size();
-        const int predOff = (int)hPredCol.size();
-        hBase.insert(hBase.end(), C.base.begin(), C.base.end());
-        hVertex.insert(hVertex.end(), C.vertexOfCol.begin(), C.vertexOfCol.end());
-        for (int v : C.predStart) hPredStart.push_back(v + predOff);
-        hPredCol.insert(hPredCol.end(), C.predCol.begin(), C.predCol.end());
-        hExit.insert(hExit.end(), C.exitPredCol.begin(), C.exitPredCol.end());
         for (int o = 0; o < (reqs[r].orient ? 2 : 1); ++o) {
-            const std::string& s = o ? rcRead[r] : reqs[r].read;
-            PoaJob J{};
+            const int j = firstJob[r] + o;
+            PoaJob& J = jobs[j];
+            J = PoaJob{};
             J.nCols = nCols;
-            J.I = (int)s.size();
+            J.I = (int)(o ? rcRead[r] : reqs[r].read).size();
             J.colStride = (J.I + 1 + kChunkRows - 1) / kChunkRows * kChunkRows;
             J.mode = reqs[r].mode;
-            J.progOff = progOff;
-            J.predStartOff = psOff;
-            J.exitOff = exOff;
+            J.progOff = (int)nBase;
+            J.predStartOff = (int)nPredStart;
+            J.exitOff = (int)nExit;
             J.nExit = (int)C.exitPredCol.size();
-            J.readOff = (long long)hRowBase.size();
+            J.readOff = nRow;
             J.wide = !(J.mode == kLocal && 3LL * J.colStride < 65536);
-            hRowBase.resize(hRowBase.size() + J.colStride + 16, 0);
-            memcpy(hRowBase.data() + J.readOff + 1, s.data(), s.size());
-            jobs.push_back(J);
-            jobReq.push_back(r);
-            jobOri.push_back(o);
+            J.traceSlot = -1;
+            nRow += J.colStride + 16;
+            jobReq[j] = r;
+            jobOri[j] = o;
         }
+        nBase += nCols;
+        nPredStart += nCols + 1;
+        nPredCol += (long long)C.predCol.size();
+        nExit += (long long)C.exitPredCol.size();
     }
-    const int nJobs = (int)jobs.size();
-    upload(dBase_, hBase, stream_);
-    upload(dVertexOfCol_, hVertex, stream_);
-    upload(dPredStart_, hPredStart, stream_);
-    upload(dPredCol_, hPredCol, stream_);
-    upload(dExitPred_, hExit, stream_);
-    upload(dRowBase_, hRowBase, stream_);
+    hBase_.reserve(nBase);
+    hVertex_.reserve(nBase);
+    hPredStart_.reserve(nPredStart);
+    hPredCol_.reserve(std::max(1LL, nPredCol));
+    hExit_.reserve(std::max(1LL, nExit));
+    hRowBase_.reserve(nRow);
+    std::vector<long long> predColOff(n + 1, 0);
+    for (int r = 0; r < n; ++r) predColOff[r + 1] = predColOff[r] + (long long)prog[r].predCol.size();
+    parallel_for(threads_, n, [&](int r) {
+        const ColumnProgram& C = prog[r];
+        const PoaJob& J = jobs[firstJob[r]];
+        memcpy(hBase_.ptr + J.progOff, C.base.data(), C.base.size());
+        memcpy(hVertex_.ptr + J.progOff, C.vertexOfCol.data(), C.vertexOfCol.size() * sizeof(int));
+        for (size_t c = 0; c < C.predStart.size(); ++c)
+            hPredStart_.ptr[J.predStartOff + c] = (int)(C.predStart[c] + predColOff[r]);
+        if (!C.predCol.empty())
+            memcpy(hPredCol_.ptr + predColOff[r], C.predCol.data(), C.predCol.size() * sizeof(int));
+        if (!C.exitPredCol.empty())
+            memcpy(hExit_.ptr + J.exitOff, C.exitPredCol.data(), C.exitPredCol.size() * sizeof(int));
+        for (int o = 0; o < (reqs[r].orient ? 2 : 1); ++o) {
+            const PoaJob& Jo = jobs[firstJob[r] + o];
+            const std::string& s = o ? rcRead[r] : reqs[r].read;
+            uint8_t* rb = hRowBase_.ptr + Jo.readOff;
+            rb[0] = 0;
+            memcpy(rb + 1, s.data(), s.size());
+            memset(rb + 1 + s.size(), 0, Jo.colStride + 16 - 1 - s.size());
+        }
+    });
+    auto upload = [&](auto& d, const auto& h, long long count) {
+        d.reserve(std::max(1LL, count), false);
+        if (count > 0)
+            check(hipMemcpyAsync(d.ptr, h.ptr, count * sizeof(*h.ptr), hipMemcpyHostToDevice, stream_), "upload");
+    };
+    upload(dBase_, hBase_, nBase);
+    upload(dVertexOfCol_, hVertex_, nBase);
+    upload(dPredStart_, hPredStart_, nPredStart);
+    upload(dPredCol_, hPredCol_, nPredCol);
+    upload(dExitPred_, hExit_, nExit);
+    upload(dRowBase_, hRowBase_, nRow);
     const PoaPools pools{dBase_.ptr, dVertexOfCol_.ptr, dPredStart_.ptr, dPredCol_.ptr, dExitPred_.ptr, dRowBase_.ptr};
 
     size_t budget = budget_;
@@ -468,48 +500,47 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
         return ((size_t)J.nCols * J.colStride * (J.wide ? 4 : 2) + 255) / 256 * 256;
     };
 
-    // ---- launch groups: the requests whose jobs fit the score-pool budget together
-    std::vector<int> scoreH(nJobs), exitH(nJobs);
-    std::vector<std::vector<TraceStep>> stepsH(n);
-    std::vector<int> nStepsH(n, 0);
+    // ---- launch groups: consecutive requests whose jobs fit the score-pool budget together
+    std::vector<uint32_t*> stepPtr(n, nullptr);
+    std::vector<TraceHeader> heads(n);
     dScore_.reserve(nJobs, false);
     dExitCol_.reserve(nJobs, false);
-    int j0 = 0;
-    while (j0 < nJobs) {
-        // group [j0, j1): whole requests
+    hScore_.reserve(nJobs);
+    hExitCol_.reserve(nJobs);
+    std::vector<std::vector<uint32_t>> keepSteps;   // a group's steps outlive the pinned buffer's next use
+    int r0 = 0;
+    while (r0 < n) {
         size_t bytes = 0;
-        int j1 = j0;
-        while (j1 < nJobs) {
-            int j2 = j1;
+        int r1 = r0;
+        while (r1 < n) {
             size_t b = 0;
-            while (j2 < nJobs && jobReq[j2] == jobReq[j1]) b += jobBytes(jobs[j2++]);
-            if (j1 > j0 && bytes + b > budget) break;
+            for (int j = firstJob[r1]; j < firstJob[r1 + 1]; ++j) b += jobBytes(jobs[j]);
+            if (r1 > r0 && bytes + b > budget) break;
             bytes += b;
-            j1 = j2;
+            r1++;
         }
-        // order the group's jobs: uint16 first, then int32 (each kernel instantiation gets a range)
+        const int j0 = firstJob[r0], j1 = firstJob[r1], gn = j1 - j0;
+        // launch order: uint16 jobs, then int32 jobs (one range per kernel instantiation)
         std::vector<int> order;
+        order.reserve(gn);
         for (int j = j0; j < j1; ++j)
             if (!jobs[j].wide) order.push_back(j);
         const int nNarrow = (int)order.size();
         for (int j = j0; j < j1; ++j)
             if (jobs[j].wide) order.push_back(j);
-        size_t off16 = 0;
-        for (int k = 0; k < nNarrow; ++k) {
-            jobs[order[k]].scoreOff = (long long)(off16 / 2);
-            off16 += jobBytes(jobs[order[k]]);
-        }
-        size_t off32 = 0;
-        for (int k = nNarrow; k < (int)order.size(); ++k) {
-            jobs[order[k]].scoreOff = (long long)(off32 / 4);
-            off32 += jobBytes(jobs[order[k]]);
+        size_t off16 = 0, off32 = 0;
+        for (int k = 0; k < gn; ++k) {
+            PoaJob& J = jobs[order[k]];
+            size_t& off = k < nNarrow ? off16 : off32;
+            J.scoreOff = (long long)(off / (J.wide ? 4 : 2));
+            off += jobBytes(J);
         }
         dPool_.reserve(off16 + off32 + 256, false);
-        // the group's jobs, in launch order, with their trace step regions
-        std::vector<PoaJob> gj;
-        for (int j : order) gj.push_back(jobs[j]);
-        upload(dJobs_, gj, stream_);
-        const int gn = (int)gj.size();
+        // the group's jobs in launch order: [nJobs, nJobs + gn) of the pinned job array
+        PoaJob* gj = hJobs_.ptr + nJobs;
+        for (int k = 0; k < gn; ++k) gj[k] = jobs[order[k]];
+        dJobs_.reserve(gn, false);
+        check(hipMemcpyAsync(dJobs_.ptr, gj, gn * sizeof(PoaJob), hipMemcpyHostToDevice, stream_), "upload jobs");
         uint16_t* pool16 = reinterpret_cast<uint16_t*>(dPool_.ptr);
         int* pool32 = reinterpret_cast<int*>(dPool_.ptr + off16);
         if (profiling) check(hipEventRecord(ev_[0], stream_), "event");
@@ -521,9 +552,7 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
                                pool32, dScore_.ptr, dExitCol_.ptr);
         check(hipGetLastError(), "k_poa_fill launch");
         if (profiling) check(hipEventRecord(ev_[1], stream_), "event");
-        std::vector<int> gScore(gn), gExit(gn);
-        check(hipMemcpyAsync(gScore.data(), dScore_.ptr, gn * sizeof(int), hipMemcpyDeviceToHost, stream_), "d2h");
-        check(hipMemcpyAsync(gExit.data(), dExitCol_.ptr, gn * sizeof(int), hipMemcpyDeviceToHost, stream_), "d2h");
+        check(hipMemcpyAsync(hScore_.ptr, dScore_.ptr, gn * sizeof(int), hipMemcpyDeviceToHost, stream_), "d2h");
         check(hipStreamSynchronize(stream_), "k_poa_fill");
         if (profiling) {
             float ms = 0.f;
@@ -533,78 +562,74 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
         stats.launches += (nNarrow > 0) + (gn > nNarrow);
         for (int k = 0; k < gn; ++k) {
             const PoaJob& J = gj[k];
-            scoreH[order[k]] = gScore[k];
-            exitH[order[k]] = gExit[k];
+            (*out)[jobReq[order[k]]].score[jobOri[order[k]]] = (float)hScore_.ptr[k];
             stats.alignments++;
             stats.cells += (long long)J.nCols * (J.I + 1);
             stats.bytes += (double)J.nCols * (J.I + 1) * (J.wide ? 4 : 2);
         }
-        // SparsePoa's choice (src/SparsePoa.cpp:112-131) / AddRead's unconditional commit
-        for (int k = 0; k < gn; ++k) {
-            const int j = order[k], r = jobReq[j];
+        // SparsePoa's choice (src/SparsePoa.cpp:112-131) / AddRead's unconditional commit (PoaGraphImpl.cpp:354-369)
+        for (int r = r0; r < r1; ++r) {
             AlignResult& R = (*out)[r];
-            R.score[jobOri[j]] = (float)scoreH[j];
-        }
-        for (int k = 0; k < gn; ++k) {
-            const int j = order[k], r = jobReq[j];
-            AlignResult& R = (*out)[r];
-            if (jobOri[j] != 0) continue;
             if (!reqs[r].orient) R.chosen = 0;
             else if (R.score[0] >= R.score[1] && R.score[0] >= reqs[r].minScore) R.chosen = 0;
             else if (R.score[1] >= R.score[0] && R.score[1] >= reqs[r].minScore) R.chosen = 1;
         }
-        long long stepTotal = 0;
+        // traceback of the committed jobs (positions in the group's launch order), uint16 first
         std::vector<int> traceNarrow, traceWide;
-        for (int k = 0; k < gn; ++k) {
-            const int j = order[k], r = jobReq[j];
-            if ((*out)[r].chosen != jobOri[j]) continue;
-            (gj[k].wide ? traceWide : traceNarrow).push_back(k);
-        }
-        std::vector<int> traceJobs(traceNarrow);
-        traceJobs.insert(traceJobs.end(), traceWide.begin(), traceWide.end());
-        std::vector<long long> stepOff(traceJobs.size());
-        for (size_t t = 0; t < traceJobs.size(); ++t) {
-            PoaJob& J = gj[traceJobs[t]];
-            J.stepOff = stepTotal;
-            stepOff[t] = stepTotal;
-            stepTotal += J.I + J.nCols + 2;
-        }
-        if (!traceJobs.empty()) {
-            upload(dJobs_, gj, stream_);
-            upload(dTraceJobs_, traceJobs, stream_);
+        for (int k = 0; k < gn; ++k)
+            if ((*out)[jobReq[order[k]]].chosen == jobOri[order[k]]) (k < nNarrow ? traceNarrow : traceWide).push_back(k);
+        const int tn = (int)traceNarrow.size(), tw = (int)traceWide.size(), nt = tn + tw;
+        if (nt > 0) {
+            hTraceJobs_.reserve(nt);
+            long long stepTotal = 0;
+            std::vector<long long> stepOff(nt);
+            for (int t = 0; t < nt; ++t) {
+                const int k = t < tn ? traceNarrow[t] : traceWide[t - tn];
+                hTraceJobs_.ptr[t] = k;
+                gj[k].stepOff = stepTotal;
+                stepOff[t] = stepTotal;
+                stepTotal += gj[k].I + gj[k].nCols + 2;
+            }
+            check(hipMemcpyAsync(dJobs_.ptr, gj, gn * sizeof(PoaJob), hipMemcpyHostToDevice, stream_), "upload jobs");
+            dTraceJobs_.reserve(nt, false);
+            check(hipMemcpyAsync(dTraceJobs_.ptr, hTraceJobs_.ptr, nt * sizeof(int), hipMemcpyHostToDevice, stream_),
+                  "upload");
             dSteps_.reserve(stepTotal, false);
-            dNSteps_.reserve(traceJobs.size(), false);
-            // exit columns were written at the jobs' group positions
+            dHeads_.reserve(nt, false);
             if (profiling) check(hipEventRecord(ev_[2], stream_), "event");
-            const int tn = (int)traceNarrow.size(), tw = (int)traceWide.size();
             if (tn > 0)
                 hipLaunchKernelGGL(k_poa_trace<uint16_t>, dim3(tn), dim3(64), 0, stream_, dJobs_.ptr, dTraceJobs_.ptr, 0,
-                                   pools, pool16, dExitCol_.ptr, dSteps_.ptr, dNSteps_.ptr);
+                                   pools, pool16, dExitCol_.ptr, dSteps_.ptr, dHeads_.ptr);
             if (tw > 0)
                 hipLaunchKernelGGL(k_poa_trace<int>, dim3(tw), dim3(64), 0, stream_, dJobs_.ptr, dTraceJobs_.ptr, tn,
-                                   pools, pool32, dExitCol_.ptr, dSteps_.ptr, dNSteps_.ptr);
+                                   pools, pool32, dExitCol_.ptr, dSteps_.ptr, dHeads_.ptr);
             check(hipGetLastError(), "k_poa_trace launch");
             if (profiling) check(hipEventRecord(ev_[3], stream_), "event");
-            std::vector<int> ns(traceJobs.size());
-            std::vector<TraceStep> st(stepTotal);
-            check(hipMemcpyAsync(ns.data(), dNSteps_.ptr, ns.size() * sizeof(int), hipMemcpyDeviceToHost, stream_), "d2h");
-            check(hipMemcpyAsync(st.data(), dSteps_.ptr, st.size() * sizeof(TraceStep), hipMemcpyDeviceToHost, stream_),
+            hSteps_.reserve(stepTotal);
+            hHeads_.reserve(nt);
+            check(hipMemcpyAsync(hHeads_.ptr, dHeads_.ptr, nt * sizeof(TraceHeader), hipMemcpyDeviceToHost, stream_),
                   "d2h");
+            check(hipMemcpyAsync(hSteps_.ptr, dSteps_.ptr, stepTotal * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                 stream_), "d2h");
             check(hipStreamSynchronize(stream_), "k_poa_trace");
             if (profiling) {
                 float ms = 0.f;
                 check(hipEventElapsedTime(&ms, ev_[2], ev_[3]), "event");
                 stats.traceMs += ms;
             }
-            for (size_t t = 0; t < traceJobs.size(); ++t) {
-                const int r = jobReq[order[traceJobs[t]]];
-                if (ns[t] < 1) throw DeviceError("POA traceback did not reach the start vertex");
-                stepsH[r].assign(st.begin() + stepOff[t], st.begin() + stepOff[t] + ns[t]);
-                nStepsH[r] = ns[t];
-                stats.traceSteps += ns[t];
+            const bool last = r1 == n;
+            if (!last) keepSteps.emplace_back(hSteps_.ptr, hSteps_.ptr + stepTotal);
+            const uint32_t* base = last ? hSteps_.ptr : keepSteps.back().data();
+            for (int t = 0; t < nt; ++t) {
+                const int k = t < tn ? traceNarrow[t] : traceWide[t - tn];
+                const int r = jobReq[order[k]];
+                if (hHeads_.ptr[t].nSteps < 1) throw DeviceError("POA traceback did not reach the start vertex");
+                heads[r] = hHeads_.ptr[t];
+                stepPtr[r] = const_cast<uint32_t*>(base) + stepOff[t];
+                stats.traceSteps += heads[r].nSteps;
             }
         }
-        j0 = j1;
+        r0 = r1;
     }
 
     // ---- host: thread the committed reads into their graphs (CommitAdd)
@@ -612,7 +637,7 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
         AlignResult& R = (*out)[r];
         if (R.chosen < 0) return;
         const std::string& s = R.chosen ? rcRead[r] : reqs[r].read;
-        reqs[r].graph->ThreadTraceback(s, reqs[r].mode, stepsH[r].data(), nStepsH[r], &R.path);
+        reqs[r].graph->ThreadTraceback(s, reqs[r].mode, stepPtr[r], heads[r], &R.path);
     });
 }
 

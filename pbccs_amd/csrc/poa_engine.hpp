@@ -30,8 +30,36 @@ struct PoaJob {
     int exitOff, nExit;   // into exitPred[]              ($'s predecessor columns, GLOBAL end move)
     long long readOff;    // into rowBase[]: byte i = read[i - 1] for rows 1..I, colStride bytes
     long long stepOff;    // into the traceback step pool (I + nCols + 2 steps)
+    int traceSlot;        // this job's TraceHeader (committed jobs), else -1
     int wide;             // score matrix stored as int32 (else uint16)
-    int pad;
+};
+
+// Page-locked host staging (hipHostMalloc): the per-round program uploads and traceback downloads run at
+// DMA speed, and the buffers persist across rounds.
+template <class T>
+struct HostVec {
+    T* ptr = nullptr;
+    size_t cap = 0;
+    void reserve(size_t n)
+    {
+        if (n <= cap) return;
+        const size_t nc = std::max(n, cap + cap / 2 + 1024);
+        T* p = nullptr;
+        if (hipHostMalloc((void**)&p, nc * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            throw DeviceOom("hipHostMalloc failed: " + std::to_string((nc * sizeof(T)) >> 20) + " MB");
+        }
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = p;
+        cap = nc;
+    }
+    HostVec() = default;
+    HostVec(const HostVec&) = delete;
+    HostVec& operator=(const HostVec&) = delete;
+    ~HostVec()
+    {
+        if (ptr) (void)hipHostFree(ptr);
+    }
 };
 
 struct PoaPools {
@@ -86,9 +114,15 @@ private:
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
     DevVec<uint8_t> dBase_, dRowBase_, dPool_;
-    DevVec<int> dVertexOfCol_, dPredStart_, dPredCol_, dExitPred_, dScore_, dExitCol_, dNSteps_, dTraceJobs_;
+    DevVec<int> dVertexOfCol_, dPredStart_, dPredCol_, dExitPred_, dScore_, dExitCol_, dTraceJobs_;
     DevVec<PoaJob> dJobs_;
-    DevVec<TraceStep> dSteps_;
+    DevVec<uint32_t> dSteps_;
+    DevVec<TraceHeader> dHeads_;
+    HostVec<uint8_t> hBase_, hRowBase_;
+    HostVec<int> hVertex_, hPredStart_, hPredCol_, hExit_, hScore_, hExitCol_, hTraceJobs_;
+    HostVec<PoaJob> hJobs_;
+    HostVec<uint32_t> hSteps_;
+    HostVec<TraceHeader> hHeads_;
 };
 
 // SparsePoa state of one ZMW (src/SparsePoa.cpp:60-201).

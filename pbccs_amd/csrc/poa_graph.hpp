@@ -15,6 +15,8 @@
 //   * tracebackAndThread / threadFirstRead / tagSpan / consensusPath as in PoaGraphTraversals.cpp:62-369.
 #pragma once
 
+#include <hip/hip_runtime.h>
+
 #include <algorithm>
 #include <cfloat>
 #include <climits>
@@ -33,12 +35,17 @@ enum Move : uint8_t { kInvalid = 0, kStart, kEnd, kMatch, kMismatch, kDelete, kE
 
 constexpr int kEnter = 0, kExit = 1;
 
-// One traceback step as the device reports it: the cell (vertex u, row i) and the move that reached it.
-// For the first step (u = $) `aux` is the row the local End move came from (ArgMax of the column it
-// names); it is unused otherwise.
-struct TraceStep {
-    int32_t u, prev, i, aux;
-    int32_t move;
+// Traceback steps as the device reports them, one uint32 per visited cell: the vertex (low 28 bits) and
+// the move that reached the cell (top 4 bits).  Step 0 is the End move into $; the walk's header gives
+// the row that move comes from (LOCAL: ArgMax of the column it names) and that column's vertex.
+constexpr uint32_t kStepVertexMask = 0x0FFFFFFFu;
+__host__ __device__ inline uint32_t pack_step(int vertex, int move) { return ((uint32_t)move << 28) | (uint32_t)vertex; }
+
+struct TraceHeader {
+    int32_t nSteps;      // < 0: the walk failed
+    int32_t endRow;      // row of the End move's source cell
+    int32_t endVertex;   // vertex of the End move's source cell (tagSpan's end)
+    int32_t pad;
 };
 
 // The per-read column program (device inputs).  Column 0 is always ^; $ is not a column.
@@ -136,17 +143,16 @@ public:
 
     // tracebackAndThread (PoaGraphTraversals.cpp:227-369), replaying the device's walk: steps[0] is the
     // End move into $, then one step per visited cell until (^, 0).
-    void ThreadTraceback(const std::string& seq, AlignMode mode, const TraceStep* steps, int nSteps,
+    void ThreadTraceback(const std::string& seq, AlignMode mode, const uint32_t* steps, const TraceHeader& h,
                          std::vector<int>* path)
     {
         const int I = (int)seq.size();
         int i = I, v = -1, fork = -1;
-        const int endSpan = steps[0].prev;
+        const int endSpan = h.endVertex;
         if (path) path->assign(I, -1);
-        for (int s = 0; s < nSteps; ++s) {
-            const TraceStep& st = steps[s];
-            const int u = st.u;
-            switch (st.move) {
+        for (int s = 0; s < h.nSteps; ++s) {
+            const int u = (int)(steps[s] & kStepVertexMask);
+            switch (steps[s] >> 28) {
                 case kStart:
                     if (fork < 0) fork = v;
                     while (i > 0) fork = Fork(seq, --i, fork, path);
@@ -154,7 +160,7 @@ public:
                 case kEnd:
                     fork = kExit;
                     if (mode == kLocal)
-                        while (i > st.aux) fork = Fork(seq, --i, fork, path);
+                        while (i > h.endRow) fork = Fork(seq, --i, fork, path);
                     break;
                 case kMatch:
                     if (path) (*path)[i - 1] = u;

@@ -130,6 +130,7 @@ bool QuiverBatch::AddRead(int zi, const QReadFeatures& f, int strand, int ts, in
     r.strand = strand;
     r.ts = ts;
     r.te = te;
+    r.len = (int)I;
     r.seqOff = (long long)hSeq_.size();
     hSeq_.insert(hSeq_.end(), f.seq.begin(), f.seq.end());
     for (const std::vector<float>* t : {&f.ins, &f.subs, &f.del, &f.tag, &f.merge})
@@ -476,6 +477,43 @@ bool QuiverBatch::Refine(int zi, const RefineOptions& ro, long long* nTested, lo
         centers.clear();
         for (const ScoredMut& s : fav) centers.push_back(mut_pos(s.code));
         if (!ApplyMutations(zi, muts)) return false;
+    }
+    return true;
+}
+
+bool QuiverBatch::Alignment(int r, std::string* target, std::string* query)
+{
+    const HRead& h = reads_.at(r);
+    if (!h.hasScorer || configs_[h.config].sumProduct) return false;   // Viterbi only (ShouldNotReachHere)
+    Upload();
+    const int I = h.len, J = h.te - h.ts;
+    put(dList_, std::vector<int>{r}, stream_);
+    put(dMoveOff_, std::vector<long long>{0}, stream_);
+    dMoves_.reserve((size_t)I + J + 1, false);
+    dOff_.reserve(1, false);
+    launch_qalign(View(), dList_.ptr, 1, dMoveOff_.ptr, dMoves_.ptr, dOff_.ptr, stream_);
+    QHIP(hipGetLastError());
+    int n = 0;
+    QHIP(hipMemcpyAsync(&n, dOff_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    QHIP(hipStreamSynchronize(stream_));
+    if (n < 0) throw DeviceError("quiver alignment: no valid move (alpha not filled?)");
+    std::vector<unsigned char> mv(n);
+    if (n) QHIP(hipMemcpy(mv.data(), dMoves_.ptr, n, hipMemcpyDeviceToHost));
+    // replay from the start (the moves are stored from the end) into the gapped strings (:228-262)
+    const std::string& tpl0 = zmws_[h.zmw].tpl;
+    const int L = (int)tpl0.size();
+    const std::string tpl = h.strand == 0 ? tpl0.substr(h.ts, J) : reverse_complement(tpl0).substr(L - h.te, J);
+    const char* seq = hSeq_.data() + h.seqOff;
+    target->clear();
+    query->clear();
+    int i = 0, j = 0;
+    for (int k = n - 1; k >= 0; --k) {
+        switch (mv[k]) {
+            case 1: *target += tpl[j]; *query += seq[i]; i++; j++; break;
+            case 2: *target += '-'; *query += seq[i]; i++; break;
+            case 4: *target += tpl[j]; *query += '-'; j++; break;
+            default: *target += tpl[j]; *target += tpl[j + 1]; *query += '-'; *query += seq[i]; i++; j += 2; break;
+        }
     }
     return true;
 }

@@ -46,6 +46,9 @@ public:
     bool ApplyMutations(int z, const std::vector<Mutation>& muts);
     bool Refine(int z, const RefineOptions& ro, long long* nTested, long long* nApplied, bool* converged);
     std::vector<int> QVs(int z);
+    // RecursorBase::Alignment (detail/RecursorBase.cpp:124-264) of read r against its template window,
+    // from the read's alpha band (Viterbi configs only): the gapped target and query strings.
+    bool Alignment(int r, std::string* target, std::string* query);
 
     const std::string& Template(int z) const { return zmws_[z].tpl; }
     int NumReads(int z) const { return (int)zmws_[z].reads.size(); }
@@ -66,7 +69,7 @@ private:
         std::vector<int> reads;
     };
     struct HRead {
-        int zmw = 0, config = 0, strand = 0, ts = 0, te = 0;
+        int zmw = 0, config = 0, strand = 0, ts = 0, te = 0, len = 0;
         bool active = false, hasScorer = false;
         long long seqOff = 0;
         long long colBase = 0;
@@ -103,6 +106,8 @@ private:
     DevVec<QAlloc> dAlloc_;
     DevVec<float> dVal_;
     DevVec<unsigned long long> dScratchTop_;
+    DevVec<long long> dMoveOff_;
+    DevVec<unsigned char> dMoves_;
 };
 
 }  // namespace quiver

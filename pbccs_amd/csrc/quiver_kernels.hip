@@ -567,6 +567,59 @@ __global__ void __launch_bounds__(64) k_qscore(QBatch B, QScoreWork W)
     W.delta[t] = W.raw ? score : score - B.rScore[r];
 }
 
+// ---- k_qalign: RecursorBase::Alignment (detail/RecursorBase.cpp:118-264) -------------------------------
+// The Viterbi path through a read's final alpha band, one lane per read, walking back from (I, J): moves
+// tried in the order Incorporate, Delete, Extra, Merge, strict '>' against -FLT_MAX, the move score added
+// to the predecessor cell in float.  The scorer's evaluator pins both ends, so no delete is free.  Writes
+// the moves from the end (1 INCORPORATE, 4 DELETE, 2 EXTRA, 8 MERGE); nMoves < 0 when no move is valid
+// (the reference asserts).
+__global__ void __launch_bounds__(64) k_qalign(QBatch B, const int* __restrict__ reads, int n,
+                                               const long long* __restrict__ moveOff, unsigned char* __restrict__ moves,
+                                               int* __restrict__ nMoves)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int r = reads[t];
+    const ReadView v = read_view(B, r);
+    const QEval& e = v.ev;
+    const QBand a = arena(v, B.rCurA[r]);
+    const bool merge = (e.p->moves & kMerge) != 0;
+    unsigned char* out = moves + moveOff[t];
+    int i = e.I(), j = e.J(), k = 0;
+    while (i > 0 || j > 0) {
+        int best = 0;
+        float bestScore = kNegInf;
+        if (i > 0 && j > 0) {
+            const float s = a.Get(i - 1, j - 1) + e.Inc(i - 1, j - 1);
+            if (s > bestScore) { best = 1; bestScore = s; }
+        }
+        if (j > 0) {
+            const float s = a.Get(i, j - 1) + e.Del(i, j - 1);
+            if (s > bestScore) { best = 4; bestScore = s; }
+        }
+        if (i > 0) {
+            const float s = a.Get(i - 1, j) + e.Extra(i - 1, j);
+            if (s > bestScore) { best = 2; bestScore = s; }
+        }
+        if (merge && i > 0 && j > 1) {
+            const float s = a.Get(i - 1, j - 2) + e.Merge(i - 1, j - 2);
+            if (s > bestScore) { best = 8; bestScore = s; }
+        }
+        if (best == 0) { k = -1; break; }
+        out[k++] = (unsigned char)best;
+        i -= (best == 4) ? 0 : 1;
+        j -= (best == 2) ? 0 : (best == 8 ? 2 : 1);
+    }
+    nMoves[t] = k;
+}
+
+void launch_qalign(const QBatch& B, const int* reads, int n, const long long* moveOff, unsigned char* moves,
+                   int* nMoves, hipStream_t s)
+{
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_qalign, dim3((n + 63) / 64), dim3(64), 0, s, B, reads, n, moveOff, moves, nMoves);
+}
+
 void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s)
 {
     if (n <= 0) return;

@@ -64,6 +64,9 @@ struct QScoreWork {
 
 void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s);
 void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s);
+// RecursorBase::Alignment per listed read: moves (from the end) at moveOff[t], nMoves[t] of them
+void launch_qalign(const QBatch& B, const int* reads, int n, const long long* moveOff, unsigned char* moves,
+                   int* nMoves, hipStream_t s);
 
 }  // namespace quiver
 }  // namespace pbccs

@@ -160,6 +160,7 @@ SIGNATURES = {
     "pbccs_quiver_scorer_baseline_scores": (I, [P, PF, I, PI]),
     "pbccs_quiver_scorer_num_flipflops": (I, [P, PI]),
     "pbccs_quiver_scorer_allocated_entries": (I, [P, I, PLL, PLL]),
+    "pbccs_quiver_scorer_alignment": (I, [P, I, ctypes.c_char_p, ctypes.c_char_p, I, PI]),
     "pbccs_quiver_refine_consensus": (I, [P, ctypes.POINTER(CRefineOptions), PLL, PLL, PI]),
     "pbccs_quiver_consensus_qvs": (I, [P, PI, I, PI]),
     # POA draft

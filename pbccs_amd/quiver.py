@@ -197,6 +197,21 @@ class QuiverMultiReadMutationScorer:
         _lib_mod.check(load().pbccs_quiver_scorer_num_flipflops(self._h, out))
         return list(out[: self.NumReads()])
 
+    def Alignment(self, i):
+        """RecursorBase::Alignment of read i (Viterbi): (Target(), Query()) of the PairwiseAlignment."""
+        cap = 2 * len(self.Template()) + 4096
+        for _ in range(2):
+            t = ctypes.create_string_buffer(cap)
+            q = ctypes.create_string_buffer(cap)
+            n = ctypes.c_int()
+            rc = load().pbccs_quiver_scorer_alignment(self._h, i, t, q, cap, ctypes.byref(n))
+            if rc == -5 and n.value > cap:
+                cap = n.value
+                continue
+            _lib_mod.check(rc)
+            return t.raw[:n.value].decode(), q.raw[:n.value].decode()
+        raise _lib_mod.PbccsError(-5, "buffer too small")
+
     def AllocatedEntries(self, i):
         a, b = ctypes.c_longlong(), ctypes.c_longlong()
         _lib_mod.check(load().pbccs_quiver_scorer_allocated_entries(self._h, i, ctypes.byref(a), ctypes.byref(b)))

@@ -135,12 +135,16 @@ def make_quiver_kats():
         return {"kind": "read_score_mutation", "mut": [t, pos, base], "expected": exp}
 
     kats = [
+        # + RecursorBase::Alignment's Target() / Query() (:117-119, :147-149, :172-174)
         case("SmallMatch", "src/Tests/TestRecursors.cpp:99-126", "GATG", [rd("GATG")],
-             [{"kind": "baseline", "expected": 0.0}], moves=7, score_diff=nb),
+             [{"kind": "baseline", "expected": 0.0},
+              {"kind": "alignment", "read": 0, "target": "GATG", "query": "GATG"}], moves=7, score_diff=nb),
         case("SmallMismatch", "src/Tests/TestRecursors.cpp:128-152", "GATG", [rd("GATC")],
-             [{"kind": "baseline", "expected": -10.0}], moves=7, score_diff=nb),
+             [{"kind": "baseline", "expected": -10.0},
+              {"kind": "alignment", "read": 0, "target": "GATG", "query": "GATC"}], moves=7, score_diff=nb),
         case("SmallMerge", "src/Tests/TestRecursors.cpp:154-182", "GATT", [rd("GAT")],
-             [{"kind": "baseline", "expected": -2.0}], moves=15, score_diff=nb),
+             [{"kind": "baseline", "expected": -2.0},
+              {"kind": "alignment", "read": 0, "target": "GATT", "query": "GA-T"}], moves=15, score_diff=nb),
         case("MediumSized", "src/Tests/TestRecursors.cpp:184-204 (FillAlphaBeta)", medium_tpl, [rd(medium_read)],
              [{"kind": "baseline", "expected": -80.0}], moves=7, score_diff=std),
         case("MutationScorer.Basic", "src/Tests/TestMutationScorer.cpp:100-124", "GATTACA", [rd("GATTACA")],

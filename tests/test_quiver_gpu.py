@@ -49,6 +49,9 @@ class GpuQuiver:
     def template(self):
         return self.s.Template()
 
+    def alignment(self, r):
+        return self.s.Alignment(r)
+
 
 @pytest.mark.parametrize("idx", range(len(KATS["kats"])))
 def test_quiver_kats_on_gpu(idx):
@@ -131,3 +134,33 @@ def test_quiver_add_threshold_memory_gate():
         info = o.read_info(k)
         if info["active"]:
             assert g.s.AllocatedEntries(k) == info["allocated"]
+
+
+@pytest.mark.parametrize("seed,length,passes,moves", [(111, 60, 3, 15), (112, 300, 4, 15), (113, 500, 3, 7)])
+def test_quiver_alignment_matches_oracle(seed, length, passes, moves):
+    """RecursorFuzzTest.Alignment (TestRecursors.cpp:351-366) against the restatement: the Viterbi traceback
+    of every read (both strands, banded, merges on/off) is the same gapped Target / Query pair."""
+    tpl, reads = _zmw(seed, length, passes)
+    g = GpuQuiver(tpl, PARAMS2, moves=moves)
+    o = O.QuiverScorer(tpl, PARAMS2, moves=moves)
+    for k, r in enumerate(reads):
+        a = g.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"])
+        b = o.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"])
+        assert bool(a) == bool(b)
+        if a:
+            t, q = g.alignment(k)
+            assert (t, q) == o.alignment(k)
+            L = len(tpl)
+            window = tpl[r["ts"]:r["te"]] if r["strand"] == 0 else \
+                tpl[::-1].translate(str.maketrans("ACGT", "TGCA"))[L - r["te"]:L - r["ts"]]
+            assert len(t) == len(q) and t.replace("-", "") == window and q.replace("-", "") == r["seq"]
+
+
+def test_quiver_alignment_sum_product_refused():
+    """Alignment is Viterbi-only (RecursorBase.cpp:128-131 ShouldNotReachHere): the ABI refuses it."""
+    from pbccs_amd.lib import PbccsError
+    tpl, reads = _zmw(114, 60, 2)
+    g = GpuQuiver(tpl, PARAMS2, sum_product=True)
+    g.add_read(reads[0]["seq"], reads[0]["strand"], reads[0]["ts"], reads[0]["te"], reads[0]["features"])
+    with pytest.raises(PbccsError):
+        g.alignment(0)

@@ -37,6 +37,8 @@ def run_kat(make_scorer, k, params):
         elif kind == "add_read":
             r = c["read"]
             s.add_read(r["seq"], r["strand"], r["ts"], r["te"] if r["te"] is not None else len(s.template()))
+        elif kind == "alignment":
+            assert s.alignment(c["read"]) == (c["target"], c["query"]), (k["name"], s.alignment(c["read"]))
         elif kind == "apply":
             s.apply([tuple(m) for m in c["muts"]])
             assert s.template() == c["template"]
