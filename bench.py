@@ -355,7 +355,8 @@ def poa_stage(args, rank, world, eng, barrier, sync, seed0):
     def subreads(n, seed):
         return [[r["seq"] for r in z["reads"]] for z in synth.make_zmws(n, args.length, args.passes, seed=seed)]
 
-    poa.poa_batch(subreads(min(args.zmws_per_step, 256), seed0 + 1000), engine=eng)
+    for w in range(args.warmup):   # full-size steps: the score pool and staging buffers reach their high-water
+        poa.poa_batch(subreads(args.zmws_per_step, seed0 + 1000 + w), engine=eng)
     steps_in = [subreads(args.zmws_per_step, seed0 + k) for k in range(args.steps)]
     poa.poa_stats(eng, reset=True)
     barrier()
@@ -389,6 +390,8 @@ def poa_stage(args, rank, world, eng, barrier, sync, seed0):
         "poa": {"alignments": st["alignments"], "gcells": round(st["cells"] / 1e9, 3),
                 "fill_ms": round(st["fill_ms"], 2), "trace_ms": round(st["trace_ms"], 2),
                 "trace_steps": st["trace_steps"],
+                "host_ms": {k: round(st[k], 1) for k in ("prog_ms", "device_ms", "thread_ms", "consensus_ms",
+                                                             "total_ms")},
                 "draft_len_mean": round(sum(len(r["consensus"]) for b in res for r in b) / max(1, total // world), 1)},
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:

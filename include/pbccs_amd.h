@@ -361,6 +361,7 @@ int pbccs_poa_consensus(pbccs_engine* eng, const char* const* reads, const int* 
 typedef struct {
     long long alignments, cells, launches, trace_steps;
     double fill_ms, trace_ms, bytes;
+    double prog_ms, device_ms, thread_ms, consensus_ms, total_ms;   /* host wall time of each phase */
 } pbccs_poa_stats;
 int pbccs_poa_stats_get(pbccs_engine* eng, pbccs_poa_stats* out, int reset);
 

@@ -42,13 +42,24 @@ struct pbccs_engine {
     std::mutex statsMu;        // counters / stats are merged from the slots' worker threads
     long long oomRetries = 0;   // device batches rerun after PBCCS_EOOM
     std::vector<std::unique_ptr<Workspace>> slots;
-    std::unique_ptr<poa::PoaRunner> poa;   // the POA draft step's device state (made on first use)
+    // the POA draft step's device state (made on first use): kPoaSlices runners, one per concurrent slice
+    static constexpr int kPoaSlices = 2;
+    std::vector<std::unique_ptr<poa::PoaRunner>> poa;
     std::mutex poaMu;
-    poa::PoaRunner& Poa()
+    poa::PoaRunner& Poa(int k = 0)
     {
-        if (!poa) poa.reset(new poa::PoaRunner(device));
-        poa->profiling = profiling;
-        return *poa;
+        if (poa.empty()) {
+            const int hw = std::max(2, std::min(16, (int)std::thread::hardware_concurrency()));
+            for (int i = 0; i < kPoaSlices; ++i) poa.emplace_back(new poa::PoaRunner(device, hw / kPoaSlices));
+        }
+        poa[k]->profiling = profiling;
+        return *poa[k];
+    }
+    std::vector<poa::PoaRunner*> PoaRunners()
+    {
+        std::vector<poa::PoaRunner*> v;
+        for (int k = 0; k < kPoaSlices; ++k) v.push_back(&Poa(k));
+        return v;
     }
     Workspace* Slot(int s)
     {
@@ -1280,7 +1291,7 @@ int pbccs_poa_batch(pbccs_engine* eng, const pbccs_poa_input* in, int n, long lo
         std::vector<std::vector<char>> rc;
         {
             std::lock_guard<std::mutex> lk(eng->poaMu);
-            poa::PoaBatch(eng->Poa(), reads, max_coverage, min_coverage, &css, &keys, &rc, &ext);
+            poa::PoaBatch(eng->PoaRunners(), reads, max_coverage, min_coverage, &css, &keys, &rc, &ext);
         }
         bool range = false;
         for (int z = 0; z < n; ++z) {
@@ -1405,9 +1416,25 @@ int pbccs_poa_stats_get(pbccs_engine* eng, pbccs_poa_stats* out, int reset)
     if (!eng || !out) return fail(PBCCS_EINVAL, "bad argument");
     return guarded([&] {
         std::lock_guard<std::mutex> lk(eng->poaMu);
-        const poa::PoaStats& s = eng->Poa().stats;
-        *out = pbccs_poa_stats{s.alignments, s.cells, s.launches, s.traceSteps, s.fillMs, s.traceMs, s.bytes};
-        if (reset) eng->Poa().stats = poa::PoaStats();
+        poa::PoaStats s;
+        for (poa::PoaRunner* r : eng->PoaRunners()) {   // counts add up; wall times are the slices' maxima
+            const poa::PoaStats& x = r->stats;
+            s.alignments += x.alignments;
+            s.cells += x.cells;
+            s.launches += x.launches;
+            s.traceSteps += x.traceSteps;
+            s.fillMs += x.fillMs;
+            s.traceMs += x.traceMs;
+            s.bytes += x.bytes;
+            s.progMs = std::max(s.progMs, x.progMs);
+            s.deviceMs = std::max(s.deviceMs, x.deviceMs);
+            s.threadMs = std::max(s.threadMs, x.threadMs);
+            s.consensusMs = std::max(s.consensusMs, x.consensusMs);
+            s.totalMs = std::max(s.totalMs, x.totalMs);
+            if (reset) r->stats = poa::PoaStats();
+        }
+        *out = pbccs_poa_stats{s.alignments, s.cells,  s.launches, s.traceSteps, s.fillMs,     s.traceMs,
+                               s.bytes,      s.progMs, s.deviceMs, s.threadMs,  s.consensusMs, s.totalMs};
         return PBCCS_OK;
     });
 }

@@ -25,8 +25,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <climits>
 #include <cstring>
+#include <memory>
 #include <thread>
 
 namespace pbccs {
@@ -337,6 +339,11 @@ std::string reverse_complement(const std::string& s)
     return r;
 }
 
+double ms_since(std::chrono::steady_clock::time_point t0)
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 template <class F>
 void parallel_for(int threads, int n, F&& f)
 {
@@ -389,6 +396,7 @@ PoaRunner::PoaRunner(int device, int hostThreads) : device_(device)
     check(hipSetDevice(device_), "hipSetDevice");
     check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
     for (auto& e : ev_) check(hipEventCreate(&e), "hipEventCreate");
+    dPool_.allowVmm = true;
 }
 
 PoaRunner::~PoaRunner()
@@ -408,6 +416,7 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
     if (n == 0) return;
 
     // ---- host: column programs, then the job layout (sizes -> prefix offsets -> parallel fill)
+    auto t0 = std::chrono::steady_clock::now();
     std::vector<ColumnProgram> prog(n);
     std::vector<std::string> rcRead(n);
     parallel_for(threads_, n, [&](int r) {
@@ -481,6 +490,8 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
         if (count > 0)
             check(hipMemcpyAsync(d.ptr, h.ptr, count * sizeof(*h.ptr), hipMemcpyHostToDevice, stream_), "upload");
     };
+    stats.progMs += ms_since(t0);
+    t0 = std::chrono::steady_clock::now();
     upload(dBase_, hBase_, nBase);
     upload(dVertexOfCol_, hVertex_, nBase);
     upload(dPredStart_, hPredStart_, nPredStart);
@@ -493,7 +504,7 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
     if (budget == 0) {
         size_t fr = 0, tot = 0;
         check(hipMemGetInfo(&fr, &tot), "hipMemGetInfo");
-        budget = std::min<size_t>((size_t)(0.5 * (double)fr), 48ull << 30) + dPool_.cap;
+        budget = std::min<size_t>((size_t)(0.6 * (double)fr) + dPool_.mapped_bytes(), 96ull << 30);
         budget = std::max<size_t>(budget, 64ull << 20);
     }
     auto jobBytes = [&](const PoaJob& J) {
@@ -535,14 +546,14 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
             J.scoreOff = (long long)(off / (J.wide ? 4 : 2));
             off += jobBytes(J);
         }
-        dPool_.reserve(off16 + off32 + 256, false);
+        dPool_.reserve((off16 + off32 + 256 + 7) / 8, false);
         // the group's jobs in launch order: [nJobs, nJobs + gn) of the pinned job array
         PoaJob* gj = hJobs_.ptr + nJobs;
         for (int k = 0; k < gn; ++k) gj[k] = jobs[order[k]];
         dJobs_.reserve(gn, false);
         check(hipMemcpyAsync(dJobs_.ptr, gj, gn * sizeof(PoaJob), hipMemcpyHostToDevice, stream_), "upload jobs");
         uint16_t* pool16 = reinterpret_cast<uint16_t*>(dPool_.ptr);
-        int* pool32 = reinterpret_cast<int*>(dPool_.ptr + off16);
+        int* pool32 = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(dPool_.ptr) + off16);
         if (profiling) check(hipEventRecord(ev_[0], stream_), "event");
         if (nNarrow > 0)
             hipLaunchKernelGGL(k_poa_fill<uint16_t>, dim3(nNarrow), dim3(64), 0, stream_, dJobs_.ptr, 0, pools, pool16,
@@ -632,13 +643,16 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
         r0 = r1;
     }
 
+    stats.deviceMs += ms_since(t0);
     // ---- host: thread the committed reads into their graphs (CommitAdd)
+    t0 = std::chrono::steady_clock::now();
     parallel_for(threads_, n, [&](int r) {
         AlignResult& R = (*out)[r];
         if (R.chosen < 0) return;
         const std::string& s = R.chosen ? rcRead[r] : reqs[r].read;
         reqs[r].graph->ThreadTraceback(s, reqs[r].mode, stepPtr[r], heads[r], &R.path);
     });
+    stats.threadMs += ms_since(t0);
 }
 
 std::string ZmwPoa::FindConsensus(int minCoverage, std::vector<int>* extents, std::vector<int>* cssPath)
@@ -669,38 +683,44 @@ std::string ZmwPoa::FindConsensus(int minCoverage, std::vector<int>* extents, st
     return graph.Sequence(path);
 }
 
-void PoaBatch(PoaRunner& R, const std::vector<std::vector<const std::string*>>& reads, long long maxCov, int minCov,
-              std::vector<std::string>* consensus, std::vector<std::vector<int>>* keys,
+namespace {
+
+// One slice [z0, z1) of a PoaBatch on one runner: lock-step read rounds over the slice's ZMWs.
+void PoaSlice(PoaRunner& R, const std::vector<std::vector<const std::string*>>& reads, int z0, int z1, long long maxCov,
+              int minCov, std::vector<std::string>* consensus, std::vector<std::vector<int>>* keys,
               std::vector<std::vector<char>>* rc, std::vector<std::vector<int>>* extents)
 {
-    const int nz = (int)reads.size();
-    std::vector<ZmwPoa> Z(nz);
+    const auto tStart = std::chrono::steady_clock::now();
+    const int nz = z1 - z0;
+    std::vector<std::unique_ptr<ZmwPoa>> Z(nz);
+    for (auto& p : Z) p.reset(new ZmwPoa());
     std::vector<int> next(nz, 0);
     std::vector<long long> cov(nz, 0);
     std::vector<char> done(nz, 0);
-    keys->assign(nz, std::vector<int>());
-    for (int z = 0; z < nz; ++z) (*keys)[z].assign(reads[z].size(), -2);
+    for (int z = 0; z < nz; ++z) (*keys)[z0 + z].assign(reads[z0 + z].size(), -2);
     auto record = [&](int z, int key) {
-        (*keys)[z][next[z]++] = key;
+        (*keys)[z0 + z][next[z]++] = key;
         if (key >= 0 && ++cov[z] >= maxCov) done[z] = 1;
-        if (next[z] >= (int)reads[z].size()) done[z] = 1;
+        if (next[z] >= (int)reads[z0 + z].size()) done[z] = 1;
     };
+    for (int z = 0; z < nz; ++z)
+        if (reads[z0 + z].empty()) done[z] = 1;
     for (;;) {
         std::vector<AlignRequest> reqs;
         std::vector<int> reqZ;
         for (int z = 0; z < nz; ++z) {
             while (!done[z]) {
-                const std::string* s = reads[z][next[z]];
+                const std::string* s = reads[z0 + z][next[z]];
                 if (s == nullptr) {
                     record(z, -1);
-                } else if (Z[z].graph.NumReads() == 0) {
+                } else if (Z[z]->graph.NumReads() == 0) {
                     std::vector<int> path;
-                    Z[z].graph.AddFirstRead(*s, &path);
-                    Z[z].readPaths.push_back(std::move(path));
-                    Z[z].rc.push_back(0);
+                    Z[z]->graph.AddFirstRead(*s, &path);
+                    Z[z]->readPaths.push_back(std::move(path));
+                    Z[z]->rc.push_back(0);
                     record(z, 0);
                 } else {
-                    reqs.push_back(AlignRequest{&Z[z].graph, *s, kLocal, true, 0.0f});
+                    reqs.push_back(AlignRequest{&Z[z]->graph, *s, kLocal, true, 0.0f});
                     reqZ.push_back(z);
                     break;
                 }
@@ -715,19 +735,59 @@ void PoaBatch(PoaRunner& R, const std::vector<std::vector<const std::string*>>& 
                 record(z, -1);
                 continue;
             }
-            Z[z].readPaths.push_back(std::move(res[q].path));
-            Z[z].rc.push_back((char)res[q].chosen);
-            record(z, (int)Z[z].readPaths.size() - 1);
+            Z[z]->readPaths.push_back(std::move(res[q].path));
+            Z[z]->rc.push_back((char)res[q].chosen);
+            record(z, (int)Z[z]->readPaths.size() - 1);
         }
     }
-    consensus->assign(nz, std::string());
-    rc->assign(nz, std::vector<char>());
-    extents->assign(nz, std::vector<int>());
+    const auto t0 = std::chrono::steady_clock::now();
     parallel_for(R.HostThreads(), nz, [&](int z) {
         const int mc = minCov >= 0 ? minCov : (cov[z] < 5 ? 1 : (int)((cov[z] + 1) / 2 - 1));
-        (*consensus)[z] = Z[z].readPaths.empty() ? std::string() : Z[z].FindConsensus(mc, &(*extents)[z]);
-        (*rc)[z] = Z[z].rc;
+        (*consensus)[z0 + z] = Z[z]->readPaths.empty() ? std::string() : Z[z]->FindConsensus(mc, &(*extents)[z0 + z]);
+        (*rc)[z0 + z] = Z[z]->rc;
+        Z[z].reset();   // the graphs' many small blocks are freed on all host threads
     });
+    R.stats.consensusMs += ms_since(t0);
+    R.stats.totalMs += ms_since(tStart);
+}
+
+}  // namespace
+
+void PoaBatch(const std::vector<PoaRunner*>& runners, const std::vector<std::vector<const std::string*>>& reads,
+              long long maxCov, int minCov, std::vector<std::string>* consensus, std::vector<std::vector<int>>* keys,
+              std::vector<std::vector<char>>* rc, std::vector<std::vector<int>>* extents)
+{
+    const int nz = (int)reads.size();
+    consensus->assign(nz, std::string());
+    keys->assign(nz, std::vector<int>());
+    rc->assign(nz, std::vector<char>());
+    extents->assign(nz, std::vector<int>());
+    // slices of about equal read-base totals, one per runner; small batches use one runner
+    const int ns = std::max(1, std::min((int)runners.size(), nz / 64));
+    std::vector<long long> pre(nz + 1, 0);
+    for (int z = 0; z < nz; ++z) {
+        long long b = 0;
+        for (const std::string* s : reads[z]) b += s ? (long long)s->size() : 0;
+        pre[z + 1] = pre[z] + b;
+    }
+    std::vector<int> cut(ns + 1, nz);
+    cut[0] = 0;
+    for (int k = 1; k < ns; ++k)
+        cut[k] = (int)(std::lower_bound(pre.begin(), pre.end(), pre[nz] * k / ns) - pre.begin());
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(ns);
+    for (int k = 0; k < ns; ++k)
+        th.emplace_back([&, k] {
+            try {
+                PoaSlice(*runners[k], reads, cut[k], std::max(cut[k], cut[k + 1]), maxCov, minCov, consensus, keys, rc,
+                         extents);
+            } catch (...) {
+                err[k] = std::current_exception();
+            }
+        });
+    for (auto& t : th) t.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
 }
 
 }  // namespace poa

@@ -89,6 +89,9 @@ struct PoaStats {
     long long alignments = 0, cells = 0, launches = 0, traceSteps = 0;
     double fillMs = 0.0, traceMs = 0.0;
     double bytes = 0.0;   // algorithmic score-matrix bytes written by the fills
+    // host wall time (ms): column programs + staging, device phase (uploads, kernels, downloads),
+    // threading the reads into the graphs, FindConsensus
+    double progMs = 0.0, deviceMs = 0.0, threadMs = 0.0, consensusMs = 0.0, totalMs = 0.0;
 };
 
 class PoaRunner {
@@ -113,7 +116,8 @@ private:
     size_t budget_ = 0;   // score-matrix bytes per launch group; 0 = from free memory
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
-    DevVec<uint8_t> dBase_, dRowBase_, dPool_;
+    DevVec<uint8_t> dBase_, dRowBase_;
+    VmPool dPool_;   // score matrices: 1 GB granules mapped as rounds grow, never copied or freed between rounds
     DevVec<int> dVertexOfCol_, dPredStart_, dPredCol_, dExitPred_, dScore_, dExitCol_, dTraceJobs_;
     DevVec<PoaJob> dJobs_;
     DevVec<uint32_t> dSteps_;
@@ -138,8 +142,10 @@ struct ZmwPoa {
 // Consensus.h's PoaConsensus (include/pacbio/ccs/Consensus.h:352-390) over a batch of ZMWs: reads
 // (nullptr = dropped by FilterReads, key -1) are added in order with OrientAndAddRead until maxCov were
 // taken; keys[z][r] = key, -2 past the coverage stop.  minCov < 0: (cov < 5) ? 1 : (cov + 1) / 2 - 1.
-void PoaBatch(PoaRunner& R, const std::vector<std::vector<const std::string*>>& reads, long long maxCov, int minCov,
-              std::vector<std::string>* consensus, std::vector<std::vector<int>>* keys,
+// The ZMWs are split into one slice per runner (about equal read bases each); the slices run concurrently,
+// so one slice's host work (column programs, threading) overlaps the other's kernels.
+void PoaBatch(const std::vector<PoaRunner*>& runners, const std::vector<std::vector<const std::string*>>& reads,
+              long long maxCov, int minCov, std::vector<std::string>* consensus, std::vector<std::vector<int>>* keys,
               std::vector<std::vector<char>>* rc, std::vector<std::vector<int>>* extents);
 
 }  // namespace poa

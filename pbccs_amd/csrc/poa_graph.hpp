@@ -65,6 +65,7 @@ public:
         int reads;
         int spanning;
         float score, reaching;
+        int outHead, inHead;   // edge lists in the pool: out-edges by descending target, in-edges by ascending source
     };
 
     PoaGraph()
@@ -105,14 +106,17 @@ public:
         std::vector<std::pair<int, int>> stack;   // (vertex, next out-edge)
         stack.emplace_back(kEnter, 0);
         state[kEnter] = 1;
+        // (vertex, next out-edge): successors taken largest id first, so a vertex's oldest successor -- the
+        // chain it lies on -- is finished first and follows it directly in the reversed order
+        stack[0].second = v_[kEnter].outHead;
         while (!stack.empty()) {
             auto& top = stack.back();
-            const std::vector<int>& o = out_[top.first];
-            if (top.second < (int)o.size()) {
-                const int w = o[o.size() - 1 - top.second++];   // last-added successor first
+            if (top.second >= 0) {
+                const int w = e_[top.second].dst;
+                top.second = e_[top.second].nextOut;
                 if (!state[w]) {
                     state[w] = 1;
-                    stack.emplace_back(w, 0);
+                    stack.emplace_back(w, v_[w].outHead);
                 }
             } else {
                 order.push_back(top.first);
@@ -134,11 +138,11 @@ public:
         for (int c = 0; c < cols; ++c) {
             const int v = P->vertexOfCol[c];
             P->base[c] = (uint8_t)v_[v].base;
-            for (int u : in_[v]) P->predCol.push_back(P->colOfVertex[u]);
+            for (int e = v_[v].inHead; e >= 0; e = e_[e].nextIn) P->predCol.push_back(P->colOfVertex[e_[e].src]);
             P->predStart[c + 1] = (int)P->predCol.size();
         }
         P->exitPredCol.clear();
-        for (int u : in_[kExit]) P->exitPredCol.push_back(P->colOfVertex[u]);
+        for (int e = v_[kExit].inHead; e >= 0; e = e_[e].nextIn) P->exitPredCol.push_back(P->colOfVertex[e_[e].src]);
     }
 
     // tracebackAndThread (PoaGraphTraversals.cpp:227-369), replaying the device's walk: steps[0] is the
@@ -211,7 +215,8 @@ public:
                                                   : (2 * x.reads - 1 * total - 0.0001f);
             x.score = score;
             x.reaching = score;
-            for (int u : in_[v]) {
+            for (int e = x.inHead; e >= 0; e = e_[e].nextIn) {
+                const int u = e_[e].src;
                 const float rsc = score + v_[u].reaching;
                 if (rsc > x.reaching) {
                     x.reaching = rsc;
@@ -256,40 +261,43 @@ public:
                 snprintf(buf, sizeof buf, "%zu[shape=Mrecord,%s label=\"{ %c | %d }\"];\n", v, fill, x.base, x.reads);
             s += buf;
         }
-        for (const auto& e : edges_) {
-            snprintf(buf, sizeof buf, "%d->%d ;\n", e.first, e.second);
+        for (const Edge& e : e_) {   // edge pool index = insertion order
+            snprintf(buf, sizeof buf, "%d->%d ;\n", e.src, e.dst);
             s += buf;
         }
         return s + "}\n";
     }
 
 private:
+    // Edges live in one pool (index = insertion order, which the graph dump follows) threaded into a
+    // sorted singly linked out-list and in-list per vertex: a graph is a handful of contiguous arrays,
+    // whatever its size, so building and freeing thousands of graphs costs no per-vertex allocations.
+    struct Edge {
+        int src, dst, nextOut, nextIn;
+    };
     std::vector<Vertex> v_;
-    std::vector<std::vector<int>> out_, in_;   // sorted, unique
-    std::vector<std::pair<int, int>> edges_;   // insertion order
+    std::vector<Edge> e_;
+    std::vector<uint8_t> mark_;   // TagSpan scratch
     size_t numReads_ = 0;
 
     int AddVertex(char base, int reads)
     {
-        v_.push_back(Vertex{base, reads, 0, 0.f, 0.f});
-        out_.emplace_back();
-        in_.emplace_back();
+        v_.push_back(Vertex{base, reads, 0, 0.f, 0.f, -1, -1});
         return (int)v_.size() - 1;
     }
 
-    static bool InsertSorted(std::vector<int>& xs, int x)
+    void AddEdge(int u, int w)   // add_edge on setS: a present edge is not added again
     {
-        auto it = std::lower_bound(xs.begin(), xs.end(), x);
-        if (it != xs.end() && *it == x) return false;
-        xs.insert(it, x);
-        return true;
-    }
-
-    void AddEdge(int u, int w)
-    {
-        if (!InsertSorted(out_[u], w)) return;
-        InsertSorted(in_[w], u);
-        edges_.emplace_back(u, w);
+        int* link = &v_[u].outHead;   // descending targets
+        while (*link >= 0 && e_[*link].dst > w) link = &e_[*link].nextOut;
+        if (*link >= 0 && e_[*link].dst == w) return;
+        const int id = (int)e_.size();
+        e_.push_back(Edge{u, w, *link, -1});
+        *link = id;
+        int* in = &v_[w].inHead;      // ascending sources (PoaGraphImpl.hpp:130-143)
+        while (*in >= 0 && e_[*in].src < u) in = &e_[*in].nextIn;
+        e_[id].nextIn = *in;
+        *in = id;
     }
 
     // a new vertex for read base seq[pos] in front of `fork`
@@ -304,14 +312,15 @@ private:
     // SpanningDFS + tagSpan (PoaGraphTraversals.cpp:62-113): vertices reachable from `start` that reach `end`
     void TagSpan(int start, int end)
     {
-        std::vector<uint8_t> mark(v_.size(), 0);   // bit 0: reachable from start, bit 1: also reaches end
+        std::vector<uint8_t>& mark = mark_;   // bit 0: reachable from start, bit 1: also reaches end
+        mark.assign(v_.size(), 0);
         std::vector<int> st{start};
         while (!st.empty()) {
             const int x = st.back();
             st.pop_back();
             if (mark[x] & 1) continue;
             mark[x] |= 1;
-            for (int w : out_[x]) st.push_back(w);
+            for (int e = v_[x].outHead; e >= 0; e = e_[e].nextOut) st.push_back(e_[e].dst);
         }
         st.push_back(end);
         while (!st.empty()) {
@@ -320,7 +329,7 @@ private:
             if (!(mark[x] & 1) || (mark[x] & 2)) continue;
             mark[x] |= 2;
             v_[x].spanning++;
-            for (int u : in_[x]) st.push_back(u);
+            for (int e = v_[x].inHead; e >= 0; e = e_[e].nextIn) st.push_back(e_[e].src);
         }
     }
 };

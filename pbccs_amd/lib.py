@@ -94,7 +94,8 @@ class CPoaOutput(ctypes.Structure):
 class CPoaStats(ctypes.Structure):
     _fields_ = [("alignments", ctypes.c_longlong), ("cells", ctypes.c_longlong), ("launches", ctypes.c_longlong),
                 ("trace_steps", ctypes.c_longlong), ("fill_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
-                ("bytes", ctypes.c_double)]
+                ("bytes", ctypes.c_double), ("prog_ms", ctypes.c_double), ("device_ms", ctypes.c_double),
+                ("thread_ms", ctypes.c_double), ("consensus_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
 
 
 # exported symbol -> (restype, argtypes); tests check that every symbol of include/pbccs_amd.h is exported

@@ -104,34 +104,62 @@ def poa_consensus(reads, mode=GLOBAL, min_coverage=-INT_MAX, graphviz_flags=None
 def poa_batch(zmw_reads, max_coverage=None, min_coverage=-1, engine=None):
     """Consensus.h's PoaConsensus for many ZMWs at once.  zmw_reads: per ZMW, the subreads in FilterReads
     order (None = dropped).  Returns per ZMW {"consensus", "keys" (per read: key, -1, or -2 past
-    maxPoaCov), "summaries" (per key: rc, read, tpl extents)}."""
+    maxPoaCov), "summaries" (per key: rc, read, tpl extents)}.
+
+    Marshalling is flat: all reads in one buffer with a pointer table, all outputs in shared arrays, so
+    the per-ZMW Python work is a few struct-field stores."""
+    import numpy as np
     eng = _engine(engine)
     n = len(zmw_reads)
+    counts = np.fromiter((len(r) for r in zmw_reads), dtype=np.int64, count=n)
+    flat = [r for reads in zmw_reads for r in reads]
+    enc = [b"" if r is None else r.encode() for r in flat]
+    lens = np.fromiter((len(e) for e in enc), dtype=np.int32, count=len(enc))
+    blob = ctypes.create_string_buffer(b"".join(enc), max(1, int(lens.sum())))
+    starts = np.zeros(len(enc) + 1, dtype=np.int64)
+    np.cumsum(lens, out=starts[1:])
+    ptrs = (ctypes.addressof(blob) + starts[:-1]).astype(np.uint64)
+    ptrs[lens == 0] = 0                                  # NULL: a read FilterReads dropped
+    first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(counts, out=first[1:])
+    # per-ZMW consensus capacity: its read bases + 16; per-read outputs shared
+    zbases = np.add.reduceat(lens.astype(np.int64), first[:-1]) if len(enc) else np.zeros(n, np.int64)
+    zbases = np.where(counts > 0, zbases, 0) + 16
+    cstart = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(zbases, out=cstart[1:])
+    cbuf = ctypes.create_string_buffer(max(1, int(cstart[-1])))
+    keys = np.zeros(max(1, len(enc)), dtype=np.int32)
+    rc = np.zeros(max(1, len(enc)), dtype=np.int32)
+    ext = np.zeros(max(4, 4 * len(enc)), dtype=np.int32)
     ins = (_L.CPoaInput * max(1, n))()
     outs = (_L.CPoaOutput * max(1, n))()
-    keep = []
-    for z, reads in enumerate(zmw_reads):
-        enc = [None if r is None else r.encode() for r in reads]
-        nr = len(enc)
-        seqs = (ctypes.c_char_p * max(1, nr))(*enc)
-        lens = (ctypes.c_int * max(1, nr))(*[0 if r is None else len(r) for r in enc])
-        cap = sum(len(r) for r in enc if r) + 16
-        buf = ctypes.create_string_buffer(cap)
-        keys = (ctypes.c_int * max(1, nr))()
-        rc = (ctypes.c_int * max(1, nr))()
-        ext = (ctypes.c_int * max(4, 4 * nr))()
-        ins[z].seqs, ins[z].lens, ins[z].n_reads = seqs, lens, nr
-        outs[z].consensus = ctypes.cast(buf, ctypes.c_char_p)
-        outs[z].cap, outs[z].keys, outs[z].rc, outs[z].extents = cap, keys, rc, ext
-        keep.append((seqs, lens, buf, keys, rc, ext, nr))
+    P = ctypes.POINTER
+    pbase, lbase = ptrs.ctypes.data, lens.ctypes.data
+    kbase, rbase, ebase = keys.ctypes.data, rc.ctypes.data, ext.ctypes.data
+    cb = ctypes.addressof(cbuf)
+    for z in range(n):
+        f = int(first[z])
+        ins[z].seqs = ctypes.cast(pbase + 8 * f, P(ctypes.c_char_p))
+        ins[z].lens = ctypes.cast(lbase + 4 * f, P(ctypes.c_int))
+        ins[z].n_reads = int(counts[z])
+        o = outs[z]
+        o.consensus = ctypes.cast(cb + int(cstart[z]), ctypes.c_char_p)
+        o.cap = int(zbases[z])
+        o.keys = ctypes.cast(kbase + 4 * f, P(ctypes.c_int))
+        o.rc = ctypes.cast(rbase + 4 * f, P(ctypes.c_int))
+        o.extents = ctypes.cast(ebase + 16 * f, P(ctypes.c_int))
     mc = 2**62 if max_coverage is None else int(max_coverage)
     _L.check(load().pbccs_poa_batch(eng._h, ins, n, mc, int(min_coverage), outs))
+    raw = cbuf.raw
     res = []
-    for z, (_, _, buf, keys, rc, ext, nr) in enumerate(keep):
-        nk = outs[z].n_keys
-        res.append({"consensus": buf.raw[:outs[z].len].decode(), "keys": list(keys[:nr]),
-                    "summaries": [{"rc": bool(rc[k]), "read": (ext[4 * k], ext[4 * k + 1]),
-                                   "tpl": (ext[4 * k + 2], ext[4 * k + 3])} for k in range(nk)]})
+    for z in range(n):
+        f, nr, nk = int(first[z]), int(counts[z]), outs[z].n_keys
+        e = ext[4 * f:4 * (f + nk)].reshape(-1, 4).tolist()
+        r_ = rc[f:f + nk].tolist()
+        res.append({"consensus": raw[int(cstart[z]):int(cstart[z]) + outs[z].len].decode(),
+                    "keys": keys[f:f + nr].tolist(),
+                    "summaries": [{"rc": bool(r_[k]), "read": (e[k][0], e[k][1]), "tpl": (e[k][2], e[k][3])}
+                                  for k in range(nk)]})
     return res
 
 
