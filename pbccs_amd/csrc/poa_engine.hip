@@ -209,6 +209,108 @@ __global__ __launch_bounds__(64) void k_poa_fill(const PoaJob* __restrict__ jobs
     }
 }
 
+// LDS-ring variant (LOCAL uint16 jobs of up to 64 * RMAX rows).  A lane owns R = ceil(rows / 64)
+// consecutive rows, so a column is one wave pass with no row padding beyond 64; the last K columns stay in
+// an LDS ring, and the global copy (for the traceback and for predecessors further back) is stored
+// lane-interleaved -- row i of a column at (i % R) * 64 + i / R -- so every store instruction writes 64
+// consecutive uint16.  Predecessors within the ring are read from LDS; the workgroup fence that makes the
+// global stores visible to the wave's own loads is paid only for a predecessor older than the ring.
+template <int R, int K>
+__global__ __launch_bounds__(64) void k_poa_fill_lds(const PoaJob* __restrict__ jobs, int jobBase, PoaPools P,
+                                                     uint16_t* __restrict__ pool, int* __restrict__ outScore,
+                                                     int* __restrict__ outExitCol)
+{
+    extern __shared__ uint16_t ring[];   // K columns x 64 * R
+    const int j = jobBase + blockIdx.x;
+    const PoaJob J = jobs[j];
+    const int lane = threadIdx.x;
+    uint16_t* S = pool + J.scoreOff;
+    const int I = J.I, stride = J.colStride, mode = J.mode;   // stride == 64 * R
+    const int* predStart = P.predStart + J.predStartOff;
+    const int i0 = lane * R;
+    // the lane's read bases (row i holds read[i - 1]), 4 per word
+    unsigned rbw[R / 4];
+#pragma unroll
+    for (int w = 0; w < R / 4; ++w) {
+        unsigned x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            x |= (unsigned)P.rowBase[J.readOff + i0 + 4 * w + b] << (8 * b);
+        rbw[w] = x;
+    }
+    bool dirty = false;
+    int bestVal = kNeg, bestVid = INT_MAX, bestCol = 0;
+    for (int k = 0; k < J.nCols; ++k) {
+        const int base = P.base[J.progOff + k];
+        const int vid = P.vertexOfCol[J.progOff + k];
+        const int ps = predStart[k], pe = predStart[k + 1];
+        int ne[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) ne[r] = mode == kLocal ? 0 : kNeg;
+        if (lane == 0) ne[0] = 0;   // row 0: ^ has no reaching move, everything else starts there (LOCAL)
+        // one predecessor column, streamed row by row from LDS (ring) or HBM
+        auto absorb = [&](auto col) {
+            int up = lane > 0 ? (int)col[(R - 1) * 64 + lane - 1] : kNeg;
+            const auto c = col + lane;   // rows at constant offsets r * 64 from one base
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int qr = (int)c[r * 64];
+                const int b = (rbw[r >> 2] >> ((r & 3) * 8)) & 0xFF;
+                ne[r] = max(ne[r], max(up + (b == base ? kMatchScore : kMismatchScore), qr + kDeleteScore));
+                up = qr;
+            }
+        };
+        for (int p = ps; p < pe; ++p) {
+            const int pc = P.predCol[p];
+            if (k - pc < K) {
+                absorb(ring + (pc % K) * stride);
+            } else {
+                if (dirty) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                    dirty = false;
+                }
+                absorb(S + (long long)pc * stride);
+            }
+        }
+        int run = kNeg;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            run = max(run, ne[r] - (i0 + r) * kInsertScore);
+            ne[r] = run;
+        }
+        const int incl = wave_prefix_max(run);
+        const int excl = dpp_i<0x138, 0xF>(kNeg, incl);   // wave_shr:1
+        int colBest = kNeg;
+        uint16_t* slot = ring + (k % K) * stride + lane;
+        uint16_t* out = S + (long long)k * stride + lane;
+        __syncthreads();   // the slot's previous column (k - K) has been read by every lane
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = i0 + r;
+            const int v = max(ne[r], excl) + i * kInsertScore;
+            if (i <= I) colBest = max(colBest, v);
+            slot[r * 64] = (uint16_t)v;
+            out[r * 64] = (uint16_t)v;
+        }
+        __syncthreads();   // the column is in the ring before the next column reads it
+        dirty = true;
+        if (colBest > bestVal || (colBest == bestVal && vid < bestVid)) {
+            bestVal = colBest;
+            bestVid = vid;
+            bestCol = k;
+        }
+    }
+    int key = bestVid;
+    const int v0 = bestVal;
+    wave_argmax(bestVal, key);
+    const unsigned long long m = __ballot(v0 == bestVal && bestVid == key);
+    bestCol = __shfl(bestCol, (int)__builtin_ctzll(m));
+    if (lane == 0) {
+        outScore[j] = bestVal;
+        outExitCol[j] = bestCol;
+    }
+}
+
 // tracebackAndThread's walk (PoaGraphTraversals.cpp:252-347) for the jobs whose reads are committed:
 // the End move into $, then each visited cell with the move that reached it, recomputed as
 // makeAlignmentColumn chose it (candidates in order Start, per predecessor Match/Mismatch then Delete,
@@ -224,15 +326,20 @@ __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ job
     const PoaJob J = jobs[j];
     const int lane = threadIdx.x;
     const ST* S = pool + J.scoreOff;
-    const int I = J.I, stride = J.colStride, mode = J.mode;
+    const int I = J.I, stride = J.colStride, mode = J.mode, R = J.rowsPerLane;
     const int ec = exitCol[j];
     const int* vtx = P.vertexOfCol + J.progOff;
+    // cell (column c, row i): linear rows, or lane-interleaved for the ring variants
+    auto cell = [&](int c, int i) -> int {
+        const int x = R ? (i % R) * 64 + i / R : i;
+        return (int)S[(long long)c * stride + x];
+    };
     // LOCAL: the End move comes from ArgMax of that column (first maximum, VectorL.hpp:66-69)
     int prevRow = I;
     if (mode == kLocal) {
         int bv = kNeg, br = INT_MAX;
         for (int i = lane; i <= I; i += 64) {
-            const int v = (int)S[(long long)ec * stride + i];
+            const int v = cell(ec, i);
             if (v > bv) {
                 bv = v;
                 br = i;
@@ -266,7 +373,7 @@ __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ job
                 pv = -1;
                 for (int p = ps; p < pe; ++p) {
                     const int c = P.predCol[p];
-                    const int cand = (int)S[(long long)c * stride] + kDeleteScore;
+                    const int cand = cell(c, 0) + kDeleteScore;
                     if (cand > best) {
                         best = cand;
                         pv = c;
@@ -287,21 +394,20 @@ __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ job
             const bool isMatch = rb[i] == P.base[J.progOff + k];
             for (int p = ps; p < pe; ++p) {
                 const int c = P.predCol[p];
-                const ST* q = S + (long long)c * stride;
-                int cand = (int)q[i - 1] + (isMatch ? kMatchScore : kMismatchScore);
+                int cand = cell(c, i - 1) + (isMatch ? kMatchScore : kMismatchScore);
                 if (cand > best) {
                     best = cand;
                     pv = c;
                     mv = isMatch ? kMatch : kMismatch;
                 }
-                cand = (int)q[i] + kDeleteScore;
+                cand = cell(c, i) + kDeleteScore;
                 if (cand > best) {
                     best = cand;
                     pv = c;
                     mv = kDelete;
                 }
             }
-            const int cand = (int)S[(long long)k * stride + i - 1] + kInsertScore;
+            const int cand = cell(k, i - 1) + kInsertScore;
             if (cand > best) {
                 pv = k;
                 mv = kExtra;
@@ -342,6 +448,49 @@ std::string reverse_complement(const std::string& s)
 double ms_since(std::chrono::steady_clock::time_point t0)
 {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// k_poa_fill variants: 0 = chunked, linear rows, memory-resident predecessors (any length and width);
+// v = 1..12 = LDS ring, lane-interleaved rows, uint16 (LOCAL), R = 4 v rows per lane (at most 3072 rows)
+constexpr int kRingVariants = 12;
+int fill_variant(int rows, bool wide)
+{
+    if (wide || rows > 64 * 4 * kRingVariants) return 0;
+    return (rows + 255) / 256;
+}
+int rows_per_lane(int variant, int rows) { return 4 * variant; }
+int variant_stride(int variant, int rows)
+{
+    return variant == 0 ? (rows + kChunkRows - 1) / kChunkRows * kChunkRows : 64 * rows_per_lane(variant, rows);
+}
+constexpr int kRing = 4;   // columns kept in LDS by the ring variants
+
+template <class ST>
+void launch_fill(int variant, int n, int base, hipStream_t s, const PoaJob* jobs, const PoaPools& P, ST* pool,
+                 int* score, int* exitCol)
+{
+    if (n <= 0) return;
+    switch (variant) {
+        default: hipLaunchKernelGGL(k_poa_fill<ST>, dim3(n), dim3(64), 0, s, jobs, base, P, pool, score, exitCol); break;
+    }
+}
+
+// the ring variants; lds = the launch's largest ring (kRing columns of 64 * R uint16)
+void launch_fill_lds(int variant, int n, int base, size_t lds, hipStream_t s, const PoaJob* jobs, const PoaPools& P,
+                     uint16_t* pool, int* score, int* exitCol)
+{
+    if (n <= 0) return;
+#define POA_RING_CASE(V)                                                                                         \
+    case V:                                                                                                    \
+        hipLaunchKernelGGL((k_poa_fill_lds<4 * V, kRing>), dim3(n), dim3(64), lds, s, jobs, base, P, pool, score, \
+                           exitCol);                                                                           \
+        break;
+    switch (variant) {
+        POA_RING_CASE(1) POA_RING_CASE(2) POA_RING_CASE(3) POA_RING_CASE(4) POA_RING_CASE(5) POA_RING_CASE(6)
+        POA_RING_CASE(7) POA_RING_CASE(8) POA_RING_CASE(9) POA_RING_CASE(10) POA_RING_CASE(11) POA_RING_CASE(12)
+        default: break;
+    }
+#undef POA_RING_CASE
 }
 
 template <class F>
@@ -439,14 +588,17 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
             J = PoaJob{};
             J.nCols = nCols;
             J.I = (int)(o ? rcRead[r] : reqs[r].read).size();
-            J.colStride = (J.I + 1 + kChunkRows - 1) / kChunkRows * kChunkRows;
             J.mode = reqs[r].mode;
+            // uint16 holds LOCAL scores (>= 0, at most 3 per row) of every row up to the padded stride
+            J.wide = !(J.mode == kLocal && 3LL * (J.I + 1 + kChunkRows) < 65536);
+            J.variant = fill_variant(J.I + 1, J.wide);
+            J.rowsPerLane = rows_per_lane(J.variant, J.I + 1);
+            J.colStride = variant_stride(J.variant, J.I + 1);
             J.progOff = (int)nBase;
             J.predStartOff = (int)nPredStart;
             J.exitOff = (int)nExit;
             J.nExit = (int)C.exitPredCol.size();
             J.readOff = nRow;
-            J.wide = !(J.mode == kLocal && 3LL * J.colStride < 65536);
             J.traceSlot = -1;
             nRow += J.colStride + 16;
             jobReq[j] = r;
@@ -531,14 +683,15 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
             r1++;
         }
         const int j0 = firstJob[r0], j1 = firstJob[r1], gn = j1 - j0;
-        // launch order: uint16 jobs, then int32 jobs (one range per kernel instantiation)
+        // launch order: uint16 jobs, then int32 jobs, each by fill variant (one range per kernel instantiation)
         std::vector<int> order;
         order.reserve(gn);
-        for (int j = j0; j < j1; ++j)
-            if (!jobs[j].wide) order.push_back(j);
-        const int nNarrow = (int)order.size();
-        for (int j = j0; j < j1; ++j)
-            if (jobs[j].wide) order.push_back(j);
+        for (int w = 0; w < 2; ++w)
+            for (int v = 0; v <= kRingVariants; ++v)
+                for (int j = j0; j < j1; ++j)
+                    if (jobs[j].wide == w && jobs[j].variant == v) order.push_back(j);
+        int nNarrow = 0;
+        while (nNarrow < gn && !jobs[order[nNarrow]].wide) nNarrow++;
         size_t off16 = 0, off32 = 0;
         for (int k = 0; k < gn; ++k) {
             PoaJob& J = jobs[order[k]];
@@ -555,12 +708,22 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
         uint16_t* pool16 = reinterpret_cast<uint16_t*>(dPool_.ptr);
         int* pool32 = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(dPool_.ptr) + off16);
         if (profiling) check(hipEventRecord(ev_[0], stream_), "event");
-        if (nNarrow > 0)
-            hipLaunchKernelGGL(k_poa_fill<uint16_t>, dim3(nNarrow), dim3(64), 0, stream_, dJobs_.ptr, 0, pools, pool16,
-                               dScore_.ptr, dExitCol_.ptr);
-        if (gn > nNarrow)
-            hipLaunchKernelGGL(k_poa_fill<int>, dim3(gn - nNarrow), dim3(64), 0, stream_, dJobs_.ptr, nNarrow, pools,
-                               pool32, dScore_.ptr, dExitCol_.ptr);
+        for (int k = 0; k < gn;) {   // one launch per (width, variant) run
+            int e = k;
+            while (e < gn && gj[e].wide == gj[k].wide && gj[e].variant == gj[k].variant) e++;
+            if (gj[k].wide) {
+                launch_fill<int>(0, e - k, k, stream_, dJobs_.ptr, pools, pool32, dScore_.ptr, dExitCol_.ptr);
+            } else if (gj[k].variant == 0) {
+                launch_fill<uint16_t>(0, e - k, k, stream_, dJobs_.ptr, pools, pool16, dScore_.ptr, dExitCol_.ptr);
+            } else {
+                size_t lds = 0;
+                for (int x = k; x < e; ++x) lds = std::max(lds, (size_t)kRing * gj[x].colStride * sizeof(uint16_t));
+                launch_fill_lds(gj[k].variant, e - k, k, lds, stream_, dJobs_.ptr, pools, pool16, dScore_.ptr,
+                                dExitCol_.ptr);
+            }
+            stats.launches++;
+            k = e;
+        }
         check(hipGetLastError(), "k_poa_fill launch");
         if (profiling) check(hipEventRecord(ev_[1], stream_), "event");
         check(hipMemcpyAsync(hScore_.ptr, dScore_.ptr, gn * sizeof(int), hipMemcpyDeviceToHost, stream_), "d2h");
@@ -570,7 +733,6 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
             check(hipEventElapsedTime(&ms, ev_[0], ev_[1]), "event");
             stats.fillMs += ms;
         }
-        stats.launches += (nNarrow > 0) + (gn > nNarrow);
         for (int k = 0; k < gn; ++k) {
             const PoaJob& J = gj[k];
             (*out)[jobReq[order[k]]].score[jobOri[order[k]]] = (float)hScore_.ptr[k];

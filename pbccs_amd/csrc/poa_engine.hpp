@@ -32,6 +32,8 @@ struct PoaJob {
     long long stepOff;    // into the traceback step pool (I + nCols + 2 steps)
     int traceSlot;        // this job's TraceHeader (committed jobs), else -1
     int wide;             // score matrix stored as int32 (else uint16)
+    int variant;          // k_poa_fill variant (see fill_variant)
+    int rowsPerLane;      // ring variants: rows per lane R; cell (column c, row i) at c * colStride + (i % R) * 64 + i / R
 };
 
 // Page-locked host staging (hipHostMalloc): the per-round program uploads and traceback downloads run at
