@@ -124,3 +124,27 @@ def zmw_input(chunk, poa, min_length=10, max_poa_coverage=None):
         mr = extract_mapped_read(reads[i], summaries[key], min_length) if key >= 0 else None
         out.append(mr if mr is not None else {"seq": None, "strand": 0, "ts": 0, "te": 0, "full_pass": False})
     return None, {"draft": draft, "snr": list(chunk["snr"]), "reads": out}
+
+
+def zmw_inputs_batch(chunks, min_length=10, max_poa_coverage=None, engine=None):
+    """zmw_input for many ZMWs at once, with the POA of all of them on the GPU in one pbccs_poa_batch
+    (every ZMW adds its next subread in the same device round).  Returns [(status, zmw)] as zmw_input."""
+    from . import poa as _poa
+    filtered = [filter_reads(c["reads"], min_length) for c in chunks]
+    idx = [z for z, rs in enumerate(filtered) if rs and not all(r is None for r in rs)]
+    out = [("NoSubreads", None)] * len(chunks)
+    res = _poa.poa_batch([[None if r is None else r["seq"] for r in filtered[z]] for z in idx],
+                         max_coverage=max_poa_coverage, engine=engine)
+    for z, r in zip(idx, res):
+        draft = r["consensus"]
+        if len(draft) < min_length:
+            out[z] = ("TooShort", None)
+            continue
+        reads = []
+        for i, key in enumerate(r["keys"]):
+            if key == -2:
+                break   # past maxPoaCov: Consensus.h's loop stopped before this read
+            mr = extract_mapped_read(filtered[z][i], r["summaries"][key], min_length) if key >= 0 else None
+            reads.append(mr if mr is not None else {"seq": None, "strand": 0, "ts": 0, "te": 0, "full_pass": False})
+        out[z] = (None, {"draft": draft, "snr": list(chunks[z]["snr"]), "reads": reads})
+    return out

@@ -181,6 +181,34 @@ def test_driver_zmw_input_with_gpu_poa(P):
         assert st_g == st_o and z_g == z_o
 
 
+def test_driver_batch_matches_per_zmw_driver(P):
+    """driver.zmw_inputs_batch (one pbccs_poa_batch for all ZMWs) equals zmw_input per ZMW with the oracle's
+    POA, with and without a maxPoaCov stop; a ZMW whose reads all fail FilterReads is NoSubreads."""
+    poa, eng = P
+    from pbccs_amd import driver
+
+    class OraclePoa:
+        def __init__(self):
+            self.reads = []
+
+        def orient_and_add_read(self, seq):
+            self.reads.append(seq)
+            return O.sparse_poa(self.reads)["keys"][-1]
+
+        def find_consensus(self, min_cov):
+            r = O.sparse_poa(self.reads, min_cov)
+            return r["consensus"], dict(enumerate(r["summaries"]))
+
+    chunks = [{"snr": [10.0, 7.0, 5.0, 11.0], "reads": [{"seq": s} for s in reads]}
+              for reads in _synthetic_subreads(5, (300, 700), (3, 8), seed=44)]
+    chunks.append({"snr": [8.0, 8.0, 8.0, 8.0], "reads": [{"seq": "ACGT"}]})   # median below min_length
+    for cov in (None, 3):
+        got = driver.zmw_inputs_batch(chunks, max_poa_coverage=cov, engine=eng)
+        for c, g in zip(chunks, got):
+            assert g == driver.zmw_input(c, OraclePoa(), max_poa_coverage=cov)
+    assert got[-1] == ("NoSubreads", None)
+
+
 def test_poa_stats_counted(P):
     poa, eng = P
     s = poa.poa_stats(eng)
