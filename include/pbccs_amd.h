@@ -255,6 +255,14 @@ typedef struct {
     float merge[4], merge_s[4];
 } pbccs_qv_model_params;
 
+/* Recursor types of ConsensusCore's Quiver MutationScorer typedefs (Quiver/MutationScorer.hpp:93-99):
+ * SseRecursor or SimpleRecursor (Quiver/SimpleRecursor.cpp: row-by-row fills, moves combined Inc, Extra,
+ * Del, Merge) over SparseMatrixF or DenseMatrixF storage (AllocatedEntries = Rows * Columns). */
+#define PBCCS_QV_RECURSOR_SPARSE_SSE 0
+#define PBCCS_QV_RECURSOR_SPARSE_SIMPLE 1
+#define PBCCS_QV_RECURSOR_DENSE_SSE 2
+#define PBCCS_QV_RECURSOR_DENSE_SIMPLE 3
+
 /* QuiverConfig (QuiverConfig.hpp:181-199) + the recursor's combiner */
 typedef struct {
     pbccs_qv_model_params params;
@@ -263,6 +271,7 @@ typedef struct {
     float fast_score_threshold;  /* QuiverConfig::FastScoreThreshold */
     float add_threshold;         /* QuiverConfig::AddThreshold (1.0 = no memory gate) */
     int sum_product;             /* 0: Viterbi (SparseSseQvRecursor), 1: sum-product (logAdd) */
+    int recursor;                /* PBCCS_QV_RECURSOR_*: the recursor family and matrix storage */
 } pbccs_quiver_config;
 
 /* MultiReadMutationScorer(const QuiverConfigTable&, std::string tpl)  (Quiver/MultiReadMutationScorer.cpp:123-136)

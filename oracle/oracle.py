@@ -287,13 +287,20 @@ def qv_params(d):
     return out
 
 
+QUIVER_RECURSORS = ("SparseSse", "SparseSimple", "DenseSse", "DenseSimple")
+
+
 class QuiverScorer:
-    """Mirror of ConsensusCore::MultiReadMutationScorer<SparseSse{Qv,QvSumProduct}Recursor> (CPU restatement)."""
+    """Mirror of ConsensusCore::MultiReadMutationScorer<R> (CPU restatement).  recursor: SparseSse (the MRMS
+    typedefs' SparseSseQvRecursor), SparseSimple, DenseSse (SseQvRecursor), DenseSimple (SimpleQvRecursor) --
+    the four recursor types ConsensusCore's typed tests run (MutationScorer.hpp:93-99)."""
 
     def __init__(self, tpl, params, moves=ALL_MOVES, score_diff=12.5, fast_threshold=-12.5, add_threshold=1.0,
-                 sum_product=False):
+                 sum_product=False, recursor="SparseSse"):
+        k = QUIVER_RECURSORS.index(recursor)
+        flags = (1 if sum_product else 0) | (2 if k in (1, 3) else 0) | (4 if k >= 2 else 0)
         self._h = _qlib().qorc_scorer_new(tpl.encode(), _farr(qv_params(params)), moves, score_diff, fast_threshold,
-                                          add_threshold, 1 if sum_product else 0)
+                                          add_threshold, flags)
 
     def __del__(self):
         if getattr(self, "_h", None):

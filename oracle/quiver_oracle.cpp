@@ -157,6 +157,8 @@ struct QuiverConfig {
     float fastScoreThreshold = -12.5f;
     float addThreshold = 1.0f;
     bool sumProduct = false;   // SparseSseQvRecursor (Viterbi) or SparseSseQvSumProductRecursor
+    bool simple = false;       // SimpleRecursor family (SimpleQvRecursor, SparseSimpleQvRecursor)
+    bool dense = false;        // DenseMatrixF storage (SimpleQvRecursor, SseQvRecursor)
 };
 
 // ---------------------------------------------------------------- read features (Features.hpp:52-114)
@@ -280,8 +282,11 @@ struct QMatrix {
         for (int j = 0; j < cols; ++j) s += ue[j] - ub[j];
         return s;
     }
+    bool dense = false;   // DenseMatrixF: the same values (ClearColumn resets the previous used range to
+                          // lfloat(), DenseMatrix-inl.hpp:158-172), every cell allocated
     long long AllocatedEntries() const
     {
+        if (dense) return (long long)rows * cols;   // DenseMatrix-inl.hpp:242-246
         long long s = 0;
         for (const Column& col : c) s += col.exists ? (long long)col.store.capacity() : 0;
         return s;
@@ -299,6 +304,112 @@ struct Recursor {
     int moves = ALL_MOVES;
     float scoreDiff = 12.5f;
     Combiner Cb;
+    bool simple = false;   // SimpleRecursor (Quiver/SimpleRecursor.cpp) instead of SseRecursor
+    bool dense = false;    // DenseMatrixF storage (SimpleQvRecursor / SseQvRecursor)
+
+    // ---- SimpleRecursor (Quiver/SimpleRecursor.cpp:60-405): row by row, moves combined in the order
+    // Incorporate, Extra, Delete, Merge, the band end tested after every row
+    void FillAlphaSimple(const Evaluator& e, const QMatrix& guide, QMatrix& a) const   // :60-135
+    {
+        const int I = e.I(), J = e.J();
+        int hb = 0, he = 0;
+        for (int j = 0; j <= J; ++j) {
+            Guide(j, guide, a, &hb, &he);
+            const int reqEnd = std::min(I + 1, he);
+            float score = NEG_INF, thr = NEG_INF, mx = NEG_INF;
+            a.Start(j, hb, he);
+            const int beginRow = hb;
+            int i;
+            for (i = beginRow; i < I + 1 && (score >= thr || i < reqEnd); ++i) {
+                score = NEG_INF;
+                if (i == 0 && j == 0) score = 0.0f;
+                if (i > 0 && j > 0) score = Cb.C(score, a.Get(i - 1, j - 1) + e.Inc(i - 1, j - 1));
+                if (i > 0) score = Cb.C(score, a.Get(i - 1, j) + e.Extra(i - 1, j));
+                if (j > 0) score = Cb.C(score, a.Get(i, j - 1) + e.Del(i, j - 1));
+                if ((moves & MERGE) && j > 1 && i > 0) score = Cb.C(score, a.Get(i - 1, j - 2) + e.Merge(i - 1, j - 2));
+                a.Set(i, j, score);
+                if (score > mx) { mx = score; thr = mx - scoreDiff; }
+            }
+            const int endRow = i;
+            a.Finish(j, beginRow, endRow);
+            he = endRow;
+            for (i = beginRow; i < endRow && a.Get(i, j) < thr; ++i) {}
+            hb = i;
+        }
+    }
+
+    void FillBetaSimple(const Evaluator& e, const QMatrix& guide, QMatrix& b) const   // :138-222
+    {
+        const int I = e.I(), J = e.J();
+        int hb = I + 1, he = I + 1;
+        for (int j = J; j >= 0; --j) {
+            Guide(j, guide, b, &hb, &he);
+            const int reqBegin = std::max(0, hb);
+            b.Start(j, hb, he);
+            float score = NEG_INF, thr = NEG_INF, mx = NEG_INF;
+            const int endRow = he;
+            int i;
+            for (i = endRow - 1; i >= 0 && (score >= thr || i >= reqBegin); --i) {
+                score = NEG_INF;
+                if (i == I && j == J) score = 0.0f;
+                if (i < I && j < J) score = Cb.C(score, b.Get(i + 1, j + 1) + e.Inc(i, j));
+                if (i < I) score = Cb.C(score, b.Get(i + 1, j) + e.Extra(i, j));
+                if (j < J) score = Cb.C(score, b.Get(i, j + 1) + e.Del(i, j));
+                if ((moves & MERGE) && j < J - 1 && i < I) score = Cb.C(score, b.Get(i + 1, j + 2) + e.Merge(i, j));
+                b.Set(i, j, score);
+                if (score > mx) { mx = score; thr = mx - scoreDiff; }
+            }
+            const int beginRow = i + 1;
+            b.Finish(j, beginRow, endRow);
+            hb = beginRow;
+            for (i = endRow; i > beginRow && b.Get(i - 1, j) < thr; --i) {}
+            he = i;
+        }
+    }
+
+    // :232-295 -- the merge terms are added whatever movesAvailable_ says (no MERGE test in the reference)
+    float LinkSimple(const Evaluator& e, const QMatrix& a, int ac, const QMatrix& b, int bc, int absc) const
+    {
+        const int I = e.I();
+        const int ub = RangeUnion4b(a, ac, b, bc), ue = RangeUnion4e(a, ac, b, bc);
+        float v = NEG_INF;
+        for (int i = ub; i < ue; i++) {
+            if (i < I) {
+                v = Cb.C(v, a.Get(i, ac - 1) + e.Inc(i, absc - 1) + b.Get(i + 1, bc));
+                v = Cb.C(v, a.Get(i, ac - 2) + e.Merge(i, absc - 2) + b.Get(i + 1, bc));
+                v = Cb.C(v, a.Get(i, ac - 1) + e.Merge(i, absc - 1) + b.Get(i + 1, bc + 1));
+            }
+            v = Cb.C(v, a.Get(i, ac - 1) + e.Del(i, absc - 1) + b.Get(i, bc));
+        }
+        return v;
+    }
+
+    // :303-388 (the merge term reads alpha(i - 1, j - 2) for every extension column, as the reference does)
+    void ExtendAlphaSimple(const Evaluator& e, const QMatrix& a, int beginColumn, QMatrix& ext, int numExt) const
+    {
+        for (int extCol = 0; extCol < numExt; extCol++) {
+            const int j = beginColumn + extCol;
+            int beginRow, endRow;
+            if (j < a.cols) { beginRow = a.ub[j]; endRow = a.ue[j]; }
+            else { beginRow = a.ub[a.cols - 1]; endRow = a.rows; }
+            ext.Start(extCol, beginRow, endRow);
+            for (int i = beginRow; i < endRow; i++) {
+                float score = NEG_INF;
+                if (i > 0 && j > 0) {
+                    const float prev = extCol == 0 ? a.Get(i - 1, j - 1) : ext.Get(i - 1, extCol - 1);
+                    score = Cb.C(score, prev + e.Inc(i - 1, j - 1));
+                }
+                if (i > 0) score = Cb.C(score, ext.Get(i - 1, extCol) + e.Extra(i - 1, j));
+                if (j > 0) {
+                    const float prev = extCol == 0 ? a.Get(i, j - 1) : ext.Get(i, extCol - 1);
+                    score = Cb.C(score, prev + e.Del(i, j - 1));
+                }
+                if ((moves & MERGE) && j > 1 && i > 0) score = Cb.C(score, a.Get(i - 1, j - 2) + e.Merge(i - 1, j - 2));
+                ext.Set(i, extCol, score);
+            }
+            ext.Finish(extCol, beginRow, endRow);
+        }
+    }
 
     // RowRange (RecursorBase-inl.hpp:49-82): trims the used range to the rows within scoreDiff of its max
     void RowRange(int j, const QMatrix& m, int* ob, int* oe) const
@@ -335,6 +446,7 @@ struct Recursor {
     // SseRecursor::FillAlpha (SseRecursor.cpp:73-213)
     void FillAlpha(const Evaluator& e, const QMatrix& guide, QMatrix& a) const
     {
+        if (simple) return FillAlphaSimple(e, guide, a);
         const int I = e.I(), J = e.J();
         int hb = 0, he = 0;
         for (int j = 0; j <= J; ++j) {
@@ -384,6 +496,7 @@ struct Recursor {
     // SseRecursor::FillBeta (SseRecursor.cpp:216-353)
     void FillBeta(const Evaluator& e, const QMatrix& guide, QMatrix& b) const
     {
+        if (simple) return FillBetaSimple(e, guide, b);
         const int I = e.I(), J = e.J();
         int hb = I + 1, he = I + 1;
         for (int j = J; j >= 0; --j) {
@@ -436,6 +549,7 @@ struct Recursor {
     // SseRecursor::LinkAlphaBeta (SseRecursor.cpp:355-431)
     float Link(const Evaluator& e, const QMatrix& a, int ac, const QMatrix& b, int bc, int absc) const
     {
+        if (simple) return LinkSimple(e, a, ac, b, bc, absc);
         const int I = e.I();
         // RangeUnion of the four used ranges (Interval.hpp:80-99: min of begins, max of ends)
         const int ub = RangeUnion4b(a, ac, b, bc);
@@ -481,6 +595,7 @@ struct Recursor {
     // SseRecursor::ExtendAlpha (SseRecursor.cpp:433-551)
     void ExtendAlpha(const Evaluator& e, const QMatrix& a, int beginColumn, QMatrix& ext, int numExt) const
     {
+        if (simple) return ExtendAlphaSimple(e, a, beginColumn, ext, numExt);
         for (int extCol = 0; extCol < numExt; extCol++) {
             const int j = beginColumn + extCol;
             int beginRow, endRow;
@@ -599,6 +714,7 @@ struct MutationScorer {
         alpha = QMatrix(ev.I() + 1, ev.J() + 1);
         beta = QMatrix(ev.I() + 1, ev.J() + 1);
         ext = QMatrix(ev.I() + 1, 8);   // EXTEND_BUFFER_COLUMNS
+        alpha.dense = beta.dense = rec.dense;
         flips = rec.FillAlphaBeta(ev, alpha, beta);
     }
     float Score() const { return beta.Get(0, 0); }
@@ -607,6 +723,7 @@ struct MutationScorer {
         ev.tpl = tpl;
         alpha = QMatrix(ev.I() + 1, ev.J() + 1);
         beta = QMatrix(ev.I() + 1, ev.J() + 1);
+        alpha.dense = beta.dense = rec.dense;
         rec.FillAlphaBeta(ev, alpha, beta);
     }
     float ScoreMutation(const Mut& m)   // :113-226 (absolute score of the mutated template)
@@ -785,6 +902,8 @@ struct MultiReadScorer {
         rec.moves = c.moves;
         rec.scoreDiff = c.scoreDiff;
         rec.Cb.sumProduct = c.sumProduct;
+        rec.simple = c.simple;
+        rec.dense = c.dense;
         reads.push_back(rs);
         ReadState& st = reads.back();
         MutationScorer* s = nullptr;
@@ -934,7 +1053,8 @@ float qorc_exp_ps(float x) { return exp_ps1(x); }
 float qorc_log_ps(float x) { return log_ps1(x); }
 
 // params: Match, Mismatch, MismatchS, Branch, BranchS, DeletionN, DeletionWithTag, DeletionWithTagS, Nce, NceS,
-//         Merge[4], MergeS[4]  (20 floats)
+//         Merge[4], MergeS[4]  (20 floats).  sumProduct bits: 1 sum-product combiner, 2 SimpleRecursor,
+//         4 DenseMatrixF (MutationScorer.hpp:93-99's SimpleQvRecursor / SseQvRecursor / Sparse* typedefs)
 void* qorc_scorer_new(const char* tpl, const float* params, int moves, float scoreDiff, float fastThr, float addThr,
                       int sumProduct)
 {
@@ -951,7 +1071,9 @@ void* qorc_scorer_new(const char* tpl, const float* params, int moves, float sco
     c.scoreDiff = scoreDiff;
     c.fastScoreThreshold = fastThr;
     c.addThreshold = addThr;
-    c.sumProduct = sumProduct != 0;
+    c.sumProduct = (sumProduct & 1) != 0;
+    c.simple = (sumProduct & 2) != 0;   // bit 1: SimpleRecursor, bit 2: DenseMatrixF (see qorc_scorer_new)
+    c.dense = (sumProduct & 4) != 0;
     s->configs.InsertAs("*", c);
     s->Init(tpl);
     return s;

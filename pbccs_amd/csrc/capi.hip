@@ -989,6 +989,8 @@ quiver::QParams qparams(const pbccs_quiver_config& c)
     p.addThreshold = c.add_threshold;
     p.moves = c.moves_available;
     p.sumProduct = c.sum_product ? 1 : 0;
+    p.simple = (c.recursor == PBCCS_QV_RECURSOR_SPARSE_SIMPLE || c.recursor == PBCCS_QV_RECURSOR_DENSE_SIMPLE) ? 1 : 0;
+    p.dense = (c.recursor == PBCCS_QV_RECURSOR_DENSE_SSE || c.recursor == PBCCS_QV_RECURSOR_DENSE_SIMPLE) ? 1 : 0;
     return p;
 }
 
@@ -1022,6 +1024,9 @@ int pbccs_quiver_scorer_create(pbccs_engine* eng, const pbccs_quiver_config* con
                                int n_configs, const char* tpl, int tpl_len, pbccs_quiver_scorer** out)
 {
     if (!eng || !configs || n_configs < 1 || !tpl || tpl_len <= 0 || !out) return fail(PBCCS_EINVAL, "bad argument");
+    for (int k = 0; k < n_configs; ++k)
+        if (configs[k].recursor < PBCCS_QV_RECURSOR_SPARSE_SSE || configs[k].recursor > PBCCS_QV_RECURSOR_DENSE_SIMPLE)
+            return fail(PBCCS_EINVAL, "unknown recursor type");
     return guarded([&] {
         std::unique_ptr<pbccs_quiver_scorer> s(new pbccs_quiver_scorer());
         s->eng = eng;

@@ -33,6 +33,8 @@ struct QParams {
     float scoreDiff, fastThreshold, addThreshold;
     int moves;
     int sumProduct;
+    int simple;   // SimpleRecursor fills / extend / link (else SseRecursor)
+    int dense;    // DenseMatrixF storage: column j at j * (I + 1), AllocatedEntries = (I + 1)(J + 1)
 };
 
 // ---- Cephes exp_ps / log_ps (detail/sse_mathfun.h:167-350), one lane -----------------------------------

@@ -51,6 +51,18 @@ __device__ __forceinline__ void put(const QBand& m, long long k, float v, bool& 
     else ovf = true;
 }
 
+// Where column j's first used row goes in its arena: packed after the previous columns (SparseMatrixF), or
+// at j * (I + 1) + row (DenseMatrixF: every cell has its place, DenseMatrix-inl.hpp:212-221).
+__device__ __forceinline__ long long col_base(const QEval& e, int j, int beginRow, long long used)
+{
+    return e.p->dense ? (long long)j * (e.I() + 1) + beginRow : used;
+}
+// values an arena must hold for one pass
+__device__ __forceinline__ long long values_needed(const QEval& e, long long used)
+{
+    return e.p->dense ? (long long)(e.J() + 1) * (e.I() + 1) : used;
+}
+
 // ---- SseRecursor::FillAlpha (SseRecursor.cpp:73-213) -----------------------------------------------------
 // `prev`: this matrix's previous pass (RangeGuide's self hint); `out`: the arena written now.  Rows come
 // top-down, so column j's cells are appended at `used` as they are produced.
@@ -69,14 +81,27 @@ __device__ __forceinline__ long long fill_alpha(const QEval& e, const QBand* gui
         float score = kNegInf, thr = kNegInf, mx = kNegInf;
         if (alloc) alloc_start(alloc[j], allocExists, hb, he, I + 1);
         const int beginRow = hb;
-        out.off[j] = (int)min(used, (long long)0x7fffffff);
+        const long long base = col_base(e, j, beginRow, used);
+        out.off[j] = (int)min(base, (long long)0x7fffffff);
         out.range[j] = make_int2(beginRow, beginRow);   // grows with each row, so reads of it stay exact
         auto set = [&](int r, float v) {
-            put(out, used + (r - beginRow), v, ovf);
+            put(out, base + (r - beginRow), v, ovf);
             out.range[j].y = r + 1;
             if (alloc) alloc_set(alloc[j], r, I + 1);
         };
         int i;
+        if (e.p->simple) {   // SimpleRecursor::FillAlpha (Quiver/SimpleRecursor.cpp:60-135): row by row
+            for (i = beginRow; i < I + 1 && (score >= thr || i < reqEnd); ++i) {
+                score = kNegInf;
+                if (i == 0 && j == 0) score = 0.0f;
+                if (i > 0 && j > 0) score = comb(sp, score, out.Get(i - 1, j - 1) + e.Inc(i - 1, j - 1));
+                if (i > 0) score = comb(sp, score, out.Get(i - 1, j) + e.Extra(i - 1, j));
+                if (j > 0) score = comb(sp, score, out.Get(i, j - 1) + e.Del(i, j - 1));
+                if (merge && j > 1 && i > 0) score = comb(sp, score, out.Get(i - 1, j - 2) + e.Merge(i - 1, j - 2));
+                set(i, score);
+                if (score > mx) { mx = score; thr = mx - sd; }
+            }
+        } else {
         for (i = beginRow; (i == 0 || (I - i + 1) % 4 != 0) && i <= I; i++) {
             score = kNegInf;
             if (i == 0 && j == 0) score = 0.0f;
@@ -110,6 +135,7 @@ __device__ __forceinline__ long long fill_alpha(const QEval& e, const QBand* gui
             score = pmin;
             if (pmax > mx) { mx = pmax; thr = mx - sd; }
         }
+        }
         const int endRow = i;
         out.range[j] = make_int2(beginRow, endRow);
         used += endRow - beginRow;
@@ -117,7 +143,7 @@ __device__ __forceinline__ long long fill_alpha(const QEval& e, const QBand* gui
         for (i = beginRow; i < endRow && out.Get(i, j) < thr; ++i) {}
         hb = i;
     }
-    return used;
+    return values_needed(e, used);
 }
 
 // ---- SseRecursor::FillBeta (SseRecursor.cpp:216-353) -----------------------------------------------------
@@ -149,6 +175,19 @@ __device__ __forceinline__ long long fill_beta(const QEval& e, const QBand* guid
             if (alloc) alloc_set(alloc[j], r, I + 1);
         };
         int i;
+        if (e.p->simple) {   // SimpleRecursor::FillBeta (Quiver/SimpleRecursor.cpp:138-222): row by row
+            for (i = endRow - 1; i >= 0 && (score >= thr || i >= reqBegin); --i) {
+                score = kNegInf;
+                if (i == I && j == J) score = 0.0f;
+                if (i < I && j < J) score = comb(sp, score, get(i + 1, j + 1) + e.Inc(i, j));
+                if (i < I) score = comb(sp, score, get(i + 1, j) + e.Extra(i, j));
+                if (j < J) score = comb(sp, score, get(i, j + 1) + e.Del(i, j));
+                if (merge && j < J - 1 && i < I) score = comb(sp, score, get(i + 1, j + 2) + e.Merge(i, j));
+                set(i, score);
+                if (score > mx) { mx = score; thr = mx - sd; }
+            }
+            i = i - 3;   // so that beginRow = i + 4 below is the first row set
+        } else {
         for (i = endRow - 1; (i == I || (i + 1) % 4 != 0) && i >= 0; i--) {
             score = kNegInf;
             if (i == I && j == J) score = 0.0f;
@@ -183,16 +222,18 @@ __device__ __forceinline__ long long fill_beta(const QEval& e, const QBand* guid
             score = pmin;
             if (pmax > mx) { mx = pmax; thr = mx - sd; }
         }
+        }
         const int beginRow = i + 4;
-        out.off[j] = (int)min(used, (long long)0x7fffffff);
-        for (int r = beginRow; r < endRow; ++r) put(out, used + (r - beginRow), colbuf[r], ovf);
+        const long long base = col_base(e, j, beginRow, used);
+        out.off[j] = (int)min(base, (long long)0x7fffffff);
+        for (int r = beginRow; r < endRow; ++r) put(out, base + (r - beginRow), colbuf[r], ovf);
         out.range[j] = make_int2(beginRow, endRow);
         used += endRow - beginRow;
         hb = beginRow;
         for (i = endRow; i > beginRow && out.Get(i - 1, j) < thr; i--) {}
         he = i;
     }
-    return used;
+    return values_needed(e, used);
 }
 
 // ---- SseRecursor::ExtendAlpha (SseRecursor.cpp:433-551) --------------------------------------------------
@@ -245,6 +286,41 @@ __device__ __forceinline__ void extend_alpha(const QEval& e, const QBand& a, int
     }
 }
 
+// ---- SimpleRecursor::ExtendAlpha (Quiver/SimpleRecursor.cpp:303-388) --------------------------------------
+// Row by row; the merge term reads alpha(i - 1, j - 2) for every extension column, as the reference does.
+__device__ __forceinline__ void extend_alpha_simple(const QEval& e, const QBand& a, int beginColumn, const QBand& ext,
+                                                    int numExt, bool& ovf)
+{
+    const bool sp = e.p->sumProduct != 0;
+    const bool merge = (e.p->moves & kMerge) != 0;
+    long long used = 0;
+    for (int c = 0; c < numExt; c++) {
+        const int j = beginColumn + c;
+        int beginRow, endRow;
+        if (j < a.cols) { beginRow = a.range[j].x; endRow = a.range[j].y; }
+        else { beginRow = a.range[a.cols - 1].x; endRow = e.I() + 1; }
+        ext.off[c] = (int)used;
+        ext.range[c] = make_int2(beginRow, beginRow);
+        for (int i = beginRow; i < endRow; i++) {
+            float score = kNegInf;
+            if (i > 0 && j > 0) {
+                const float prev = c == 0 ? a.Get(i - 1, j - 1) : ext.Get(i - 1, c - 1);
+                score = comb(sp, score, prev + e.Inc(i - 1, j - 1));
+            }
+            if (i > 0) score = comb(sp, score, ext.Get(i - 1, c) + e.Extra(i - 1, j));
+            if (j > 0) {
+                const float prev = c == 0 ? a.Get(i, j - 1) : ext.Get(i, c - 1);
+                score = comb(sp, score, prev + e.Del(i, j - 1));
+            }
+            if (merge && j > 1 && i > 0) score = comb(sp, score, a.Get(i - 1, j - 2) + e.Merge(i - 1, j - 2));
+            put(ext, used + (i - beginRow), score, ovf);
+            ext.range[c].y = i + 1;
+        }
+        ext.range[c] = make_int2(beginRow, endRow);
+        used += max(0, endRow - beginRow);
+    }
+}
+
 // ---- SimpleRecursor::ExtendBeta (Quiver/SimpleRecursor.cpp:407-495) ---------------------------------------
 __device__ __forceinline__ void extend_beta(const QEval& e, const QBand& b, int lastColumn, const QBand& ext, int numExt,
                             int lengthDiff, bool& ovf)
@@ -291,6 +367,18 @@ __device__ __forceinline__ float link_alpha_beta(const QEval& e, const QBand& a,
     const int I = e.I();
     const int ub = min(min(a.range[ac - 2].x, a.range[ac - 1].x), min(b.range[bc].x, b.range[bc + 1].x));
     const int ue = max(max(a.range[ac - 2].y, a.range[ac - 1].y), max(b.range[bc].y, b.range[bc + 1].y));
+    if (e.p->simple) {   // SimpleRecursor::LinkAlphaBeta (Quiver/SimpleRecursor.cpp:232-295): merges always added
+        float v = kNegInf;
+        for (int i = ub; i < ue; i++) {
+            if (i < I) {
+                v = comb(sp, v, a.Get(i, ac - 1) + e.Inc(i, absc - 1) + b.Get(i + 1, bc));
+                v = comb(sp, v, a.Get(i, ac - 2) + e.Merge(i, absc - 2) + b.Get(i + 1, bc));
+                v = comb(sp, v, a.Get(i, ac - 1) + e.Merge(i, absc - 1) + b.Get(i + 1, bc + 1));
+            }
+            v = comb(sp, v, a.Get(i, ac - 1) + e.Del(i, absc - 1) + b.Get(i, bc));
+        }
+        return v;
+    }
     float v = kNegInf;
     float v4[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
     int i;
@@ -463,8 +551,9 @@ __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ 
     B.rCurB[r] = curB - 2;
     B.rFlips[r] = flips;
     B.rScore[r] = b_start();
-    B.rAlloc[2 * r] = allocated_entries(v.allocA, J + 1);
-    B.rAlloc[2 * r + 1] = allocated_entries(v.allocB, J + 1);
+    const long long full = (long long)(I + 1) * (J + 1);   // DenseMatrix::AllocatedEntries = Rows * Columns
+    B.rAlloc[2 * r] = e.p->dense ? full : allocated_entries(v.allocA, J + 1);
+    B.rAlloc[2 * r + 1] = e.p->dense ? full : allocated_entries(v.allocB, J + 1);
     B.rStatus[r] = ((double)fabsf(a_end() - b_start()) > 0.2) ? kQMismatch : kQOk;
 }
 
@@ -538,14 +627,16 @@ __global__ void __launch_bounds__(64) k_qscore(QBatch B, QScoreWork W)
             need += (j < a.cols) ? (a.range[j].y - a.range[j].x) : (I + 1 - a.range[a.cols - 1].x);
         }
         if (!alloc(max(need, 1LL))) { W.delta[t] = __builtin_nanf(""); return; }
-        extend_alpha(e, a, extStart, ext, extLen, ovf);
+        if (e.p->simple) extend_alpha_simple(e, a, extStart, ext, extLen, ovf);
+        else extend_alpha(e, a, extStart, ext, extLen, ovf);
         score = link_alpha_beta(e, ext, extLen, b, betaLinkCol, absLinkCol);
     } else if (!atBegin && atEnd) {
         const int extStart = os - 1;
         const int extLen = newLen - extStart + 1;
         if (extLen > 8) { atomicOr(W.overflow, 2); W.delta[t] = __builtin_nanf(""); return; }
         if (!alloc((long long)extLen * (I + 1))) { W.delta[t] = __builtin_nanf(""); return; }
-        extend_alpha(e, a, extStart, ext, extLen, ovf);
+        if (e.p->simple) extend_alpha_simple(e, a, extStart, ext, extLen, ovf);
+        else extend_alpha(e, a, extStart, ext, extLen, ovf);
         score = ext.Get(I, extLen - 1);
     } else if (atBegin && !atEnd) {
         const int extLast = oe;

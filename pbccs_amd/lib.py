@@ -77,7 +77,7 @@ class CQvModelParams(ctypes.Structure):
 class CQuiverConfig(ctypes.Structure):
     _fields_ = [("params", CQvModelParams), ("moves_available", ctypes.c_int), ("score_diff", ctypes.c_float),
                 ("fast_score_threshold", ctypes.c_float), ("add_threshold", ctypes.c_float),
-                ("sum_product", ctypes.c_int)]
+                ("sum_product", ctypes.c_int), ("recursor", ctypes.c_int)]
 
 
 class CPoaInput(ctypes.Structure):

@@ -36,14 +36,21 @@ class QvModelParams:
         return c
 
 
+RECURSORS = ("SparseSse", "SparseSimple", "DenseSse", "DenseSimple")   # PBCCS_QV_RECURSOR_* order
+
+
 class QuiverConfig:
-    """QuiverConfig (QuiverConfig.hpp:181-199); BandingOptions(diagCross, scoreDiff) -> score_diff."""
+    """QuiverConfig (QuiverConfig.hpp:181-199); BandingOptions(diagCross, scoreDiff) -> score_diff.
+    recursor picks the recursor type of ConsensusCore's typedefs (Quiver/MutationScorer.hpp:93-99):
+    SparseSse (SparseSseQvRecursor, the MultiReadMutationScorer default), SparseSimple, DenseSse
+    (SseQvRecursor) or DenseSimple (SimpleQvRecursor)."""
 
     def __init__(self, params, moves=ALL_MOVES, score_diff=12.5, fast_score_threshold=-12.5, add_threshold=1.0,
-                 sum_product=False):
+                 sum_product=False, recursor="SparseSse"):
         self.QvParams, self.MovesAvailable = params, moves
         self.ScoreDiff, self.FastScoreThreshold, self.AddThreshold = score_diff, fast_score_threshold, add_threshold
         self.SumProduct = sum_product
+        self.Recursor = recursor
 
     def _c(self):
         c = _lib_mod.CQuiverConfig()
@@ -53,6 +60,7 @@ class QuiverConfig:
         c.fast_score_threshold = self.FastScoreThreshold
         c.add_threshold = self.AddThreshold
         c.sum_product = 1 if self.SumProduct else 0
+        c.recursor = RECURSORS.index(self.Recursor)
         return c
 
 

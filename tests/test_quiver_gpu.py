@@ -21,12 +21,12 @@ class GpuQuiver:
     """Adapter with the oracle's QuiverScorer call shape over pbccs_amd's QuiverMultiReadMutationScorer."""
 
     def __init__(self, tpl, params, moves=15, score_diff=12.5, fast_threshold=-12.5, add_threshold=1.0,
-                 sum_product=False):
+                 sum_product=False, recursor="SparseSse"):
         import pbccs_amd as P
         self.P = P
         qp = P.QvModelParams(**params)
         cfg = P.QuiverConfig(qp, moves=moves, score_diff=score_diff, fast_score_threshold=fast_threshold,
-                             add_threshold=add_threshold, sum_product=sum_product)
+                             add_threshold=add_threshold, sum_product=sum_product, recursor=recursor)
         self.s = P.QuiverMultiReadMutationScorer(cfg, tpl)
 
     def add_read(self, seq, strand=0, ts=0, te=None, features=None, threshold=None):
@@ -164,3 +164,39 @@ def test_quiver_alignment_sum_product_refused():
     g.add_read(reads[0]["seq"], reads[0]["strand"], reads[0]["ts"], reads[0]["te"], reads[0]["features"])
     with pytest.raises(PbccsError):
         g.alignment(0)
+
+
+@pytest.mark.parametrize("recursor", ["SparseSimple", "DenseSse", "DenseSimple"])
+def test_quiver_kats_all_recursor_types(recursor):
+    """ConsensusCore's typed Quiver tests run every recursor type (TestRecursors.cpp:63-66,
+    TestMutationScorer.cpp:59-62) against the same expectations: replay every KAT with each."""
+    for k in KATS["kats"]:
+        run_kat(lambda tpl, params, **kw: GpuQuiver(tpl, params, recursor=recursor, **kw), k, KATS["params"])
+
+
+@pytest.mark.parametrize("recursor", ["SparseSimple", "DenseSse", "DenseSimple"])
+@pytest.mark.parametrize("sum_product", [False, True])
+def test_quiver_recursor_types_match_oracle(recursor, sum_product):
+    """Simple / dense recursors against the restatement: baseline scores, flip-flops, every unique mutation's
+    score, AllocatedEntries (dense: Rows * Columns) and -- Viterbi -- every read's alignment."""
+    tpl, reads = _zmw(121, 150, 4)
+    g = GpuQuiver(tpl, PARAMS2, sum_product=sum_product, recursor=recursor)
+    o = O.QuiverScorer(tpl, PARAMS2, sum_product=sum_product, recursor=recursor)
+    for r in reads:
+        assert bool(g.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"])) == \
+            bool(o.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"]))
+    active = [k for k in range(len(reads)) if o.read_info(k)["active"]]
+    assert g.s.BaselineScores() == [o.read_info(k)["score"] for k in active]
+    assert [g.s.NumFlipFlops()[k] for k in active] == [o.read_info(k)["flipflops"] for k in active]
+    for k in active:
+        ga, gb = g.s.AllocatedEntries(k)
+        info = o.read_info(k)
+        assert (ga, gb) == info["allocated"]
+        if recursor.startswith("Dense"):
+            assert ga == (len(reads[k]["seq"]) + 1) * (reads[k]["te"] - reads[k]["ts"] + 1)
+        if not sum_product:
+            assert g.alignment(k) == o.alignment(k)
+    muts = O.unique_mutations(tpl)
+    vals = g.s.ScoreMany([g.P.Mutation(t, s, b) for (t, s, b) in muts])
+    for (t, s, b), v in zip(muts, vals):
+        assert v == o.score(t, s, b), (t, s, b)
