@@ -408,13 +408,10 @@ def poa_stage(args, rank, world, eng, barrier, sync, seed0):
 
 
 def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
-    """configs[1] end to end from raw subreads: per step, FilterReads + POA (pbccs_poa_batch) +
-    ExtractMappedRead (driver.zmw_inputs_batch) on a producer thread, then the Arrow polish of those ZMWs
-    (pbccs_batch_create + pbccs_batch_polish_many over the slots).  Steps are pipelined: the POA of the
-    next steps runs while the current group polishes.  value = ZMWs/s from raw subreads to polished
-    consensus; the ZMWs that end before the polish (NoSubreads / TooShort) count in the status table."""
-    import queue
-    import threading
+    """configs[1] end to end from raw subreads in one native call (pbccs_ccs_batch): Consensus.h's
+    FilterReads, the POA draft on the GPU, TooShort, ExtractMappedRead and the polish through the ZMW work
+    queue, for steps x zmws-per-step ZMWs.  value = ZMWs/s from raw subreads (host memory) to polished
+    consensus; the ZMWs that end before the polish count in the status table."""
     import pbccs_amd
     from pbccs_amd import driver, synth
 
@@ -422,63 +419,33 @@ def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
         return [{"snr": z["snr"], "reads": [{"seq": r["seq"]} for r in z["reads"]]}
                 for z in synth.make_zmws(n, args.length, args.passes, seed=seed)]
 
-    def run(step_chunks):
-        q = queue.Queue(maxsize=2 * slots)
-        pre = {}
-
-        def producer():
-            for k, c in enumerate(step_chunks):
-                ins = driver.zmw_inputs_batch(c, engine=eng)
-                q.put((k, ins))
-            q.put(None)
-
-        th = threading.Thread(target=producer)
-        th.start()
-        results, group, done = [], [], False
-        while not done:
-            item = q.get()
-            if item is None:
-                done = True
-            else:
-                k, ins = item
-                pre[k] = ins
-                zmws = [z for st, z in ins if st is None]
-                group.append((k, pbccs_amd.PreparedBatch(zmws, settings, eng)))
-            if group and (len(group) == slots or done):
-                pbccs_amd.polish_many([b for _, b in group])
-                for k, b in group:
-                    res = iter(b.results())
-                    results.append([next(res) if st is None else {"status": st} for st, _ in pre[k]])
-                    b.close()
-                group = []
-        th.join()
-        return results
-
-    run([chunks(args.zmws_per_step, seed0 + 1000 + w) for w in range(args.warmup)])
-    steps_in = [chunks(args.zmws_per_step, seed0 + k) for k in range(args.steps)]
+    for w in range(args.warmup):
+        driver.ccs_batch(chunks(args.zmws_per_step, seed0 + 1000 + w), settings, eng)
+    work = [c for k in range(args.steps) for c in chunks(args.zmws_per_step, seed0 + k)]
     eng.kernel_stats(reset=True)
     barrier()
     sync()
     t0 = time.perf_counter()
-    res = run(steps_in)
+    res = driver.ccs_batch(work, settings, eng)
     sync()
     barrier()
     local_time = time.perf_counter() - t0
     job_time = max_over_ranks(local_time, world)
     statuses = {}
-    for step in res:
-        for r in step:
-            statuses[r["status"]] = statuses.get(r["status"], 0) + 1
-    total = args.steps * args.zmws_per_step * world
+    for r in res:
+        statuses[r["status"]] = statuses.get(r["status"], 0) + 1
+    from pbccs_amd import poa
+    st = poa.poa_stats(eng, reset=True)
+    total = len(work) * world
     out = {"metric": "CCS ZMWs/sec end to end from raw subreads (FilterReads, POA, polish) on MI355X",
            "value": round(total / job_time, 3), "unit": "ZMWs/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(job_time / args.steps * 1e3, 3), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64 (polish) / int32-uint16 (POA)",
            "data": "synthetic subreads (SURVEY.md §8(d): truth iid ACGT; 7%/4%/1% ins/del/sub; odd passes RC)",
            "config": {"workload": f"configs[1] end to end: {args.length} bp insert, {args.passes} subreads per "
-                                  f"ZMW, {args.zmws_per_step} ZMWs per step", "slots": slots,
-                      "parallelism": f"zmw-shard x{world}"},
-           "zmw_status": statuses}
+                                  f"ZMW, {args.steps} x {args.zmws_per_step} ZMWs in one pbccs_ccs_batch",
+                      "slots": slots, "parallelism": f"zmw-shard x{world}"},
+           "zmw_status": statuses, "poa_wall_ms": round(st["total_ms"], 1)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

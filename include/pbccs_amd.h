@@ -366,6 +366,32 @@ int pbccs_sparse_poa_graphviz(pbccs_sparse_poa* p, int flags, int min_coverage, 
 int pbccs_poa_consensus(pbccs_engine* eng, const char* const* reads, const int* lens, int n, int mode,
                         int min_coverage, char* out, int cap, int* len, int flags, char* dot, int dot_cap,
                         int* dot_len);
+/* ---- ccs end to end: Consensus.h's per-ZMW driver for many ZMWs -------------------------------------
+ * Each chunk is one ZMW after ccs.cpp's grouping gates (src/main/ccs.cpp:402-475: PoorSNR, read score,
+ * TooFewPasses).  pbccs_ccs_batch runs include/pacbio/ccs/Consensus.h:395-552 for all of them:
+ * FilterReads (NO_SUBREADS when nothing is left), the POA draft on the GPU (pbccs_poa_batch, with
+ * max_poa_coverage), TOO_SHORT for a draft below opts->min_length, ExtractMappedRead per POA key, and the
+ * polish (pbccs_polish_batch: AddRead gates, RefineConsensus, ConsensusQVs, the accuracy gate).
+ * out[z].polish.add_read_results / zscores are indexed by POA key (size them by n_subreads; -1: not added).
+ * out[z].draft (optional, draft_cap bytes) receives the POA consensus. */
+typedef struct {
+    double snr[4];
+    int n_subreads;
+    const char* const* seqs;
+    const int* lens;
+    const unsigned char* flags;   /* LocalContextFlags per subread (ADAPTER_BEFORE 1, ADAPTER_AFTER 2); NULL: full passes */
+} pbccs_ccs_input;
+
+typedef struct {
+    pbccs_zmw_output polish;
+    char* draft;
+    int draft_cap;
+    int draft_len;
+} pbccs_ccs_output;
+
+int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long long max_poa_coverage,
+                    const pbccs_polish_options* opts, pbccs_ccs_output* out);
+
 /* POA work counters since the last reset: alignments, DP cells, fill/trace device ms (profiling on) */
 typedef struct {
     long long alignments, cells, launches, trace_steps;

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "engine.hpp"
+#include "driver.hpp"
 #include "poa_engine.hpp"
 
 using namespace pbccs;
@@ -1441,6 +1442,105 @@ int pbccs_poa_stats_get(pbccs_engine* eng, pbccs_poa_stats* out, int reset)
         *out = pbccs_poa_stats{s.alignments, s.cells,  s.launches, s.traceSteps, s.fillMs,     s.traceMs,
                                s.bytes,      s.progMs, s.deviceMs, s.threadMs,  s.consensusMs, s.totalMs};
         return PBCCS_OK;
+    });
+}
+
+int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long long max_poa_coverage,
+                    const pbccs_polish_options* opts, pbccs_ccs_output* out)
+{
+    if (!eng || n < 0 || (n > 0 && (!in || !out)) || max_poa_coverage < 1) return fail(PBCCS_EINVAL, "bad argument");
+    pbccs_polish_options o;
+    if (opts) o = *opts;
+    else pbccs_polish_options_default(&o);
+    return guarded([&] {
+        // FilterReads per ZMW (Consensus.h:411-420)
+        std::vector<std::vector<driver::Subread>> sub(n);
+        std::vector<std::vector<int>> order(n);
+        std::vector<int> live;
+        for (int z = 0; z < n; ++z) {
+            if (in[z].n_subreads < 0 || (in[z].n_subreads > 0 && (!in[z].seqs || !in[z].lens)))
+                return fail(PBCCS_EINVAL, "bad pbccs_ccs_input");
+            for (int r = 0; r < in[z].n_subreads; ++r) {
+                driver::Subread s;
+                s.seq.assign(in[z].seqs[r], in[z].lens[r]);
+                if (in[z].flags) s.flags = in[z].flags[r];
+                sub[z].push_back(std::move(s));
+            }
+            order[z] = driver::FilterReads(sub[z], (size_t)o.min_length);
+            bool any = false;
+            for (int k : order[z]) any = any || k >= 0;
+            if (any) live.push_back(z);
+            else {
+                out[z].polish.status = PBCCS_ZMW_NO_SUBREADS;
+                out[z].draft_len = 0;
+            }
+        }
+        // the POA of every live ZMW in one batch (Consensus.h:422-425, 352-390)
+        std::vector<std::vector<const std::string*>> poaReads(live.size());
+        for (size_t q = 0; q < live.size(); ++q)
+            for (int k : order[live[q]]) poaReads[q].push_back(k >= 0 ? &sub[live[q]][k].seq : nullptr);
+        std::vector<std::string> css;
+        std::vector<std::vector<int>> keys, ext;
+        std::vector<std::vector<char>> rc;
+        {
+            std::lock_guard<std::mutex> lk(eng->poaMu);
+            poa::PoaBatch(eng->PoaRunners(), poaReads, max_poa_coverage, -1, &css, &keys, &rc, &ext);
+            for (poa::PoaRunner* r : eng->PoaRunners()) r->ReleasePool();   // the polish sizes its batches from free HBM
+        }
+        // TooShort, ExtractMappedRead (Consensus.h:427-471) and the polish inputs
+        std::vector<std::vector<driver::MappedRead>> mapped(live.size());
+        std::vector<std::vector<const char*>> seqPtr(live.size());
+        std::vector<std::vector<int>> lens(live.size()), strands(live.size()), ts(live.size()), te(live.size());
+        std::vector<std::vector<unsigned char>> full(live.size()), added(live.size());
+        std::vector<pbccs_zmw_input> pin;
+        std::vector<int> pinZ;
+        for (size_t q = 0; q < live.size(); ++q) {
+            const int z = live[q];
+            if (out[z].draft && out[z].draft_cap >= (int)css[q].size()) memcpy(out[z].draft, css[q].data(), css[q].size());
+            out[z].draft_len = (int)css[q].size();
+            if ((int)css[q].size() < o.min_length) {
+                out[z].polish.status = PBCCS_ZMW_TOO_SHORT;
+                continue;
+            }
+            const std::vector<int>& kk = keys[q];
+            for (size_t i = 0; i < kk.size() && kk[i] != -2; ++i) {
+                driver::MappedRead mr;
+                const int key = kk[i];
+                const bool ok = key >= 0 &&
+                                driver::ExtractMappedRead(sub[z][order[z][i]], rc[q][key] != 0, ext[q][4 * key],
+                                                          ext[q][4 * key + 1], ext[q][4 * key + 2], ext[q][4 * key + 3],
+                                                          (size_t)o.min_length, &mr);
+                mapped[q].push_back(ok ? mr : driver::MappedRead());
+                added[q].push_back(ok ? 1 : 0);
+                full[q].push_back(ok && sub[z][order[z][i]].FullPass() ? 1 : 0);
+            }
+            for (size_t i = 0; i < mapped[q].size(); ++i) {
+                const bool ok = added[q][i] != 0;
+                seqPtr[q].push_back(ok ? mapped[q][i].seq.data() : nullptr);
+                lens[q].push_back((int)mapped[q][i].seq.size());
+                strands[q].push_back(mapped[q][i].strand);
+                ts[q].push_back(mapped[q][i].ts);
+                te[q].push_back(mapped[q][i].te);
+            }
+            pbccs_zmw_input zi;
+            zi.draft = css[q].data();
+            zi.draft_len = (int)css[q].size();
+            for (int b = 0; b < 4; ++b) zi.snr[b] = in[z].snr[b];
+            zi.n_reads = (int)mapped[q].size();
+            zi.seqs = seqPtr[q].data();
+            zi.lens = lens[q].data();
+            zi.strands = strands[q].data();
+            zi.tstarts = ts[q].data();
+            zi.tends = te[q].data();
+            zi.full_pass = full[q].data();
+            pin.push_back(zi);
+            pinZ.push_back(z);
+        }
+        std::vector<pbccs_zmw_output> pout;
+        for (int z : pinZ) pout.push_back(out[z].polish);
+        const int rc2 = pin.empty() ? PBCCS_OK : pbccs_polish_batch(eng, pin.data(), (int)pin.size(), &o, pout.data());
+        for (size_t q = 0; q < pinZ.size(); ++q) out[pinZ[q]].polish = pout[q];
+        return rc2;
     });
 }
 

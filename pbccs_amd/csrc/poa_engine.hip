@@ -656,7 +656,7 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
     if (budget == 0) {
         size_t fr = 0, tot = 0;
         check(hipMemGetInfo(&fr, &tot), "hipMemGetInfo");
-        budget = std::min<size_t>((size_t)(0.6 * (double)fr) + dPool_.mapped_bytes(), 96ull << 30);
+        budget = std::min<size_t>((size_t)(0.6 * (double)fr) + dPool_.mapped_bytes(), 64ull << 30);
         budget = std::max<size_t>(budget, 64ull << 20);
     }
     auto jobBytes = [&](const PoaJob& J) {

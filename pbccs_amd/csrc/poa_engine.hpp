@@ -108,6 +108,9 @@ public:
     void Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>* out);
 
     void SetPoolBudget(size_t bytes) { budget_ = bytes; }
+    // Unmap the score-matrix pool (the address reservation stays): the polish that follows the POA in a
+    // ccs run then has the device memory to itself.
+    void ReleasePool() { dPool_.unmap_all(); }
     int HostThreads() const { return threads_; }
     PoaStats stats;
     bool profiling = false;

@@ -148,3 +148,58 @@ def zmw_inputs_batch(chunks, min_length=10, max_poa_coverage=None, engine=None):
             reads.append(mr if mr is not None else {"seq": None, "strand": 0, "ts": 0, "te": 0, "full_pass": False})
         out[z] = (None, {"draft": draft, "snr": list(chunks[z]["snr"]), "reads": reads})
     return out
+
+
+def ccs_batch(chunks, settings=None, engine=None, max_poa_coverage=None):
+    """Consensus.h's per-ZMW driver for many ZMWs in one native call (pbccs_ccs_batch): FilterReads,
+    the GPU POA, TooShort, ExtractMappedRead and the GPU polish, with no Python between the stages.
+    chunks: [{"snr", "reads": [{"seq", "flags"?}]}].  Returns per ZMW the polish result dict (as
+    polish_zmws) plus "draft"; add_read_results / zscores are indexed by POA key."""
+    import ctypes
+    from . import ZMW_STATUS, default_engine
+    from . import lib as L
+    from .polish import ConsensusSettings
+    eng = engine or default_engine()
+    settings = settings or ConsensusSettings()
+    n = len(chunks)
+    ins = (L.CCcsInput * max(1, n))()
+    outs = (L.CCcsOutput * max(1, n))()
+    keep = []
+    for z, c in enumerate(chunks):
+        reads = c["reads"]
+        nr = len(reads)
+        enc = [r["seq"].encode() for r in reads]
+        seqs = (ctypes.c_char_p * max(1, nr))(*enc)
+        lens = (ctypes.c_int * max(1, nr))(*[len(e) for e in enc])
+        flags = (ctypes.c_ubyte * max(1, nr))(*[int(r.get("flags", FULL_PASS)) for r in reads])
+        cap = 2 * max([len(e) for e in enc] + [0]) + 64
+        cons, draft = ctypes.create_string_buffer(cap), ctypes.create_string_buffer(cap)
+        qv = (ctypes.c_int * cap)()
+        arr = (ctypes.c_int * max(1, nr))()
+        zs = (ctypes.c_double * max(1, nr))()
+        for k in range(4):
+            ins[z].snr[k] = float(c["snr"][k])
+        ins[z].n_subreads, ins[z].seqs, ins[z].lens, ins[z].flags = nr, seqs, lens, flags
+        o = outs[z]
+        o.polish.consensus = ctypes.cast(cons, ctypes.c_char_p)
+        o.polish.consensus_cap = cap
+        o.polish.qvs, o.polish.add_read_results, o.polish.zscores = qv, arr, zs
+        o.draft = ctypes.cast(draft, ctypes.c_char_p)
+        o.draft_cap = cap
+        keep.append((seqs, lens, flags, cons, draft, qv, arr, zs, nr))
+    opts = settings._c()
+    mc = 2**62 if max_poa_coverage is None else int(max_poa_coverage)
+    L.check(L.load().pbccs_ccs_batch(eng._h, ins, n, mc, ctypes.byref(opts), outs))
+    res = []
+    for z, (_, _, _, cons, draft, qv, arr, zs, nr) in enumerate(keep):
+        p = outs[z].polish
+        ok = p.status in (0, 6)
+        ln = max(0, p.consensus_len) if ok else 0
+        polished = p.status not in (1, 2)   # NoSubreads / TooShort end before the polish
+        res.append({"status": ZMW_STATUS[p.status], "status_code": p.status,
+                    "consensus": cons.raw[:ln].decode() if ok else "", "qvs": list(qv[:ln]) if ok else [],
+                    "draft": draft.raw[:max(0, outs[z].draft_len)].decode(),
+                    "add_read_results": list(arr[:nr]) if polished else [], "zscores": list(zs[:nr]) if polished else [],
+                    "zg": p.zg, "za": p.za, "predicted_accuracy": p.predicted_accuracy, "n_tested": p.n_tested,
+                    "n_applied": p.n_applied, "n_passes": p.n_passes, "status_counts": list(p.status_counts)})
+    return res

@@ -91,6 +91,16 @@ class CPoaOutput(ctypes.Structure):
                 ("extents", ctypes.POINTER(ctypes.c_int)), ("n_keys", ctypes.c_int)]
 
 
+class CCcsInput(ctypes.Structure):
+    _fields_ = [("snr", ctypes.c_double * 4), ("n_subreads", ctypes.c_int), ("seqs", ctypes.POINTER(ctypes.c_char_p)),
+                ("lens", ctypes.POINTER(ctypes.c_int)), ("flags", ctypes.POINTER(ctypes.c_ubyte))]
+
+
+class CCcsOutput(ctypes.Structure):
+    _fields_ = [("polish", CZmwOutput), ("draft", ctypes.c_char_p), ("draft_cap", ctypes.c_int),
+                ("draft_len", ctypes.c_int)]
+
+
 class CPoaStats(ctypes.Structure):
     _fields_ = [("alignments", ctypes.c_longlong), ("cells", ctypes.c_longlong), ("launches", ctypes.c_longlong),
                 ("trace_steps", ctypes.c_longlong), ("fill_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
@@ -174,6 +184,8 @@ SIGNATURES = {
     "pbccs_poa_consensus": (I, [P, ctypes.POINTER(ctypes.c_char_p), PI, I, I, I, ctypes.c_char_p, I, PI, I,
                                 ctypes.c_char_p, I, PI]),
     "pbccs_poa_stats_get": (I, [P, ctypes.POINTER(CPoaStats), I]),
+    "pbccs_ccs_batch": (I, [P, ctypes.POINTER(CCcsInput), I, ctypes.c_longlong, ctypes.POINTER(CPolishOptions),
+                            ctypes.POINTER(CCcsOutput)]),
 }
 
 

@@ -209,6 +209,34 @@ def test_driver_batch_matches_per_zmw_driver(P):
     assert got[-1] == ("NoSubreads", None)
 
 
+def test_native_ccs_batch_matches_python_driver(P):
+    """pbccs_ccs_batch (FilterReads, POA, ExtractMappedRead, polish in one native call) equals the Python
+    driver (zmw_inputs_batch) followed by polish_zmws: statuses, drafts, consensus, QVs, per-key AddRead
+    results and counts.  Includes partial passes (flags) and a ZMW with no usable subread."""
+    poa, eng = P
+    import pbccs_amd
+    from pbccs_amd import driver
+    rng = np.random.default_rng(8)
+    chunks = []
+    for reads in _synthetic_subreads(6, (300, 900), (3, 9), seed=55):
+        chunks.append({"snr": [10.0, 7.0, 5.0, 11.0],
+                       "reads": [{"seq": s, "flags": int(rng.choice([3, 3, 3, 1, 2]))} for s in reads]})
+    chunks.append({"snr": [9.0, 9.0, 9.0, 9.0], "reads": [{"seq": "ACGTA"}]})
+    native = driver.ccs_batch(chunks, engine=eng)
+    ins = driver.zmw_inputs_batch(chunks, engine=eng)
+    pol = iter(pbccs_amd.polish_zmws([z for st, z in ins if st is None], engine=eng))
+    for (st, z), got in zip(ins, native):
+        if st is not None:
+            assert got["status"] == st
+            continue
+        exp = next(pol)
+        assert got["draft"] == z["draft"]
+        for k in ("status", "consensus", "qvs", "n_tested", "n_applied", "n_passes", "status_counts",
+                  "add_read_results"):
+            assert got[k] == exp[k], k
+    assert native[-1]["status"] == "NoSubreads"
+
+
 def test_poa_stats_counted(P):
     poa, eng = P
     s = poa.poa_stats(eng)
