@@ -445,7 +445,8 @@ def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
            "config": {"workload": f"configs[1] end to end: {args.length} bp insert, {args.passes} subreads per "
                                   f"ZMW, {args.steps} x {args.zmws_per_step} ZMWs in one pbccs_ccs_batch",
                       "slots": slots, "parallelism": f"zmw-shard x{world}"},
-           "zmw_status": statuses, "poa_wall_ms": round(st["total_ms"], 1)}
+           "zmw_status": statuses, "poa_wall_ms": round(st["total_ms"], 1),
+           "poa_device_ms": round(st["device_ms"], 1), "poa_thread_ms": round(st["thread_ms"], 1)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -1220,6 +1220,77 @@ __global__ void __launch_bounds__(256) k_sel_ranges(ScoreWork W, const long long
     nSel[k] = (int)(e - b);
 }
 
+// BestSubset (Consensus-inl.hpp:98-118) per work item, on its favourable list compacted in list order:
+// greedily the first maximum of the float-cast scores, then every entry whose Start lies within
+// [best - sep, best + sep] leaves the list; again until it is empty.  One wavefront per work item; lane l
+// owns entries q = l mod 64 (kept in LDS up to ldsCap <= kBestLds entries, read from HBM beyond), so the per-entry
+// state needs no cross-lane ordering.  rank[q] = k for the k-th pick (1-based), 0 for a removed entry.
+// sep = 0 keeps the whole list in order (the reference returns its input).
+constexpr int kBestLds = 2048;
+
+__device__ inline unsigned order_key(float f)   // float order as unsigned order (no NaN reaches here)
+{
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ void __launch_bounds__(64) k_best_subset(const long long* __restrict__ selBase, const int* __restrict__ nSel,
+                                                    const int* __restrict__ code, const double* __restrict__ score,
+                                                    int sep, int ldsCap, int* __restrict__ rank)
+{
+    __shared__ unsigned sKey[kBestLds];
+    __shared__ int sPos[kBestLds];
+    __shared__ int sRank[kBestLds];
+    const int k = blockIdx.x, lane = threadIdx.x;
+    const long long b = selBase[k];
+    const int m = nSel[k];
+    const int* c = code + b;
+    const double* sc = score + b;
+    int* rk = rank + b;
+    if (sep == 0) {
+        for (int q = lane; q < m; q += 64) rk[q] = q + 1;
+        return;
+    }
+    const int ml = m < ldsCap ? m : ldsCap;
+    for (int q = lane; q < ml; q += 64) {
+        sKey[q] = order_key((float)sc[q]);
+        sPos[q] = mut_pos(c[q]);
+        sRank[q] = -1;   // alive
+    }
+    for (int q = ml + lane; q < m; q += 64) rk[q] = -1;
+    for (int picks = 1;; ++picks) {
+        // first maximum: the highest key, then the lowest index (the key's low word is ~q)
+        unsigned long long best = 0;
+        for (int q = lane; q < ml; q += 64)
+            if (sRank[q] < 0) {
+                const unsigned long long v = ((unsigned long long)sKey[q] << 32) | (0xFFFFFFFFu - (unsigned)q);
+                best = v > best ? v : best;
+            }
+        for (int q = ml + lane; q < m; q += 64)
+            if (rk[q] < 0) {
+                const unsigned long long v = ((unsigned long long)order_key((float)sc[q]) << 32) |
+                                             (0xFFFFFFFFu - (unsigned)q);
+                best = v > best ? v : best;
+            }
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(best, off, 64);
+            best = o > best ? o : best;
+        }
+        if (best == 0) break;   // order_key is never 0 for a finite score: the list is empty
+        const int bq = (int)(0xFFFFFFFFu - (unsigned)(best & 0xFFFFFFFFu));
+        const int bp = mut_pos(c[bq]);
+        const int lo = bp - sep, hi = bp + sep;
+        for (int q = lane; q < ml; q += 64)
+            if (sRank[q] < 0 && lo <= sPos[q] && sPos[q] <= hi) sRank[q] = q == bq ? picks : 0;
+        for (int q = ml + lane; q < m; q += 64)
+            if (rk[q] < 0) {
+                const int pq = mut_pos(c[q]);
+                if (lo <= pq && pq <= hi) rk[q] = q == bq ? picks : 0;
+            }
+    }
+    for (int q = lane; q < ml; q += 64) rk[q] = sRank[q];
+}
+
 // ConsensusQVs + ProbabilityToQV (Consensus-inl.hpp:130-138, 274-295).
 __global__ void __launch_bounds__(256) k_qv(DevBatch B, ScoreWork W, const long long* __restrict__ posBase,
                                             const int* __restrict__ posOff, const double* __restrict__ score,
@@ -1302,6 +1373,14 @@ void launch_sel_ranges(const ScoreWork& W, const long long* sel, const long long
 {
     if (W.nWork <= 0) return;
     hipLaunchKernelGGL(k_sel_ranges, dim3((W.nWork + 255) / 256), dim3(256), 0, s, W, sel, count, selBase, nSel);
+}
+
+void launch_best_subset(int nWork, const long long* selBase, const int* nSel, const int* code, const double* score,
+                        int sep, int ldsCap, int* rank, hipStream_t s)
+{
+    if (nWork <= 0) return;
+    ldsCap = ldsCap < 0 || ldsCap > kBestLds ? kBestLds : ldsCap;
+    hipLaunchKernelGGL(k_best_subset, dim3(nWork), dim3(64), 0, s, selBase, nSel, code, score, sep, ldsCap, rank);
 }
 
 void launch_qv(const DevBatch& B, const ScoreWork& W, long long nPos, const long long* posBase, const int* posOff,

@@ -102,6 +102,11 @@ void launch_sel_ranges(const ScoreWork& W, const long long* sel, const long long
                        int* nSel, hipStream_t s);
 void launch_reduce(const DevBatch& B, const ScoreWork& W, long long nMut, double fastThr, double* score,
                    unsigned char* fav, hipStream_t s);
+// BestSubset (Consensus-inl.hpp:98-118) on the compacted favourable list: one wavefront per work item over
+// [selBase[k], selBase[k] + nSel[k]); rank = pick order (1-based) or 0.  The first ldsCap entries
+// (-1 = the kernel's maximum) of a list are staged in LDS, the rest read from HBM.
+void launch_best_subset(int nWork, const long long* selBase, const int* nSel, const int* code, const double* score,
+                        int sep, int ldsCap, int* rank, hipStream_t s);
 void launch_qv(const DevBatch& B, const ScoreWork& W, long long nPos, const long long* posBase, const int* posOff,
                const double* score, const long long* qvBase, int* qv, hipStream_t s);
 

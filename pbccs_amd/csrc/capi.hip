@@ -5,7 +5,11 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -853,8 +857,18 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
         // every slot polishes at once: split what is free beyond the growth margin between them
         const double spare = std::max(0.0, (double)freeB - (double)kQueueMargin);
         const double budget = std::max(1.0 * (1 << 30), 0.9 * spare / slots);
-        const int rc = pbccs_plan_batches(in, n, budget, kQueueMaxZmws, 1.5, order.data(), start.data(), nullptr, &nb);
+        int rc = pbccs_plan_batches(in, n, budget, kQueueMaxZmws, 1.5, order.data(), start.data(), nullptr, &nb);
         if (rc != PBCCS_OK) return rc;
+        // a last wave with fewer batches than slots leaves slots idle through its whole polish: cap the batch
+        // size so the batches come in whole waves (smaller batches stay within the per-slot budget); small
+        // inputs keep their plan, since batches of under ~256 ZMWs pay the per-round latency for too few
+        if (nb % slots != 0 && n >= 256 * slots) {
+            const int waves = (nb + slots - 1) / slots;
+            const int per = std::max(1, (n + waves * slots - 1) / (waves * slots));
+            rc = pbccs_plan_batches(in, n, budget, std::min(per, kQueueMaxZmws), 1.5, order.data(), start.data(),
+                                    nullptr, &nb);
+            if (rc != PBCCS_OK) return rc;
+        }
     }
     // the workspace slots exist before the workers start (Slot() grows a shared vector)
     for (int s = 0; s < slots; ++s) eng->Slot(s);
@@ -1445,6 +1459,86 @@ int pbccs_poa_stats_get(pbccs_engine* eng, pbccs_poa_stats* out, int reset)
     });
 }
 
+// One POA chunk of the pipelined ccs batch: its live ZMWs and everything their polish inputs point into.
+struct CcsChunk {
+    std::vector<int> zs;   // caller indices of the chunk's ZMWs
+    std::vector<std::string> css;
+    std::vector<std::vector<driver::MappedRead>> mapped;
+    std::vector<std::vector<const char*>> seqPtr;
+    std::vector<std::vector<int>> lens, strands, ts, te;
+    std::vector<std::vector<unsigned char>> full;
+    std::vector<pbccs_zmw_input> pin;   // the ZMWs that reach the polish
+    std::vector<int> pinZ;
+    std::vector<pbccs_zmw_output> pout;
+};
+
+// The POA draft of one chunk (Consensus.h:422-425, 352-390), then TooShort and ExtractMappedRead
+// (Consensus.h:427-471) into the chunk's polish inputs.
+static void ccs_draft_chunk(pbccs_engine* eng, const pbccs_ccs_input* in, const pbccs_polish_options& o,
+                            long long max_poa_coverage, const std::vector<std::vector<driver::Subread>>& sub,
+                            const std::vector<std::vector<int>>& order, pbccs_ccs_output* out, CcsChunk* C)
+{
+    const size_t m = C->zs.size();
+    std::vector<std::vector<const std::string*>> poaReads(m);
+    for (size_t q = 0; q < m; ++q)
+        for (int k : order[C->zs[q]]) poaReads[q].push_back(k >= 0 ? &sub[C->zs[q]][k].seq : nullptr);
+    std::vector<std::vector<int>> keys, ext;
+    std::vector<std::vector<char>> rc;
+    poa::PoaBatch(eng->PoaRunners(), poaReads, max_poa_coverage, -1, &C->css, &keys, &rc, &ext);
+    C->mapped.resize(m);
+    C->seqPtr.resize(m);
+    C->lens.resize(m);
+    C->strands.resize(m);
+    C->ts.resize(m);
+    C->te.resize(m);
+    C->full.resize(m);
+    for (size_t q = 0; q < m; ++q) {
+        const int z = C->zs[q];
+        const std::string& css = C->css[q];
+        if (out[z].draft && out[z].draft_cap >= (int)css.size()) memcpy(out[z].draft, css.data(), css.size());
+        out[z].draft_len = (int)css.size();
+        if ((int)css.size() < o.min_length) {
+            out[z].polish.status = PBCCS_ZMW_TOO_SHORT;
+            continue;
+        }
+        std::vector<unsigned char> added;
+        const std::vector<int>& kk = keys[q];
+        for (size_t i = 0; i < kk.size() && kk[i] != -2; ++i) {
+            driver::MappedRead mr;
+            const int key = kk[i];
+            const bool ok = key >= 0 &&
+                            driver::ExtractMappedRead(sub[z][order[z][i]], rc[q][key] != 0, ext[q][4 * key],
+                                                      ext[q][4 * key + 1], ext[q][4 * key + 2], ext[q][4 * key + 3],
+                                                      (size_t)o.min_length, &mr);
+            C->mapped[q].push_back(ok ? mr : driver::MappedRead());
+            added.push_back(ok ? 1 : 0);
+            C->full[q].push_back(ok && sub[z][order[z][i]].FullPass() ? 1 : 0);
+        }
+        for (size_t i = 0; i < C->mapped[q].size(); ++i) {
+            const driver::MappedRead& mr = C->mapped[q][i];
+            C->seqPtr[q].push_back(added[i] ? mr.seq.data() : nullptr);
+            C->lens[q].push_back((int)mr.seq.size());
+            C->strands[q].push_back(mr.strand);
+            C->ts[q].push_back(mr.ts);
+            C->te[q].push_back(mr.te);
+        }
+        pbccs_zmw_input zi;
+        zi.draft = css.data();
+        zi.draft_len = (int)css.size();
+        for (int b = 0; b < 4; ++b) zi.snr[b] = in[z].snr[b];
+        zi.n_reads = (int)C->mapped[q].size();
+        zi.seqs = C->seqPtr[q].data();
+        zi.lens = C->lens[q].data();
+        zi.strands = C->strands[q].data();
+        zi.tstarts = C->ts[q].data();
+        zi.tends = C->te[q].data();
+        zi.full_pass = C->full[q].data();
+        C->pin.push_back(zi);
+        C->pinZ.push_back(z);
+        C->pout.push_back(out[z].polish);
+    }
+}
+
 int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long long max_poa_coverage,
                     const pbccs_polish_options* opts, pbccs_ccs_output* out)
 {
@@ -1475,72 +1569,165 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
                 out[z].draft_len = 0;
             }
         }
-        // the POA of every live ZMW in one batch (Consensus.h:422-425, 352-390)
-        std::vector<std::vector<const std::string*>> poaReads(live.size());
-        for (size_t q = 0; q < live.size(); ++q)
-            for (int k : order[live[q]]) poaReads[q].push_back(k >= 0 ? &sub[live[q]][k].seq : nullptr);
-        std::vector<std::string> css;
-        std::vector<std::vector<int>> keys, ext;
-        std::vector<std::vector<char>> rc;
-        {
-            std::lock_guard<std::mutex> lk(eng->poaMu);
-            poa::PoaBatch(eng->PoaRunners(), poaReads, max_poa_coverage, -1, &css, &keys, &rc, &ext);
-            for (poa::PoaRunner* r : eng->PoaRunners()) r->ReleasePool();   // the polish sizes its batches from free HBM
-        }
-        // TooShort, ExtractMappedRead (Consensus.h:427-471) and the polish inputs
-        std::vector<std::vector<driver::MappedRead>> mapped(live.size());
-        std::vector<std::vector<const char*>> seqPtr(live.size());
-        std::vector<std::vector<int>> lens(live.size()), strands(live.size()), ts(live.size()), te(live.size());
-        std::vector<std::vector<unsigned char>> full(live.size()), added(live.size());
-        std::vector<pbccs_zmw_input> pin;
-        std::vector<int> pinZ;
+        if (live.empty()) return PBCCS_OK;
+        std::lock_guard<std::mutex> poaLock(eng->poaMu);
+        // Chunks: one POA batch each, polished as one device batch on a workspace slot while the next chunk's
+        // POA runs.  They are planned like pbccs_polish_batch's batches, from each ZMW's filtered subreads
+        // (the median length standing in for the draft): length buckets, the per-slot share of the HBM left
+        // beside the POA's score pools, whole waves over the slots.
+        const int slots = std::max(1, eng->concurrency);
+        constexpr size_t kPoaPoolPerSlice = 32ull << 30;
+        for (poa::PoaRunner* r : eng->PoaRunners()) r->SetPoolBudget(kPoaPoolPerSlice);
+        std::vector<std::vector<int>> liveLens(live.size());
+        std::vector<pbccs_zmw_input> est(live.size());
         for (size_t q = 0; q < live.size(); ++q) {
             const int z = live[q];
-            if (out[z].draft && out[z].draft_cap >= (int)css[q].size()) memcpy(out[z].draft, css[q].data(), css[q].size());
-            out[z].draft_len = (int)css[q].size();
-            if ((int)css[q].size() < o.min_length) {
-                out[z].polish.status = PBCCS_ZMW_TOO_SHORT;
-                continue;
-            }
-            const std::vector<int>& kk = keys[q];
-            for (size_t i = 0; i < kk.size() && kk[i] != -2; ++i) {
-                driver::MappedRead mr;
-                const int key = kk[i];
-                const bool ok = key >= 0 &&
-                                driver::ExtractMappedRead(sub[z][order[z][i]], rc[q][key] != 0, ext[q][4 * key],
-                                                          ext[q][4 * key + 1], ext[q][4 * key + 2], ext[q][4 * key + 3],
-                                                          (size_t)o.min_length, &mr);
-                mapped[q].push_back(ok ? mr : driver::MappedRead());
-                added[q].push_back(ok ? 1 : 0);
-                full[q].push_back(ok && sub[z][order[z][i]].FullPass() ? 1 : 0);
-            }
-            for (size_t i = 0; i < mapped[q].size(); ++i) {
-                const bool ok = added[q][i] != 0;
-                seqPtr[q].push_back(ok ? mapped[q][i].seq.data() : nullptr);
-                lens[q].push_back((int)mapped[q][i].seq.size());
-                strands[q].push_back(mapped[q][i].strand);
-                ts[q].push_back(mapped[q][i].ts);
-                te[q].push_back(mapped[q][i].te);
-            }
-            pbccs_zmw_input zi;
-            zi.draft = css[q].data();
-            zi.draft_len = (int)css[q].size();
-            for (int b = 0; b < 4; ++b) zi.snr[b] = in[z].snr[b];
-            zi.n_reads = (int)mapped[q].size();
-            zi.seqs = seqPtr[q].data();
-            zi.lens = lens[q].data();
-            zi.strands = strands[q].data();
-            zi.tstarts = ts[q].data();
-            zi.tends = te[q].data();
-            zi.full_pass = full[q].data();
-            pin.push_back(zi);
-            pinZ.push_back(z);
+            std::vector<int> kept;
+            for (int k : order[z])
+                if (k >= 0) liveLens[q].push_back(in[z].lens[k]);
+            kept = liveLens[q];
+            std::sort(kept.begin(), kept.end());
+            std::memset(&est[q], 0, sizeof(est[q]));
+            est[q].draft_len = kept[kept.size() / 2];
+            est[q].n_reads = (int)liveLens[q].size();
+            est[q].lens = liveLens[q].data();
         }
-        std::vector<pbccs_zmw_output> pout;
-        for (int z : pinZ) pout.push_back(out[z].polish);
-        const int rc2 = pin.empty() ? PBCCS_OK : pbccs_polish_batch(eng, pin.data(), (int)pin.size(), &o, pout.data());
-        for (size_t q = 0; q < pinZ.size(); ++q) out[pinZ[q]].polish = pout[q];
-        return rc2;
+        size_t freeB = 0, totalB = 0;
+        if (hipSetDevice(eng->device) != hipSuccess || hipMemGetInfo(&freeB, &totalB) != hipSuccess)
+            return fail(PBCCS_EDEVICE, "hipMemGetInfo failed");
+        size_t poaMapped = 0;
+        for (poa::PoaRunner* r : eng->PoaRunners()) poaMapped += r->PoolMappedBytes();
+        const double spare = std::max(0.0, (double)freeB + (double)poaMapped - kQueueMargin -
+                                               (double)(kPoaPoolPerSlice * eng->PoaRunners().size()));
+        const double budget = std::max(1.0 * (1 << 30), 0.9 * spare / slots);
+        const int nl = (int)live.size();
+        std::vector<int> perm(nl), start(nl + 1);
+        int nb = 0;
+        int rcp = PBCCS_OK;
+        if (o.zmws_per_batch > 0) {   // caller-sized consecutive chunks
+            for (int i = 0; i < nl; ++i) perm[i] = i;
+            for (int b0 = 0; b0 < nl; b0 += o.zmws_per_batch) start[nb++] = b0;
+            start[nb] = nl;
+        } else {
+            rcp = pbccs_plan_batches(est.data(), nl, budget, kQueueMaxZmws, 1.5, perm.data(), start.data(), nullptr, &nb);
+        }
+        if (rcp == PBCCS_OK && o.zmws_per_batch <= 0 && nb % slots != 0 && nl >= 256 * slots) {
+            const int waves = (nb + slots - 1) / slots;
+            const int per = std::max(1, (nl + waves * slots - 1) / (waves * slots));
+            rcp = pbccs_plan_batches(est.data(), nl, budget, std::min(per, kQueueMaxZmws), 1.5, perm.data(),
+                                     start.data(), nullptr, &nb);
+        }
+        if (rcp != PBCCS_OK) return rcp;
+        std::vector<CcsChunk> chunks(nb);
+        for (int c = 0; c < nb; ++c)
+            for (int k = start[c]; k < start[c + 1]; ++k) chunks[c].zs.push_back(live[perm[k]]);
+        // consumers: the polish slots pull drafted chunks as the producer (this thread) finishes them
+        for (int s = 0; s < slots; ++s) eng->Slot(s);
+        std::mutex qmu;
+        std::condition_variable qcv;
+        int drafted = 0, next = 0;
+        bool stop = false;
+        std::vector<int> prc(nb, PBCCS_OK);
+        std::vector<std::string> perr(nb);
+        // PBCCS_CCS_TRACE=1: one stderr line per chunk stage (ms since the call began)
+        static const bool trace = std::getenv("PBCCS_CCS_TRACE") != nullptr;
+        const auto tBegin = std::chrono::steady_clock::now();
+        auto since = [&] {
+            return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tBegin).count();
+        };
+        auto worker = [&](int slot) {
+            for (;;) {
+                int c;
+                {
+                    std::unique_lock<std::mutex> lk(qmu);
+                    qcv.wait(lk, [&] { return stop || next < drafted; });
+                    if (next >= drafted) return;   // stopped with nothing left
+                    c = next++;
+                }
+                CcsChunk& C = chunks[c];
+                if (C.pin.empty()) continue;
+                const double p0 = since();
+                prc[c] = polish_span(eng, slot, C.pin.data(), (int)C.pin.size(), &o, C.pout.data());
+                if (trace)
+                    std::fprintf(stderr, "[ccs] chunk %d polish slot %d zmws %zu %.1f-%.1f ms\n", c, slot, C.pin.size(),
+                                 p0, since());
+                if (prc[c] != PBCCS_OK && prc[c] != PBCCS_EOOM) {
+                    perr[c] = g_lastError;
+                    std::lock_guard<std::mutex> lk(qmu);
+                    stop = true;
+                    qcv.notify_all();
+                    return;
+                }
+            }
+        };
+        // PBCCS_CCS_SERIAL=1: every chunk drafted before the first polishes (the A/B reference schedule)
+        const char* serialEnv = std::getenv("PBCCS_CCS_SERIAL");
+        const bool serial = serialEnv && serialEnv[0] == '1';
+        std::vector<std::thread> pool;
+        if (!serial)
+            for (int s = 0; s < std::min(slots, nb); ++s) pool.emplace_back(worker, s);
+        int rcDraft = PBCCS_OK;
+        std::string errDraft;
+        for (int c = 0; c < nb; ++c) {
+            {
+                std::lock_guard<std::mutex> lk(qmu);
+                if (stop) break;
+            }
+            const double d0 = since();
+            try {
+                ccs_draft_chunk(eng, in, o, max_poa_coverage, sub, order, out, &chunks[c]);
+                if (trace)
+                    std::fprintf(stderr, "[ccs] chunk %d draft zmws %zu %.1f-%.1f ms\n", c, chunks[c].zs.size(), d0,
+                                 since());
+            } catch (const std::bad_alloc&) {
+                rcDraft = PBCCS_EOOM;
+                errDraft = "out of memory in the POA draft";
+            } catch (const std::exception& e) {
+                rcDraft = PBCCS_EDEVICE;
+                errDraft = e.what();
+            }
+            std::lock_guard<std::mutex> lk(qmu);
+            if (rcDraft != PBCCS_OK) {
+                stop = true;
+            } else {
+                drafted = c + 1;
+            }
+            qcv.notify_all();
+            if (rcDraft != PBCCS_OK) break;
+        }
+        {
+            std::lock_guard<std::mutex> lk(qmu);
+            stop = true;   // every drafted chunk is still taken: workers leave once next == drafted
+            qcv.notify_all();
+        }
+        if (serial) {
+            for (poa::PoaRunner* r : eng->PoaRunners()) r->ReleasePool();
+            for (int s = 0; s < std::min(slots, nb); ++s) pool.emplace_back(worker, s);
+        }
+        for (std::thread& t : pool) t.join();
+        for (poa::PoaRunner* r : eng->PoaRunners()) {
+            r->ReleasePool();
+            r->SetPoolBudget(0);
+        }
+        if (rcDraft != PBCCS_OK) return fail(rcDraft, errDraft.c_str());
+        for (int c = 0; c < nb; ++c)
+            if (prc[c] != PBCCS_OK && prc[c] != PBCCS_EOOM) return fail(prc[c], perr[c].c_str());
+        // chunks that ran the device out of memory beside the others: rerun alone once every pool is unmapped
+        bool unmapped = false;
+        for (int c = 0; c < nb; ++c) {
+            if (prc[c] != PBCCS_EOOM) continue;
+            if (!unmapped) {
+                for (int s = 0; s < slots; ++s) eng->Slot(s)->val.unmap_all();
+                unmapped = true;
+            }
+            CcsChunk& C = chunks[c];
+            for (size_t q = 0; q < C.pinZ.size(); ++q) C.pout[q] = out[C.pinZ[q]].polish;
+            const int r = polish_retry(eng, 0, C.pin.data(), (int)C.pin.size(), &o, C.pout.data());
+            if (r != PBCCS_OK) return r;
+        }
+        for (const CcsChunk& C : chunks)
+            for (size_t q = 0; q < C.pinZ.size(); ++q) out[C.pinZ[q]].polish = C.pout[q];
+        return PBCCS_OK;
     });
 }
 

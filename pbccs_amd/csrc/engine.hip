@@ -23,7 +23,7 @@ namespace pbccs {
     } while (0)
 
 const char* const kKernelNames[kKernelKinds] = {"k_fill", "k_suffix", "k_enumerate", "k_score",
-                                                 "k_reduce", "k_qv", "select", "k_compact"};
+                                                 "k_reduce", "k_qv", "k_best_subset", "k_compact"};
 
 namespace {
 
@@ -352,6 +352,7 @@ void ArrowBatch::Prepare()
     ws_->sel.reserve(std::max<long long>(mut, 1), false);
     ws_->selScore.reserve(std::max<long long>(mut, 1), false);
     ws_->selCode.reserve(std::max<long long>(mut, 1), false);
+    ws_->selRank.reserve(std::max<long long>(mut, 1), false);
     ws_->selCount.reserve(2, false);
     {   // hipCUB temp storage of the refine rounds' selections (a later growth would synchronise the device)
         size_t a = 0, b = 0, c = 0;
@@ -1473,37 +1474,54 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
                                                 (int)rTotalMut_, stream_));
         PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tmpBytes2, dScore_.ptr, dFav_.ptr, dSelScore.ptr,
                                                 dCount.ptr + 1, (int)rTotalMut_, stream_));
+        // the codes of the favourable entries (round 0's exist only on the device; later rounds' were uploaded)
+        DevVec<int>& dSelCode = ws_->selCode;
+        dSelCode.reserve(std::max<long long>(rTotalMut_, 1), false);
+        size_t tb = 0;
+        PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,
+                                                (int)rTotalMut_, stream_));
+        tmp.reserve(std::max<size_t>(tb, 1), false);
+        PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,
+                                                (int)rTotalMut_, stream_));
+        // BestSubset on the device: per ZMW its range of the compacted list, then one wavefront per ZMW
+        const int nAct = (int)act.size();
+        dSelBase_.reserve(std::max(nAct, 1), false);
+        dNSel_.reserve(std::max(nAct, 1), false);
+        DevVec<int>& dSelRank = ws_->selRank;
+        dSelRank.reserve(std::max<long long>(rTotalMut_, 1), false);
+        ScoreWork SW;
+        SW.nWork = nAct;
+        SW.mutStart = dWMutStart_.ptr;
+        launch_sel_ranges(SW, dSel.ptr, dCount.ptr, dSelBase_.ptr, dNSel_.ptr, stream_);
+        const char* capEnv = std::getenv("PBCCS_BEST_LDS");   // tests: force the HBM path of long lists
+        Timed(kKSelect, [&] {
+            launch_best_subset(nAct, dSelBase_.ptr, dNSel_.ptr, dSelCode.ptr, dSelScore.ptr, ro.mutationSeparation,
+                               capEnv ? std::atoi(capEnv) : -1, dSelRank.ptr, stream_);
+        });
+        PBCCS_HIP(hipGetLastError());
         long long cnt[2] = {0, 0};
         PBCCS_HIP(hipMemcpyAsync(cnt, dCount.ptr, 2 * sizeof(long long), hipMemcpyDeviceToHost, stream_));
         PBCCS_HIP(hipStreamSynchronize(stream_));
         std::vector<long long> sel;
         std::vector<double> selScore;
-        std::vector<int> selCode;
+        std::vector<int> selCode, selRank;
         download(sel, dSel, cnt[0], stream_);
         download(selScore, dSelScore, cnt[0], stream_);
-        if (round == 0) {
-            // the enumerated codes live only on the device: select them too
-            DevVec<int>& dSelCode = ws_->selCode;
-            dSelCode.reserve(std::max<long long>(cnt[0], 1), false);
-            size_t tb = 0;
-            PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,
-                                                    (int)rTotalMut_, stream_));
-            tmp.reserve(std::max<size_t>(tb, 1), false);
-            PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,
-                                                    (int)rTotalMut_, stream_));
-            download(selCode, dSelCode, cnt[0], stream_);
-            PBCCS_HIP(hipStreamSynchronize(stream_));
-        }
+        download(selCode, dSelCode, cnt[0], stream_);
+        download(selRank, dSelRank, cnt[0], stream_);
         PBCCS_HIP(hipStreamSynchronize(stream_));
 
         std::vector<std::vector<Scored>> fav(act.size());
+        std::vector<std::vector<std::pair<int, Scored>>> picked(act.size());   // (rank, entry)
         for (size_t q = 0; q < sel.size(); ++q) {
             const long long g = sel[q];
             const size_t a = std::upper_bound(rMutStart_.begin(), rMutStart_.end(), g) - rMutStart_.begin() - 1;
-            const long long m = g - rMutStart_[a];
-            const int code = (round == 0) ? selCode[q] : lists[a][m];
-            fav[a].push_back({code, (float)selScore[q]});
+            const Scored e{selCode[q], (float)selScore[q]};
+            fav[a].push_back(e);
+            if (selRank[q] > 0) picked[a].emplace_back(selRank[q], e);
         }
+        // PBCCS_CHECK_BEST_SUBSET=1: the host restatement beside the device select, any difference fatal
+        const bool checkBest = std::getenv("PBCCS_CHECK_BEST_SUBSET") != nullptr;
         std::vector<int> changed;
         for (size_t a = 0; a < act.size(); ++a) {
             const int k = idx[a];
@@ -1514,7 +1532,17 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
                 done[k] = 1;
                 continue;
             }
-            std::vector<Scored> best = best_subset(fav[a], ro.mutationSeparation);
+            std::sort(picked[a].begin(), picked[a].end(),
+                      [](const std::pair<int, Scored>& x, const std::pair<int, Scored>& y) { return x.first < y.first; });
+            std::vector<Scored> best;
+            for (const std::pair<int, Scored>& p : picked[a]) best.push_back(p.second);
+            if (checkBest) {
+                const std::vector<Scored> host = best_subset(fav[a], ro.mutationSeparation);
+                bool same = host.size() == best.size();
+                for (size_t i = 0; same && i < host.size(); ++i)
+                    same = host[i].code == best[i].code && host[i].score == best[i].score;
+                if (!same) throw DeviceError("k_best_subset differs from the host BestSubset");
+            }
             std::vector<Mutation> muts;
             for (const Scored& s : best) muts.push_back(mutation_from_code(s.code));
             if (best.size() > 1) {

@@ -166,7 +166,7 @@ struct Workspace {
     // favourable-mutation selection (persistent: a per-round hipFree would synchronise the whole device)
     DevVec<long long> sel, selCount;
     DevVec<double> selScore;
-    DevVec<int> selCode;
+    DevVec<int> selCode, selRank;
     DevVec<unsigned char> selTmp;
 };
 

@@ -652,11 +652,11 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
     upload(dRowBase_, hRowBase_, nRow);
     const PoaPools pools{dBase_.ptr, dVertexOfCol_.ptr, dPredStart_.ptr, dPredCol_.ptr, dExitPred_.ptr, dRowBase_.ptr};
 
-    size_t budget = budget_;
-    if (budget == 0) {
+    size_t budget = 0;
+    {
         size_t fr = 0, tot = 0;
         check(hipMemGetInfo(&fr, &tot), "hipMemGetInfo");
-        budget = std::min<size_t>((size_t)(0.6 * (double)fr) + dPool_.mapped_bytes(), 64ull << 30);
+        budget = std::min<size_t>((size_t)(0.6 * (double)fr) + dPool_.mapped_bytes(), budget_ ? budget_ : 64ull << 30);
         budget = std::max<size_t>(budget, 64ull << 20);
     }
     auto jobBytes = [&](const PoaJob& J) {

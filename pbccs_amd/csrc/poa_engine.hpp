@@ -111,6 +111,7 @@ public:
     // Unmap the score-matrix pool (the address reservation stays): the polish that follows the POA in a
     // ccs run then has the device memory to itself.
     void ReleasePool() { dPool_.unmap_all(); }
+    size_t PoolMappedBytes() const { return dPool_.mapped_bytes(); }
     int HostThreads() const { return threads_; }
     PoaStats stats;
     bool profiling = false;
@@ -118,7 +119,7 @@ public:
 private:
     int device_;
     int threads_;
-    size_t budget_ = 0;   // score-matrix bytes per launch group; 0 = from free memory
+    size_t budget_ = 0;   // cap on the score-matrix bytes per launch group (0 = 64 GB); also <= 0.6 x free HBM
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
     DevVec<uint8_t> dBase_, dRowBase_;

@@ -159,6 +159,30 @@ def test_polish_batch_matches_oracle(P):
         assert _close(r["zg"], e["zg"], 1e-9) and _close(r["za"], e["za"], 1e-9)
 
 
+@pytest.mark.parametrize("sep,lds_cap", [(10, None), (10, "5"), (3, "0"), (0, None)])
+def test_device_best_subset_matches_host(P, monkeypatch, sep, lds_cap):
+    """k_best_subset (BestSubset, Consensus-inl.hpp:98-118, on the device) against the host restatement on
+    every refine round of a batch (PBCCS_CHECK_BEST_SUBSET=1 makes any difference fatal), with the LDS
+    stage, the HBM path of lists longer than the LDS cap (PBCCS_BEST_LDS), another separation and
+    separation 0 (the whole list, in order); the batch then matches the oracle bit-exactly.  Separation 0
+    is checked device-against-host only: it applies overlapping mutations, whose transcript runs past the
+    template (Mutation.cpp:131-170), so the window remap leaves the reference's contract there."""
+    from pbccs_amd import synth
+    from pbccs_amd.polish import ConsensusSettings
+    monkeypatch.setenv("PBCCS_CHECK_BEST_SUBSET", "1")
+    if lds_cap is not None:
+        monkeypatch.setenv("PBCCS_BEST_LDS", lds_cap)
+    zs = synth.make_zmws(5, 500, 6, seed=52 + sep)
+    res = P.polish_zmws(zs, ConsensusSettings(mutation_separation=sep))
+    if sep == 0:
+        return
+    for z, r in zip(zs, res):
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"], separation=sep)
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        if e["converged"]:
+            assert r["consensus"] == e["template"]
+
+
 def test_zmw6251_reference_record_on_gpu(P):
     z = json.load(open(os.path.join(GOLD, "zmw6251.json")))
     r = P.polish_zmws([{"draft": z["draft"], "snr": z["snr"], "reads": z["reads"]}])[0]

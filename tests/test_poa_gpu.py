@@ -237,6 +237,21 @@ def test_native_ccs_batch_matches_python_driver(P):
     assert native[-1]["status"] == "NoSubreads"
 
 
+def test_native_ccs_batch_pipelined_chunks(P):
+    """The pipelined form: ZMWs drafted in chunks of 3 (zmws_per_batch) while earlier chunks polish on the
+    workspace slots; the results equal the one-chunk call's, ZMW for ZMW."""
+    poa, eng = P
+    from pbccs_amd import driver
+    from pbccs_amd.polish import ConsensusSettings
+    chunks = [{"snr": [10.0, 7.0, 5.0, 11.0], "reads": [{"seq": s} for s in reads]}
+              for reads in _synthetic_subreads(11, (200, 600), (3, 7), seed=66)]
+    chunks.insert(4, {"snr": [9.0, 9.0, 9.0, 9.0], "reads": [{"seq": "ACG"}]})
+    one = driver.ccs_batch(chunks, engine=eng)
+    many = driver.ccs_batch(chunks, ConsensusSettings(zmws_per_batch=3), engine=eng)
+    assert many == one
+    assert one[4]["status"] == "NoSubreads"
+
+
 def test_poa_stats_counted(P):
     poa, eng = P
     s = poa.poa_stats(eng)
