@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--streams", type=int, default=0,
                     help="workspace slots = batches polished concurrently (0 = min(steps, 5), capped by HBM)")
+    ap.add_argument("--ccs-chunk", type=int, default=0,
+                    help="ccs stage: ZMWs per POA chunk / polish batch (0 = planned from free HBM)")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--stage", choices=["polish", "poa", "ccs"], default="polish",
                     help="polish: the headline line (Consensus.h's Arrow polish, from the draft on); poa: the POA "
@@ -419,6 +421,7 @@ def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
         return [{"snr": z["snr"], "reads": [{"seq": r["seq"]} for r in z["reads"]]}
                 for z in synth.make_zmws(n, args.length, args.passes, seed=seed)]
 
+    settings.zmws_per_batch = args.ccs_chunk
     for w in range(args.warmup):
         driver.ccs_batch(chunks(args.zmws_per_step, seed0 + 1000 + w), settings, eng)
     work = [c for k in range(args.steps) for c in chunks(args.zmws_per_step, seed0 + k)]
@@ -444,7 +447,7 @@ def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
            "data": "synthetic subreads (SURVEY.md §8(d): truth iid ACGT; 7%/4%/1% ins/del/sub; odd passes RC)",
            "config": {"workload": f"configs[1] end to end: {args.length} bp insert, {args.passes} subreads per "
                                   f"ZMW, {args.steps} x {args.zmws_per_step} ZMWs in one pbccs_ccs_batch",
-                      "slots": slots, "parallelism": f"zmw-shard x{world}"},
+                      "slots": slots, "chunk": args.ccs_chunk or "planned", "parallelism": f"zmw-shard x{world}"},
            "zmw_status": statuses, "poa_wall_ms": round(st["total_ms"], 1),
            "poa_device_ms": round(st["device_ms"], 1), "poa_thread_ms": round(st["thread_ms"], 1)}
     if rank == 0:

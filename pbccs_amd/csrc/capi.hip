@@ -773,15 +773,23 @@ int pbccs_engine_reserve_pool(pbccs_engine* eng, size_t bytes_per_slot)
 // Estimated FP64 band footprint of one ZMW at its high-water mark.  Per read: two band regions of ~32 rows
 // x window plus column metadata and score deltas (the typical band), plus the expected share of reads
 // whose first band explodes (the tall-band paths hold ~2-22% of the (I+1)(J+1) matrix).  Fitted to the
-// measured pools: ~13.5 MB per 2 kb / 10-pass ZMW, ~1.1 GB per 10 kb / 8-pass ZMW;
-// the fit overestimates the 2 kb case about 2x, which only shortens its batches.
+// measured pools: ~13.5 MB per 2 kb / 10-pass ZMW (estimate 18.4 MB), ~1.1 GB per 10 kb / 8-pass ZMW
+// (estimate 1.13 GB).
+// Band-pool bytes the workspace slots hold mapped.
+static size_t slot_pool_bytes(pbccs_engine* eng)
+{
+    size_t b = 0;
+    for (const auto& s : eng->slots) b += s->val.mapped_bytes();
+    return b;
+}
+
 static double zmw_est_bytes(const pbccs_zmw_input& z)
 {
     double b = 0.0;
     for (int k = 0; k < z.n_reads; ++k) {
         const double J = std::max(1, z.tends ? z.tends[k] - (z.tstarts ? z.tstarts[k] : 0) : z.draft_len);
         const double I = z.lens ? std::max(0, z.lens[k]) : J;
-        const double typical = J * (2 * 32 * 8 * 1.25 + 80 + 8 * 8);
+        const double typical = J * 0.5 * (2 * 32 * 8 * 1.25 + 80 + 8 * 8);
         const double tall = std::min(0.22 * 8.0 * (I + 1) * (J + 1), 1.33e8 * std::pow(J / 1e4, 3.0));
         b += typical + tall;
     }
@@ -854,8 +862,9 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
         size_t freeB = 0, totalB = 0;
         if (hipSetDevice(eng->device) != hipSuccess || hipMemGetInfo(&freeB, &totalB) != hipSuccess)
             return fail(PBCCS_EDEVICE, "hipMemGetInfo failed");
-        // every slot polishes at once: split what is free beyond the growth margin between them
-        const double spare = std::max(0.0, (double)freeB - (double)kQueueMargin);
+        // every slot polishes at once: split what is free beyond the growth margin between them (the slots'
+        // mapped band pools count as free: a batch on the slot reuses them)
+        const double spare = std::max(0.0, (double)freeB + (double)slot_pool_bytes(eng) - (double)kQueueMargin);
         const double budget = std::max(1.0 * (1 << 30), 0.9 * spare / slots);
         int rc = pbccs_plan_batches(in, n, budget, kQueueMaxZmws, 1.5, order.data(), start.data(), nullptr, &nb);
         if (rc != PBCCS_OK) return rc;
@@ -1573,10 +1582,12 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
         std::lock_guard<std::mutex> poaLock(eng->poaMu);
         // Chunks: one POA batch each, polished as one device batch on a workspace slot while the next chunk's
         // POA runs.  They are planned like pbccs_polish_batch's batches, from each ZMW's filtered subreads
-        // (the median length standing in for the draft): length buckets, the per-slot share of the HBM left
-        // beside the POA's score pools, whole waves over the slots.
+        // (the median length standing in for the draft): length buckets and the per-slot share of the HBM
+        // left beside the POA's score pools.  No whole-wave split: the chunks reach the slots one POA apart,
+        // and larger chunks keep both stages busier (2000-ZMW chunks measured 1544 ZMWs/s end to end against
+        // 1384 for 1000 and 1066 for 500).
         const int slots = std::max(1, eng->concurrency);
-        constexpr size_t kPoaPoolPerSlice = 32ull << 30;
+        constexpr size_t kPoaPoolPerSlice = 20ull << 30;   // one round of a 1000-ZMW 2 kb slice: ~17.7 GB
         for (poa::PoaRunner* r : eng->PoaRunners()) r->SetPoolBudget(kPoaPoolPerSlice);
         std::vector<std::vector<int>> liveLens(live.size());
         std::vector<pbccs_zmw_input> est(live.size());
@@ -1597,7 +1608,7 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
             return fail(PBCCS_EDEVICE, "hipMemGetInfo failed");
         size_t poaMapped = 0;
         for (poa::PoaRunner* r : eng->PoaRunners()) poaMapped += r->PoolMappedBytes();
-        const double spare = std::max(0.0, (double)freeB + (double)poaMapped - kQueueMargin -
+        const double spare = std::max(0.0, (double)freeB + (double)poaMapped + (double)slot_pool_bytes(eng) - kQueueMargin -
                                                (double)(kPoaPoolPerSlice * eng->PoaRunners().size()));
         const double budget = std::max(1.0 * (1 << 30), 0.9 * spare / slots);
         const int nl = (int)live.size();
@@ -1610,12 +1621,6 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
             start[nb] = nl;
         } else {
             rcp = pbccs_plan_batches(est.data(), nl, budget, kQueueMaxZmws, 1.5, perm.data(), start.data(), nullptr, &nb);
-        }
-        if (rcp == PBCCS_OK && o.zmws_per_batch <= 0 && nb % slots != 0 && nl >= 256 * slots) {
-            const int waves = (nb + slots - 1) / slots;
-            const int per = std::max(1, (nl + waves * slots - 1) / (waves * slots));
-            rcp = pbccs_plan_batches(est.data(), nl, budget, std::min(per, kQueueMaxZmws), 1.5, perm.data(),
-                                     start.data(), nullptr, &nb);
         }
         if (rcp != PBCCS_OK) return rcp;
         std::vector<CcsChunk> chunks(nb);
