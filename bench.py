@@ -62,11 +62,13 @@ def parse():
     ap.add_argument("--ccs-chunk", type=int, default=0,
                     help="ccs stage: ZMWs per POA chunk / polish batch (0 = planned from free HBM)")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--stage", choices=["polish", "poa", "ccs"], default="polish",
+    ap.add_argument("--stage", choices=["polish", "poa", "ccs", "quiver"], default="polish",
                     help="polish: the headline line (Consensus.h's Arrow polish, from the draft on); poa: the POA "
                          "draft step before it (SparsePoa over each ZMW's raw subreads, SURVEY.md §8(f) row 1) on "
                          "the same configs[1] ZMWs; ccs: both, end to end from raw subreads (FilterReads, POA, "
-                         "ExtractMappedRead, polish), the POA of the next steps overlapping the polish")
+                         "ExtractMappedRead, polish), the POA of the next steps overlapping the polish; quiver: "
+                         "the Quiver family (QV-feature reads, FP32 log-space recursions) through "
+                         "pbccs_quiver_polish_batch on configs[1]-shaped ZMWs")
     return ap.parse_args()
 
 
@@ -278,6 +280,8 @@ def main():
         return poa_stage(args, rank, world, eng, barrier, sync, seed0)
     if args.stage == "ccs":
         return ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0)
+    if args.stage == "quiver":
+        return quiver_stage(args, rank, world, eng, barrier, sync, seed0)
     if args.workload != "2kb":
         job_time, local_time, res, workload, scaling, total = queue_workload(args, rank, world, eng, settings, seed0)
         return report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total)
@@ -402,6 +406,76 @@ def poa_stage(args, rank, world, eng, barrier, sync, seed0):
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"] = poa_cpu_baseline(args, min(args.cpu_sample, 48))
         out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def quiver_cpu_baseline(args, n):
+    """The Quiver CPU restatement (oracle/quiver_oracle.cpp: the SSE recursor's single-precision operations
+    in order) on host threads, one ZMW per task: AddRead, RefineConsensus, ConsensusQVs."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    from pbccs_amd import synth
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    threads = max(1, min(args.cpu_threads or share, n))
+    zs = synth.make_quiver_zmws(n, args.length, args.passes, seed=args.seed + 99991)
+    O.lib()
+
+    def one(z):
+        o = O.QuiverScorer(z["tpl"], synth.QUIVER_PARAMS, score_diff=synth.QUIVER_SCORE_DIFF)
+        for r in z["reads"]:
+            o.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"])
+        o.refine()
+        o.qvs()
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(one, zs))
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+            "nproc": os.cpu_count(),
+            "sample": f"{n} synthetic Quiver ZMWs of the same config (seed {args.seed + 99991}), "
+                      f"oracle/quiver_oracle.cpp AddRead + RefineConsensus + ConsensusQVs one ZMW per task on "
+                      f"{threads} host threads, {dt:.1f} s wall"}
+
+
+def quiver_stage(args, rank, world, eng, barrier, sync, seed0):
+    """The Quiver family on configs[1]-shaped ZMWs with QV features: per ZMW a
+    scorer over the default QuiverConfig, AddRead of every read, RefineConsensus and ConsensusQVs, all
+    steps x zmws-per-step scorers in one pbccs_quiver_polish_batch.  value = ZMWs/s, inputs in host memory."""
+    import pbccs_amd as P
+    from pbccs_amd import quiver, synth
+    cfg = P.QuiverConfig(P.QvModelParams(**synth.QUIVER_PARAMS), score_diff=synth.QUIVER_SCORE_DIFF)
+    for w in range(args.warmup):
+        quiver.polish_batch(synth.make_quiver_zmws(min(args.zmws_per_step, 200), args.length, args.passes,
+                                                   seed=seed0 + 1000 + w), cfg, engine=eng)
+    zs = synth.make_quiver_zmws(args.steps * args.zmws_per_step, args.length, args.passes, seed=seed0)
+    eng.kernel_stats(reset=True)
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    res = quiver.polish_batch(zs, cfg, engine=eng)
+    sync()
+    barrier()
+    local_time = time.perf_counter() - t0
+    job_time = max_over_ranks(local_time, world)
+    total = len(zs) * world
+    out = {"metric": "Quiver ZMWs/sec (AddRead, RefineConsensus, ConsensusQVs per scorer) on MI355X",
+           "value": round(total / job_time, 3), "unit": "ZMWs/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(job_time / args.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32 (log space)",
+           "data": "synthetic QV-feature reads (synth.make_quiver_zmws)",
+           "config": {"workload": f"configs[1]-shaped Quiver: {args.length} bp draft, {args.passes} reads per ZMW "
+                                  f"(ins/del/sub {synth.QUIVER_READ_ERRORS}), ScoreDiff {synth.QUIVER_SCORE_DIFF}, "
+                                  f"{len(zs)} scorers in one pbccs_quiver_polish_batch",
+                      "parallelism": f"zmw-shard x{world}"},
+           "converged": sum(r["converged"] for r in res), "mean_iterations_applied":
+               round(sum(r["n_applied"] for r in res) / max(1, len(res)), 2)}
+    if rank == 0 and args.cpu_sample:
+        out["cpu_baseline"] = quiver_cpu_baseline(args, args.cpu_sample)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

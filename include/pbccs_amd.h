@@ -313,6 +313,47 @@ int pbccs_quiver_refine_consensus(pbccs_quiver_scorer* s, const pbccs_refine_opt
                                   long long* n_applied, int* converged);
 int pbccs_quiver_consensus_qvs(pbccs_quiver_scorer* s, int* qvs, int cap, int* n);
 
+/* Batched Quiver polish: for every ZMW, what a caller of the scorer API above does with one scorer --
+ * create over (configs, chemistries), AddRead each read (threshold NaN = its config's add_threshold),
+ * RefineConsensus(opts), ConsensusQVs -- with every scorer's fills, mutation scores, Score /
+ * FastIsFavorable reduction and BestSubset on the device in lock-step rounds (one refill launch per
+ * round).  Results equal the per-scorer calls'.  consensus / qvs: caller buffers of consensus_cap; qvs
+ * NULL skips ConsensusQVs.  ok = 0: RefineConsensus refused an edit (the scorer call's PBCCS_EINVAL). */
+typedef struct {
+    const char* seq;
+    int len;
+    const float* ins_qv;
+    const float* subs_qv;
+    const float* del_qv;
+    const float* del_tag;   /* float(char) per base, as pbccs_quiver_scorer_add_read */
+    const float* merge_qv;
+    const char* chemistry;  /* NULL = "*" */
+    int strand, tstart, tend;
+    float threshold;
+} pbccs_quiver_read;
+
+typedef struct {
+    const char* tpl;
+    int tpl_len;
+    const pbccs_quiver_read* reads;
+    int n_reads;
+} pbccs_quiver_zmw;
+
+typedef struct {
+    char* consensus;
+    int consensus_cap;
+    int consensus_len;
+    int* qvs;
+    long long n_tested, n_applied;
+    int converged;
+    int ok;
+    int n_active;           /* reads AddRead kept */
+} pbccs_quiver_result;
+
+int pbccs_quiver_polish_batch(pbccs_engine* eng, const pbccs_quiver_config* configs, const char* const* chemistries,
+                              int n_configs, const pbccs_quiver_zmw* zmws, int n, const pbccs_refine_options* opts,
+                              pbccs_quiver_result* out);
+
 /* ---- POA draft (pbccs src/SparsePoa.cpp, ConsensusCore/src/C++/Poa) ---------------------------------
  * The read-vs-graph DP and its traceback run on the device (k_poa_fill / k_poa_trace); the graph lives on
  * the host.  Scores use DefaultPoaConfig (match 3, mismatch -5, insert -4, delete -4). */

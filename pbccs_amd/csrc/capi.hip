@@ -1279,6 +1279,111 @@ int pbccs_quiver_consensus_qvs(pbccs_quiver_scorer* s, int* qvs, int cap, int* n
     });
 }
 
+int pbccs_quiver_polish_batch(pbccs_engine* eng, const pbccs_quiver_config* configs, const char* const* chemistries,
+                              int n_configs, const pbccs_quiver_zmw* zmws, int n, const pbccs_refine_options* opts,
+                              pbccs_quiver_result* out)
+{
+    if (!eng || !configs || n_configs < 1 || n < 0 || (n > 0 && (!zmws || !out))) return fail(PBCCS_EINVAL, "bad argument");
+    for (int k = 0; k < n_configs; ++k)
+        if (configs[k].recursor < PBCCS_QV_RECURSOR_SPARSE_SSE || configs[k].recursor > PBCCS_QV_RECURSOR_DENSE_SIMPLE)
+            return fail(PBCCS_EINVAL, "unknown recursor type");
+    for (int z = 0; z < n; ++z) {
+        if (!zmws[z].tpl || zmws[z].tpl_len <= 0 || zmws[z].n_reads < 0 || (zmws[z].n_reads > 0 && !zmws[z].reads))
+            return fail(PBCCS_EINVAL, "bad pbccs_quiver_zmw");
+        for (int r = 0; r < zmws[z].n_reads; ++r) {
+            const pbccs_quiver_read& q = zmws[z].reads[r];
+            if (!q.seq || q.len <= 0 || (q.strand != 0 && q.strand != 1)) return fail(PBCCS_EINVAL, "bad pbccs_quiver_read");
+        }
+    }
+    if (n == 0) return PBCCS_OK;
+    return guarded([&] {
+        quiver::QuiverBatch qb(eng->device);
+        // the QuiverConfigTable, as pbccs_quiver_scorer_create builds it
+        std::vector<std::pair<std::string, int>> table;
+        std::vector<const pbccs_quiver_config*> cfgs;
+        float fast = 0.0f;
+        for (int k = 0; k < n_configs; ++k) {
+            const std::string name = (chemistries && chemistries[k]) ? chemistries[k] : "*";
+            bool dup = false;
+            for (auto& kv : table) dup = dup || kv.first == name;
+            if (dup) continue;
+            table.emplace_back(name, qb.AddConfig(qparams(configs[k])));
+            cfgs.push_back(&configs[k]);
+            fast = std::min(fast, configs[k].fast_score_threshold);
+        }
+        std::vector<int> zs(n);
+        std::vector<quiver::QuiverBatch::ReadSpec> specs;
+        std::vector<int> specZmw;
+        for (int z = 0; z < n; ++z) {
+            zs[z] = qb.AddZmw(std::string(zmws[z].tpl, zmws[z].tpl_len), fast);
+            for (int r = 0; r < zmws[z].n_reads; ++r) {
+                const pbccs_quiver_read& q = zmws[z].reads[r];
+                const std::string chem = q.chemistry ? q.chemistry : "*";
+                int cfg = -1;
+                size_t pos = 0;
+                for (size_t k = 0; k < table.size(); ++k)
+                    if (table[k].first == chem) { cfg = table[k].second; pos = k; }
+                if (cfg < 0)
+                    for (size_t k = 0; k < table.size(); ++k)
+                        if (table[k].first == "*") { cfg = table[k].second; pos = k; }
+                if (cfg < 0) return fail(PBCCS_EINVAL, "Chemistry not found in QuiverConfigTable");
+                quiver::QuiverBatch::ReadSpec sp;
+                sp.z = zs[z];
+                sp.strand = q.strand;
+                sp.ts = q.tstart;
+                sp.te = q.tend < 0 ? zmws[z].tpl_len : q.tend;
+                sp.config = cfg;
+                sp.threshold = std::isnan(q.threshold) ? cfgs[pos]->add_threshold : q.threshold;
+                sp.f.seq.assign(q.seq, q.len);
+                auto track = [&](std::vector<float>& v, const float* src) {
+                    v.assign(q.len, 0.0f);
+                    if (src) std::copy(src, src + q.len, v.begin());
+                };
+                track(sp.f.ins, q.ins_qv);
+                track(sp.f.subs, q.subs_qv);
+                track(sp.f.del, q.del_qv);
+                track(sp.f.tag, q.del_tag);
+                track(sp.f.merge, q.merge_qv);
+                specs.push_back(std::move(sp));
+                specZmw.push_back(z);
+            }
+        }
+        const std::vector<char> act = qb.AddReads(&specs);
+        for (int z = 0; z < n; ++z) out[z].n_active = 0;
+        for (size_t k = 0; k < act.size(); ++k) out[specZmw[k]].n_active += act[k];
+        RefineOptions ro;
+        if (opts) {
+            ro.maxIterations = opts->max_iterations;
+            ro.mutationSeparation = opts->mutation_separation;
+            ro.mutationNeighborhood = opts->mutation_neighborhood;
+        }
+        std::vector<long long> nt, na;
+        std::vector<char> conv, ok;
+        qb.RefineMany(zs, ro, &nt, &na, &conv, &ok);
+        std::vector<int> wantQv;
+        for (int z = 0; z < n; ++z)
+            if (out[z].qvs && ok[z]) wantQv.push_back(z);
+        std::vector<int> qz;
+        for (int z : wantQv) qz.push_back(zs[z]);
+        const std::vector<std::vector<int>> qv = qz.empty() ? std::vector<std::vector<int>>() : qb.QVsMany(qz);
+        for (int z = 0; z < n; ++z) {
+            pbccs_quiver_result& o = out[z];
+            o.n_tested = nt[z];
+            o.n_applied = na[z];
+            o.converged = conv[z];
+            o.ok = ok[z];
+            const std::string& t = qb.Template(zs[z]);
+            o.consensus_len = (int)t.size();
+            if (o.consensus && o.consensus_cap >= (int)t.size()) memcpy(o.consensus, t.data(), t.size());
+        }
+        for (size_t k = 0; k < wantQv.size(); ++k) {
+            pbccs_quiver_result& o = out[wantQv[k]];
+            if (o.consensus_cap >= (int)qv[k].size()) std::copy(qv[k].begin(), qv[k].end(), o.qvs);
+        }
+        return PBCCS_OK;
+    });
+}
+
 // ---------------------------------------------------------------- POA draft
 
 struct pbccs_sparse_poa {

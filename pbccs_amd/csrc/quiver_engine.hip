@@ -1,12 +1,18 @@
 // pbccs_amd/csrc/quiver_engine.hip -- QuiverBatch (quiver_engine.hpp).
 #include "quiver_engine.hpp"
 
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <set>
 #include <stdexcept>
+#include <unordered_set>
+
+#include "arrow_kernels.hpp"
 
 namespace pbccs {
 namespace quiver {
@@ -117,6 +123,43 @@ void QuiverBatch::EnsureCapacity(int ri)
 
 bool QuiverBatch::AddRead(int zi, const QReadFeatures& f, int strand, int ts, int te, int config, float threshold)
 {
+    std::vector<ReadSpec> one(1);
+    one[0].z = zi;
+    one[0].strand = strand;
+    one[0].ts = ts;
+    one[0].te = te;
+    one[0].config = config;
+    one[0].threshold = threshold;
+    one[0].f = f;
+    return AddReads(&one)[0] != 0;
+}
+
+std::vector<char> QuiverBatch::AddReads(std::vector<ReadSpec>* specs)
+{
+    std::vector<int> added;
+    for (ReadSpec& sp : *specs)
+        added.push_back(Register(sp.z, sp.f, sp.strand, sp.ts, sp.te, sp.config));
+    Fill(added);
+    std::vector<char> act(specs->size());
+    for (size_t k = 0; k < specs->size(); ++k) {
+        // AddRead: a scorer whose construction threw (alpha/beta mismatch) is dropped; so is one whose
+        // matrices allocate more than `threshold` of the full matrix (:263-276)
+        HRead& h = reads_[added[k]];
+        const float threshold = (*specs)[k].threshold;
+        h.hasScorer = h.active;
+        if (h.active && threshold < 1.0f) {
+            const int J = h.te - h.ts;
+            // float threshold * int * int is float; 0.5 + float is double (:268)
+            const int maxSize = static_cast<int>(0.5 + threshold * (float)(int)(h.len + 1) * (float)(J + 1));
+            if (h.alloc[0] >= maxSize || h.alloc[1] >= maxSize) h.active = h.hasScorer = false;
+        }
+        act[k] = h.active ? 1 : 0;
+    }
+    return act;
+}
+
+int QuiverBatch::Register(int zi, const QReadFeatures& f, int strand, int ts, int te, int config)
+{
     HZmw& z = zmws_.at(zi);
     const int L = (int)z.tpl.size();
     const size_t I = f.seq.size();
@@ -144,17 +187,7 @@ bool QuiverBatch::AddRead(int zi, const QReadFeatures& f, int strand, int ts, in
     valTop_ += (long long)I + 8;
     EnsureCapacity(ri);
     dirty_ = true;
-    Fill({ri});
-    // AddRead: a scorer whose construction threw (alpha/beta mismatch) is dropped; so is one whose
-    // matrices allocate more than `threshold` of the full matrix (:263-276)
-    h.hasScorer = h.active;
-    if (h.active && threshold < 1.0f) {
-        const int J = te - ts;
-        // float threshold * int * int is float; 0.5 + float is double (:268)
-        const int maxSize = static_cast<int>(0.5 + threshold * (float)(int)(I + 1) * (float)(J + 1));
-        if (h.alloc[0] >= maxSize || h.alloc[1] >= maxSize) h.active = h.hasScorer = false;
-    }
-    return h.active;
+    return ri;
 }
 
 void QuiverBatch::Upload()
@@ -272,9 +305,27 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
     for (int attempt = 0; !todo.empty(); ++attempt) {
         if (attempt > 8) throw DeviceError("quiver band storage keeps overflowing");
         Upload();
-        put(dList_, todo, stream_);
+        // SparseSse configs with reads below kQCoopRows rows: one wavefront per read (k_qfill_coop); the
+        // Simple / Dense recursors and longer reads: one lane per read (k_qfill).  PBCCS_QFILL_LANE=1 sends
+        // every read to the lane kernel.
+        static const bool laneOnly = std::getenv("PBCCS_QFILL_LANE") != nullptr;
+        std::vector<int> coop, lane;
+        int maxRows = 1;
+        for (int r : todo) {
+            const QParams& p = configs_[reads_[r].config];
+            if (!laneOnly && !p.simple && !p.dense && reads_[r].len + 1 <= kQCoopRows) {
+                coop.push_back(r);
+                maxRows = std::max(maxRows, reads_[r].len + 1);
+            } else {
+                lane.push_back(r);
+            }
+        }
+        std::vector<int> both(coop);
+        both.insert(both.end(), lane.begin(), lane.end());
+        put(dList_, both, stream_);
         const QBatch B = View();
-        launch_qfill(B, dList_.ptr, (int)todo.size(), stream_);
+        launch_qfill_coop(B, dList_.ptr, (int)coop.size(), maxRows, stream_);
+        launch_qfill(B, dList_.ptr + coop.size(), (int)lane.size(), stream_);
         QHIP(hipGetLastError());
         const size_t R = reads_.size();
         std::vector<int> st, ca, cb, fl;
@@ -537,6 +588,267 @@ std::vector<int> QuiverBatch::QVs(int zi)   // ConsensusQVs (Consensus-inl.hpp:2
             if (s < 0.0) sum += std::exp(s);
         }
         qv.push_back(probability_to_qv(1.0 - 1.0 / (1.0 + sum)));
+    }
+    return qv;
+}
+
+
+// ---- batched rounds ---------------------------------------------------------------------------------------
+// Tasks per scorer laid out [mutation][read] (the Deltas layout), scored in launches of at most kTaskChunk
+// tasks so that the extend buffers' bump scratch stays bounded; then k_qreduce (Score / FastIsFavorable),
+// hipCUB compaction of the favourable list and k_best_subset (BestSubset) on the device.
+constexpr long long kTaskChunk = 1LL << 21;
+
+void QuiverBatch::ScoreRound(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes, int sep,
+                             std::vector<std::vector<Scored>>* fav, std::vector<std::vector<Scored>>* picked,
+                             std::vector<std::vector<float>>* all)
+{
+    const int n = (int)zs.size();
+    std::vector<long long> taskStart(n + 1, 0), mutStart(n + 1, 0);
+    std::vector<int> readBase(n), nReads(n), readList, flat;
+    std::vector<float> fastThr(n);
+    for (int w = 0; w < n; ++w) {
+        const HZmw& z = zmws_[zs[w]];
+        readBase[w] = (int)readList.size();
+        nReads[w] = (int)z.reads.size();
+        readList.insert(readList.end(), z.reads.begin(), z.reads.end());
+        fastThr[w] = z.fastThreshold;
+        flat.insert(flat.end(), codes[w].begin(), codes[w].end());
+        mutStart[w + 1] = mutStart[w] + (long long)codes[w].size();
+        taskStart[w + 1] = taskStart[w] + (long long)codes[w].size() * nReads[w];
+    }
+    const long long nMut = mutStart[n], nTask = taskStart[n];
+    std::vector<int> active(reads_.size());
+    for (size_t r = 0; r < reads_.size(); ++r) active[r] = reads_[r].active ? 1 : 0;
+    Upload();
+    put(dWTaskStart_, taskStart, stream_);
+    std::vector<long long> mutBase(mutStart.begin(), mutStart.begin() + n);
+    put(dWMutBase_, mutStart, stream_);
+    put(dWReadBase_, readBase, stream_);
+    put(dWNReads_, nReads, stream_);
+    put(dReadList_, readList, stream_);
+    put(dRActive_, active, stream_);
+    put(dWFast_, fastThr, stream_);
+    put(dCodes_, flat, stream_);
+    dDelta_.reserve(std::max<long long>(nTask, 1), false);
+    for (long long t0 = 0; t0 < nTask;) {
+        const long long m = std::min(kTaskChunk, nTask - t0);
+        for (int attempt = 0;; ++attempt) {
+            QHIP(hipMemsetAsync(dScratchTop_.ptr, 0, sizeof(unsigned long long), stream_));
+            QHIP(hipMemsetAsync(dOverflow_.ptr, 0, sizeof(int), stream_));
+            QScoreWork W;
+            W.codes = dCodes_.ptr;
+            W.delta = dDelta_.ptr;
+            W.scratch = dScratch_.ptr;
+            W.scratchTop = dScratchTop_.ptr;
+            W.scratchCap = dScratch_.cap;
+            W.overflow = dOverflow_.ptr;
+            W.nTasks = m;
+            W.raw = 0;
+            W.nWork = n;
+            W.taskBase = t0;
+            W.wTaskStart = dWTaskStart_.ptr;
+            W.wMutBase = dWMutBase_.ptr;
+            W.wReadBase = dWReadBase_.ptr;
+            W.wNReads = dWNReads_.ptr;
+            W.readList = dReadList_.ptr;
+            W.rActive = dRActive_.ptr;
+            launch_qscore(View(), W, stream_);
+            QHIP(hipGetLastError());
+            int ovf = 0;
+            QHIP(hipMemcpyAsync(&ovf, dOverflow_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
+            QHIP(hipStreamSynchronize(stream_));
+            if (!ovf) break;
+            if ((ovf & 2) || attempt > 6) throw DeviceError("quiver extend buffer exceeds 8 columns / scratch");
+            dScratch_.reserve(dScratch_.cap * 4, false);
+        }
+        t0 += m;
+    }
+    dMScore_.reserve(std::max<long long>(nMut, 1), false);
+    dFav_.reserve(std::max<long long>(nMut, 1), false);
+    QReduceWork R;
+    R.nWork = n;
+    R.wMutStart = dWMutBase_.ptr;
+    R.wTaskStart = dWTaskStart_.ptr;
+    R.wNReads = dWNReads_.ptr;
+    R.wFastThreshold = dWFast_.ptr;
+    R.delta = dDelta_.ptr;
+    R.score = dMScore_.ptr;
+    R.fav = dFav_.ptr;
+    R.nMut = nMut;
+    launch_qreduce(R, stream_);
+    QHIP(hipGetLastError());
+    if (all) {
+        std::vector<double> sc;
+        get(sc, dMScore_, nMut, stream_);
+        QHIP(hipStreamSynchronize(stream_));
+        all->assign(n, {});
+        for (int w = 0; w < n; ++w)
+            for (long long g = mutStart[w]; g < mutStart[w + 1]; ++g) (*all)[w].push_back((float)sc[g]);
+        return;
+    }
+    // favourable entries in list order, then BestSubset per scorer
+    const int nm = (int)std::max<long long>(nMut, 1);
+    dSel_.reserve(nm, false);
+    dSelScore_.reserve(nm, false);
+    dSelCode_.reserve(nm, false);
+    dSelRank_.reserve(nm, false);
+    dSelCount_.reserve(3, false);
+    dSelBase_.reserve(std::max(n, 1), false);
+    dNSel_.reserve(std::max(n, 1), false);
+    hipcub::CountingInputIterator<long long> it(0);
+    size_t a = 0, b = 0, c = 0;
+    QHIP(hipcub::DeviceSelect::Flagged(nullptr, a, it, dFav_.ptr, dSel_.ptr, dSelCount_.ptr, nm, stream_));
+    QHIP(hipcub::DeviceSelect::Flagged(nullptr, b, dMScore_.ptr, dFav_.ptr, dSelScore_.ptr, dSelCount_.ptr + 1, nm,
+                                       stream_));
+    QHIP(hipcub::DeviceSelect::Flagged(nullptr, c, dCodes_.ptr, dFav_.ptr, dSelCode_.ptr, dSelCount_.ptr + 2, nm,
+                                       stream_));
+    dSelTmp_.reserve(std::max<size_t>(std::max(a, std::max(b, c)), 1), false);
+    if (nMut > 0) {
+        QHIP(hipcub::DeviceSelect::Flagged(dSelTmp_.ptr, a, it, dFav_.ptr, dSel_.ptr, dSelCount_.ptr, nm, stream_));
+        QHIP(hipcub::DeviceSelect::Flagged(dSelTmp_.ptr, b, dMScore_.ptr, dFav_.ptr, dSelScore_.ptr,
+                                           dSelCount_.ptr + 1, nm, stream_));
+        QHIP(hipcub::DeviceSelect::Flagged(dSelTmp_.ptr, c, dCodes_.ptr, dFav_.ptr, dSelCode_.ptr,
+                                           dSelCount_.ptr + 2, nm, stream_));
+    } else {
+        QHIP(hipMemsetAsync(dSelCount_.ptr, 0, 3 * sizeof(long long), stream_));
+    }
+    pbccs::ScoreWork SW;
+    SW.nWork = n;
+    SW.mutStart = dWMutBase_.ptr;
+    pbccs::launch_sel_ranges(SW, dSel_.ptr, dSelCount_.ptr, dSelBase_.ptr, dNSel_.ptr, stream_);
+    pbccs::launch_best_subset(n, dSelBase_.ptr, dNSel_.ptr, dSelCode_.ptr, dSelScore_.ptr, std::max(sep, 0), -1,
+                              dSelRank_.ptr, stream_);
+    QHIP(hipGetLastError());
+    long long cnt = 0;
+    QHIP(hipMemcpyAsync(&cnt, dSelCount_.ptr, sizeof(long long), hipMemcpyDeviceToHost, stream_));
+    QHIP(hipStreamSynchronize(stream_));
+    std::vector<long long> sel;
+    std::vector<double> selScore;
+    std::vector<int> selCode, selRank;
+    get(sel, dSel_, cnt, stream_);
+    get(selScore, dSelScore_, cnt, stream_);
+    get(selCode, dSelCode_, cnt, stream_);
+    get(selRank, dSelRank_, cnt, stream_);
+    QHIP(hipStreamSynchronize(stream_));
+    fav->assign(n, {});
+    picked->assign(n, {});
+    std::vector<std::vector<std::pair<int, Scored>>> pk(n);
+    for (long long q = 0; q < cnt; ++q) {
+        const int w = (int)(std::upper_bound(mutStart.begin(), mutStart.end(), sel[q]) - mutStart.begin() - 1);
+        const Scored e{selCode[q], (float)selScore[q]};
+        (*fav)[w].push_back(e);
+        if (selRank[q] > 0) pk[w].emplace_back(selRank[q], e);
+    }
+    for (int w = 0; w < n; ++w) {
+        std::sort(pk[w].begin(), pk[w].end(),
+                  [](const std::pair<int, Scored>& x, const std::pair<int, Scored>& y) { return x.first < y.first; });
+        for (const std::pair<int, Scored>& p : pk[w]) (*picked)[w].push_back(p.second);
+    }
+}
+
+void QuiverBatch::RefineMany(const std::vector<int>& zs, const RefineOptions& ro, std::vector<long long>* nTested,
+                             std::vector<long long>* nApplied, std::vector<char>* converged, std::vector<char>* ok)
+{
+    const int n = (int)zs.size();
+    nTested->assign(n, 0);
+    nApplied->assign(n, 0);
+    converged->assign(n, 0);
+    ok->assign(n, 1);
+    std::vector<char> done(n, 0);
+    std::vector<int> iter(n, 0);
+    std::vector<std::unordered_set<std::string>> history(n);
+    std::vector<std::vector<int>> centers(n);
+    if (ro.maxIterations <= 0) return;
+    for (;;) {
+        std::vector<int> act, idx;
+        for (int k = 0; k < n; ++k)
+            if (!done[k]) { act.push_back(zs[k]); idx.push_back(k); }
+        if (act.empty()) break;
+        std::vector<std::vector<int>> codes(act.size());
+        for (size_t a = 0; a < act.size(); ++a) {
+            const std::string& tpl = zmws_[act[a]].tpl;
+            const int k = idx[a];
+            if (iter[k] == 0) unique_mutations(tpl, 0, (int)tpl.size(), &codes[a]);
+            else nearby_mutations(tpl, centers[k], ro.mutationNeighborhood, &codes[a]);
+            (*nTested)[k] += (long long)codes[a].size();
+        }
+        std::vector<std::vector<Scored>> fav, picked;
+        ScoreRound(act, codes, ro.mutationSeparation, &fav, &picked, nullptr);
+        std::vector<int> refill;
+        for (size_t a = 0; a < act.size(); ++a) {
+            const int k = idx[a];
+            HZmw& z = zmws_[act[a]];
+            if (fav[a].empty()) {
+                (*converged)[k] = 1;
+                done[k] = 1;
+                continue;
+            }
+            std::vector<Scored>& best = picked[a];
+            std::vector<Mutation> muts;
+            for (const Scored& b : best) muts.push_back(mutation_from_code(b.code));
+            if (best.size() > 1) {
+                std::string nx;
+                std::vector<int> mtp;
+                if (apply_mutations(z.tpl, muts, &nx, &mtp) && history[k].count(nx)) {
+                    best.resize(1);
+                    muts.resize(1);
+                }
+            }
+            (*nApplied)[k] += (long long)best.size();
+            history[k].insert(z.tpl);
+            centers[k].clear();
+            for (const Scored& f : fav[a]) centers[k].push_back(mut_pos(f.code));
+            std::string next;
+            std::vector<int> mtp;
+            if (!apply_mutations(z.tpl, muts, &next, &mtp)) {   // ApplyMutations refused: Refine returns false
+                (*ok)[k] = 0;
+                done[k] = 1;
+                continue;
+            }
+            z.tpl = next;
+            for (int r : z.reads) {
+                HRead& h = reads_[r];
+                h.ts = mtp[h.ts];
+                h.te = mtp[h.te];
+                if (h.active) {
+                    EnsureCapacity(r);
+                    refill.push_back(r);
+                }
+            }
+            dirty_ = true;
+            if (++iter[k] >= ro.maxIterations) done[k] = 1;
+        }
+        if (!refill.empty()) Fill(refill);   // a refill that mismatches marks the read inactive
+    }
+}
+
+std::vector<std::vector<int>> QuiverBatch::QVsMany(const std::vector<int>& zs)   // ConsensusQVs (:274-295)
+{
+    const int n = (int)zs.size();
+    std::vector<std::vector<int>> codes(n), posOff(n);
+    for (int w = 0; w < n; ++w) {
+        const std::string& tpl = zmws_[zs[w]].tpl;
+        for (int p = 0; p < (int)tpl.size(); ++p) {
+            posOff[w].push_back((int)codes[w].size());
+            unique_mutations(tpl, p, p + 1, &codes[w]);
+        }
+        posOff[w].push_back((int)codes[w].size());
+    }
+    std::vector<std::vector<Scored>> fav, picked;
+    std::vector<std::vector<float>> all;
+    ScoreRound(zs, codes, -1, &fav, &picked, &all);
+    std::vector<std::vector<int>> qv(n);
+    for (int w = 0; w < n; ++w) {
+        const int L = (int)posOff[w].size() - 1;
+        for (int p = 0; p < L; ++p) {
+            double sum = 0.0;
+            for (int m = posOff[w][p]; m < posOff[w][p + 1]; ++m) {
+                const double sc = all[w][m];
+                if (sc < 0.0) sum += std::exp(sc);
+            }
+            qv[w].push_back(probability_to_qv(1.0 - 1.0 / (1.0 + sum)));
+        }
     }
     return qv;
 }

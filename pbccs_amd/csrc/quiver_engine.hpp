@@ -46,6 +46,20 @@ public:
     bool ApplyMutations(int z, const std::vector<Mutation>& muts);
     bool Refine(int z, const RefineOptions& ro, long long* nTested, long long* nApplied, bool* converged);
     std::vector<int> QVs(int z);
+
+    // ---- batched forms (pbccs_quiver_polish_batch): many scorers in lock-step rounds ------------------
+    struct ReadSpec {
+        int z, strand, ts, te, config;
+        float threshold;
+        QReadFeatures f;
+    };
+    // AddRead for every spec, one fill launch for all; returns each read's active flag
+    std::vector<char> AddReads(std::vector<ReadSpec>* specs);
+    // RefineConsensus on every listed scorer: one scoring launch series, one device reduction / select and
+    // one refill per round.  ok[k] = 0 where ApplyMutations refused an edit (the scorer's Refine returns false).
+    void RefineMany(const std::vector<int>& zs, const RefineOptions& ro, std::vector<long long>* nTested,
+                    std::vector<long long>* nApplied, std::vector<char>* converged, std::vector<char>* ok);
+    std::vector<std::vector<int>> QVsMany(const std::vector<int>& zs);
     // RecursorBase::Alignment (detail/RecursorBase.cpp:124-264) of read r against its template window,
     // from the read's alpha band (Viterbi configs only): the gapped target and query strings.
     bool Alignment(int r, std::string* target, std::string* query);
@@ -79,12 +93,23 @@ private:
         float score = 0.0f;
         long long alloc[2] = {0, 0};
     };
+    int Register(int z, const QReadFeatures& f, int strand, int ts, int te, int config);   // a read, unfilled
     void Upload();
     void EnsureCapacity(int r);
     QBatch View();
     void Fill(const std::vector<int>& reads);
     void RunScore(const std::vector<int>& taskRead, const std::vector<int>& taskMut, const std::vector<int>& codes,
                   bool raw, std::vector<float>* d);
+    // One batched scoring round over scorers zs with their mutation lists: per scorer the favourable
+    // mutations (list order, float scores) and, with sep >= 0, BestSubset's picks (pick order) from the
+    // device select; with all != nullptr every mutation's Score instead.
+    struct Scored {
+        int code;
+        float score;
+    };
+    void ScoreRound(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes, int sep,
+                    std::vector<std::vector<Scored>>* fav, std::vector<std::vector<Scored>>* picked,
+                    std::vector<std::vector<float>>* all);
 
     int device_ = 0;
     hipStream_t stream_ = nullptr;
@@ -108,6 +133,12 @@ private:
     DevVec<unsigned long long> dScratchTop_;
     DevVec<long long> dMoveOff_;
     DevVec<unsigned char> dMoves_;
+    // batched rounds
+    DevVec<long long> dWTaskStart_, dWMutBase_, dSel_, dSelCount_, dSelBase_;
+    DevVec<int> dWReadBase_, dWNReads_, dReadList_, dRActive_, dSelCode_, dSelRank_, dNSel_;
+    DevVec<float> dWFast_;
+    DevVec<double> dMScore_, dSelScore_;
+    DevVec<unsigned char> dFav_, dSelTmp_;
 };
 
 }  // namespace quiver

@@ -481,7 +481,387 @@ __device__ __forceinline__ long long allocated_entries(const QAlloc* a, int cols
     return s;
 }
 
+// ==== cooperative fill: one wavefront per read ===========================================================
+// The SSE recursor's fills with the rows of a column spread over the 64 lanes (SseRecursor.cpp:73-353).
+// Per column, every lane evaluates its row's Inc / Merge / Del terms from the two previous columns (held in
+// an LDS ring indexed by absolute row), then the Extra cascade -- the one serial dependency, kept in the
+// reference's row order -- walks the lanes through v_readlane.  Rows are mapped so that the SSE 4-row blocks
+// are lane quads: alpha groups start at rows = I + 1 (mod 4), beta groups at rows = 0 (mod 4).  A chunk of 64
+// rows is evaluated speculatively; the band's stopping rule (block min against the running max - ScoreDiff,
+// or the guide's reqEnd / reqBegin) is then resolved for all 16 quads at once with a max-scan, and rows past
+// the stop are dropped before anything is stored.  Cells and band decisions equal the lane fill's.
+constexpr int kQCoopMaxRows = 4096;   // reads of up to 4095 bases (three LDS columns: 48 KB)
+
+__device__ __forceinline__ float rl(float x, int k) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), k)); }
+__device__ __forceinline__ float fmax_ref(float a, float b) { return b > a ? b : a; }   // keeps a on ties
+
+__device__ __forceinline__ float wave_max(float x)
+{
+    for (int o = 32; o > 0; o >>= 1) x = fmax_ref(x, __shfl_xor(x, o, 64));
+    return x;
+}
+
+// RowRange (RecursorBase-inl.hpp:49-84) over a previous pass's column, cooperatively
+__device__ __forceinline__ void coop_row_range(const QBand& m, int j, float sd, int lane, int* ob, int* oe)
+{
+    const int2 rg = m.range[j];
+    const int b = rg.x, e = rg.y;
+    // maxRow: the first row holding the maximum (strict '>' scanning down from b)
+    float best = kNegInf;
+    int bestRow = 0x7fffffff;
+    for (int i = b + lane; i < e; i += 64) {
+        const float v = m.Get(i, j);
+        if (bestRow == 0x7fffffff || v > best) { best = v; bestRow = i; }   // a lane's rows ascend: first max
+    }
+    const float mxv = wave_max(best);
+    int cand = (bestRow != 0x7fffffff && best == mxv) ? bestRow : 0x7fffffff;
+    for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+    const int maxRow = cand;
+    const float thr = mxv - sd;
+    // b' = first row in [b, maxRow) with value >= thr, else maxRow
+    int nb = maxRow;
+    for (int i0 = b; i0 < maxRow; i0 += 64) {
+        const int i = i0 + lane;
+        const bool hit = i < maxRow && !(m.Get(i, j) < thr);
+        const unsigned long long bal = __ballot(hit);
+        if (bal) { nb = i0 + __ffsll((long long)bal) - 1; break; }
+    }
+    // e' = last row in [maxRow, e) with value >= thr, plus one; else maxRow
+    int ne = maxRow;
+    for (int i1 = e; i1 > maxRow; i1 -= 64) {
+        const int i = i1 - 1 - lane;
+        const bool hit = i >= maxRow && !(m.Get(i, j) < thr);
+        const unsigned long long bal = __ballot(hit);
+        if (bal) { ne = i1 - 1 - (__ffsll((long long)bal) - 1) + 1; break; }
+    }
+    *ob = nb;
+    *oe = ne;
+}
+
+__device__ __forceinline__ void coop_range_guide(int j, const QBand* guide, const QBand* self, float sd, int lane,
+                                                 int* hb, int* he)
+{
+    const bool useG = guide && !guide->Empty(j);
+    const bool useS = self && !self->Empty(j);
+    if (!useG && !useS) return;
+    int b = *hb, e = *he, rb, re;
+    if (useG) { coop_row_range(*guide, j, sd, lane, &rb, &re); b = min(rb, b); e = max(re, e); }
+    if (useS) { coop_row_range(*self, j, sd, lane, &rb, &re); b = min(rb, b); e = max(re, e); }
+    *hb = b;
+    *he = e;
+}
+
+struct LdsCol {
+    float* v;
+    int b, e;   // valid rows [b, e)
+    __device__ __forceinline__ float at(int i) const { return (i >= b && i < e) ? v[i] : kNegInf; }
+};
+
+// One column of one pass.  BETA: rows run downwards (lane l <-> row top - l), the chain from row + 1.
+// Returns the column's [begin, end) in *ob / *oe and leaves its cells in cur.v (rows of the range) and in
+// the arena at out.off[j].  thrOut: the running threshold after the last evaluated block.
+template <bool BETA>
+__device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int hb, int he, const LdsCol& c1,
+                                            const LdsCol& c2, float* cur, const QBand& out, long long base, QAlloc* alloc,
+                                            bool& ovf, int* ob, int* oe, float* thrOut)
+{
+    const int I = e.I(), J = e.J();
+    const bool sp = e.p->sumProduct != 0;
+    const bool merge = (e.p->moves & kMerge) != 0;
+    const float sd = e.p->scoreDiff;
+    // first row in processing order, the band guard, and the quad alignment
+    const int req = BETA ? max(0, hb) : min(I + 1, he);
+    const int first = BETA ? he - 1 : hb;
+    int chunk;   // alpha: row of lane 0; beta: row of lane 0 (the top row)
+    bool prefix;
+    if (!BETA) {
+        const int gs = first - ((((first - (I + 1)) % 4) + 4) % 4);
+        chunk = gs;
+        prefix = first != gs || first == 0;
+    } else {
+        chunk = first | 3;
+        prefix = (first & 3) != 3 || first == I;
+    }
+    float carry = kNegInf;              // chain value of the previous row in processing order
+    float score = kNegInf, mx = kNegInf, thr = kNegInf;
+    int stop = BETA ? -1 : I + 1;       // alpha: endRow; beta: beginRow
+    const bool empty = BETA ? (first < 0) : (first > I);
+    bool done = empty;
+    if (empty) stop = BETA ? first + 1 : first;
+    for (int c = 0; !done; ++c) {
+        const int row = BETA ? chunk - 64 * c - lane : chunk + 64 * c + lane;
+        const bool valid = BETA ? (row <= first && row >= 0) : (row >= first && row <= I);
+        const int g = lane >> 2;
+        const bool pre = prefix && c == 0 && g == 0;
+        float v = kNegInf, x = 0.0f;
+        bool has = false;
+        if (valid) {
+            if (!BETA) {
+                if (pre) {
+                    if (row == 0 && j == 0) v = 0.0f;
+                    if (row > 0 && j > 0) v = comb(sp, v, c1.at(row - 1) + e.Inc(row - 1, j - 1));
+                    if (merge && row > 0 && j > 1) v = comb(sp, v, c2.at(row - 1) + e.Merge(row - 1, j - 2));
+                    if (j > 0) v = comb(sp, v, c1.at(row) + e.Del(row, j - 1));
+                } else {
+                    if (j > 0) v = comb4(sp, v, c1.at(row - 1) + e.Inc(row - 1, j - 1));
+                    if (merge && j >= 2) v = comb4(sp, v, c2.at(row - 1) + e.Merge(row - 1, j - 2));
+                    if (j > 0) v = comb4(sp, v, c1.at(row) + e.Del(row, j - 1));
+                }
+                has = row > 0;
+                if (has) x = e.Extra(row - 1, j);
+            } else {
+                if (pre) {
+                    if (row == I && j == J) v = 0.0f;
+                    if (row < I && j < J) v = comb(sp, v, c1.at(row + 1) + e.Inc(row, j));
+                    if (merge && j < J - 1 && row < I) v = comb(sp, v, c2.at(row + 1) + e.Merge(row, j));
+                    if (j < J) v = comb(sp, v, c1.at(row) + e.Del(row, j));
+                } else {
+                    if (j < J) v = comb4(sp, v, c1.at(row + 1) + e.Inc(row, j));
+                    if (merge && j < J - 1) v = comb4(sp, v, c2.at(row + 1) + e.Merge(row, j));
+                    if (j < J) v = comb4(sp, v, c1.at(row) + e.Del(row, j));
+                }
+                has = row < I;
+                if (has) x = e.Extra(row, j);
+            }
+        }
+        // the Extra cascade, in processing order through the valid lanes
+        float sv = valid ? v : kNegInf;
+        const int k0 = BETA ? max(0, chunk - 64 * c - first) : max(0, first - (chunk + 64 * c));
+        const int k1 = BETA ? min(63, chunk - 64 * c) : min(63, I - (chunk + 64 * c));
+        for (int k = k0; k <= k1; ++k) {
+            if (lane == k && has) sv = comb(sp, v, carry + x);
+            carry = rl(sv, k);
+        }
+        // band stopping rule per quad: gmin = the quad's block min (the prefix quad: its last row), gmax
+        const int qb = lane & ~3;
+        const float q0 = __shfl(sv, qb, 64), q1 = __shfl(sv, qb + 1, 64), q2 = __shfl(sv, qb + 2, 64),
+                    q3 = __shfl(sv, qb + 3, 64);
+        float gmin, gmax;
+        if (pre) {
+            // rows in processing order within the prefix quad: the valid ones, last = the quad's last valid
+            gmax = kNegInf;
+            gmin = kNegInf;
+            auto visit = [&](int t2, float qv) {
+                const int rr = BETA ? chunk - (qb + t2) : chunk + qb + t2;
+                const bool vv = BETA ? (rr <= first && rr >= 0) : (rr >= first && rr <= I);
+                if (vv) {
+                    if (qv > gmax) gmax = qv;
+                    gmin = qv;
+                }
+            };
+            visit(0, q0);
+            visit(1, q1);
+            visit(2, q2);
+            visit(3, q3);
+        } else {   // std::max_element / std::min_element over the block
+            gmax = q0;
+            gmin = q0;
+            if (gmax < q1) gmax = q1;
+            if (q1 < gmin) gmin = q1;
+            if (gmax < q2) gmax = q2;
+            if (q2 < gmin) gmin = q2;
+            if (gmax < q3) gmax = q3;
+            if (q3 < gmin) gmin = q3;
+        }
+        // running max before each quad (exclusive scan over quads, seeded with mx)
+        float inc = gmax;
+        for (int o = 1; o < 64; o <<= 1) {
+            const float y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc = fmax_ref(inc, y);
+        }
+        const float prevInc = __shfl_up(inc, 1, 64);
+        const float mxBefore = fmax_ref(mx, lane >= 1 ? prevInc : kNegInf);
+        const float prevMin = __shfl_up(gmin, 4, 64);
+        const float scoreBefore = lane >= 4 ? prevMin : score;
+        // the quad's block start (its lowest row) and test; the prefix quad never stops
+        const int lowRow = BETA ? chunk - 64 * c - qb - 3 : chunk + 64 * c + qb;
+        bool ok;
+        if (pre) ok = true;
+        else {
+            // thr = mx - ScoreDiff once some score raised mx; -FLT_MAX (the literal) before
+            const float thrB = mxBefore == kNegInf ? kNegInf : mxBefore - sd;
+            ok = BETA ? (lowRow >= 0 && (scoreBefore >= thrB || lowRow >= req))
+                      : (lowRow <= I && (scoreBefore >= thrB || lowRow < req));
+        }
+        const unsigned long long fails = __ballot((lane & 3) == 0 && !ok);
+        const int stopQuad = fails ? (__ffsll((long long)fails) - 1) >> 2 : 16;
+        // rows of the quads before the stop are the column's
+        const bool keep = valid && g < stopQuad;
+        if (keep) cur[row] = sv;
+        // state after the last kept quad
+        if (stopQuad > 0) {
+            const int lastLane = 4 * stopQuad - 1;
+            score = __shfl(gmin, lastLane, 64);
+            mx = fmax_ref(mx, __shfl(inc, lastLane, 64));
+            thr = mx == kNegInf ? kNegInf : mx - sd;
+        }
+        if (stopQuad < 16) {
+            const int lr = BETA ? chunk - 64 * c - 4 * stopQuad - 3 : chunk + 64 * c + 4 * stopQuad;
+            stop = BETA ? lr + 4 : lr;
+            done = true;
+        } else if (BETA ? (chunk - 64 * c - 63 <= 0) : (chunk + 64 * c + 63 >= I)) {
+            stop = BETA ? 0 : I + 1;
+            done = true;
+        }
+    }
+    const int beginRow = BETA ? stop : first;
+    const int endRow = BETA ? first + 1 : stop;
+    // store the column top-down into the arena
+    for (int r = beginRow + lane; r < endRow; r += 64) {
+        const long long k = base + (r - beginRow);
+        if (k < out.cap) out.val[k] = cur[r];
+        else ovf = true;
+    }
+    // SparseVector allocation bookkeeping, rows in the order the reference sets them
+    if (alloc && lane == 0) {
+        if (!BETA) {
+            for (int r = beginRow; r < endRow; ++r) alloc_set(*alloc, r, I + 1);
+        } else {
+            for (int r = endRow - 1; r >= beginRow; --r) alloc_set(*alloc, r, I + 1);
+        }
+    }
+    *ob = beginRow;
+    *oe = endRow;
+    *thrOut = thr;
+}
+
+template <bool BETA>
+__device__ long long coop_fill(const QEval& e, const QBand* guide, const QBand* prev, const QBand& out, QAlloc* alloc,
+                               bool allocExists, bool& ovf, float* lds, int ldsRows, int lane)
+{
+    const int I = e.I(), J = e.J();
+    const float sd = e.p->scoreDiff;
+    // the LDS ring: cur (column being filled), c1 (previous), c2 (the one before), rotated by value
+    LdsCol cur{lds, 0, 0}, c1{lds + ldsRows, 0, 0}, c2{lds + 2 * ldsRows, 0, 0};
+    long long used = 0;
+    int hb = BETA ? I + 1 : 0, he = BETA ? I + 1 : 0;
+    for (int s = 0; s <= J; ++s) {
+        const int j = BETA ? J - s : s;
+        coop_range_guide(j, guide, prev, sd, lane, &hb, &he);
+        if (alloc && lane == 0) alloc_start(alloc[j], allocExists, hb, he, I + 1);
+        int b, en;
+        float thr;
+        coop_column<BETA>(e, j, lane, hb, he, c1, c2, cur.v, out, used, alloc ? &alloc[j] : nullptr, ovf, &b, &en, &thr);
+        cur.b = b;
+        cur.e = en;
+        if (lane == 0) {
+            out.off[j] = (int)min(used, (long long)0x7fffffff);
+            out.range[j] = make_int2(b, en);
+        }
+        used += en - b;
+        if (!BETA) {
+            he = en;
+            // hb = first row of the column at or above the threshold (else endRow)
+            int nb = en;
+            for (int i0 = b; i0 < en; i0 += 64) {
+                const int i = i0 + lane;
+                const bool hit = i < en && !(cur.v[i] < thr);
+                const unsigned long long bal = __ballot(hit);
+                if (bal) { nb = i0 + __ffsll((long long)bal) - 1; break; }
+            }
+            hb = nb;
+        } else {
+            hb = b;
+            int ne = b;
+            for (int i1 = en; i1 > b; i1 -= 64) {
+                const int i = i1 - 1 - lane;
+                const bool hit = i >= b && !(cur.v[i] < thr);
+                const unsigned long long bal = __ballot(hit);
+                if (bal) { ne = i1 - (__ffsll((long long)bal) - 1); break; }
+            }
+            he = ne;
+        }
+        const LdsCol old2 = c2;
+        c2 = c1;
+        c1 = cur;
+        cur = old2;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the pass's stores before later passes read them
+    return used;
+}
+
 }  // namespace
+
+// ---- k_qfill_coop: FillAlphaBeta with one wavefront per read (SparseSse recursors, reads < kQCoopMaxRows) --
+__global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restrict__ reads, int n, int ldsRows)
+{
+    extern __shared__ float qlds[];
+    const int t = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (t >= n) return;
+    const int r = reads[t];
+    const ReadView v = read_view(B, r);
+    const QEval& e = v.ev;
+    const int I = e.I(), J = e.J();
+    if (I < 1 || J < 1 || J + 1 > B.rColCap[r] || I + 1 > ldsRows) {
+        if (lane == 0) B.rStatus[r] = kQBad;
+        return;
+    }
+    for (int k = 0; k < 4; ++k) {
+        const QBand m = arena(v, k);
+        for (int j = lane; j <= J; j += 64) m.range[j] = make_int2(0, 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    bool ovf = false;
+    long long needA = 0, needB = 0;
+    int curA = 0, curB = 2;
+    bool aPassed = false, bPassed = false;
+    auto passA = [&](bool guided) {
+        const int nxt = aPassed ? (curA ^ 1) : 0;
+        const QBand g = arena(v, curB), self = arena(v, curA), out = arena(v, nxt);
+        const long long u = coop_fill<false>(e, guided ? &g : nullptr, aPassed ? &self : nullptr, out, v.allocA, aPassed,
+                                             ovf, qlds, ldsRows, lane);
+        needA = max(needA, u);
+        curA = nxt;
+        aPassed = true;
+        return u;
+    };
+    auto passB = [&]() {
+        const int nxt = bPassed ? (curB ^ 1) : 2;
+        const QBand g = arena(v, curA), self = arena(v, curB), out = arena(v, nxt);
+        const long long u = coop_fill<true>(e, &g, bPassed ? &self : nullptr, out, v.allocB, bPassed, ovf, qlds, ldsRows,
+                                            lane);
+        needB = max(needB, u);
+        curB = nxt;
+        bPassed = true;
+        return u;
+    };
+    // RecursorBase::FillAlphaBeta (detail/RecursorBase.cpp:70-116)
+    const long long ua = passA(false);
+    const long long ub = passB();
+    ovf = __ballot(ovf) != 0;
+    int flips = 0;
+    const int maxSize = (int)(0.5 + 0.04 * (I + 1) * (J + 1));
+    if (!ovf && (ua >= maxSize || ub >= maxSize)) {
+        passA(true);
+        passB();
+        passA(true);
+        flips += 3;
+        ovf = __ballot(ovf) != 0;
+    }
+    auto a_end = [&]() { return arena(v, curA).Get(I, J); };
+    auto b_start = [&]() { return arena(v, curB).Get(0, 0); };
+    while (!ovf && (double)fabsf(a_end() - b_start()) > 0.2 && flips <= kMaxFlipFlops) {
+        if (flips % 2 == 0) passA(true);
+        else passB();
+        flips++;
+        ovf = __ballot(ovf) != 0;
+    }
+    if (lane != 0) return;
+    B.rUsed[2 * r] = needA;
+    B.rUsed[2 * r + 1] = needB;
+    if (ovf) {
+        B.rStatus[r] = kQOverflow;
+        return;
+    }
+    B.rCurA[r] = curA;
+    B.rCurB[r] = curB - 2;
+    B.rFlips[r] = flips;
+    B.rScore[r] = b_start();
+    B.rAlloc[2 * r] = allocated_entries(v.allocA, J + 1);
+    B.rAlloc[2 * r + 1] = allocated_entries(v.allocB, J + 1);
+    B.rStatus[r] = ((double)fabsf(a_end() - b_start()) > 0.2) ? kQMismatch : kQOk;
+}
 
 // ---- k_qfill: MutationScorer ctor / Template() -> FillAlphaBeta ------------------------------------------
 __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ reads, int n)
@@ -560,10 +940,28 @@ __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ 
 // ---- k_qscore: MultiReadMutationScorer::Score terms (Quiver/MultiReadMutationScorer.cpp:60-120, 312-326)
 __global__ void __launch_bounds__(64) k_qscore(QBatch B, QScoreWork W)
 {
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= W.nTasks) return;
-    const int r = W.taskRead[t];
-    const int code = W.codes[W.taskMut[t]];
+    const long long lt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lt >= W.nTasks) return;
+    const long long t = W.taskBase + lt;
+    int r, code;
+    if (W.nWork > 0) {   // batched round: decode (item, mutation, read) from the task number
+        int lo = 0, hi = W.nWork;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (W.wTaskStart[mid] <= t) lo = mid; else hi = mid;
+        }
+        const long long local = t - W.wTaskStart[lo];
+        const int nr = W.wNReads[lo];
+        r = W.readList[W.wReadBase[lo] + (int)(local % nr)];
+        code = W.codes[W.wMutBase[lo] + local / nr];
+        if (!W.rActive[r]) {
+            W.delta[t] = __builtin_nanf("");
+            return;
+        }
+    } else {
+        r = W.taskRead[t];
+        code = W.codes[W.taskMut[t]];
+    }
     const int type = (code >> 2) & 3, pos = code >> 4, base = code & 3;
     const int ms = pos, me = (type == 0) ? pos : pos + 1;
     const int ts = B.rTs[r], te = B.rTe[r];
@@ -658,6 +1056,31 @@ __global__ void __launch_bounds__(64) k_qscore(QBatch B, QScoreWork W)
     W.delta[t] = W.raw ? score : score - B.rScore[r];
 }
 
+// ---- k_qreduce: Score / FastIsFavorable of a batched round, one lane per mutation ----------------------
+__global__ void __launch_bounds__(256) k_qreduce(QReduceWork W)
+{
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= W.nMut) return;
+    int lo = 0, hi = W.nWork;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (W.wMutStart[mid] <= g) lo = mid; else hi = mid;
+    }
+    const int nr = W.wNReads[lo];
+    const float* d = W.delta + W.wTaskStart[lo] + (g - W.wMutStart[lo]) * nr;
+    const float thr = W.wFastThreshold[lo];
+    float sum = 0.0f;
+    bool fast = true;
+    for (int k = 0; k < nr; ++k) {
+        const float x = d[k];
+        if (x != x) continue;
+        sum += x;
+        if (sum < thr) fast = false;   // FastIsFavorable returns here; Score keeps summing
+    }
+    W.score[g] = (double)sum;
+    W.fav[g] = (fast && (double)sum > 0.04) ? 1 : 0;   // MIN_FAVORABLE_SCOREDIFF (:52), a double
+}
+
 // ---- k_qalign: RecursorBase::Alignment (detail/RecursorBase.cpp:118-264) -------------------------------
 // The Viterbi path through a read's final alpha band, one lane per read, walking back from (I, J): moves
 // tried in the order Incorporate, Delete, Extra, Merge, strict '>' against -FLT_MAX, the move score added
@@ -717,10 +1140,23 @@ void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s)
     hipLaunchKernelGGL(k_qfill, dim3((n + 63) / 64), dim3(64), 0, s, B, reads, n);
 }
 
+void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, hipStream_t s)
+{
+    if (n <= 0) return;
+    const int rows = (maxRows + 63) / 64 * 64;
+    hipLaunchKernelGGL(k_qfill_coop, dim3(n), dim3(64), (size_t)3 * rows * sizeof(float), s, B, reads, n, rows);
+}
+
 void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s)
 {
     if (W.nTasks <= 0) return;
     hipLaunchKernelGGL(k_qscore, dim3((unsigned)((W.nTasks + 63) / 64)), dim3(64), 0, s, B, W);
+}
+
+void launch_qreduce(const QReduceWork& W, hipStream_t s)
+{
+    if (W.nMut <= 0) return;
+    hipLaunchKernelGGL(k_qreduce, dim3((unsigned)((W.nMut + 255) / 256)), dim3(256), 0, s, W);
 }
 
 }  // namespace quiver

@@ -60,10 +60,42 @@ struct QScoreWork {
     long long nTasks;
     int raw;                   // 1: codes are already in the read's own coordinates (MutationScorer API):
                                //    no ReadScoresMutation / orientation, delta = the absolute score
+    // Batched form (nWork > 0): tasks [taskBase, taskBase + nTasks) of work items laid out as
+    // [item][mutation][read]; item w owns tasks [wTaskStart[w], wTaskStart[w + 1]), its mutations are
+    // codes[wMutBase[w] ...] and its reads readList[wReadBase[w] ...] (wNReads of them).  taskRead /
+    // taskMut are unused; delta is indexed by the global task number; inactive reads give NaN.
+    int nWork = 0;
+    long long taskBase = 0;
+    const long long* wTaskStart = nullptr;
+    const long long* wMutBase = nullptr;
+    const int* wReadBase = nullptr;
+    const int* wNReads = nullptr;
+    const int* readList = nullptr;
+    const int* rActive = nullptr;
+};
+
+// MultiReadMutationScorer::Score / FastIsFavorable per mutation of a batched round (Quiver/
+// MultiReadMutationScorer.cpp:312-353, 392-409): the float sum over the item's reads in read order (NaN
+// deltas skipped); fav = the fast sum never fell below the item's fast threshold and ends > 0.04.
+struct QReduceWork {
+    int nWork;
+    const long long* wMutStart;   // item w's mutations [wMutStart[w], wMutStart[w + 1])
+    const long long* wTaskStart;
+    const int* wNReads;
+    const float* wFastThreshold;
+    const float* delta;
+    double* score;                // the full float sum, widened (k_best_subset casts back to float)
+    unsigned char* fav;
+    long long nMut;
 };
 
 void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s);
+// FillAlphaBeta with one wavefront per read (SparseSse recursors; reads of I + 1 <= kQCoopRows rows); maxRows =
+// the largest I + 1 of the listed reads
+constexpr int kQCoopRows = 4096;
+void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, hipStream_t s);
 void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s);
+void launch_qreduce(const QReduceWork& W, hipStream_t s);
 // RecursorBase::Alignment per listed read: moves (from the end) at moveOff[t], nMoves[t] of them
 void launch_qalign(const QBatch& B, const int* reads, int n, const long long* moveOff, unsigned char* moves,
                    int* nMoves, hipStream_t s);

@@ -80,6 +80,26 @@ class CQuiverConfig(ctypes.Structure):
                 ("sum_product", ctypes.c_int), ("recursor", ctypes.c_int)]
 
 
+class CQuiverRead(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_char_p), ("len", ctypes.c_int), ("ins_qv", ctypes.POINTER(ctypes.c_float)),
+                ("subs_qv", ctypes.POINTER(ctypes.c_float)), ("del_qv", ctypes.POINTER(ctypes.c_float)),
+                ("del_tag", ctypes.POINTER(ctypes.c_float)), ("merge_qv", ctypes.POINTER(ctypes.c_float)),
+                ("chemistry", ctypes.c_char_p), ("strand", ctypes.c_int), ("tstart", ctypes.c_int),
+                ("tend", ctypes.c_int), ("threshold", ctypes.c_float)]
+
+
+class CQuiverZmw(ctypes.Structure):
+    _fields_ = [("tpl", ctypes.c_char_p), ("tpl_len", ctypes.c_int), ("reads", ctypes.POINTER(CQuiverRead)),
+                ("n_reads", ctypes.c_int)]
+
+
+class CQuiverResult(ctypes.Structure):
+    _fields_ = [("consensus", ctypes.c_char_p), ("consensus_cap", ctypes.c_int), ("consensus_len", ctypes.c_int),
+                ("qvs", ctypes.POINTER(ctypes.c_int)), ("n_tested", ctypes.c_longlong),
+                ("n_applied", ctypes.c_longlong), ("converged", ctypes.c_int), ("ok", ctypes.c_int),
+                ("n_active", ctypes.c_int)]
+
+
 class CPoaInput(ctypes.Structure):
     _fields_ = [("seqs", ctypes.POINTER(ctypes.c_char_p)), ("lens", ctypes.POINTER(ctypes.c_int)),
                 ("n_reads", ctypes.c_int)]
@@ -174,6 +194,9 @@ SIGNATURES = {
     "pbccs_quiver_scorer_alignment": (I, [P, I, ctypes.c_char_p, ctypes.c_char_p, I, PI]),
     "pbccs_quiver_refine_consensus": (I, [P, ctypes.POINTER(CRefineOptions), PLL, PLL, PI]),
     "pbccs_quiver_consensus_qvs": (I, [P, PI, I, PI]),
+    "pbccs_quiver_polish_batch": (I, [P, ctypes.POINTER(CQuiverConfig), ctypes.POINTER(ctypes.c_char_p), I,
+                                      ctypes.POINTER(CQuiverZmw), I, ctypes.POINTER(CRefineOptions),
+                                      ctypes.POINTER(CQuiverResult)]),
     # POA draft
     "pbccs_poa_batch": (I, [P, ctypes.POINTER(CPoaInput), I, ctypes.c_longlong, I, ctypes.POINTER(CPoaOutput)]),
     "pbccs_sparse_poa_create": (I, [P, ctypes.POINTER(P)]),

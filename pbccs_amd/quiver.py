@@ -240,3 +240,79 @@ def ConsensusQVs(mms):
     n = ctypes.c_int()
     _lib_mod.check(load().pbccs_quiver_consensus_qvs(mms._h, out, cap, ctypes.byref(n)))
     return list(out[: n.value])
+
+
+def polish_batch(zmws, configs, max_iterations=40, mutation_separation=10, mutation_neighborhood=20, qvs=True,
+                 engine=None):
+    """Many Quiver scorers at once (pbccs_quiver_polish_batch): per ZMW, create the scorer over `configs`,
+    AddRead every read, RefineConsensus and (qvs) ConsensusQVs -- the per-scorer call sequence, with the
+    scorers' rounds in lock-step on the device.
+
+    zmws: [{"tpl", "reads": [{"seq", "strand", "ts", "te", "features": {ins, subs, del, del_tag, merge},
+    "chemistry"?}]}].  Returns per ZMW {"consensus", "qvs", "n_tested", "n_applied", "converged", "ok",
+    "n_active"}."""
+    from . import default_engine
+    eng = engine or default_engine()
+    if isinstance(configs, QuiverConfig):
+        t = QuiverConfigTable()
+        t.InsertDefault(configs)
+        configs = t
+    nc = len(configs.entries)
+    carr = (_lib_mod.CQuiverConfig * nc)(*[c._c() for _, c in configs.entries])
+    names = (ctypes.c_char_p * nc)(*[name.encode() for name, _ in configs.entries])
+    n = len(zmws)
+    cz = (_lib_mod.CQuiverZmw * max(1, n))()
+    res = (_lib_mod.CQuiverResult * max(1, n))()
+    keep = []
+
+    def farr(v, tag=False):
+        if v is None:
+            return None
+        vals = [float(ord(x)) if tag and isinstance(x, str) else float(x) for x in v]
+        a = (ctypes.c_float * len(vals))(*vals)
+        keep.append(a)
+        return a
+
+    bufs = []
+    for k, z in enumerate(zmws):
+        reads = z["reads"]
+        ra = (_lib_mod.CQuiverRead * max(1, len(reads)))()
+        for i, r in enumerate(reads):
+            f = r.get("features") or {}
+            seq = r["seq"].encode()
+            keep.append(seq)
+            ra[i].seq, ra[i].len = seq, len(seq)
+            ra[i].ins_qv, ra[i].subs_qv, ra[i].del_qv = farr(f.get("ins")), farr(f.get("subs")), farr(f.get("del"))
+            ra[i].del_tag, ra[i].merge_qv = farr(f.get("del_tag"), True), farr(f.get("merge"))
+            chem = r.get("chemistry", "*").encode()
+            keep.append(chem)
+            ra[i].chemistry = chem
+            ra[i].strand = r.get("strand", 0)
+            ra[i].tstart = r.get("ts", 0)
+            te = r.get("te")
+            ra[i].tend = -1 if te is None else te
+            ra[i].threshold = float("nan") if r.get("threshold") is None else r["threshold"]
+        keep.append(ra)
+        tpl = z["tpl"].encode()
+        keep.append(tpl)
+        cz[k].tpl, cz[k].tpl_len, cz[k].reads, cz[k].n_reads = tpl, len(tpl), ra, len(reads)
+        cap = 2 * len(tpl) + 64
+        cons = ctypes.create_string_buffer(cap)
+        qv = (ctypes.c_int * cap)() if qvs else None
+        bufs.append((cons, qv))
+        res[k].consensus = ctypes.cast(cons, ctypes.c_char_p)
+        res[k].consensus_cap = cap
+        res[k].qvs = qv
+    o = _lib_mod.CRefineOptions(max_iterations, mutation_separation, mutation_neighborhood)
+    _lib_mod.check(load().pbccs_quiver_polish_batch(eng._h, carr, names, nc, cz, n, ctypes.byref(o), res))
+    out = []
+    for k in range(n):
+        r = res[k]
+        cons, qv = bufs[k]
+        ln = r.consensus_len
+        if ln > res[k].consensus_cap:
+            raise _lib_mod.PbccsError(-5, "consensus outgrew its buffer")
+        out.append({"consensus": cons.raw[:ln].decode(), "qvs": list(qv[:ln]) if qv is not None and r.ok else None,
+                    "n_tested": r.n_tested, "n_applied": r.n_applied, "converged": bool(r.converged),
+                    "ok": bool(r.ok), "n_active": r.n_active})
+    return out

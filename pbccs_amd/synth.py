@@ -37,12 +37,12 @@ def _mutate(rng, seq, p_ins, p_del, p_sub):
     return res
 
 
-def make_zmw(rng, length, passes, snr=(10.0, 7.0, 5.0, 11.0)):
+def make_zmw(rng, length, passes, snr=(10.0, 7.0, 5.0, 11.0), read_errors=(0.07, 0.04, 0.01)):
     truth = BASES[rng.integers(0, 4, size=length)]
     draft = _mutate(rng, truth, 0.005, 0.005, 0.002)
     reads = []
     for k in range(passes):
-        r = _mutate(rng, truth, 0.07, 0.04, 0.01)
+        r = _mutate(rng, truth, *read_errors)
         strand = k % 2
         if strand == 1:
             r = COMP[r[::-1]]
@@ -89,3 +89,32 @@ CONFIGS = {
     "10kb_8pass": dict(length=10000, passes=8, seed=2),
     "mixed": dict(length=None, passes=None, seed=3, length_range=(500, 20000), passes_range=(3, 30), random_snr=True),
 }
+
+
+# Quiver model parameters of the synthetic Quiver workload (a QvModelParams set of the reference's magnitude;
+# the same set tests/test_quiver_gpu.py scores with)
+QUIVER_PARAMS = dict(Match=-0.2, Mismatch=-8.0, MismatchS=-0.15, Branch=-3.5, BranchS=-0.12, DeletionN=-7.5,
+                     DeletionWithTag=-4.5, DeletionWithTagS=-0.2, Nce=-6.0, NceS=-0.1, Merge=[-3.0, -3.2, -2.9, -3.1],
+                     MergeS=[-0.1, -0.12, -0.09, -0.11])
+
+QUIVER_READ_ERRORS = (0.04, 0.03, 0.01)
+QUIVER_SCORE_DIFF = 18.0   # at 12.5 the FP32 band loses nearly every 2 kb read to an alpha/beta mismatch
+
+
+def make_quiver_zmws(n, length, passes, seed, read_errors=QUIVER_READ_ERRORS):
+    """n Quiver ZMWs: make_zmw's draft and mapped reads (at read_errors ins/del/sub rates, a little
+    cleaner than configs[1]'s; scored at QUIVER_SCORE_DIFF), each read with five QV feature tracks (InsQv, SubsQv, DelQv, MergeQv uniform integers in
+    [0, 25), DelTag uniform over ACGTN)."""
+    zrng = np.random.Generator(np.random.PCG64(seed))
+    rng = np.random.Generator(np.random.PCG64(seed + 17))
+    out = []
+    for z in [make_zmw(zrng, length, passes, read_errors=read_errors) for _ in range(n)]:
+        reads = []
+        for r in z["reads"]:
+            m = len(r["seq"])
+            f = {"ins": rng.integers(0, 25, m).tolist(), "subs": rng.integers(0, 25, m).tolist(),
+                 "del": rng.integers(0, 25, m).tolist(), "del_tag": rng.choice(list("ACGTN"), size=m).tolist(),
+                 "merge": rng.integers(0, 25, m).tolist()}
+            reads.append(dict(r, features=f))
+        out.append({"tpl": z["draft"], "reads": reads})
+    return out

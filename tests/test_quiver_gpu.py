@@ -200,3 +200,73 @@ def test_quiver_recursor_types_match_oracle(recursor, sum_product):
     vals = g.s.ScoreMany([g.P.Mutation(t, s, b) for (t, s, b) in muts])
     for (t, s, b), v in zip(muts, vals):
         assert v == o.score(t, s, b), (t, s, b)
+
+
+@pytest.mark.parametrize("sum_product", [False, True])
+def test_quiver_polish_batch_matches_scorers(sum_product):
+    """pbccs_quiver_polish_batch (every scorer's rounds in lock-step: batched fills, device Score /
+    FastIsFavorable reduction and BestSubset) equals the per-scorer call sequence -- AddRead, RefineConsensus,
+    ConsensusQVs -- ZMW for ZMW, and the oracle on the first ZMWs; one ZMW has a read AddRead drops."""
+    import pbccs_amd as P
+    from pbccs_amd import quiver
+    zs = []
+    for k, (length, passes) in enumerate([(120, 4), (200, 5), (90, 3), (160, 6), (60, 2)]):
+        tpl, reads = _zmw(200 + k, length, passes)
+        zs.append({"tpl": tpl, "reads": reads})
+    zs[2]["reads"][0] = dict(zs[2]["reads"][0], threshold=0.001)   # the memory gate drops it
+    cfg = P.QuiverConfig(P.QvModelParams(**PARAMS2), sum_product=sum_product)
+    got = quiver.polish_batch(zs, cfg)
+    for z, g in zip(zs, got):
+        s = P.QuiverMultiReadMutationScorer(cfg, z["tpl"])
+        na = 0
+        for r in z["reads"]:
+            f = r["features"]
+            na += s.AddRead(r["seq"], r["strand"], r["ts"], r["te"], ins_qv=f["ins"], subs_qv=f["subs"],
+                            del_qv=f["del"], del_tag=f["del_tag"], merge_qv=f["merge"], threshold=r.get("threshold"))
+        conv, nt, nap = P.RefineConsensus(s)
+        assert g["ok"] and g["n_active"] == na
+        assert (g["converged"], g["n_tested"], g["n_applied"]) == (conv, nt, nap)
+        assert g["consensus"] == s.Template()
+        assert g["qvs"] == P.ConsensusQVs(s)
+    for z, g in list(zip(zs, got))[:2]:
+        tpl, reads = z["tpl"], z["reads"]
+        o = O.QuiverScorer(tpl, PARAMS2, sum_product=sum_product)
+        for r in reads:
+            o.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"])
+        ref = o.refine()
+        assert (g["converged"], g["n_tested"], g["n_applied"]) == (ref["converged"], ref["n_tested"], ref["n_applied"])
+        assert g["consensus"] == o.template()
+        assert g["qvs"] == o.qvs()
+
+
+def test_quiver_coop_fill_long_reads_match_oracle():
+    """k_qfill_coop (one wavefront per read) at configs[1]-like sizes: 1.5 kb reads whose bands span several
+    64-row chunks, ScoreDiff 18 -- active flags, baseline scores, flip-flop counts and AllocatedEntries
+    equal the oracle's; then the batch polish of those ZMWs equals the oracle's refine and QVs."""
+    import pbccs_amd as P
+    from pbccs_amd import quiver, synth
+    zs = synth.make_quiver_zmws(2, 1500, 6, seed=7)
+    cfg = P.QuiverConfig(P.QvModelParams(**synth.QUIVER_PARAMS), score_diff=synth.QUIVER_SCORE_DIFF)
+    for z in zs:
+        g = P.QuiverMultiReadMutationScorer(cfg, z["tpl"])
+        o = O.QuiverScorer(z["tpl"], synth.QUIVER_PARAMS, score_diff=synth.QUIVER_SCORE_DIFF)
+        for r in z["reads"]:
+            f = r["features"]
+            a = g.AddRead(r["seq"], r["strand"], r["ts"], r["te"], ins_qv=f["ins"], subs_qv=f["subs"], del_qv=f["del"],
+                          del_tag=f["del_tag"], merge_qv=f["merge"])
+            b = o.add_read(r["seq"], r["strand"], r["ts"], r["te"], f)
+            assert bool(a) == bool(b)
+        act = [k for k in range(len(z["reads"])) if o.read_info(k)["active"]]
+        assert len(act) >= 4
+        assert g.BaselineScores() == [o.read_info(k)["score"] for k in act]
+        assert [g.NumFlipFlops()[k] for k in act] == [o.read_info(k)["flipflops"] for k in act]
+        assert [g.AllocatedEntries(k) for k in act] == [tuple(o.read_info(k)["allocated"]) for k in act]
+    got = quiver.polish_batch(zs, cfg)
+    for z, r in zip(zs, got):
+        o = O.QuiverScorer(z["tpl"], synth.QUIVER_PARAMS, score_diff=synth.QUIVER_SCORE_DIFF)
+        for rd in z["reads"]:
+            o.add_read(rd["seq"], rd["strand"], rd["ts"], rd["te"], rd["features"])
+        ref = o.refine()
+        assert (r["converged"], r["n_tested"], r["n_applied"]) == (ref["converged"], ref["n_tested"], ref["n_applied"])
+        assert r["consensus"] == o.template()
+        assert r["qvs"] == o.qvs()
