@@ -250,6 +250,7 @@ void QuiverBatch::Upload()
     dRange_.reserve(std::max<long long>(colTop_, 1), true);
     dOff_.reserve(std::max<long long>(colTop_, 1), true);
     dAlloc_.reserve(std::max<long long>(colTop_ / 2, 1), true);
+    dHint_.reserve(std::max<long long>(colTop_ / 4 + 1, 1), false);
     dVal_.reserve(std::max<long long>(valTop_, 1), true);
     dRCurA_.reserve(std::max<size_t>(R, 1), true);
     dRCurB_.reserve(std::max<size_t>(R, 1), true);
@@ -287,6 +288,7 @@ QBatch QuiverBatch::View()
     b.range = dRange_.ptr;
     b.off = dOff_.ptr;
     b.alloc = dAlloc_.ptr;
+    b.hint = dHint_.ptr;
     b.valPool = dVal_.ptr;
     b.rCurA = dRCurA_.ptr;
     b.rCurB = dRCurB_.ptr;
@@ -310,12 +312,14 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         // every read to the lane kernel.
         static const bool laneOnly = std::getenv("PBCCS_QFILL_LANE") != nullptr;
         std::vector<int> coop, lane;
-        int maxRows = 1;
+        int maxRows = 1, maxCols = 1;
         for (int r : todo) {
             const QParams& p = configs_[reads_[r].config];
-            if (!laneOnly && !p.simple && !p.dense && reads_[r].len + 1 <= kQCoopRows) {
+            const int cols = reads_[r].te - reads_[r].ts + 1;
+            if (!laneOnly && !p.simple && !p.dense && reads_[r].len + 1 <= kQCoopRows && cols <= kQCoopCols) {
                 coop.push_back(r);
                 maxRows = std::max(maxRows, reads_[r].len + 1);
+                maxCols = std::max(maxCols, cols);
             } else {
                 lane.push_back(r);
             }
@@ -324,7 +328,7 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         both.insert(both.end(), lane.begin(), lane.end());
         put(dList_, both, stream_);
         const QBatch B = View();
-        launch_qfill_coop(B, dList_.ptr, (int)coop.size(), maxRows, stream_);
+        launch_qfill_coop(B, dList_.ptr, (int)coop.size(), maxRows, maxCols, stream_);
         launch_qfill(B, dList_.ptr + coop.size(), (int)lane.size(), stream_);
         QHIP(hipGetLastError());
         const size_t R = reads_.size();

@@ -129,6 +129,7 @@ private:
     DevVec<QParams> dParams_;
     DevVec<int2> dRange_;
     DevVec<QAlloc> dAlloc_;
+    DevVec<int4> dHint_;
     DevVec<float> dVal_;
     DevVec<unsigned long long> dScratchTop_;
     DevVec<long long> dMoveOff_;

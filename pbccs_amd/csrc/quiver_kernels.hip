@@ -421,6 +421,7 @@ struct ReadView {
     QAlloc* allocA;
     QAlloc* allocB;
     float* colbuf;
+    int4* hint;
 };
 
 __device__ __forceinline__ QBand arena(const ReadView& v, int k)
@@ -464,6 +465,7 @@ __device__ __forceinline__ ReadView read_view(const QBatch& B, int r)
     v.allocA = B.alloc + cb / 2;   // 2 x colCap alloc slots per read (colBase advances by 4 x colCap)
     v.allocB = v.allocA + cc;
     v.colbuf = B.valPool + B.rColBuf[r];
+    v.hint = B.hint + cb / 4;
     return v;
 }
 
@@ -712,14 +714,6 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
         if (k < out.cap) out.val[k] = cur[r];
         else ovf = true;
     }
-    // SparseVector allocation bookkeeping, rows in the order the reference sets them
-    if (alloc && lane == 0) {
-        if (!BETA) {
-            for (int r = beginRow; r < endRow; ++r) alloc_set(*alloc, r, I + 1);
-        } else {
-            for (int r = endRow - 1; r >= beginRow; --r) alloc_set(*alloc, r, I + 1);
-        }
-    }
     *ob = beginRow;
     *oe = endRow;
     *thrOut = thr;
@@ -727,26 +721,39 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
 
 template <bool BETA>
 __device__ long long coop_fill(const QEval& e, const QBand* guide, const QBand* prev, const QBand& out, QAlloc* alloc,
-                               bool allocExists, bool& ovf, float* lds, int ldsRows, int lane)
+                               bool allocExists, bool& ovf, float* lds, int ldsRows, int4* hint, int lane)
 {
     const int I = e.I(), J = e.J();
     const float sd = e.p->scoreDiff;
+    // RowRange of the guide and self matrices for every column, up front and one lane per column: both are
+    // finished passes, and only RangeGuide's min / max with the running hints is sequential
+    for (int j = lane; j <= J; j += 64) {
+        int4 h = make_int4(-1, -1, -1, -1);
+        if (guide && !guide->Empty(j)) row_range(*guide, j, sd, &h.x, &h.y);
+        if (prev && !prev->Empty(j)) row_range(*prev, j, sd, &h.z, &h.w);
+        hint[j] = h;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     // the LDS ring: cur (column being filled), c1 (previous), c2 (the one before), rotated by value
     LdsCol cur{lds, 0, 0}, c1{lds + ldsRows, 0, 0}, c2{lds + 2 * ldsRows, 0, 0};
     long long used = 0;
     int hb = BETA ? I + 1 : 0, he = BETA ? I + 1 : 0;
+    int4 hNext = hint[BETA ? J : 0];
     for (int s = 0; s <= J; ++s) {
         const int j = BETA ? J - s : s;
-        coop_range_guide(j, guide, prev, sd, lane, &hb, &he);
-        if (alloc && lane == 0) alloc_start(alloc[j], allocExists, hb, he, I + 1);
+        const int4 h = hNext;
+        if (s < J) hNext = hint[BETA ? j - 1 : j + 1];   // one column ahead: its latency hides behind this one
+        if (h.x >= 0) { hb = min(h.x, hb); he = max(h.y, he); }   // RangeGuide (RecursorBase-inl.hpp:87-114)
+        if (h.z >= 0) { hb = min(h.z, hb); he = max(h.w, he); }
         int b, en;
         float thr;
-        coop_column<BETA>(e, j, lane, hb, he, c1, c2, cur.v, out, used, alloc ? &alloc[j] : nullptr, ovf, &b, &en, &thr);
+        coop_column<BETA>(e, j, lane, hb, he, c1, c2, cur.v, out, used, nullptr, ovf, &b, &en, &thr);
         cur.b = b;
         cur.e = en;
         if (lane == 0) {
             out.off[j] = (int)min(used, (long long)0x7fffffff);
             out.range[j] = make_int2(b, en);
+            hint[j] = make_int4(hb, he, b, en);   // for the allocation bookkeeping below
         }
         used += en - b;
         if (!BETA) {
@@ -777,26 +784,46 @@ __device__ long long coop_fill(const QEval& e, const QBand* guide, const QBand* 
         cur = old2;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the pass's stores before later passes read them
+    // SparseVector allocation bookkeeping (SparseVector-inl.hpp): per column independent, one lane per column,
+    // rows in the order the reference sets them
+    if (alloc) {
+        for (int j = lane; j <= J; j += 64) {
+            const int4 h = hint[j];
+            QAlloc a = alloc[j];
+            alloc_start(a, allocExists, h.x, h.y, I + 1);
+            if (!BETA) {
+                for (int r = max(h.z, a.ae); r < h.w; ++r) alloc_set(a, r, I + 1);   // rows inside [ab, ae) are no-ops
+            } else {
+                for (int r = h.w - 1; r >= h.z; --r) alloc_set(a, r, I + 1);
+            }
+            alloc[j] = a;
+        }
+    }
     return used;
 }
 
 }  // namespace
 
 // ---- k_qfill_coop: FillAlphaBeta with one wavefront per read (SparseSse recursors, reads < kQCoopMaxRows) --
-__global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restrict__ reads, int n, int ldsRows)
+__global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restrict__ reads, int n, int ldsRows,
+                                                    int ldsCols)
 {
     extern __shared__ float qlds[];
     const int t = blockIdx.x;
     const int lane = threadIdx.x;
     if (t >= n) return;
     const int r = reads[t];
-    const ReadView v = read_view(B, r);
-    const QEval& e = v.ev;
-    const int I = e.I(), J = e.J();
-    if (I < 1 || J < 1 || J + 1 > B.rColCap[r] || I + 1 > ldsRows) {
+    ReadView v = read_view(B, r);
+    const int I = v.ev.I(), J = v.ev.J();
+    if (I < 1 || J < 1 || J + 1 > B.rColCap[r] || I + 1 > ldsRows || J + 1 > ldsCols) {
         if (lane == 0) B.rStatus[r] = kQBad;
         return;
     }
+    // the template window in LDS after the column ring: every column reads its bases
+    char* tpl = reinterpret_cast<char*>(qlds + 3 * ldsRows);
+    for (int j = lane; j < J; j += 64) tpl[j] = v.ev.t.base[j];
+    v.ev.t.base = tpl;
+    const QEval& e = v.ev;
     for (int k = 0; k < 4; ++k) {
         const QBand m = arena(v, k);
         for (int j = lane; j <= J; j += 64) m.range[j] = make_int2(0, 0);
@@ -810,7 +837,7 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
         const int nxt = aPassed ? (curA ^ 1) : 0;
         const QBand g = arena(v, curB), self = arena(v, curA), out = arena(v, nxt);
         const long long u = coop_fill<false>(e, guided ? &g : nullptr, aPassed ? &self : nullptr, out, v.allocA, aPassed,
-                                             ovf, qlds, ldsRows, lane);
+                                             ovf, qlds, ldsRows, v.hint, lane);
         needA = max(needA, u);
         curA = nxt;
         aPassed = true;
@@ -820,7 +847,7 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
         const int nxt = bPassed ? (curB ^ 1) : 2;
         const QBand g = arena(v, curA), self = arena(v, curB), out = arena(v, nxt);
         const long long u = coop_fill<true>(e, &g, bPassed ? &self : nullptr, out, v.allocB, bPassed, ovf, qlds, ldsRows,
-                                            lane);
+                                            v.hint, lane);
         needB = max(needB, u);
         curB = nxt;
         bPassed = true;
@@ -1140,11 +1167,13 @@ void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s)
     hipLaunchKernelGGL(k_qfill, dim3((n + 63) / 64), dim3(64), 0, s, B, reads, n);
 }
 
-void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, hipStream_t s)
+void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, int maxCols, hipStream_t s)
 {
     if (n <= 0) return;
     const int rows = (maxRows + 63) / 64 * 64;
-    hipLaunchKernelGGL(k_qfill_coop, dim3(n), dim3(64), (size_t)3 * rows * sizeof(float), s, B, reads, n, rows);
+    const int cols = (maxCols + 15) / 16 * 16;
+    hipLaunchKernelGGL(k_qfill_coop, dim3(n), dim3(64), (size_t)3 * rows * sizeof(float) + cols, s, B, reads, n, rows,
+                       cols);
 }
 
 void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s)

@@ -34,6 +34,7 @@ struct QBatch {
     int2* range;
     int* off;
     QAlloc* alloc;             // 2 x colCap per read (alpha, beta): AllocatedEntries bookkeeping
+    int4* hint;                // colCap per read: k_qfill_coop's per-column RangeGuide rows / band record
     float* valPool;
     // fill results
     int* rCurA;                // arena (0/1) holding the final alpha / beta
@@ -90,10 +91,11 @@ struct QReduceWork {
 };
 
 void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s);
-// FillAlphaBeta with one wavefront per read (SparseSse recursors; reads of I + 1 <= kQCoopRows rows); maxRows =
-// the largest I + 1 of the listed reads
+// FillAlphaBeta with one wavefront per read (SparseSse recursors; reads of I + 1 <= kQCoopRows rows and windows
+// of J + 1 <= kQCoopCols columns); maxRows / maxCols = the largest I + 1 / J + 1 of the listed reads
 constexpr int kQCoopRows = 4096;
-void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, hipStream_t s);
+constexpr int kQCoopCols = 8192;
+void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, int maxCols, hipStream_t s);
 void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s);
 void launch_qreduce(const QReduceWork& W, hipStream_t s);
 // RecursorBase::Alignment per listed read: moves (from the end) at moveOff[t], nMoves[t] of them

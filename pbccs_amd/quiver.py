@@ -265,13 +265,19 @@ def polish_batch(zmws, configs, max_iterations=40, mutation_separation=10, mutat
     res = (_lib_mod.CQuiverResult * max(1, n))()
     keep = []
 
+    import numpy as np
+
     def farr(v, tag=False):
         if v is None:
             return None
-        vals = [float(ord(x)) if tag and isinstance(x, str) else float(x) for x in v]
-        a = (ctypes.c_float * len(vals))(*vals)
+        if isinstance(v, np.ndarray):   # numeric tracks (tags as character codes): no per-base Python
+            a = np.ascontiguousarray(v, dtype=np.float32)
+        elif tag:
+            a = np.array([float(ord(x)) if isinstance(x, str) else float(x) for x in v], dtype=np.float32)
+        else:
+            a = np.asarray(v, dtype=np.float32)
         keep.append(a)
-        return a
+        return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
 
     bufs = []
     for k, z in enumerate(zmws):

@@ -103,8 +103,8 @@ QUIVER_SCORE_DIFF = 18.0   # at 12.5 the FP32 band loses nearly every 2 kb read 
 
 def make_quiver_zmws(n, length, passes, seed, read_errors=QUIVER_READ_ERRORS):
     """n Quiver ZMWs: make_zmw's draft and mapped reads (at read_errors ins/del/sub rates, a little
-    cleaner than configs[1]'s; scored at QUIVER_SCORE_DIFF), each read with five QV feature tracks (InsQv, SubsQv, DelQv, MergeQv uniform integers in
-    [0, 25), DelTag uniform over ACGTN)."""
+    cleaner than configs[1]'s; scored at QUIVER_SCORE_DIFF), each read with five QV feature tracks as numpy arrays (InsQv, SubsQv, DelQv, MergeQv: float32
+    uniform integers in [0, 25); DelTag: uint8 character codes uniform over ACGTN)."""
     zrng = np.random.Generator(np.random.PCG64(seed))
     rng = np.random.Generator(np.random.PCG64(seed + 17))
     out = []
@@ -112,9 +112,10 @@ def make_quiver_zmws(n, length, passes, seed, read_errors=QUIVER_READ_ERRORS):
         reads = []
         for r in z["reads"]:
             m = len(r["seq"])
-            f = {"ins": rng.integers(0, 25, m).tolist(), "subs": rng.integers(0, 25, m).tolist(),
-                 "del": rng.integers(0, 25, m).tolist(), "del_tag": rng.choice(list("ACGTN"), size=m).tolist(),
-                 "merge": rng.integers(0, 25, m).tolist()}
+            f = {"ins": rng.integers(0, 25, m).astype(np.float32), "subs": rng.integers(0, 25, m).astype(np.float32),
+                 "del": rng.integers(0, 25, m).astype(np.float32),
+                 "del_tag": np.frombuffer(b"ACGTN", dtype=np.uint8)[rng.integers(0, 5, m)].copy(),
+                 "merge": rng.integers(0, 25, m).astype(np.float32)}
             reads.append(dict(r, features=f))
         out.append({"tpl": z["draft"], "reads": reads})
     return out
