@@ -576,8 +576,10 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
                 if (q.zscores) q.zscores[k] = std::numeric_limits<double>::quiet_NaN();
             }
         }
+        // bands of ZMWs the batch is done with are dropped as it goes (ArrowBatch::Relayout)
+        B.SetReclaim(true);
         B.FillReads(b->allReads);
-        std::vector<int> refineZ, refineIdx;
+        std::vector<int> refineZ, refineIdx, dropZ;
         for (int i = 0; i < n; ++i) {
             if (b->zOf[i] < 0) continue;
             pbccs_zmw_output& q = out[i];
@@ -592,9 +594,17 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
                 else if (st != PBCCS_ADD_SUCCESS) ++nDropped;
             }
             q.n_passes = nPasses;
-            if (nPasses < o.min_passes) { q.status = PBCCS_ZMW_TOO_FEW_PASSES; continue; }
+            if (nPasses < o.min_passes) {
+                q.status = PBCCS_ZMW_TOO_FEW_PASSES;
+                dropZ.push_back(b->zOf[i]);
+                continue;
+            }
             const double frac = (double)nDropped / b->nReads[i];
-            if (frac > o.max_drop_fraction) { q.status = PBCCS_ZMW_TOO_MANY_UNUSABLE; continue; }
+            if (frac > o.max_drop_fraction) {
+                q.status = PBCCS_ZMW_TOO_MANY_UNUSABLE;
+                dropZ.push_back(b->zOf[i]);
+                continue;
+            }
             std::vector<double> zs;
             B.ZScores(b->zOf[i], &q.zg, &q.za, &zs);
             if (q.zscores) {
@@ -609,19 +619,24 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
         ro.maxIterations = o.refine.max_iterations;
         ro.mutationSeparation = o.refine.mutation_separation;
         ro.mutationNeighborhood = o.refine.mutation_neighborhood;
+        B.Retire(dropZ);
         std::vector<int> conv;
         std::vector<long long> nt, na;
-        B.Refine(refineZ, ro, &conv, &nt, &na, false);
+        // ConsensusQVs (Consensus.h:496-512) run inside the refine loop, in the round each ZMW converges
+        std::vector<std::vector<int>> qvAll;
+        B.Refine(refineZ, ro, &conv, &nt, &na, false, &qvAll);
         std::vector<int> qvZ, qvIdx;
+        std::vector<std::vector<int>> qvs;
         for (size_t k = 0; k < refineZ.size(); ++k) {
             pbccs_zmw_output& q = out[refineIdx[k]];
             q.n_tested = nt[k];
             q.n_applied = na[k];
-            if (conv[k] == 1) { qvZ.push_back(refineZ[k]); qvIdx.push_back(refineIdx[k]); }
-            else q.status = conv[k] < 0 ? PBCCS_ZMW_OTHER : PBCCS_ZMW_NON_CONVERGENT;
+            if (conv[k] == 1) {
+                qvZ.push_back(refineZ[k]);
+                qvIdx.push_back(refineIdx[k]);
+                qvs.push_back(std::move(qvAll[k]));
+            } else q.status = conv[k] < 0 ? PBCCS_ZMW_OTHER : PBCCS_ZMW_NON_CONVERGENT;
         }
-        std::vector<std::vector<int>> qvs;
-        B.QVs(qvZ, &qvs);
         for (size_t k = 0; k < qvZ.size(); ++k) {
             pbccs_zmw_output& q = out[qvIdx[k]];
             const std::string& t = B.Template(qvZ[k]);

@@ -34,6 +34,10 @@ constexpr int kCoopTallRows = 1024;           // LDS column rows of the first 64
 constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill block
 constexpr size_t kCoopTallLdsBytes = 150 * 1024;   // the 16-lane tall path's block (gfx950: 160 KB per CU)
 constexpr size_t kHeadroomMargin = 24ull << 30;   // device bytes band-growth headroom leaves free
+// First region of a read that moves to the tall paths, as a fraction 1 / kTallFirstDiv of its (I+1)(J+1)
+// matrix: exploded bands hold ~8% of it per pass at 2 kb (oracle, 400 reads).  Measured: a 2% first region
+// (growing in-kernel from there) raised a 2000-ZMW batch's band high-water from 40 to 45 GB.
+constexpr long long kTallFirstDiv = 10;
 constexpr long long kPhasedMinTasks = 1 << 21;   // (mutation, read) tasks from which a round scores in phases
 constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
 
@@ -459,6 +463,63 @@ void ArrowBatch::EnsureCapacity(int ri)
         }
         descDirty_ = true;
     }
+    if (r.valCap == 0) {   // its region was dropped by a reclaiming layout (Relayout)
+        r.valCap = (long long)r.colCap * initialBandHeight_;
+        r.valA = valTop_;
+        r.valB = valTop_ + r.valCap;
+        valTop_ += 2 * r.valCap;
+        descDirty_ = true;
+    }
+}
+
+void ArrowBatch::Retire(const std::vector<int>& zl)
+{
+    for (int zi : zl) {
+        const HZmw& z = zmws_[zi];
+        for (int k = 0; k < z.nReads; ++k) reads_[z.readBegin + k].retired = true;
+    }
+}
+
+// Reclaiming layout (reclaim_ only): when every read whose bands are still live is about to be refilled,
+// nothing in the value pool is needed any more, so the regions are handed out afresh from offset 0 in list
+// order instead of bumping the pool's top.  A region is sized from the read's last fill (its larger matrix
+// + 1/8 + 64: refills follow a template that moved by a few bases); a read never filled keeps the first
+// estimate of its path.  Regions of reads outside the list are dropped (valCap 0; EnsureCapacity gives
+// one back if such a read is ever filled again).  Without this the pool's top only grows: regions abandoned
+// by growth and by moves to the tall paths were never reused (43.6 GB top against 18.2 GB of bands in use
+// for a 2000-ZMW batch, profiles/r2h1_bench.json).
+bool ArrowBatch::Relayout(const std::vector<int>& list)
+{
+    if (!reclaim_ || !ws_->val.allowVmm) return false;
+    std::vector<char> in(reads_.size(), 0);
+    for (int r : list) in[r] = 1;
+    for (size_t r = 0; r < reads_.size(); ++r) {
+        const HRead& h = reads_[r];
+        if (h.filled && h.active && !h.retired && !in[r]) return false;   // live bands outside the list
+    }
+    for (HRead& h : reads_) {
+        h.valCap = 0;
+        h.valA = h.valB = 0;
+    }
+    valTop_ = 0;
+    for (int r : list) {
+        HRead& h = reads_[r];
+        const long long m = std::max(h.usedA, h.usedB);
+        long long cap;
+        if (h.filled && m > 0) cap = m + m / 8 + 64;
+        else if (h.fillPath >= 2 && h.fillPath < 5)
+            cap = ((long long)h.seq.size() + 1) * (h.te - h.ts + 1) / kTallFirstDiv + 64;
+        else cap = (long long)h.colCap * initialBandHeight_;
+        h.valCap = cap;
+        h.valA = valTop_;
+        h.valB = valTop_ + cap;
+        valTop_ += 2 * cap;
+    }
+    for (size_t r = 0; r < reads_.size(); ++r)
+        if (!in[r]) reads_[r].usedA = reads_[r].usedB = 0;   // dropped: no bands held
+    descDirty_ = true;
+    counters_.relayouts += 1;
+    return true;
 }
 
 void ArrowBatch::UploadDescriptors()
@@ -599,6 +660,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     const char* laneEnv = std::getenv("PBCCS_FILL_LANE");   // read per call: a test switches it at run time
     const bool laneFill = laneEnv && std::strcmp(laneEnv, "1") == 0;
     for (int r : readsIn) EnsureCapacity(r);
+    Relayout(readsIn);
     std::vector<int> todo[kPaths], serial, done;
     for (int r : readsIn) {
         const int p = reads_[r].fillPath;
@@ -725,6 +787,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             static const int jacobiMax = std::getenv("PBCCS_JACOBI_MAX") ? std::atoi(std::getenv("PBCCS_JACOBI_MAX")) : 0;
             F.jacobi = chainMode ? std::strcmp(chainMode, "jacobi") == 0 : (p > 1 && n <= jacobiMax);
             F.prio = !(prioEnv && std::strcmp(prioEnv, "0") == 0);
+            static const char* exitEnv = std::getenv("PBCCS_CHAIN_EXIT");   // "0" disables (A/B)
+            F.chainExit = !(exitEnv && std::strcmp(exitEnv, "0") == 0);
             if (grow) {
                 F.valBump = dBump_.ptr;
                 F.valLimit = valLimit;
@@ -791,12 +855,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                     h.fillPath = q;
                     if (q >= kPaths) serial.push_back(r);
                     else next[q].push_back(r);
-                    // A read that moves to the tall paths gets a region of its expected tall size now: exploded
-                    // bands hold ~8% of the (I+1)(J+1) matrix per pass at 2 kb (oracle, 400 reads), so growing
-                    // from the typical region inside the kernel would copy and abandon two or three regions.
+                    // A read that moves to the tall paths gets a first tall region now (kTallFirstDiv): growing
+                    // from the typical 16-row region inside the kernel would copy and abandon two or three.
                     if (q >= 2 && q < kPaths) {
                         const long long I = (long long)h.seq.size(), J = h.te - h.ts;
-                        const long long want = (I + 1) * (J + 1) / 10 + 64;
+                        const long long want = (I + 1) * (J + 1) / kTallFirstDiv + 64;
                         if (want > h.valCap) {
                             h.valCap = want;
                             h.valA = valTop_;
@@ -1292,10 +1355,15 @@ std::vector<Scored> best_subset(std::vector<Scored> in, int sep)   // Consensus-
 }  // namespace
 
 void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std::vector<int>* converged,
-                        std::vector<long long>* nTested, std::vector<long long>* nApplied, bool needFinalState)
+                        std::vector<long long>* nTested, std::vector<long long>* nApplied, bool needFinalState,
+                        std::vector<std::vector<int>>* qvsOnConverge)
 {
     const int n = (int)zl.size();
     converged->assign(n, 0);
+    if (qvsOnConverge) qvsOnConverge->assign(n, {});
+    // ZMWs whose bands nobody reads again once they are done (needFinalState = false: the batch polish reads
+    // only converged ZMWs, through their QVs): retired so the reclaiming layout can drop them
+    const bool retireDone = reclaim_ && !needFinalState;
     nTested->assign(n, 0);
     nApplied->assign(n, 0);
     std::vector<char> done(n, 0);
@@ -1350,6 +1418,8 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
     const double fastThr = zl.empty() ? -12.5 : zmws_[zl[0]].opt.fastScoreThreshold;
     // PBCCS_ROUND_TRACE=1: one stderr line per round (active ZMWs, refilled reads, phase wall times)
     static const bool roundTrace = std::getenv("PBCCS_ROUND_TRACE") != nullptr;
+    if (roundTrace)
+        std::fprintf(stderr, "[round] batch=%p start zmws=%d bandtop=%.2fGB\n", (void*)this, n, valTop_ * 8.0 / 1e9);
     using Clock = std::chrono::steady_clock;
     auto ms = [](Clock::time_point a, Clock::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
@@ -1426,7 +1496,10 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
             descDirty_ = true;
             if (!ended) memo[k].push_back(std::move(cur));   // a real iteration follows from this state
             std::vector<int>& dst = ended ? finalRefill : preRefill;
-            if (ended && !needFinalState) continue;
+            if (ended && !needFinalState) {
+                if (retireDone) Retire({zl[k]});
+                continue;
+            }
             for (int q = 0; q < z.nReads; ++q)
                 if (reads_[z.readBegin + q].active) {
                     EnsureCapacity(z.readBegin + q);
@@ -1522,7 +1595,7 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
         }
         // PBCCS_CHECK_BEST_SUBSET=1: the host restatement beside the device select, any difference fatal
         const bool checkBest = std::getenv("PBCCS_CHECK_BEST_SUBSET") != nullptr;
-        std::vector<int> changed;
+        std::vector<int> changed, qvNow, qvIdx;
         for (size_t a = 0; a < act.size(); ++a) {
             const int k = idx[a];
             const int zi = act[a];
@@ -1530,6 +1603,10 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
             if (fav[a].empty()) {
                 converged->at(k) = 1;
                 done[k] = 1;
+                if (qvsOnConverge) {
+                    qvNow.push_back(zi);
+                    qvIdx.push_back(k);
+                }
                 continue;
             }
             std::sort(picked[a].begin(), picked[a].end(),
@@ -1563,21 +1640,34 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
             if (!apply_host(&z.tpl, muts, &mtp)) {
                 done[k] = 1;   // the reference throws out of RefineConsensus here (ZMW -> Other)
                 converged->at(k) = -1;
+                if (retireDone) Retire({zi});
                 continue;
             }
             UploadTemplate(zi);
+            // NonConvergent after this iteration: the refill only matters to a caller that reads the final state
+            const bool last = zit[k] + 1 >= ro.maxIterations;
+            const bool refill = !(last && retireDone);
             for (int q = 0; q < z.nReads; ++q) {
                 HRead& r = reads_[z.readBegin + q];
                 r.ts = mtp[r.ts];
                 r.te = mtp[r.te];
-                if (r.active) {
+                if (r.active && refill) {
                     EnsureCapacity(z.readBegin + q);
                     changed.push_back(z.readBegin + q);
                 }
             }
+            if (!refill) Retire({zi});
             if (++zit[k] >= ro.maxIterations) done[k] = 1;   // NonConvergent
         }
         descDirty_ = true;
+        // ConsensusQVs of the ZMWs that converged this round, from their final bands; after that (reclaim) their
+        // bands are dead, so the refill below holds every live read and can lay the value pool out afresh
+        if (!qvNow.empty()) {
+            std::vector<std::vector<int>> q;
+            QVs(qvNow, &q);
+            for (size_t i = 0; i < qvNow.size(); ++i) (*qvsOnConverge)[qvIdx[i]] = std::move(q[i]);
+            if (reclaim_) Retire(qvNow);
+        }
         const Clock::time_point t2 = Clock::now();
         if (!changed.empty()) {
             FillReads(changed);
@@ -1588,9 +1678,9 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
         if (roundTrace) {
             const Clock::time_point t3 = Clock::now();
             std::fprintf(stderr, "[round] batch=%p round=%d zmws=%zu muts=%lld refill=%zu prerefill=%zu replayed=%lld "
-                                 "score=%.1fms select=%.1fms fill=%.1fms\n",
+                                 "score=%.1fms select=%.1fms fill=%.1fms bandtop=%.2fGB\n",
                          (void*)this, round, act.size(), rTotalMut_, changed.size(), preRefill.size(), replayed,
-                         ms(t0, t1), ms(t1, t2), ms(t2, t3));
+                         ms(t0, t1), ms(t1, t2), ms(t2, t3), valTop_ * 8.0 / 1e9);
         }
     }
     if (!finalRefill.empty()) {   // the scorer API observes the final state: give replayed ZMWs their bands

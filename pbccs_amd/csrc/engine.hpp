@@ -128,6 +128,7 @@ struct Counters {   // work counters for the roofline report (bench.py)
     long long scoreTasks = 0, scoreLaunches = 0;
     long long mutations = 0;
     long long bandGrowths = 0;   // fill launch sets in which some read grew its band region in-kernel
+    long long relayouts = 0;     // fills that laid the band pool out afresh (ArrowBatch::Relayout)
     // band value pool of the batch, bytes (maxima over the batches merged into an engine's counters):
     // bump top (everything ever handed out), current regions (2 x capacity per read), cells in use
     long long bandTopBytes = 0, bandRegionBytes = 0, bandUsedBytes = 0;
@@ -195,8 +196,16 @@ public:
     // RefineConsensus for the listed ZMWs (all in lock-step rounds).
     // needFinalState = false: ZMWs that end NonConvergent may be left without the bands of their final
     // template (the batch polish never reads them).
+    // qvsOnConverge != nullptr: ConsensusQVs of each ZMW in the round it converges (its bands are final then),
+    // per listed ZMW (empty for the ones that do not converge); with reclaim on, their bands are then dropped.
     void Refine(const std::vector<int>& zmws, const RefineOptions& ro, std::vector<int>* converged,
-                std::vector<long long>* nTested, std::vector<long long>* nApplied, bool needFinalState = true);
+                std::vector<long long>* nTested, std::vector<long long>* nApplied, bool needFinalState = true,
+                std::vector<std::vector<int>>* qvsOnConverge = nullptr);
+    // Band reclaim (batch polish): a fill whose list holds every read with live bands lays the value pool out
+    // afresh from offset 0, each region sized from the read's last band.  Live = filled, active
+    // and not retired; the caller retires the ZMWs whose bands it will not read again.
+    void SetReclaim(bool on) { reclaim_ = on; }
+    void Retire(const std::vector<int>& zmws);
     // ConsensusQVs for the listed ZMWs.
     void QVs(const std::vector<int>& zmws, std::vector<std::vector<int>>* qvs);
     // ApplyMutations (MultiReadMutationScorer.cpp:235-267).  Returns false on an invalid edit.
@@ -244,6 +253,7 @@ private:
         int zmw = 0;
         bool active = false;
         bool filled = false;
+        bool retired = false;   // bands no longer read (Retire): the reclaiming layout may drop them
         double baseline = 0.0;
         int flips = 0;
         int status = 0;
@@ -259,6 +269,7 @@ private:
     void UploadDescriptors();
     void UploadTemplate(int z);
     void EnsureCapacity(int r);
+    bool Relayout(const std::vector<int>& reads);
     DevBatch View() const;
     void TraceSummary(size_t n, int H, long long capSlots);
     void MeanVar(const HZmw& z, int strand, int ts, int te, double* mean, double* var) const;
@@ -285,6 +296,7 @@ private:
     long long tplTop_ = 0, seqTop_ = 0, colTop_ = 0, valTop_ = 0;
     int initialBandHeight_ = 16;   // compact band values per column, first estimate
     bool descDirty_ = true;
+    bool reclaim_ = false;
     size_t seqUploaded_ = 0;
 
     // host mirrors of pools

@@ -169,6 +169,43 @@ __device__ __forceinline__ double insertion_chain(const Group<G>& g, double m, d
     return x;
 }
 
+// G = 64 serial chain with an early exit: after step q, lanes <= q hold their final value.  From lane
+// `first` on (the first lane the reference loop may stop at; >= G: none in this chunk) the chain is checked
+// every 8 steps with `maybe_stop`, a conservative form of the loop's stop test (it never reports a lane the
+// exact test continues at).  Once a lane <= q would stop, every lane past it is discarded by the caller, so
+// the remaining steps are skipped; the caller's exact test then finds the same stop lane among the final
+// lanes.  Narrow passes of tall reads (the first alpha / beta, bands of ~15-30 rows) and the last chunk of a
+// tall column no longer pay the full 64 steps.
+template <class MaybeStop>
+__device__ __forceinline__ double insertion_chain64_exit(double m, double k, double d, double carry, int first,
+                                                         MaybeStop maybe_stop)
+{
+    double x = 0.0, up = carry;
+    int q = 0;
+    const int check0 = max(first, 0) + 3;   // first check: a few rows past the first possible stop
+    if (check0 < 63) {
+        for (; q < 64; q += 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                up = shift_up<64>(x, up);
+                x = (m + up * k) + d;
+            }
+            const int last = q + 7;   // lanes <= last are final
+            if (last >= check0 && last < 63) {
+                const unsigned long long st = maybe_stop(x) & ((2ull << last) - 1);
+                if (st) return x;
+            }
+        }
+        return x;
+    }
+#pragma unroll
+    for (int s = 0; s < 64; ++s) {
+        up = shift_up<64>(x, up);
+        x = (m + up * k) + d;
+    }
+    return x;
+}
+
 // Everything a group needs about its read (group-uniform values) + LDS views.
 template <int G>
 struct Task {
@@ -183,7 +220,9 @@ struct Task {
     bool gcol;             // column buffers live in global memory (CoopFill::colScratch), not LDS
     unsigned long long* dbg;   // chain diagnostics (nullptr: off)
     bool jacobi;               // G = 64: Jacobi sweeps instead of 64 serial DPP steps
+    bool chainExit;            // G = 64 serial steps with the early exit (insertion_chain64_exit)
     double prNot, prThird, sdn;
+    double sdnInvLow;   // a double strictly below 1 / sdn (early-exit test of the 64-lane chain)
     // in-kernel band growth (CoopFill::valBump): pool, bump pointer, mapped limit, descriptor arrays
     int r;
     double* pool;
@@ -349,8 +388,17 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                     const double pmv = fmax(mx, prefix_max<G>(xv));
                     return T.g.bits(!((i + 1 < I) && (xv >= pmv / T.sdn || i + 1 < reqEnd)));
                 };
-                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0)
-                    x = insertion_chain<G>(T.g, m, k, d, carry, stop_bits, T.jacobi, T.dbg);
+                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0) {
+                    if (G == 64 && T.chainExit) {
+                        auto maybe_stop = [&](double xv) {   // x < pm * invLow implies x < pm / sdn
+                            const double pmv = fmax(mx, prefix_max<G>(xv));
+                            return T.g.bits((i + 1 >= I) || (xv < pmv * T.sdnInvLow && i + 1 >= reqEnd));
+                        };
+                        x = insertion_chain64_exit(m, k, d, carry, min(reqEnd, I) - 1 - i0, maybe_stop);
+                    } else {
+                        x = insertion_chain<G>(T.g, m, k, d, carry, stop_bits, T.jacobi, T.dbg);
+                    }
+                }
                 const double pm = fmax(mx, prefix_max<G>(x));
                 const double thr = pm / T.sdn;
                 const bool cont = (i + 1 < I) && (x >= thr || i + 1 < reqEnd);
@@ -508,8 +556,17 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                     const double pmv = fmax(mx, prefix_max<G>(xv));
                     return T.g.bits(!((i - 1 > 0) && (xv >= pmv / T.sdn || i - 1 >= reqBegin)));
                 };
-                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0)
-                    x = insertion_chain<G>(T.g, m, k, d, carry, stop_bits, T.jacobi, T.dbg);
+                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0) {
+                    if (G == 64 && T.chainExit) {
+                        auto maybe_stop = [&](double xv) {   // x < pm * invLow implies x < pm / sdn
+                            const double pmv = fmax(mx, prefix_max<G>(xv));
+                            return T.g.bits((i - 1 <= 0) || (xv < pmv * T.sdnInvLow && i - 1 < reqBegin));
+                        };
+                        x = insertion_chain64_exit(m, k, d, carry, e - 1 - max(1, reqBegin) - c * G, maybe_stop);
+                    } else {
+                        x = insertion_chain<G>(T.g, m, k, d, carry, stop_bits, T.jacobi, T.dbg);
+                    }
+                }
                 const double pm = fmax(mx, prefix_max<G>(x));
                 const double thr = pm / T.sdn;
                 const bool cont = (i - 1 > 0) && (x >= thr || i - 1 >= reqBegin);
@@ -680,9 +737,11 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     T.gcol = GC;
     T.dbg = F.chainStats;
     T.jacobi = F.jacobi;
+    T.chainExit = F.chainExit && !F.jacobi;
     T.prNot = B.prNot;
     T.prThird = B.prThird;
     T.sdn = B.sdn;
+    T.sdnInvLow = (1.0 / B.sdn) * (1.0 - 0x1p-50);
     T.r = r;
     T.pool = B.valPool;
     T.bump = F.valBump;
