@@ -68,6 +68,7 @@ struct CoopFill {
     bool jacobi = false;     // G = 64 chain by Jacobi sweeps (see fill_coop.hip)
     bool prio = true;        // G = 64 waves at raised issue priority
     bool chainExit = true;   // G = 64 serial chain leaves a chunk early once its stop row is final
+    int regrowSlackDiv = 16;   // regrow_bands: a re-homed region holds need + need / regrowSlackDiv + 64
     // In-kernel band growth: a read whose alpha/beta region overflows takes a larger region pair from
     // the pool's free top (valBump, in values; mapped up to valLimit), copies what it must keep, and
     // carries on -- no count-only pass and no relaunch.  The new region is written back to the

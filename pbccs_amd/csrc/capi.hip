@@ -576,8 +576,13 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
                 if (q.zscores) q.zscores[k] = std::numeric_limits<double>::quiet_NaN();
             }
         }
-        // bands of ZMWs the batch is done with are dropped as it goes (ArrowBatch::Relayout)
-        B.SetReclaim(true);
+        // PBCCS_RECLAIM=1: bands of ZMWs the batch is done with are dropped as it goes and every refill relays
+        // the value pool out (ArrowBatch::Relayout), with ConsensusQVs run in the round a ZMW
+        // converges.  Opt-in: it cuts the refine rounds' band top (42.5 -> 39.9 GB per 2000-ZMW batch; the
+        // initial fill sets the high-water) but the per-round QVs cost 5.5% (profiles/r2h5_reclaim_ab)
+        const char* reclaimEnv = std::getenv("PBCCS_RECLAIM");
+        const bool reclaim = reclaimEnv && std::strcmp(reclaimEnv, "1") == 0;
+        B.SetReclaim(reclaim);
         B.FillReads(b->allReads);
         std::vector<int> refineZ, refineIdx, dropZ;
         for (int i = 0; i < n; ++i) {
@@ -624,7 +629,7 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
         std::vector<long long> nt, na;
         // ConsensusQVs (Consensus.h:496-512) run inside the refine loop, in the round each ZMW converges
         std::vector<std::vector<int>> qvAll;
-        B.Refine(refineZ, ro, &conv, &nt, &na, false, &qvAll);
+        B.Refine(refineZ, ro, &conv, &nt, &na, false, reclaim ? &qvAll : nullptr);
         std::vector<int> qvZ, qvIdx;
         std::vector<std::vector<int>> qvs;
         for (size_t k = 0; k < refineZ.size(); ++k) {
@@ -634,9 +639,10 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
             if (conv[k] == 1) {
                 qvZ.push_back(refineZ[k]);
                 qvIdx.push_back(refineIdx[k]);
-                qvs.push_back(std::move(qvAll[k]));
+                if (reclaim) qvs.push_back(std::move(qvAll[k]));
             } else q.status = conv[k] < 0 ? PBCCS_ZMW_OTHER : PBCCS_ZMW_NON_CONVERGENT;
         }
+        if (!reclaim) B.QVs(qvZ, &qvs);
         for (size_t k = 0; k < qvZ.size(); ++k) {
             pbccs_zmw_output& q = out[qvIdx[k]];
             const std::string& t = B.Template(qvZ[k]);

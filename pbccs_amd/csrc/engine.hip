@@ -35,9 +35,16 @@ constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill 
 constexpr size_t kCoopTallLdsBytes = 150 * 1024;   // the 16-lane tall path's block (gfx950: 160 KB per CU)
 constexpr size_t kHeadroomMargin = 24ull << 30;   // device bytes band-growth headroom leaves free
 // First region of a read that moves to the tall paths, as a fraction 1 / kTallFirstDiv of its (I+1)(J+1)
-// matrix: exploded bands hold ~8% of it per pass at 2 kb (oracle, 400 reads).  Measured: a 2% first region
-// (growing in-kernel from there) raised a 2000-ZMW batch's band high-water from 40 to 45 GB.
-constexpr long long kTallFirstDiv = 10;
+// matrix.  Exploded bands at 2 kb hold 0.8-21% of it per matrix (oracle, mean 9.9%); a read that outgrows
+// its region re-runs that pass into an exact one (fill_coop.hip regrow_bands), so the first region only
+// trades the memory left behind (all of it, for the reads that outgrow it) against one extra pass.
+constexpr long long kTallFirstDivDefault = 25;
+long long tall_first_div()   // PBCCS_TALL_FIRST_DIV overrides (A/B)
+{
+    static const long long d = std::getenv("PBCCS_TALL_FIRST_DIV") ? std::max(1, std::atoi(std::getenv("PBCCS_TALL_FIRST_DIV")))
+                                                                  : kTallFirstDivDefault;
+    return d;
+}
 constexpr long long kPhasedMinTasks = 1 << 21;   // (mutation, read) tasks from which a round scores in phases
 constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
 
@@ -420,7 +427,7 @@ int ArrowBatch::AppendRead(int z, const std::string& seq, int strand, int ts, in
     r.colCap = J + J / 4 + 66;
     r.colBase = colTop_;
     colTop_ += r.colCap;
-    r.valCap = (long long)r.colCap * initialBandHeight_;
+    r.valCap = (long long)(J + 66) * initialBandHeight_;   // regrown exactly by the fill if outgrown
     r.valA = valTop_;
     r.valB = valTop_ + r.valCap;
     valTop_ += 2 * r.valCap;
@@ -508,7 +515,7 @@ bool ArrowBatch::Relayout(const std::vector<int>& list)
         long long cap;
         if (h.filled && m > 0) cap = m + m / 8 + 64;
         else if (h.fillPath >= 2 && h.fillPath < 5)
-            cap = ((long long)h.seq.size() + 1) * (h.te - h.ts + 1) / kTallFirstDiv + 64;
+            cap = ((long long)h.seq.size() + 1) * (h.te - h.ts + 1) / tall_first_div() + 64;
         else cap = (long long)h.colCap * initialBandHeight_;
         h.valCap = cap;
         h.valA = valTop_;
@@ -789,6 +796,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.prio = !(prioEnv && std::strcmp(prioEnv, "0") == 0);
             static const char* exitEnv = std::getenv("PBCCS_CHAIN_EXIT");   // "0" disables (A/B)
             F.chainExit = !(exitEnv && std::strcmp(exitEnv, "0") == 0);
+            static const int slackDiv = std::getenv("PBCCS_REGROW_SLACK_DIV") ? std::atoi(std::getenv("PBCCS_REGROW_SLACK_DIV")) : 16;
+            F.regrowSlackDiv = slackDiv;
             if (grow) {
                 F.valBump = dBump_.ptr;
                 F.valLimit = valLimit;
@@ -859,7 +868,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                     // from the typical 16-row region inside the kernel would copy and abandon two or three.
                     if (q >= 2 && q < kPaths) {
                         const long long I = (long long)h.seq.size(), J = h.te - h.ts;
-                        const long long want = (I + 1) * (J + 1) / kTallFirstDiv + 64;
+                        const long long want = (I + 1) * (J + 1) / tall_first_div() + 64;
                         if (want > h.valCap) {
                             h.valCap = want;
                             h.valA = valTop_;

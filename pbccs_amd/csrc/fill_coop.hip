@@ -221,6 +221,7 @@ struct Task {
     unsigned long long* dbg;   // chain diagnostics (nullptr: off)
     bool jacobi;               // G = 64: Jacobi sweeps instead of 64 serial DPP steps
     bool chainExit;            // G = 64 serial steps with the early exit (insertion_chain64_exit)
+    int slackDiv;              // regrow_bands slack: need / slackDiv
     double prNot, prThird, sdn;
     double sdnInvLow;   // a double strictly below 1 / sdn (early-exit test of the 64-lane chain)
     // in-kernel band growth (CoopFill::valBump): pool, bump pointer, mapped limit, descriptor arrays
@@ -245,6 +246,7 @@ struct PassOut {
     double sumL;      // accumulate(logScales, 0.0) left to right
     bool tall;        // a column exceeded the LDS buffer
     bool changed;     // some column's [begin, end) differs from the previous pass of this matrix
+    bool regrow;      // the pass outgrew its region and ran to its end counting only: `used` is its exact need
 };
 
 // Column buffers in global memory (the all-rows path for columns taller than LDS holds): a column's
@@ -272,20 +274,20 @@ __device__ __forceinline__ void copy_vals(int lane, double* __restrict__ dst, co
     for (; k < n; k += G) dst[k] = src[k];
 }
 
-// Move the read's alpha/beta region pair to a larger one taken from the pool's free top.  `m` is the
-// matrix being filled (keep its first keepM values: the columns of the running pass), `o` the other
-// one (keep its first keepO values: its last complete pass).  The new capacity is the larger of twice
-// the old one and 1.25x the projected need; `done`/`total` columns give the projection.  Returns
-// false when the mapped headroom is exhausted (the caller then falls back to count-only mode).
+// Move the read's alpha/beta region pair to a larger one taken from the pool's free top, for a pass of
+// matrix `m` that outgrew it.  That pass ran to its end counting only (no value, range, offset or scale
+// stores: its inputs -- the other matrix's ranges and this matrix's previous ranges -- are untouched), so
+// `need` is its exact size; the caller re-runs it into the new region.  `o` keeps its first keepO values (its
+// last complete pass).  Both regions get max(need, keepO) + 1/slackDiv + 64: an exploded alpha band and the
+// beta band after it are the same size to within a few cells.  Returns false when the mapped headroom is
+// exhausted (the caller then falls back to count-only mode and the host re-runs the read).
 template <int G>
-__device__ bool grow_bands(const Task<G>& T, Band& m, Band& o, bool mIsAlpha, long long need, long long keepM,
-                           long long keepO, int done, int total)
+__device__ bool regrow_bands(const Task<G>& T, Band& m, Band& o, bool mIsAlpha, long long need, long long keepO)
 {
     if (!T.bump) return false;
     const long long full = (long long)(T.I + 1) * (T.J + 1) + 1;
-    const long long proj = need * (long long)total / (long long)max(done, 1);
-    long long cap = max(2 * m.cap, proj + proj / 4 + 64);
-    cap = max(min(cap, full), need);
+    long long cap = max(need, keepO);
+    cap = max(min(cap + cap / T.slackDiv + 64, full), max(need, keepO));
     unsigned long long base = 0;
     if (T.g.lane == 0) base = atomicAdd(T.bump, (unsigned long long)(2 * cap));
     base = (unsigned long long)__shfl((long long)base, 0, G);
@@ -295,7 +297,6 @@ __device__ bool grow_bands(const Task<G>& T, Band& m, Band& o, bool mIsAlpha, lo
     double* nb = na + cap;
     double* nm = mIsAlpha ? na : nb;
     double* no = mIsAlpha ? nb : na;
-    copy_vals<G>(T.g.lane, nm, m.val, keepM);
     copy_vals<G>(T.g.lane, no, o.val, keepO);
     m.val = nm;
     o.val = no;
@@ -315,7 +316,9 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
 {
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0.0, 0.0, false, !selfValid};
+    PassOut out{0, 0.0, 0.0, false, !selfValid, false};
+    bool counting = false;   // outgrew the region: finish the pass without stores (regrow_bands)
+    (void)keepO;
     if (a.cap < 1) ovf = true;
     if (lane == 0) {
         if (!ovf) a.V(0) = 1.0;
@@ -415,9 +418,11 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                 carry = T.g.bcast(x, G - 1);
             }
         }
-        if (!ovf && used + (e - b) + 1 > a.cap &&
-            !grow_bands<G>(T, a, o, true, used + (e - b) + 1, used, keepO, j + 1, J + 1))
-            ovf = true;
+        if (!ovf && !counting && used + (e - b) + 1 > a.cap) {
+            if (T.bump) counting = true;
+            else ovf = true;
+        }
+        const bool store = !ovf && !counting;
         // ScaledMatrix::FinishEditingColumn (ScaledMatrix-inl.hpp:35-60) + the next begin hint (:166)
         const double thrF = mx / T.sdn;
         const bool scale = (mx != 0.0 && mx != 1.0);
@@ -430,7 +435,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
             const double v = scale ? x / mx : x;
             if (ok) {
                 cur[kk] = v;
-                if (!ovf && used + kk < a.cap) a.V(used + kk) = v;
+                if (store && used + kk < a.cap) a.V(used + kk) = v;
             }
             const unsigned long long hit = T.g.bits(ok && !(v < thrF));
             if (!found && hit) {
@@ -438,10 +443,10 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                 found = true;
             }
         }
-        if (used + (e - b) > a.cap) ovf = true;
+        if (!counting && used + (e - b) > a.cap) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
         const double lsj = scale ? log(mx) : 0.0;
-        if (lane == 0) {
+        if (lane == 0 && !counting) {
             a.R(j) = make_int2(b, e);
             a.O(j) = (int)used;
             a.L(j) = lsj;
@@ -466,9 +471,12 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     const double c = (0.0 < lik) ? lik : 0.0;
     double v = lik, ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = lik / c; ls = log(c); }
-    if (!ovf && used + 1 > a.cap && !grow_bands<G>(T, a, o, true, used + 1, used, keepO, J + 1, J + 1)) ovf = true;
-    if (used + 1 > a.cap) ovf = true;
-    if (lane == 0) {
+    if (!ovf && !counting && used + 1 > a.cap) {
+        if (T.bump) counting = true;
+        else ovf = true;
+    }
+    out.regrow = counting;
+    if (lane == 0 && !counting) {
         if (!ovf) a.V(used) = v;
         a.R(J) = make_int2(I, I + 1);
         a.O(J) = (int)used;
@@ -486,7 +494,9 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 {
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0.0, 0.0, false, !selfValid};
+    PassOut out{0, 0.0, 0.0, false, !selfValid, false};
+    bool counting = false;   // outgrew the region: finish the pass without stores (regrow_bands)
+    (void)keepO;
     if (bm.cap < 1) ovf = true;
     if (lane == 0) {
         if (!ovf) bm.V(0) = 1.0;
@@ -583,9 +593,11 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                 carry = T.g.bcast(x, G - 1);
             }
         }
-        if (!ovf && used + (e - b) + 1 > bm.cap &&
-            !grow_bands<G>(T, bm, o, false, used + (e - b) + 1, used, keepO, J - j + 1, J + 1))
-            ovf = true;
+        if (!ovf && !counting && used + (e - b) + 1 > bm.cap) {
+            if (T.bump) counting = true;
+            else ovf = true;
+        }
+        const bool store = !ovf && !counting;
         const double thrF = mx / T.sdn;
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhe = b;
@@ -597,7 +609,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
             const double v = scale ? x / mx : x;
             if (ok) {
                 cur[off] = v;
-                if (!ovf && used + off < bm.cap) bm.V(used + off) = v;
+                if (store && used + off < bm.cap) bm.V(used + off) = v;
             }
             const unsigned long long hit = T.g.bits(ok && !(v < thrF));
             if (!found && hit) {
@@ -605,10 +617,10 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                 found = true;
             }
         }
-        if (used + (e - b) > bm.cap) ovf = true;
+        if (!counting && used + (e - b) > bm.cap) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
         const double lsj = scale ? log(mx) : 0.0;
-        if (lane == 0) {
+        if (lane == 0 && !counting) {
             bm.R(j) = make_int2(b, e);
             bm.O(j) = (int)used;
             bm.L(j) = lsj;
@@ -629,10 +641,13 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     const double c = (0.0 < raw) ? raw : 0.0;
     double v = raw, ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = raw / c; ls = log(c); }
-    if (!ovf && used + 1 > bm.cap && !grow_bands<G>(T, bm, o, false, used + 1, used, keepO, J + 1, J + 1)) ovf = true;
-    if (used + 1 > bm.cap) ovf = true;
+    if (!ovf && !counting && used + 1 > bm.cap) {
+        if (T.bump) counting = true;
+        else ovf = true;
+    }
+    out.regrow = counting;
     double s = 0.0;
-    if (lane == 0) {
+    if (lane == 0 && !counting) {
         if (!ovf) bm.V(used) = v;
         bm.R(0) = make_int2(0, 1);
         bm.O(0) = (int)used;
@@ -738,6 +753,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     T.dbg = F.chainStats;
     T.jacobi = F.jacobi;
     T.chainExit = F.chainExit && !F.jacobi;
+    T.slackDiv = max(1, F.regrowSlackDiv);
     T.prNot = B.prNot;
     T.prThird = B.prThird;
     T.sdn = B.sdn;
@@ -779,11 +795,12 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     // its own previous pass (hint), never on previous values.  Once an alpha pass and the beta pass after
     // it both reproduce their predecessors' ranges, every later pass repeats them bit for bit, so the
     // remaining flip-flops are skipped and only the count the reference reports is kept.
-    PassOut pa{0, 0.0, 0.0, false, false}, pb{0, 0.0, 0.0, false, false};
+    PassOut pa{0, 0.0, 0.0, false, false, false}, pb{0, 0.0, 0.0, false, false, false};
     long long ua = 0, ub = 0;
     const int maxSize = (int)(0.5 + kRebandFrac * (I + 1) * (J + 1));
     bool mismatched = false;
     int unchanged = 0;
+    int regrows = 0;
     for (int step = 0;; ++step) {
         bool doAlpha;
         if (step < 2) doAlpha = step == 0;
@@ -805,6 +822,13 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
         if (doAlpha) o = coop_alpha<G>(T, a, bm, guided, self, ovf, ub);
         else o = coop_beta<G>(T, bm, a, guided, self, ovf, ua);
         if (o.tall) return fail_tall();
+        if (o.regrow) {   // exact region for this pass, then run it again (count-only if the pool is full)
+            if (++regrows > 8 ||
+                !regrow_bands<G>(T, doAlpha ? a : bm, doAlpha ? bm : a, doAlpha, o.used, doAlpha ? ub : ua))
+                ovf = true;
+            --step;
+            continue;
+        }
         cells += o.used;
         passes += 1;
         if (doAlpha) {

@@ -289,6 +289,32 @@ def test_band_growth_in_kernel_matches_oracle(P, monkeypatch):
             assert r["consensus"] == e["template"]
 
 
+def test_band_reclaim_matches_oracle(P, monkeypatch):
+    """PBCCS_RECLAIM=1: the refills relay the band pool out afresh (ArrowBatch::Relayout), ConsensusQVs run
+    in the round each ZMW converges, and gated / NonConvergent ZMWs are retired -- with 2-row first regions,
+    so every fill also re-runs passes into exact regions (regrow_bands).  Results must not change."""
+    from pbccs_amd import synth
+    monkeypatch.setenv("PBCCS_RECLAIM", "1")
+    monkeypatch.setenv("PBCCS_INITIAL_BAND_HEIGHT", "2")
+    seed, idx = NONCONVERGENT_2KB
+    allz = synth.make_zmws(max(idx) + 1, 2000, 10, seed=seed)
+    zs = synth.make_zmws(4, 2000, 10, seed=73) + [allz[idx[0]]]
+    zs += synth.make_zmws(2, 600, 2, seed=74)   # too few passes: gated, retired after AddRead
+    res = P.polish_zmws(zs)
+    for k, (z, r) in enumerate(zip(zs, res)):
+        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
+        assert r["add_read_results"] == e["add_read_results"]
+        if k >= 5:
+            assert r["status"] == "TooFewPasses"
+            continue
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        if e["converged"]:
+            assert r["consensus"] == e["template"]
+            assert max(abs(a - b) for a, b in zip(r["qvs"], e["qvs"])) <= 1
+        else:
+            assert r["status"] == "NonConvergent"
+
+
 # configs[1] ZMWs (seed 1, the bench's first step) that the reference loop leaves NonConvergent: their
 # templates oscillate until MaximumIterations, which the engine replays instead of re-running
 # (engine.hip, Refine: cycle replay).  Found with tools/find_nonconvergent.py 2000 2000 10 1.
