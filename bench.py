@@ -34,8 +34,8 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 TRAFFIC_PROFILE = "r2_traffic_fill.json"   # PMC HBM bytes of the roofline kernel (tools/gpu_traffic.sh)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
-BEST_SLOTS = 5                 # measured best split of 2 kb batches
-SLOT_BYTES_PER_ZMW = 18 << 20  # measured band + score high-water per 2 kb / 10-pass ZMW in a slot
+BEST_SLOTS = 6                 # measured split of 2 kb batches: 5 / 6 / 7 slots 3132 / 3170 / 3203
+SLOT_BYTES_PER_ZMW = 15 << 20  # measured band high-water per 2 kb / 10-pass ZMW in a slot (13.4 MB, exact regrow)
 HBM_MARGIN = 24 << 30          # device memory left to scratch, selection buffers and the runtime
 
 
@@ -227,7 +227,7 @@ def max_over_ranks(t, world):
 # ---------------------------------------------------------------------------------------------------------
 def choose_slots(args, local):
     """Workspace slots: the measured best split, capped by the steps and by the HBM the slots' band pools
-    need at their high-water mark (a 2 kb / 10-pass batch of 2000 ZMWs peaks near 36 GB)."""
+    need at their high-water mark (a 2 kb / 10-pass batch of 2000 ZMWs peaks near 27 GB)."""
     import torch
     want = args.streams or max(1, min(args.steps, BEST_SLOTS))
     if not torch.cuda.is_available():
@@ -298,7 +298,7 @@ def main():
     # ---- engine pools mapped before the timed region (a long run maps them once and reuses them) ----
     if torch.cuda.is_available():
         free_b, _ = torch.cuda.mem_get_info(local)
-        per_slot = int(min(0.6 * free_b / slots, 36 << 30))
+        per_slot = int(min(0.6 * free_b / slots, 30 << 30))
         eng.reserve_pool(per_slot)
         log(rank, f"[bench] band pools: {per_slot / 2**30:.1f} GB mapped per slot x {slots}")
 

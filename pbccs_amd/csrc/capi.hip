@@ -793,9 +793,10 @@ int pbccs_engine_reserve_pool(pbccs_engine* eng, size_t bytes_per_slot)
 // ---- ZMW work queue ------------------------------------------------------------------------------
 // Estimated FP64 band footprint of one ZMW at its high-water mark.  Per read: two band regions of ~32 rows
 // x window plus column metadata and score deltas (the typical band), plus the expected share of reads
-// whose first band explodes (the tall-band paths hold ~2-22% of the (I+1)(J+1) matrix).  Fitted to the
-// measured pools: ~13.5 MB per 2 kb / 10-pass ZMW (estimate 18.4 MB), ~1.1 GB per 10 kb / 8-pass ZMW
-// (estimate 1.13 GB).
+// whose first band explodes (the tall-band paths hold ~1-22% of the (I+1)(J+1) matrix).  Fitted to the
+// measured pools with exact band regrow (fill_coop.hip regrow_bands): 13.4 MB per 2 kb / 10-pass ZMW
+// (estimate 14.8 MB, profiles/r2h6_regrow_slots), ~0.75 GB per 10 kb / 8-pass ZMW (estimate 0.73 GB,
+// profiles/r2h7_regrow_ab).
 // Band-pool bytes the workspace slots hold mapped.
 static size_t slot_pool_bytes(pbccs_engine* eng)
 {
@@ -811,7 +812,7 @@ static double zmw_est_bytes(const pbccs_zmw_input& z)
         const double J = std::max(1, z.tends ? z.tends[k] - (z.tstarts ? z.tstarts[k] : 0) : z.draft_len);
         const double I = z.lens ? std::max(0, z.lens[k]) : J;
         const double typical = J * 0.5 * (2 * 32 * 8 * 1.25 + 80 + 8 * 8);
-        const double tall = std::min(0.22 * 8.0 * (I + 1) * (J + 1), 1.33e8 * std::pow(J / 1e4, 3.0));
+        const double tall = std::min(0.15 * 8.0 * (I + 1) * (J + 1), 8.7e7 * std::pow(J / 1e4, 3.0));
         b += typical + tall;
     }
     return std::max(b, 4096.0);
