@@ -714,8 +714,18 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         }
         if (std::all_of(todo, todo + kPaths, [](const std::vector<int>& v) { return v.empty(); })) break;
         if (attempt > 8) throw DeviceError("band storage keeps overflowing");
-        for (auto& v : todo)   // similar lengths share a launch (LDS is sized by the longest)
+        // Wave composition: a 16-lane wavefront fills four consecutive reads of the list in lock-step and runs
+        // until its slowest read's passes end.  A refill's pass count follows the read's last fill -- about half
+        // of the typical reads at 2 kb end after alpha + beta (0 flip-flops), the rest run the flip-flop loop
+        // (oracle: 101 / 110 of 211) -- so reads with flip-flops last time come first, then the others, each
+        // group by window length (similar lengths share a wave; LDS is sized by the launch's longest).
+        // PBCCS_FLIP_SORT=0: length only (A/B).
+        static const bool flipSort = !(std::getenv("PBCCS_FLIP_SORT") && std::strcmp(std::getenv("PBCCS_FLIP_SORT"), "0") == 0);
+        auto quick = [&](int x) { return flipSort && reads_[x].filled && reads_[x].flips == 0 ? 1 : 0; };
+        for (auto& v : todo)
             std::stable_sort(v.begin(), v.end(), [&](int x, int y) {
+                const int qx = quick(x), qy = quick(y);
+                if (qx != qy) return qx < qy;
                 return reads_[x].te - reads_[x].ts > reads_[y].te - reads_[y].ts;
             });
         UploadDescriptors();
