@@ -322,6 +322,8 @@ void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
         stats_[kKFill].bytes += (double)h[2 * kStatFill + 1];
         stats_[kKScore].cells += (double)h[2 * kStatScore];
         stats_[kKScore].bytes += (double)h[2 * kStatScore + 1];
+        static const bool trace = std::getenv("PBCCS_ROUND_TRACE") != nullptr;
+        if (trace) std::fprintf(stderr, "[fillcells] g16=%llu g64=%llu\n", h[8], h[9]);
         PBCCS_HIP(hipMemsetAsync(dStats_.ptr, 0, sizeof(h), stream_));
     }
     for (int k = 0; k < kKernelKinds; ++k) {

@@ -310,6 +310,34 @@ __device__ bool regrow_bands(const Task<G>& T, Band& m, Band& o, bool mIsAlpha, 
     return true;
 }
 
+// Log-scales of a finished pass (ScaledMatrix::FinishEditingColumn's log, off the column path).  Columns
+// [1, J) hold their scale factor (1.0: the column was not scaled); the group's lanes turn a strided share of
+// them into log(factor) (0.0 for 1.0, as the reference's `scale ? log(max) : 0`) at once, instead of one
+// FP64 log per column on every lane.  Column 0 and J already hold their log-scales.  Then one lane sums all
+// J + 1 in column order from 0.0 -- accumulate(logScales, 0.0) -- and the group gets the sum.
+template <int G>
+__device__ double finish_log_scales(const Task<G>& T, const Band& m, int J)
+{
+    for (int k = 1 + T.g.lane; k < J; k += G) {
+        const double f = m.L(k);
+        m.L(k) = (f != 1.0) ? log(f) : 0.0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the group's stores before lane 0's loads
+    double s = 0.0;
+    if (T.g.lane == 0) {   // loads batched 8 at a time so the serial adds, not the load latency, set the pace
+        int k = 0;
+        for (; k + 7 <= J; k += 8) {
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = m.L(k + q);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) s = s + v[q];
+        }
+        for (; k <= J; ++k) s = s + m.L(k);
+    }
+    return T.g.bcast(s, 0);
+}
+
 // ---- FillAlpha (SimpleRecursor.cpp:60-181) --------------------------------------------------------
 template <int G>
 __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO)
@@ -335,7 +363,6 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     int hb = 1, he = 1;
     int prevCtx = kCtxZero;
     int curBase = T.TBase(0), curCtx = T.TCtx(0);
-    double s = 0.0;   // 0.0 + L(0)
     // ranges of the guide and of this matrix's previous pass, prefetched one G-column block ahead
     // (a.R(jj) of a later block is read before this pass overwrites it)
     int2 gR = make_int2(0, 0), sR = make_int2(0, 0), gN = make_int2(0, 0), sN = make_int2(0, 0);
@@ -445,13 +472,11 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         }
         if (!counting && used + (e - b) > a.cap) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
-        const double lsj = scale ? log(mx) : 0.0;
         if (lane == 0 && !counting) {
             a.R(j) = make_int2(b, e);
             a.O(j) = (int)used;
-            a.L(j) = lsj;
+            a.L(j) = scale ? mx : 1.0;   // the scale factor; finish_log_scales takes its log
         }
-        s = s + lsj;
         used += e - b;
         col_fence(T.gcol);   // the next column's lanes read rows this column's lanes wrote
         double* t = prev;
@@ -484,7 +509,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     }
     out.used = used + 1;
     out.last = v;
-    out.sumL = s + ls;
+    if (!counting) out.sumL = finish_log_scales<G>(T, a, J);
     return out;
 }
 
@@ -619,11 +644,10 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         }
         if (!counting && used + (e - b) > bm.cap) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
-        const double lsj = scale ? log(mx) : 0.0;
         if (lane == 0 && !counting) {
             bm.R(j) = make_int2(b, e);
             bm.O(j) = (int)used;
-            bm.L(j) = lsj;
+            bm.L(j) = scale ? mx : 1.0;   // the scale factor; finish_log_scales takes its log
         }
         used += e - b;
         col_fence(T.gcol);
@@ -646,28 +670,15 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         else ovf = true;
     }
     out.regrow = counting;
-    double s = 0.0;
     if (lane == 0 && !counting) {
         if (!ovf) bm.V(used) = v;
         bm.R(0) = make_int2(0, 1);
         bm.O(0) = (int)used;
         bm.L(0) = ls;
-        // accumulate(logScales, 0.0) in column order; lane 0 wrote every L(j) of this pass itself
-        // (loads batched 32 at a time so the serial adds, not the load latency, set the pace)
-        s = s + ls;
-        int k = 1;
-        for (; k + 7 <= J; k += 8) {
-            double v[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] = bm.L(k + q);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) s = s + v[q];
-        }
-        for (; k <= J; ++k) s = s + bm.L(k);
     }
     out.used = used + 1;
     out.last = v;
-    out.sumL = T.g.bcast(s, 0);
+    if (!counting) out.sumL = finish_log_scales<G>(T, bm, J);
     return out;
 }
 
@@ -867,6 +878,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
             if (B.stats) {   // algorithmic: 8 B per stored cell + 16 B per column per fill pass
                 atomicAdd(&B.stats[2 * kStatFill], cells);
                 atomicAdd(&B.stats[2 * kStatFill + 1], 8ull * cells + 16ull * passes * (unsigned long long)(J + 1));
+                atomicAdd(&B.stats[G == 64 ? 9 : 8], cells);   // per path (diagnostics: VALU per cell)
             }
         }
     }
