@@ -103,6 +103,17 @@ struct Group {
         if constexpr (G == 64) return __builtin_amdgcn_readlane(x, src);
         else return __shfl(x, src, G);
     }
+    // value of the group's last lane: G = 16 is one DPP row, whose lane 15 a single v_mov_b64 row_newbcast:15
+    // hands to the whole row (instead of two LDS permutes on the chunk-to-chunk carry path)
+    __device__ __forceinline__ double bcast_last(double x) const
+    {
+        if constexpr (G == 64) {
+            return bcast(x, 63);
+        } else {
+            const long long r = __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x15F, 0xF, 0xF, false);
+            return __longlong_as_double(r);
+        }
+    }
 };
 
 // The in-column insertion chain x_i = (m_i + x_{i-1} k_i) + d_i over the G rows of a chunk (lane l = row
@@ -365,29 +376,39 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     int curBase = T.TBase(0), curCtx = T.TCtx(0);
     // ranges of the guide and of this matrix's previous pass, prefetched one G-column block ahead
     // (a.R(jj) of a later block is read before this pass overwrites it)
+    // G = 64: lane l holds column (block + l) and v_readlane hands it out; G = 16 (LDS permutes would sit on
+    // the column path): every lane of the group loads the next column's ranges one column ahead
     int2 gR = make_int2(0, 0), sR = make_int2(0, 0), gN = make_int2(0, 0), sN = make_int2(0, 0);
     {
-        const int jj = 1 + lane;
+        const int jj = G == 64 ? 1 + lane : 1;
         if (guide && jj < J) gN = guide->R(jj);
         if (selfValid && jj < J) sN = a.R(jj);
     }
     for (int j = 1; j < J; ++j) {
         const int jb = (j - 1) & (G - 1);
-        if (jb == 0) {
+        int gx = 0, gy = 0, sx = 0, sy = 0;
+        if constexpr (G == 64) {
+            if (jb == 0) {
+                gR = gN;
+                sR = sN;
+                const int jj = j + G + lane;
+                if (guide && jj < J) gN = guide->R(jj);
+                if (selfValid && jj < J) sN = a.R(jj);
+            }
+            if (guide) { gx = T.g.bcast(gR.x, jb); gy = T.g.bcast(gR.y, jb); }
+            if (selfValid) { sx = T.g.bcast(sR.x, jb); sy = T.g.bcast(sR.y, jb); }
+        } else {
             gR = gN;
             sR = sN;
-            const int jj = j + G + lane;
-            if (guide && jj < J) gN = guide->R(jj);
-            if (selfValid && jj < J) sN = a.R(jj);
+            if (guide && j + 1 < J) gN = guide->R(j + 1);
+            if (selfValid && j + 1 < J) sN = a.R(j + 1);   // read before this pass writes column j + 1
+            gx = gR.x; gy = gR.y; sx = sR.x; sy = sR.y;
         }
+        (void)jb;
         if (guide) {   // RangeGuide (SimpleRecursor.cpp:728-757)
-            const int gx = T.g.bcast(gR.x, jb), gy = T.g.bcast(gR.y, jb);
             if (gx < gy) { hb = min(gx, hb); he = max(gy, he); }
         }
-        int sx = 0, sy = 0;
         if (selfValid) {
-            sx = T.g.bcast(sR.x, jb);
-            sy = T.g.bcast(sR.y, jb);
             if (sx < sy) { hb = min(sx, hb); he = max(sy, he); }
         }
         const int reqEnd = min(I, he);
@@ -442,7 +463,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                     break;
                 }
                 cur[(nc - 1) * G + lane] = x;
-                carry = T.g.bcast(x, G - 1);
+                carry = T.g.bcast_last(x);
             }
         }
         if (!ovf && !counting && used + (e - b) + 1 > a.cap) {
@@ -540,28 +561,36 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     int nextBase = T.TBase(J - 1);
     int2 gR = make_int2(0, 0), sR = make_int2(0, 0), gN = make_int2(0, 0), sN = make_int2(0, 0);
     {
-        const int jj = J - 1 - lane;
+        const int jj = G == 64 ? J - 1 - lane : J - 1;
         if (guide && jj > 0) gN = guide->R(jj);
         if (selfValid && jj > 0) sN = bm.R(jj);
     }
     for (int j = J - 1; j > 0; --j) {
         const int jb = (J - 1 - j) & (G - 1);
-        if (jb == 0) {   // block of columns (j - G, j]; prefetch the next one
+        int gx = 0, gy = 0, sx = 0, sy = 0;
+        if constexpr (G == 64) {
+            if (jb == 0) {   // block of columns (j - G, j]; prefetch the next one
+                gR = gN;
+                sR = sN;
+                const int jj = j - G - lane;
+                if (guide && jj > 0) gN = guide->R(jj);
+                if (selfValid && jj > 0) sN = bm.R(jj);
+            }
+            if (guide) { gx = T.g.bcast(gR.x, jb); gy = T.g.bcast(gR.y, jb); }
+            if (selfValid) { sx = T.g.bcast(sR.x, jb); sy = T.g.bcast(sR.y, jb); }
+        } else {   // G = 16: the next column's ranges one column ahead (see coop_alpha)
             gR = gN;
             sR = sN;
-            const int jj = j - G - lane;
-            if (guide && jj > 0) gN = guide->R(jj);
-            if (selfValid && jj > 0) sN = bm.R(jj);
+            if (guide && j - 1 > 0) gN = guide->R(j - 1);
+            if (selfValid && j - 1 > 0) sN = bm.R(j - 1);
+            gx = gR.x; gy = gR.y; sx = sR.x; sy = sR.y;
         }
+        (void)jb;
         const int curBase = T.TBase(j - 1), curCtx = T.TCtx(j - 1);
         if (guide) {
-            const int gx = T.g.bcast(gR.x, jb), gy = T.g.bcast(gR.y, jb);
             if (gx < gy) { hb = min(gx, hb); he = max(gy, he); }
         }
-        int sx = 0, sy = 0;
         if (selfValid) {
-            sx = T.g.bcast(sR.x, jb);
-            sy = T.g.bcast(sR.y, jb);
             if (sx < sy) { hb = min(sx, hb); he = max(sy, he); }
         }
         const int reqBegin = max(0, hb);
@@ -615,7 +644,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                     break;
                 }
                 cur[off] = x;
-                carry = T.g.bcast(x, G - 1);
+                carry = T.g.bcast_last(x);
             }
         }
         if (!ovf && !counting && used + (e - b) + 1 > bm.cap) {
