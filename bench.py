@@ -247,6 +247,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PBCCS_BENCH_DEVICE pins every rank to one device: a rehearsal of the multi-rank launch, gather and
+    # max-over-ranks timing on a one-GPU box (ranks then share the device; give them few --streams)
+    if os.environ.get("PBCCS_BENCH_DEVICE"):
+        local = int(os.environ["PBCCS_BENCH_DEVICE"])
     if world != args.gpus:
         log(rank, f"[bench] note: --gpus {args.gpus} but the launcher started {world} rank(s); using {world}")
     # torch first: the engine then binds to the same HIP runtime instance (both carry soname libamdhip64.so.7)
