@@ -72,6 +72,24 @@ def parse():
     return ap.parse_args()
 
 
+_JSON_OUT = None   # the process's real stdout while fd 1 is pointed at stderr (multi-rank runs)
+
+
+def quiet_stdout():
+    """Point fd 1 at stderr for the rest of the run: libraries (gloo's connection report) print to stdout, and
+    the bench's stdout must be exactly its one JSON line.  emit() writes to the saved stdout."""
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
+def emit(out):
+    f = _JSON_OUT or sys.stdout
+    f.write(json.dumps(out) + "\n")
+    f.flush()
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -259,6 +277,7 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
     if world > 1:
+        quiet_stdout()
         dist.init_process_group(backend="gloo")   # barrier + max-time + the queue's counter: no device collective
 
     import pbccs_amd
@@ -411,7 +430,7 @@ def poa_stage(args, rank, world, eng, barrier, sync, seed0):
         out["cpu_baseline"] = poa_cpu_baseline(args, min(args.cpu_sample, 48))
         out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
@@ -481,7 +500,7 @@ def quiver_stage(args, rank, world, eng, barrier, sync, seed0):
     if rank == 0 and args.cpu_sample:
         out["cpu_baseline"] = quiver_cpu_baseline(args, args.cpu_sample)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
@@ -529,7 +548,7 @@ def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
            "zmw_status": statuses, "poa_wall_ms": round(st["total_ms"], 1),
            "poa_device_ms": round(st["device_ms"], 1), "poa_thread_ms": round(st["thread_ms"], 1)}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
@@ -613,7 +632,7 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
         out["cpu_baseline"] = cpu_baseline(args)
         out["vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
