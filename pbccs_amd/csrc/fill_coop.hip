@@ -195,7 +195,10 @@ __device__ __forceinline__ double insertion_chain64_exit(double m, double k, dou
     int q = 0;
     const int check0 = max(first, 0) + 3;   // first check: a few rows past the first possible stop
     if (check0 < 63) {
-        for (; q < 64; q += 8) {
+        // fully unrolled like the check-free path below (a rolled block loop measured 4% slower end to end,
+        // profiles/r2h17_code_size_ab): the checks sit at fixed positions and only their branch is dynamic
+#pragma unroll
+        for (q = 0; q < 64; q += 8) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 up = shift_up<64>(x, up);
