@@ -479,6 +479,8 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhb = e;
         bool found = false;
+        // two chunks per iteration: their divisions and LDS round trips overlap (tall columns have many chunks)
+#pragma unroll 2
         for (int c = 0; c < nc; ++c) {
             const int kk = c * G + lane;
             const bool ok = b + kk < e;
@@ -659,6 +661,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhe = b;
         bool found = false;
+#pragma unroll 2
         for (int c = 0; c < nc; ++c) {
             const int off = c * G + lane;
             const bool ok = e - 1 - off >= b;
