@@ -826,6 +826,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             static const int jacobiMax = std::getenv("PBCCS_JACOBI_MAX") ? std::atoi(std::getenv("PBCCS_JACOBI_MAX")) : 0;
             F.jacobi = chainMode ? std::strcmp(chainMode, "jacobi") == 0 : (p > 1 && n <= jacobiMax);
             F.prio = !(prioEnv && std::strcmp(prioEnv, "0") == 0);
+            static const char* prio16Env = std::getenv("PBCCS_G16_PRIO");   // "1": 16-lane fill waves above scoring
+            F.prio16 = (prio16Env && std::strcmp(prio16Env, "1") == 0) ? 1 : 0;
             static const char* exitEnv = std::getenv("PBCCS_CHAIN_EXIT");   // "0" disables (A/B)
             F.chainExit = !(exitEnv && std::strcmp(exitEnv, "0") == 0);
             static const int slackDiv = std::getenv("PBCCS_REGROW_SLACK_DIV") ? std::atoi(std::getenv("PBCCS_REGROW_SLACK_DIV")) : 16;

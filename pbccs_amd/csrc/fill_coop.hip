@@ -731,6 +731,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     // tall reads are the latency-critical path of every refine round: issue ahead of the 16-lane fills
     // and score waves that share the SIMD (F.prio = 0 leaves the default priority)
     if (G == 64 && F.prio) __builtin_amdgcn_s_setprio(3);
+    if (G == 16 && F.prio16 > 0) __builtin_amdgcn_s_setprio(1);
     const int grp = threadIdx.x / G;
     const int t = blockIdx.x * (64 / G) + grp;
     const int lane = threadIdx.x & (G - 1);
