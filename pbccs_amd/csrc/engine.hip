@@ -811,8 +811,12 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.tplWords = (maxJ + 8) / 8;
             F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
             hcapOf[p] = F.hcap;
-            const int G = (p == 1 || (p == 2 && tall16)) ? 16 : 64;
+            int G = (p == 1 || (p == 2 && tall16)) ? 16 : 64;
             F.groupBytes = coop_group_bytes(p == 4 ? 0 : F.hcap, F.readWords, F.tplWords);
+            // PBCCS_G8=1 (experiment): typical reads in 8-lane groups, eight reads per wavefront (the per-column
+            // work is shared by twice the reads), when eight groups' LDS fits the block budget
+            static const bool g8 = std::getenv("PBCCS_G8") && std::strcmp(std::getenv("PBCCS_G8"), "1") == 0;
+            if (p == 1 && g8 && 8 * F.groupBytes <= kCoopLdsBytes) G = 8;
             if (p == 4) {   // two column buffers of hcap rows per read, in global memory
                 dColScratch_.reserve((size_t)n * 2 * F.hcap, false);
                 F.colScratch = dColScratch_.ptr;

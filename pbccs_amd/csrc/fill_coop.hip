@@ -51,18 +51,36 @@ __device__ __forceinline__ double dpp_d(double old, double x)
     return __hiloint2double(rh, rl);
 }
 
+__device__ __forceinline__ bool group8_lane0() { return (threadIdx.x & 7) == 0; }
+
 // value of lane l-1 of the group; lane 0 receives `first`
 template <int G>
 __device__ __forceinline__ double shift_up(double x, double first)
 {
-    if constexpr (G == 16) return dpp_d<0x111, 0xF, false>(first, x);   // row_shr:1
-    else return dpp_d<0x138, 0xF, false>(first, x);                     // wave_shr:1
+    if constexpr (G == 8) {   // row_shr:1, then the second group of each 16-lane row takes its own `first`
+        const double s = dpp_d<0x111, 0xF, false>(first, x);
+        return group8_lane0() ? first : s;
+    } else if constexpr (G == 16) {
+        return dpp_d<0x111, 0xF, false>(first, x);   // row_shr:1
+    } else {
+        return dpp_d<0x138, 0xF, false>(first, x);   // wave_shr:1
+    }
 }
 
 // inclusive prefix maximum over the group's lanes (values >= 0)
 template <int G>
 __device__ __forceinline__ double prefix_max(double x)
 {
+    if constexpr (G == 8) {   // row shifts stay in the 8-lane group: lanes below the shift take 0 (values >= 0)
+        const int l = threadIdx.x & 7;
+        double y = dpp_d<0x111, 0xF, true>(0.0, x);
+        x = fmax(x, l >= 1 ? y : 0.0);
+        y = dpp_d<0x112, 0xF, true>(0.0, x);
+        x = fmax(x, l >= 2 ? y : 0.0);
+        y = dpp_d<0x114, 0xF, true>(0.0, x);
+        x = fmax(x, l >= 4 ? y : 0.0);
+        return x;
+    }
     x = fmax(x, dpp_d<0x111, 0xF, true>(0.0, x));
     x = fmax(x, dpp_d<0x112, 0xF, true>(0.0, x));
     x = fmax(x, dpp_d<0x114, 0xF, true>(0.0, x));
@@ -109,6 +127,10 @@ struct Group {
     {
         if constexpr (G == 64) {
             return bcast(x, 63);
+        } else if constexpr (G == 8) {   // lane 7 of each row for the first group, lane 15 for the second
+            const long long a = __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x157, 0xF, 0xF, false);
+            const long long b = __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x15F, 0xF, 0xF, false);
+            return __longlong_as_double((threadIdx.x & 8) ? b : a);
         } else {
             const long long r = __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x15F, 0xF, 0xF, false);
             return __longlong_as_double(r);
@@ -937,9 +959,12 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     if (gc && G != 64) throw std::runtime_error("global column buffers need 64-lane groups");
     // two waves per SIMD: the register budget that leaves these kernels without spills (higher occupancy
     // was measured slower and needs a private segment, which the resource check in the Makefile forbids)
-    const K k = gc ? (K)k_fill_coop<64, 2, true> : G == 16 ? (K)k_fill_coop<16, 2, false> : (K)k_fill_coop<64, 2, false>;
-    static bool attrSet[3] = {false, false, false};   // dynamic LDS beyond 64 KB must be enabled per kernel
-    const int ak = gc ? 2 : (G == 64);
+    const K k = gc        ? (K)k_fill_coop<64, 2, true>
+                : G == 16 ? (K)k_fill_coop<16, 2, false>
+                : G == 8  ? (K)k_fill_coop<8, 2, false>
+                          : (K)k_fill_coop<64, 2, false>;
+    static bool attrSet[4] = {false, false, false, false};   // dynamic LDS beyond 64 KB must be enabled per kernel
+    const int ak = gc ? 2 : G == 8 ? 3 : (G == 64);
     if (!attrSet[ak]) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attrSet[ak] = true;
