@@ -1259,15 +1259,31 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
     const long long minTasks = minEnv ? std::atoll(minEnv) : kPhasedMinTasks;
     long long tasks = rTotalDelta_;
     if (phased && minTasks >= 0 && rTotalDelta_ >= minTasks && rTotalMut_ <= INT_MAX) {
-        const int bounds[] = {0, 3, 5, 1 << 30};
-        std::vector<std::vector<long long>> ws(3);
+        // phase boundaries (read indices); PBCCS_PHASE_BOUNDS="3,5" is the default, e.g. "3,4,5" adds a phase
+        static const std::vector<int> bounds = [] {
+            std::vector<int> b{0};
+            const char* e = std::getenv("PBCCS_PHASE_BOUNDS");
+            std::string spec = e ? e : "3,5";
+            size_t pos = 0;
+            while (pos < spec.size()) {
+                const size_t c = spec.find(',', pos);
+                const int v = std::atoi(spec.substr(pos, c == std::string::npos ? std::string::npos : c - pos).c_str());
+                if (v > b.back()) b.push_back(v);
+                if (c == std::string::npos) break;
+                pos = c + 1;
+            }
+            b.push_back(1 << 30);
+            return b;
+        }();
+        const int nPhases = (int)bounds.size() - 1;
+        std::vector<std::vector<long long>> ws(nPhases);
         std::vector<int> nSel;
         ws_->sel.reserve(std::max<long long>(rTotalMut_, 1), false);
         ws_->selCount.reserve(2, false);
         dSelBase_.reserve(std::max(n, 1), false);
         dNSel_.reserve(std::max(n, 1), false);
         tasks = 0;
-        for (int ph = 0; ph < 3; ++ph) {
+        for (int ph = 0; ph < nPhases; ++ph) {
             const int lo = bounds[ph], hi = bounds[ph + 1];
             if (ph > 0) {
                 Timed(kKReduce, [&] { launch_alive(B, W, rTotalMut_, fastThr, lo, dFav_.ptr, stream_); });
