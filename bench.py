@@ -32,7 +32,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-TRAFFIC_PROFILE = "r2h14_traffic_fill.json"   # PMC HBM bytes of the roofline kernel (tools/gpu_traffic.sh)
+TRAFFIC_PROFILE = "r2hP_traffic_fill.json"   # PMC HBM bytes of the roofline kernel (tools/gpu_traffic.sh)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
 BEST_SLOTS = 5                 # measured best split of 2 kb batches: 5 slots divide the driver's 20 steps into 4 full waves (6 slots: 2868 vs 3357 ZMWs/s at --steps 20, the last wave half empty)
 SLOT_BYTES_PER_ZMW = 15 << 20  # measured band high-water per 2 kb / 10-pass ZMW in a slot (13.4 MB, exact regrow)
