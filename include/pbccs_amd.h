@@ -383,7 +383,7 @@ typedef struct {
  * max_coverage reads were added, then FindConsensus(min_coverage) with the per-read summaries.
  * min_coverage < 0 uses Consensus.h's rule ((cov < 5) ? 1 : (cov + 1) / 2 - 1).  A consensus longer
  * than its buffer sets that output's len and makes the call return PBCCS_ERANGE after all outputs are
- * written. */
+ * written.  A NULL sequence is a dropped read; an empty one is never added either (key -1). */
 int pbccs_poa_batch(pbccs_engine* eng, const pbccs_poa_input* in, int n, long long max_coverage, int min_coverage,
                     pbccs_poa_output* out);
 
@@ -413,8 +413,14 @@ int pbccs_poa_consensus(pbccs_engine* eng, const char* const* reads, const int* 
  * FilterReads (NO_SUBREADS when nothing is left), the POA draft on the GPU (pbccs_poa_batch, with
  * max_poa_coverage), TOO_SHORT for a draft below opts->min_length, ExtractMappedRead per POA key, and the
  * polish (pbccs_polish_batch: AddRead gates, RefineConsensus, ConsensusQVs, the accuracy gate).
- * out[z].polish.add_read_results / zscores are indexed by POA key (size them by n_subreads; -1: not added).
- * out[z].draft (optional, draft_cap bytes) receives the POA consensus. */
+ * out[z].polish.add_read_results / zscores are indexed like in[z].seqs, the caller's subread order (size
+ * them by n_subreads): a read FilterReads dropped, the POA did not add, ExtractMappedRead rejected or the
+ * maxPoaCov stop never reached reads -1 / NaN, as does every read of a ZMW that ended before the polish.
+ * A zero-length subread takes part in FilterReads but is never added to the POA (key -1); the same rule
+ * holds in pbccs_poa_batch and pbccs_sparse_poa_orient_and_add_read.  A NULL sequence with a positive
+ * length or a negative length is PBCCS_EINVAL.  out[z].draft (optional, draft_cap bytes) receives the POA
+ * consensus; a draft longer than its buffer sets draft_len and makes the call return PBCCS_ERANGE after
+ * all outputs are written. */
 typedef struct {
     double snr[4];
     int n_subreads;

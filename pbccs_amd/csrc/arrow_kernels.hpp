@@ -64,10 +64,7 @@ struct CoopFill {
     int readWords = 0;       // nibble-packed read words per group (>= ceil(I / 8) of every read)
     int tplWords = 0;        // nibble-packed template words per group (>= ceil((J + 1) / 8))
     size_t groupBytes = 0;   // coop_group_bytes(hcap, readWords, tplWords)
-    unsigned long long* chainStats = nullptr;   // diagnostics (PBCCS_CHAIN_STATS): [chunks, sweeps, cycles, stops]
-    bool jacobi = false;     // G = 64 chain by Jacobi sweeps (see fill_coop.hip)
     bool prio = true;        // G = 64 waves at raised issue priority
-    int prio16 = 0;          // G = 16 waves' issue priority (0: default)
     bool chainExit = true;   // G = 64 serial chain leaves a chunk early once its stop row is final
     int regrowSlackDiv = 16;   // regrow_bands: a re-homed region holds need + need / regrowSlackDiv + 64
     // In-kernel band growth: a read whose alpha/beta region overflows takes a larger region pair from

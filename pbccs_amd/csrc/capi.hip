@@ -1437,8 +1437,8 @@ int pbccs_poa_batch(pbccs_engine* eng, const pbccs_poa_input* in, int n, long lo
                 return fail(PBCCS_EINVAL, "bad pbccs_poa_input");
             own[z].resize(in[z].n_reads);
             for (int r = 0; r < in[z].n_reads; ++r) {
-                if (in[z].seqs[r] && in[z].lens[r] <= 0) return fail(PBCCS_EINVAL, "empty read");
-                if (in[z].seqs[r]) own[z][r].assign(in[z].seqs[r], in[z].lens[r]);
+                if (in[z].seqs[r] && in[z].lens[r] < 0) return fail(PBCCS_EINVAL, "negative read length");
+                if (in[z].seqs[r]) own[z][r].assign(in[z].seqs[r], in[z].lens[r]);   // empty: key -1
             }
             for (int r = 0; r < in[z].n_reads; ++r) reads[z].push_back(in[z].seqs[r] ? &own[z][r] : nullptr);
         }
@@ -1482,8 +1482,12 @@ void pbccs_sparse_poa_destroy(pbccs_sparse_poa* p) { delete p; }
 int pbccs_sparse_poa_orient_and_add_read(pbccs_sparse_poa* p, const char* seq, int len, float min_score_to_add,
                                          int* key)
 {
-    if (!p || !seq || len <= 0 || !key) return fail(PBCCS_EINVAL, "bad argument");
+    if (!p || (!seq && len > 0) || len < 0 || !key) return fail(PBCCS_EINVAL, "bad argument");
     return guarded([&] {
+        if (len == 0) {   // an empty read is never added (the rule of pbccs_poa_batch / pbccs_ccs_batch)
+            *key = -1;
+            return PBCCS_OK;
+        }
         const std::string s(seq, len);
         if (p->z.graph.NumReads() == 0) {
             std::vector<int> path;
@@ -1606,7 +1610,22 @@ struct CcsChunk {
     std::vector<pbccs_zmw_input> pin;   // the ZMWs that reach the polish
     std::vector<int> pinZ;
     std::vector<pbccs_zmw_output> pout;
+    // per-read polish outputs by position in the polish input (FilterReads order up to the maxPoaCov stop);
+    // scattered back to the caller's subread order once the chunk's polish is final
+    std::vector<std::vector<int>> arr;
+    std::vector<std::vector<double>> zsc;
+    bool draftRange = false;   // a draft longer than its caller buffer
 };
+
+// The chunk's polish outputs: the caller's pbccs_zmw_output fields, but per-read arrays owned by the chunk.
+static void bind_polish_outputs(CcsChunk* C, const pbccs_ccs_output* out)
+{
+    for (size_t q = 0; q < C->pinZ.size(); ++q) {
+        C->pout[q] = out[C->pinZ[q]].polish;
+        C->pout[q].add_read_results = C->arr[q].data();
+        C->pout[q].zscores = C->zsc[q].data();
+    }
+}
 
 // The POA draft of one chunk (Consensus.h:422-425, 352-390), then TooShort and ExtractMappedRead
 // (Consensus.h:427-471) into the chunk's polish inputs.
@@ -1631,7 +1650,10 @@ static void ccs_draft_chunk(pbccs_engine* eng, const pbccs_ccs_input* in, const 
     for (size_t q = 0; q < m; ++q) {
         const int z = C->zs[q];
         const std::string& css = C->css[q];
-        if (out[z].draft && out[z].draft_cap >= (int)css.size()) memcpy(out[z].draft, css.data(), css.size());
+        if (out[z].draft) {
+            if (out[z].draft_cap >= (int)css.size()) memcpy(out[z].draft, css.data(), css.size());
+            else C->draftRange = true;
+        }
         out[z].draft_len = (int)css.size();
         if ((int)css.size() < o.min_length) {
             out[z].polish.status = PBCCS_ZMW_TOO_SHORT;
@@ -1672,7 +1694,10 @@ static void ccs_draft_chunk(pbccs_engine* eng, const pbccs_ccs_input* in, const 
         C->pin.push_back(zi);
         C->pinZ.push_back(z);
         C->pout.push_back(out[z].polish);
+        C->arr.emplace_back(std::max<size_t>(1, C->mapped[q].size()), -1);
+        C->zsc.emplace_back(std::max<size_t>(1, C->mapped[q].size()), std::numeric_limits<double>::quiet_NaN());
     }
+    bind_polish_outputs(C, out);
 }
 
 int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long long max_poa_coverage,
@@ -1690,9 +1715,20 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
         for (int z = 0; z < n; ++z) {
             if (in[z].n_subreads < 0 || (in[z].n_subreads > 0 && (!in[z].seqs || !in[z].lens)))
                 return fail(PBCCS_EINVAL, "bad pbccs_ccs_input");
+            for (int r = 0; r < in[z].n_subreads; ++r)
+                if (in[z].lens[r] < 0 || (in[z].lens[r] > 0 && !in[z].seqs[r]))
+                    return fail(PBCCS_EINVAL, "bad subread (NULL sequence or negative length)");
+        }
+        for (int z = 0; z < n; ++z) {   // every per-read slot starts as "not added"
+            for (int r = 0; r < in[z].n_subreads; ++r) {
+                if (out[z].polish.add_read_results) out[z].polish.add_read_results[r] = -1;
+                if (out[z].polish.zscores) out[z].polish.zscores[r] = std::numeric_limits<double>::quiet_NaN();
+            }
+        }
+        for (int z = 0; z < n; ++z) {
             for (int r = 0; r < in[z].n_subreads; ++r) {
                 driver::Subread s;
-                s.seq.assign(in[z].seqs[r], in[z].lens[r]);
+                if (in[z].lens[r] > 0) s.seq.assign(in[z].seqs[r], in[z].lens[r]);
                 if (in[z].flags) s.flags = in[z].flags[r];
                 sub[z].push_back(std::move(s));
             }
@@ -1853,13 +1889,31 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
                 unmapped = true;
             }
             CcsChunk& C = chunks[c];
-            for (size_t q = 0; q < C.pinZ.size(); ++q) C.pout[q] = out[C.pinZ[q]].polish;
+            bind_polish_outputs(&C, out);
             const int r = polish_retry(eng, 0, C.pin.data(), (int)C.pin.size(), &o, C.pout.data());
             if (r != PBCCS_OK) return r;
         }
-        for (const CcsChunk& C : chunks)
-            for (size_t q = 0; q < C.pinZ.size(); ++q) out[C.pinZ[q]].polish = C.pout[q];
-        return PBCCS_OK;
+        bool draftRange = false;
+        for (const CcsChunk& C : chunks) {
+            draftRange = draftRange || C.draftRange;
+            for (size_t q = 0; q < C.pinZ.size(); ++q) {
+                const int z = C.pinZ[q];
+                pbccs_zmw_output& po = out[z].polish;
+                int* const arrOut = po.add_read_results;
+                double* const zsOut = po.zscores;
+                po = C.pout[q];
+                po.add_read_results = arrOut;
+                po.zscores = zsOut;
+                // polish position i is FilterReads' i-th read, i.e. caller subread order[z][i]
+                for (size_t i = 0; i < C.mapped[q].size(); ++i) {
+                    const int k = order[z][i];
+                    if (k < 0) continue;
+                    if (arrOut) arrOut[k] = C.arr[q][i];
+                    if (zsOut) zsOut[k] = C.zsc[q][i];
+                }
+            }
+        }
+        return draftRange ? fail(PBCCS_ERANGE, "draft buffer too small") : PBCCS_OK;
     });
 }
 

@@ -32,7 +32,6 @@ constexpr double kFillScratchBudget = 24.0 * (1ull << 30);
 constexpr int kCoopNarrowRows = 64;           // LDS column rows of the 16-lane fill path
 constexpr int kCoopTallRows = 1024;           // LDS column rows of the first 64-lane fill path
 constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill block
-constexpr size_t kCoopTallLdsBytes = 150 * 1024;   // the 16-lane tall path's block (gfx950: 160 KB per CU)
 constexpr size_t kHeadroomMargin = 24ull << 30;   // device bytes band-growth headroom leaves free
 // First region of a read that moves to the tall paths, as a fraction 1 / kTallFirstDiv of its (I+1)(J+1)
 // matrix.  Exploded bands at 2 kb hold 0.8-21% of it per matrix (oracle, mean 9.9%); a read that outgrows
@@ -306,14 +305,6 @@ const Counters& ArrowBatch::counters()
 void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
 {
     ResolveEvents();
-    if (chainInit_) {
-        unsigned long long c[4];
-        PBCCS_HIP(hipMemcpyAsync(c, dChain_.ptr, sizeof(c), hipMemcpyDeviceToHost, stream_));
-        PBCCS_HIP(hipStreamSynchronize(stream_));
-        std::fprintf(stderr, "[chain64] chunks=%llu sweeps/chunk=%.2f cycles/sweep=%.1f stop-exits=%.3f\n", c[0],
-                     c[0] ? (double)c[1] / c[0] : 0.0, c[1] ? (double)c[2] / c[1] : 0.0, c[0] ? (double)c[3] / c[0] : 0.0);
-        PBCCS_HIP(hipMemsetAsync(dChain_.ptr, 0, sizeof(c), stream_));
-    }
     if (profiling_) {
         unsigned long long h[16];
         PBCCS_HIP(hipMemcpyAsync(h, dStats_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
@@ -680,21 +671,13 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         return (int)(reads_[r].seq.size() + 7) / 8 + (reads_[r].te - reads_[r].ts + 8) / 8;
     };
     // rows a column buffer of path p gets for reads with these sizes (0: does not fit in LDS)
-    // Path 1 (tall bands) runs 16 lanes per read by default, with column buffers of up to 1024 rows in a
-    // block of up to 150 KB of LDS: the serial insertion chain then costs G = 16 wave-instructions per 16
-    // rows of four reads instead of 64 per 64 rows of one read -- 4x fewer VALU issue slots for the few
-    // reads per ZMW whose first band explodes (~36% of all fill work with 64 lanes).  Measured slower end to
-    // end (1290 vs 2480 ZMWs/s): the tall reads are each round's critical path and 16-row chunks pay the
-    // per-chunk band logic 4x as often, so it is opt-in (PBCCS_TALL16=1); the default is 64 lanes.
-    static const bool tall16 = std::getenv("PBCCS_TALL16") && std::strcmp(std::getenv("PBCCS_TALL16"), "1") == 0;
+    // Tall bands run on 64 lanes (one read per wavefront).  16-lane groups for them (4x fewer VALU issue
+    // slots per chain step) measured 1290 against 2480 ZMWs/s and were removed: the tall reads are each
+    // round's critical path and 16-row chunks pay the per-chunk band logic 4x as often.
     auto rows_for = [&](int p, int maxI, int w) -> int {
         if (p == 0) return laneFill ? kFillLaneRows : 0;
         if (p == 4) return coop_group_bytes(0, w, 0) <= kCoopLdsBytes ? (maxI + 64) / 64 * 64 : 0;
         if (p == 1) return 4 * coop_group_bytes(kCoopNarrowRows, w, 0) <= kCoopLdsBytes ? kCoopNarrowRows : 0;
-        if (p == 2 && tall16) {
-            const int want = std::min<int>(kCoopTallRows, (maxI + 16) / 16 * 16);
-            return 4 * coop_group_bytes(want, w, 0) <= kCoopTallLdsBytes ? want : 0;
-        }
         const long long room = ((long long)kCoopLdsBytes - (long long)coop_group_bytes(0, w, 0)) / 16 / 64 * 64;
         const long long full = (maxI + 64) / 64 * 64;   // a column never exceeds I + 1 rows
         const long long want = p == 2 ? std::min<long long>(kCoopTallRows, full) : full;
@@ -811,27 +794,14 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.tplWords = (maxJ + 8) / 8;
             F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
             hcapOf[p] = F.hcap;
-            int G = (p == 1 || (p == 2 && tall16)) ? 16 : 64;
+            const int G = p == 1 ? 16 : 64;
             F.groupBytes = coop_group_bytes(p == 4 ? 0 : F.hcap, F.readWords, F.tplWords);
-            // PBCCS_G8=1 (experiment): typical reads in 8-lane groups, eight reads per wavefront (the per-column
-            // work is shared by twice the reads), when eight groups' LDS fits the block budget
-            static const bool g8 = std::getenv("PBCCS_G8") && std::strcmp(std::getenv("PBCCS_G8"), "1") == 0;
-            if (p == 1 && g8 && 8 * F.groupBytes <= kCoopLdsBytes) G = 8;
             if (p == 4) {   // two column buffers of hcap rows per read, in global memory
                 dColScratch_.reserve((size_t)n * 2 * F.hcap, false);
                 F.colScratch = dColScratch_.ptr;
             }
-            static const bool chainStats = std::getenv("PBCCS_CHAIN_STATS") != nullptr;
-            static const char* chainMode = std::getenv("PBCCS_CHAIN_MODE");   // "serial" | "jacobi"
             static const char* prioEnv = std::getenv("PBCCS_TALL_PRIO");      // "0" disables
-            // Jacobi sweeps cut a tall chunk's latency but not its instruction count: use them when the
-            // launch is latency-bound (few tall reads, e.g. a batch's convergence tail), serial steps when
-            // the tall fills compete for issue slots with a full device.
-            static const int jacobiMax = std::getenv("PBCCS_JACOBI_MAX") ? std::atoi(std::getenv("PBCCS_JACOBI_MAX")) : 0;
-            F.jacobi = chainMode ? std::strcmp(chainMode, "jacobi") == 0 : (p > 1 && n <= jacobiMax);
             F.prio = !(prioEnv && std::strcmp(prioEnv, "0") == 0);
-            static const char* prio16Env = std::getenv("PBCCS_G16_PRIO");   // "1": 16-lane fill waves above scoring
-            F.prio16 = (prio16Env && std::strcmp(prio16Env, "1") == 0) ? 1 : 0;
             static const char* exitEnv = std::getenv("PBCCS_CHAIN_EXIT");   // "0" disables (A/B)
             F.chainExit = !(exitEnv && std::strcmp(exitEnv, "0") == 0);
             static const int slackDiv = std::getenv("PBCCS_REGROW_SLACK_DIV") ? std::atoi(std::getenv("PBCCS_REGROW_SLACK_DIV")) : 16;
@@ -842,14 +812,6 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 F.rValA = dRValA_.ptr;
                 F.rValB = dRValB_.ptr;
                 F.rValCap = dRValCap_.ptr;
-            }
-            if (chainStats && p > 1) {
-                dChain_.reserve(4, false);
-                if (!chainInit_) {
-                    PBCCS_HIP(hipMemsetAsync(dChain_.ptr, 0, 4 * sizeof(unsigned long long), stream_));
-                    chainInit_ = true;
-                }
-                F.chainStats = dChain_.ptr;
             }
             const int* lp = dList_.ptr + off;
             const hipStream_t st = p <= 1 ? stream_ : p == 2 ? stream2_ : stream3_;

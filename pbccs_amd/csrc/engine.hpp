@@ -342,8 +342,6 @@ private:
     bool profiling_ = false;
     DevVec<unsigned long long> dStats_;
     DevVec<long long> dTrace_;   // PBCCS_FILL_TRACE diagnostics
-    DevVec<unsigned long long> dChain_;   // PBCCS_CHAIN_STATS diagnostics
-    bool chainInit_ = false;
     struct Pending {
         int kind;
         hipEvent_t a, b;

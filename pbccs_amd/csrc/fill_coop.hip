@@ -51,16 +51,11 @@ __device__ __forceinline__ double dpp_d(double old, double x)
     return __hiloint2double(rh, rl);
 }
 
-__device__ __forceinline__ bool group8_lane0() { return (threadIdx.x & 7) == 0; }
-
 // value of lane l-1 of the group; lane 0 receives `first`
 template <int G>
 __device__ __forceinline__ double shift_up(double x, double first)
 {
-    if constexpr (G == 8) {   // row_shr:1, then the second group of each 16-lane row takes its own `first`
-        const double s = dpp_d<0x111, 0xF, false>(first, x);
-        return group8_lane0() ? first : s;
-    } else if constexpr (G == 16) {
+    if constexpr (G == 16) {
         return dpp_d<0x111, 0xF, false>(first, x);   // row_shr:1
     } else {
         return dpp_d<0x138, 0xF, false>(first, x);   // wave_shr:1
@@ -71,16 +66,6 @@ __device__ __forceinline__ double shift_up(double x, double first)
 template <int G>
 __device__ __forceinline__ double prefix_max(double x)
 {
-    if constexpr (G == 8) {   // row shifts stay in the 8-lane group: lanes below the shift take 0 (values >= 0)
-        const int l = threadIdx.x & 7;
-        double y = dpp_d<0x111, 0xF, true>(0.0, x);
-        x = fmax(x, l >= 1 ? y : 0.0);
-        y = dpp_d<0x112, 0xF, true>(0.0, x);
-        x = fmax(x, l >= 2 ? y : 0.0);
-        y = dpp_d<0x114, 0xF, true>(0.0, x);
-        x = fmax(x, l >= 4 ? y : 0.0);
-        return x;
-    }
     x = fmax(x, dpp_d<0x111, 0xF, true>(0.0, x));
     x = fmax(x, dpp_d<0x112, 0xF, true>(0.0, x));
     x = fmax(x, dpp_d<0x114, 0xF, true>(0.0, x));
@@ -127,10 +112,6 @@ struct Group {
     {
         if constexpr (G == 64) {
             return bcast(x, 63);
-        } else if constexpr (G == 8) {   // lane 7 of each row for the first group, lane 15 for the second
-            const long long a = __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x157, 0xF, 0xF, false);
-            const long long b = __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x15F, 0xF, 0xF, false);
-            return __longlong_as_double((threadIdx.x & 8) ? b : a);
         } else {
             const long long r = __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x15F, 0xF, 0xF, false);
             return __longlong_as_double(r);
@@ -139,60 +120,13 @@ struct Group {
 };
 
 // The in-column insertion chain x_i = (m_i + x_{i-1} k_i) + d_i over the G rows of a chunk (lane l = row
-// l; lane 0's predecessor is `carry`), in the reference's operation order (SimpleRecursor.cpp:117-150).
-//  G = 16: G serial shift-by-one DPP steps; after step q lanes <= q hold their final value.
-//  G = 64: Jacobi sweeps -- every lane recomputes its row from its neighbour's current value at once.
-//          Lanes below `exact` hold the serial result: each sweep extends that prefix by one lane, and
-//          a prefix of lanes whose bits did not move in a sweep satisfies the recurrence from `carry`,
-//          whose solution is unique, so it IS the serial result bit for bit.  Influence decays along
-//          the chain (k_i << 1), so inside a tall band the prefix jumps to the whole chunk after ~7
-//          sweeps instead of 64 serial steps.  Rows past the band end decay without damping relative to
-//          themselves and would settle only one per sweep; they are never stored, so the sweeps stop as
-//          soon as the band-end row (`stop_bits`, checked every 4 sweeps) lies inside the exact prefix.
-//          At most G sweeps in any case.
-template <int G, class StopBits>
-__device__ __forceinline__ double insertion_chain(const Group<G>& g, double m, double k, double d, double carry,
-                                                  StopBits stop_bits, bool jacobi, unsigned long long* dbg)
+// l; lane 0's predecessor is `carry`), in the reference's operation order (SimpleRecursor.cpp:117-150):
+// G serial shift-by-one DPP steps; after step q lanes <= q hold their final value.  (Jacobi sweeps for
+// G = 64 -- exact by fixed-point uniqueness -- measured 157 ms against 67 ms per tall fill and were
+// removed)
+template <int G>
+__device__ __forceinline__ double insertion_chain(double m, double k, double d, double carry)
 {
-    if constexpr (G == 64) {
-        if (jacobi) {
-            const long long c0 = dbg ? clock64() : 0;
-            double x = m + d;
-            int exact = 0, q = 0;
-            bool stopped = false;
-            // blocks of 4 sweeps with one convergence test each (a VALU -> SALU round trip per test)
-            while (q < G) {
-                double prev = x;
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    prev = x;
-                    x = (m + shift_up<G>(x, carry) * k) + d;
-                }
-                q += 4;
-                // lanes that did not move in the last sweep form a fixed-point prefix
-                const unsigned long long moved = g.bits(__double_as_longlong(x) != __double_as_longlong(prev));
-                exact = max(exact + 4, moved ? __ffsll((long long)moved) - 1 : G);
-                if (exact >= G) break;
-                if ((q & 7) == 0) {
-                    const unsigned long long st = stop_bits(x);
-                    if (st && __ffsll((long long)st) - 1 < exact) {
-                        stopped = true;
-                        break;
-                    }
-                }
-            }
-            if (dbg && g.lane == 0) {
-                atomicAdd(dbg + 0, 1ull);
-                atomicAdd(dbg + 1, (unsigned long long)q);
-                atomicAdd(dbg + 2, (unsigned long long)(clock64() - c0));
-                atomicAdd(dbg + 3, stopped ? 1ull : 0ull);
-            }
-            return x;
-        }
-    }
-    (void)stop_bits;
-    (void)jacobi;
-    (void)dbg;
     double x = 0.0, up = carry;   // lane 0's `up` stays the carry: DPP leaves it untouched
 #pragma unroll
     for (int q = 0; q < G; ++q) {
@@ -254,8 +188,6 @@ struct Task {
     double* col1;
     int hcap;              // rows per column buffer
     bool gcol;             // column buffers live in global memory (CoopFill::colScratch), not LDS
-    unsigned long long* dbg;   // chain diagnostics (nullptr: off)
-    bool jacobi;               // G = 64: Jacobi sweeps instead of 64 serial DPP steps
     bool chainExit;            // G = 64 serial steps with the early exit (insertion_chain64_exit)
     int slackDiv;              // regrow_bands slack: need / slackDiv
     double prNot, prThird, sdn;
@@ -460,10 +392,6 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                 double x = 0.0;
                 // a chunk whose inputs are all exactly zero stays zero: skip its chain (bit-exact; common
                 // in the far rows of tall bands)
-                auto stop_bits = [&](double xv) {   // the reference loop's continue test (:110-112), per row
-                    const double pmv = fmax(mx, prefix_max<G>(xv));
-                    return T.g.bits(!((i + 1 < I) && (xv >= pmv / T.sdn || i + 1 < reqEnd)));
-                };
                 if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0) {
                     if (G == 64 && T.chainExit) {
                         auto maybe_stop = [&](double xv) {   // x < pm * invLow implies x < pm / sdn
@@ -472,7 +400,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                         };
                         x = insertion_chain64_exit(m, k, d, carry, min(reqEnd, I) - 1 - i0, maybe_stop);
                     } else {
-                        x = insertion_chain<G>(T.g, m, k, d, carry, stop_bits, T.jacobi, T.dbg);
+                        x = insertion_chain<G>(m, k, d, carry);
                     }
                 }
                 const double pm = fmax(mx, prefix_max<G>(x));
@@ -643,10 +571,6 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                 double x = 0.0;
                 // a chunk whose inputs are all exactly zero stays zero: skip its chain (bit-exact; common
                 // in the far rows of tall bands)
-                auto stop_bits = [&](double xv) {   // the reference loop's continue test (:227-229), per row
-                    const double pmv = fmax(mx, prefix_max<G>(xv));
-                    return T.g.bits(!((i - 1 > 0) && (xv >= pmv / T.sdn || i - 1 >= reqBegin)));
-                };
                 if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0) {
                     if (G == 64 && T.chainExit) {
                         auto maybe_stop = [&](double xv) {   // x < pm * invLow implies x < pm / sdn
@@ -655,7 +579,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                         };
                         x = insertion_chain64_exit(m, k, d, carry, e - 1 - max(1, reqBegin) - c * G, maybe_stop);
                     } else {
-                        x = insertion_chain<G>(T.g, m, k, d, carry, stop_bits, T.jacobi, T.dbg);
+                        x = insertion_chain<G>(m, k, d, carry);
                     }
                 }
                 const double pm = fmax(mx, prefix_max<G>(x));
@@ -753,7 +677,6 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     // tall reads are the latency-critical path of every refine round: issue ahead of the 16-lane fills
     // and score waves that share the SIMD (F.prio = 0 leaves the default priority)
     if (G == 64 && F.prio) __builtin_amdgcn_s_setprio(3);
-    if (G == 16 && F.prio16 > 0) __builtin_amdgcn_s_setprio(1);
     const int grp = threadIdx.x / G;
     const int t = blockIdx.x * (64 / G) + grp;
     const int lane = threadIdx.x & (G - 1);
@@ -819,9 +742,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     T.col1 = col + F.hcap;
     T.hcap = F.hcap;
     T.gcol = GC;
-    T.dbg = F.chainStats;
-    T.jacobi = F.jacobi;
-    T.chainExit = F.chainExit && !F.jacobi;
+    T.chainExit = F.chainExit;
     T.slackDiv = max(1, F.regrowSlackDiv);
     T.prNot = B.prNot;
     T.prThird = B.prThird;
@@ -959,12 +880,12 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     if (gc && G != 64) throw std::runtime_error("global column buffers need 64-lane groups");
     // two waves per SIMD: the register budget that leaves these kernels without spills (higher occupancy
     // was measured slower and needs a private segment, which the resource check in the Makefile forbids)
+    if (G != 16 && G != 64) throw std::runtime_error("fill groups are 16 or 64 lanes");
     const K k = gc        ? (K)k_fill_coop<64, 2, true>
                 : G == 16 ? (K)k_fill_coop<16, 2, false>
-                : G == 8  ? (K)k_fill_coop<8, 2, false>
                           : (K)k_fill_coop<64, 2, false>;
-    static bool attrSet[4] = {false, false, false, false};   // dynamic LDS beyond 64 KB must be enabled per kernel
-    const int ak = gc ? 2 : G == 8 ? 3 : (G == 64);
+    static bool attrSet[3] = {false, false, false};   // dynamic LDS beyond 64 KB must be enabled per kernel
+    const int ak = gc ? 2 : (G == 64);
     if (!attrSet[ak]) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attrSet[ak] = true;

@@ -873,7 +873,7 @@ void PoaSlice(PoaRunner& R, const std::vector<std::vector<const std::string*>>& 
         for (int z = 0; z < nz; ++z) {
             while (!done[z]) {
                 const std::string* s = reads[z0 + z][next[z]];
-                if (s == nullptr) {
+                if (s == nullptr || s->empty()) {   // a dropped or empty read is never added (key -1)
                     record(z, -1);
                 } else if (Z[z]->graph.NumReads() == 0) {
                     std::vector<int> path;

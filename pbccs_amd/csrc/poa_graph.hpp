@@ -81,6 +81,8 @@ public:
     // threadFirstRead (PoaGraphTraversals.cpp:194-225)
     void AddFirstRead(const std::string& seq, std::vector<int>* path)
     {
+        // callers never add an empty read (key -1); TagSpan(-1, ^) below would index mark[-1]
+        if (seq.empty()) throw std::invalid_argument("AddFirstRead: empty read");
         if (path) path->clear();
         int prev = kEnter, first = -1;
         for (char b : seq) {

@@ -154,7 +154,10 @@ def ccs_batch(chunks, settings=None, engine=None, max_poa_coverage=None):
     """Consensus.h's per-ZMW driver for many ZMWs in one native call (pbccs_ccs_batch): FilterReads,
     the GPU POA, TooShort, ExtractMappedRead and the GPU polish, with no Python between the stages.
     chunks: [{"snr", "reads": [{"seq", "flags"?}]}].  Returns per ZMW the polish result dict (as
-    polish_zmws) plus "draft"; add_read_results / zscores are indexed by POA key."""
+    polish_zmws) plus "draft"; add_read_results / zscores hold one entry per input subread, in the
+    chunk's read order: -1 / NaN for a read that never reached AddRead (dropped by FilterReads, not added
+    by the POA, rejected by ExtractMappedRead, past the maxPoaCov stop, or the ZMW ended earlier).
+    Raises on a draft longer than its buffer (PBCCS_ERANGE)."""
     import ctypes
     from . import ZMW_STATUS, default_engine
     from . import lib as L
@@ -172,7 +175,8 @@ def ccs_batch(chunks, settings=None, engine=None, max_poa_coverage=None):
         seqs = (ctypes.c_char_p * max(1, nr))(*enc)
         lens = (ctypes.c_int * max(1, nr))(*[len(e) for e in enc])
         flags = (ctypes.c_ubyte * max(1, nr))(*[int(r.get("flags", FULL_PASS)) for r in reads])
-        cap = 2 * max([len(e) for e in enc] + [0]) + 64
+        # a POA consensus never exceeds the bases of the reads it was built from
+        cap = sum(len(e) for e in enc) + 64
         cons, draft = ctypes.create_string_buffer(cap), ctypes.create_string_buffer(cap)
         qv = (ctypes.c_int * cap)()
         arr = (ctypes.c_int * max(1, nr))()
@@ -199,7 +203,7 @@ def ccs_batch(chunks, settings=None, engine=None, max_poa_coverage=None):
         res.append({"status": ZMW_STATUS[p.status], "status_code": p.status,
                     "consensus": cons.raw[:ln].decode() if ok else "", "qvs": list(qv[:ln]) if ok else [],
                     "draft": draft.raw[:max(0, outs[z].draft_len)].decode(),
-                    "add_read_results": list(arr[:nr]) if polished else [], "zscores": list(zs[:nr]) if polished else [],
+                    "add_read_results": list(arr[:nr]), "zscores": list(zs[:nr]), "polished": polished,
                     "zg": p.zg, "za": p.za, "predicted_accuracy": p.predicted_accuracy, "n_tested": p.n_tested,
                     "n_applied": p.n_applied, "n_passes": p.n_passes, "status_counts": list(p.status_counts)})
     return res

@@ -222,18 +222,43 @@ def test_native_ccs_batch_matches_python_driver(P):
         chunks.append({"snr": [10.0, 7.0, 5.0, 11.0],
                        "reads": [{"seq": s, "flags": int(rng.choice([3, 3, 3, 1, 2]))} for s in reads]})
     chunks.append({"snr": [9.0, 9.0, 9.0, 9.0], "reads": [{"seq": "ACGTA"}]})
-    native = driver.ccs_batch(chunks, engine=eng)
-    ins = driver.zmw_inputs_batch(chunks, engine=eng)
+    # zero-length subreads, first and later in the input: they count in FilterReads but the POA never adds them
+    chunks[0]["reads"].insert(0, {"seq": ""})
+    chunks[1]["reads"].insert(2, {"seq": "", "flags": 3})
+    for cov in (None, 3):
+        _check_native_ccs(chunks, cov, eng)
+
+
+def _check_native_ccs(chunks, cov, eng):
+    """pbccs_ccs_batch against the Python driver + polish_zmws, per-read outputs in subread order."""
+    import math
+    import pbccs_amd
+    from pbccs_amd import driver
+    native = driver.ccs_batch(chunks, engine=eng, max_poa_coverage=cov)
+    ins = driver.zmw_inputs_batch(chunks, max_poa_coverage=cov, engine=eng)
     pol = iter(pbccs_amd.polish_zmws([z for st, z in ins if st is None], engine=eng))
-    for (st, z), got in zip(ins, native):
+    for c, (st, z), got in zip(chunks, ins, native):
+        nr = len(c["reads"])
+        assert len(got["add_read_results"]) == nr and len(got["zscores"]) == nr
         if st is not None:
             assert got["status"] == st
+            assert got["add_read_results"] == [-1] * nr and all(math.isnan(v) for v in got["zscores"])
             continue
         exp = next(pol)
         assert got["draft"] == z["draft"]
-        for k in ("status", "consensus", "qvs", "n_tested", "n_applied", "n_passes", "status_counts",
-                  "add_read_results"):
+        for k in ("status", "consensus", "qvs", "n_tested", "n_applied", "n_passes", "status_counts"):
             assert got[k] == exp[k], k
+        # polish input position i is FilterReads' i-th read; map it back to the subread's input index
+        order = [next(j for j, x in enumerate(c["reads"]) if x is r)
+                 for r in driver.filter_reads(c["reads"], 10) if r is not None]
+        want_arr, want_z = [-1] * nr, [float("nan")] * nr
+        for i, (a, zz) in enumerate(zip(exp["add_read_results"], exp["zscores"])):
+            want_arr[order[i]], want_z[order[i]] = a, zz
+        assert got["add_read_results"] == want_arr
+        for a, b in zip(got["zscores"], want_z):
+            assert (math.isnan(a) and math.isnan(b)) or a == b
+        if cov is not None:
+            assert sum(1 for a in got["add_read_results"] if a >= 0) <= cov
     assert native[-1]["status"] == "NoSubreads"
 
 
