@@ -32,8 +32,13 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-TRAFFIC_PROFILE = "r2hP_traffic_fill.json"   # PMC HBM bytes of the roofline kernel (tools/gpu_traffic.sh)
+# PMC HBM bytes per launch of each fill kind (tools/gpu_traffic.sh -> tools/pmc_traffic.py); used only while
+# the kernel sources still hash to the digest the profile was taken at
+TRAFFIC_PROFILES = {"k_fill_tall": "r3_traffic_fill_tall.json", "k_fill": "r3_traffic_fill.json",
+                    "k_score": "r3_traffic_score.json"}
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
+FLOP_PER_CELL = 11             # fill cell 6 mul + 3 add + <= 1 div, + the column rescale
+CHAIN_STEP_CYCLES = 29.7       # one dependent insertion-chain step (tools/ubench/chain_step.hip)
 BEST_SLOTS = 5                 # measured best split of 2 kb batches: 5 slots divide the driver's 20 steps into 4 full waves (6 slots: 2868 vs 3357 ZMWs/s at --steps 20, the last wave half empty)
 SLOT_BYTES_PER_ZMW = 15 << 20  # measured band high-water per 2 kb / 10-pass ZMW in a slot (13.4 MB, exact regrow)
 HBM_MARGIN = 24 << 30          # device memory left to scratch, selection buffers and the runtime
@@ -157,6 +162,19 @@ def cpu_baseline(args):
                       f"on {threads} host threads, {dt:.1f} s wall"}
 
 
+def kernel_source_digest():
+    """sha256 (16 hex) of the HIP/C++ sources of the engine: a PMC traffic profile is valid for the build it was
+    taken on, and stale once any kernel source changes."""
+    import hashlib
+    d = os.path.join(ROOT, "pbccs_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".hpp", ".cpp", ".h")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def workload_kw(args):
     """synth.make_zmws keywords of the workload (SURVEY.md §8(d) configs #2-#4)."""
     if args.workload == "10kb":
@@ -213,9 +231,11 @@ def queue_workload(args, rank, world, eng, settings, seed0):
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     done = heartbeat(rank, t0)
+    qstats = {}
     try:
         if kw is None:
-            res = shard.polish_dynamic(zs, settings, eng, rank, world, chunk=max(1, args.zmws_per_step // 4))
+            res = shard.polish_dynamic(zs, settings, eng, rank, world, chunk=max(1, args.zmws_per_step // 4),
+                                       stats=qstats)
         else:
             res = pbccs_amd.polish_stream(zs, settings, eng)
     finally:
@@ -227,9 +247,9 @@ def queue_workload(args, rank, world, eng, settings, seed0):
     local_time = time.perf_counter() - t0
     job_time = max_over_ranks(local_time, world)
     if kw is None:   # rank 0 holds the whole cell's records; the count is the cell
-        return job_time, local_time, (res or []), desc, "strong", n
+        return job_time, local_time, (res or []), desc, "strong", n, qstats
     return job_time, local_time, res, desc + " (work queue; timed region includes the read upload)", "weak", \
-        n * world
+        n * world, None
 
 
 def max_over_ranks(t, world):
@@ -306,8 +326,9 @@ def main():
     if args.stage == "quiver":
         return quiver_stage(args, rank, world, eng, barrier, sync, seed0)
     if args.workload != "2kb":
-        job_time, local_time, res, workload, scaling, total = queue_workload(args, rank, world, eng, settings, seed0)
-        return report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total)
+        job_time, local_time, res, workload, scaling, total, qstats = queue_workload(args, rank, world, eng, settings,
+                                                                                     seed0)
+        return report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total, qstats)
 
     # ---- warmup (untimed): W steps, concurrently over the slots like the timed ones ------------------
     wb = [pbccs_amd.PreparedBatch(synth.make_zmws(args.zmws_per_step, args.length, args.passes,
@@ -554,7 +575,54 @@ def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
         dist.destroy_process_group()
 
 
-def report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total_zmws):
+def make_roofline(stats, local_time, workload):
+    """The dominant kernel (by device time) priced three ways, each labelled:
+    - per launch (the bench contract): algorithmic bytes per launch / the launch's average duration from HIP
+      events on its own stream.  With several workspace slots the slots' launches of one kind run at the same
+      time, so this duration is time-shared (`in_flight` = device time / wall time);
+    - on wall time: the kernel's algorithmic bytes over the whole timed region / the region's wall time;
+    - FP64 VALU: FLOP_PER_CELL x its DP cell-updates over the wall time, against the FP64 vector peak.
+    Neither roof binds: the fill is a serial insertion chain (one dependent DPP + mul + add + add step per row,
+    CHAIN_STEP_CYCLES), so its bound is latency; `binding` says so.  `traffic` = PMC HBM bytes per launch of
+    the same kernel from a committed profile, only while the kernel sources hash to the profile's digest."""
+    dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["device_ms"])
+    launches = max(1, dom["launches"])
+    avg_ms = dom["device_ms"] / launches
+    bytes_per_launch = dom["bytes"] / launches
+    achieved = (bytes_per_launch / (avg_ms / 1e3)) / 1e9 if avg_ms > 0 else 0.0
+    wall_gbs = dom["bytes"] / local_time / 1e9 if local_time > 0 else 0.0
+    fp64_tf = FLOP_PER_CELL * dom["cells"] / local_time / 1e12 if local_time > 0 else 0.0
+    traffic, traffic_src = None, None
+    digest = kernel_source_digest()
+    prof = TRAFFIC_PROFILES.get(dom_name)
+    tpath = os.path.join(ROOT, "profiles", prof) if prof else None
+    if tpath and os.path.exists(tpath):
+        t = json.load(open(tpath))
+        if t.get("bench_kernel") == dom_name and t.get("workload") == workload:
+            if t.get("source_digest") == digest:
+                traffic = t["traffic_bytes_per_launch"]
+                traffic_src = (f"profiles/{prof} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, "
+                               f"{t['dispatches_fetch_pass']} dispatches, sources {digest})")
+            else:
+                traffic_src = f"profiles/{prof} is stale: taken at sources {t.get('source_digest')}, built {digest}"
+    return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": dom_name, "avg_launch_ms": round(avg_ms, 4), "launches": dom["launches"],
+            "bytes_per_launch": bytes_per_launch, "cells_per_launch": dom["cells"] / launches,
+            "per_launch_note": "achieved/frac: algorithmic bytes per launch / HIP-event launch time on the "
+                               "kernel's stream; time-shared when in_flight > 1",
+            "in_flight": round(dom["device_ms"] / (local_time * 1e3), 3) if local_time > 0 else None,
+            "wall": {"achieved": round(wall_gbs, 3), "frac": round(wall_gbs / HBM_PEAK_GBS, 6), "unit": "GB/s",
+                     "note": "the kernel's algorithmic bytes over the timed region / its wall time"},
+            "fp64_valu": {"achieved": round(fp64_tf, 4), "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": round(fp64_tf / FP64_VALU_PEAK_TFLOPS, 6),
+                          "note": f"{FLOP_PER_CELL} FLOP per DP cell-update over the timed region's wall time"},
+            "binding": f"latency: the serial insertion chain, one dependent DPP + mul + add + add step per band "
+                       f"row (~{CHAIN_STEP_CYCLES} cycles, tools/ubench/chain_step.hip); neither HBM nor FP64 VALU",
+            "source_digest": digest}
+
+
+def report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total_zmws, qstats=None):
     import torch.distributed as dist
     stats = eng.kernel_stats(reset=True)
     counters = eng.counters(reset=True)
@@ -572,30 +640,11 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         gcups = float(t.item()) / job_time / 1e9
 
-    # dominant kernel (by device time) -> roofline: algorithmic band bytes / its device time
-    dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["device_ms"])
-    launches = max(1, dom["launches"])
-    avg_ms = dom["device_ms"] / launches
-    bytes_per_launch = dom["bytes"] / launches
-    achieved = (bytes_per_launch / (avg_ms / 1e3)) / 1e9 if avg_ms > 0 else 0.0
-    # HBM traffic per launch: PMC counters cannot be read from inside this process, so `traffic` comes from
-    # the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same default command
-    # (tools/gpu_traffic.sh -> tools/pmc_traffic.py, gfx950 correction 2*FETCH_SIZE + WRITE_SIZE) when
-    # they were taken on this kernel family and workload; null otherwise.
-    traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE)
-    if os.path.exists(tpath):
-        t = json.load(open(tpath))
-        if t.get("kernel") == dom_name and t.get("workload") == workload:
-            traffic = t["traffic_bytes_per_launch"]
-            traffic_src = f"profiles/{TRAFFIC_PROFILE} (rocprofv3 --pmc, {t['dispatches_fetch_pass']} dispatches)"
-    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": dom_name, "avg_launch_ms": round(avg_ms, 4), "launches": dom["launches"],
-                "bytes_per_launch": bytes_per_launch, "cells_per_launch": dom["cells"] / launches}
-
+    roofline = make_roofline(stats, local_time, workload)
     out = {
         "metric": "CCS ZMWs/sec (and GCUPS) at 1/2/4/8 MI355X vs host-CPU ccs",
+        "stage": "polish: Consensus.h:436-552 from the POA draft on (AddRead gates, RefineConsensus, "
+                 "ConsensusQVs); FilterReads and the POA are the --stage ccs line",
         "value": round(value, 3),
         "unit": "ZMWs/s",
         "n_gpus": world,
@@ -628,6 +677,8 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
                            ("band_top_bytes", "band_region_bytes", "band_used_bytes", "pool_mapped_bytes")},
         "oom_retries": counters["oom_retries"],
     }
+    if qstats:   # configs[4]: records stream to rank 0 per chunk; tail_ms = rank 0's wait after its last chunk
+        out["queue"] = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in qstats.items()}
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(args)
         out["vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)

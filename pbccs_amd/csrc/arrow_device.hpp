@@ -104,7 +104,7 @@ struct DevBatch {
     unsigned long long* stats;
 };
 
-enum StatKind : int { kStatFill = 0, kStatSuffix = 1, kStatScore = 2 };
+enum StatKind : int { kStatFill = 0, kStatSuffix = 1, kStatScore = 2, kStatFillTall = 3 };   // stats[] has 16 slots
 
 struct TaskStat {
     unsigned long long cells = 0;

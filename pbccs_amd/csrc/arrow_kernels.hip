@@ -158,8 +158,8 @@ __global__ void __launch_bounds__(64) k_fill(DevBatch B, FillScratch F, const in
         tr[7] = ub;
     }
     if (B.stats) {   // algorithmic: 8 B per stored cell + 16 B per column per fill pass
-        atomicAdd(&B.stats[2 * kStatFill], cells);
-        atomicAdd(&B.stats[2 * kStatFill + 1], 8ull * cells + 16ull * passes * (unsigned long long)(J + 1));
+        atomicAdd(&B.stats[2 * kStatFillTall], cells);   // the lane-serial fallback takes only very tall reads
+        atomicAdd(&B.stats[2 * kStatFillTall + 1], 8ull * cells + 16ull * passes * (unsigned long long)(J + 1));
     }
 }
 

@@ -22,8 +22,8 @@ namespace pbccs {
         if (e_ != hipSuccess) throw DeviceError(hipGetErrorString(e_));      \
     } while (0)
 
-const char* const kKernelNames[kKernelKinds] = {"k_fill", "k_suffix", "k_enumerate", "k_score",
-                                                 "k_reduce", "k_qv", "k_best_subset", "k_compact"};
+const char* const kKernelNames[kKernelKinds] = {"k_fill", "k_suffix", "k_enumerate", "k_score",  "k_reduce",
+                                                 "k_qv",   "k_best_subset", "k_compact", "k_fill_tall"};
 
 namespace {
 
@@ -311,6 +311,8 @@ void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
         PBCCS_HIP(hipStreamSynchronize(stream_));
         stats_[kKFill].cells += (double)h[2 * kStatFill];
         stats_[kKFill].bytes += (double)h[2 * kStatFill + 1];
+        stats_[kKFillTall].cells += (double)h[2 * kStatFillTall];
+        stats_[kKFillTall].bytes += (double)h[2 * kStatFillTall + 1];
         stats_[kKScore].cells += (double)h[2 * kStatScore];
         stats_[kKScore].bytes += (double)h[2 * kStatScore + 1];
         static const bool trace = std::getenv("PBCCS_ROUND_TRACE") != nullptr;
@@ -816,7 +818,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             const int* lp = dList_.ptr + off;
             const hipStream_t st = p <= 1 ? stream_ : p == 2 ? stream2_ : stream3_;
             if (p == 0) Timed(kKFill, [&] { launch_fill_lane(B, F, lp, n, st); }, st);
-            else Timed(kKFill, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
+            else Timed(p == 1 ? kKFill : kKFillTall, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
             PBCCS_HIP(hipGetLastError());
             counters_.fillLaunches += 1;
             off += n;
@@ -958,7 +960,7 @@ void ArrowBatch::FillReadsSerial(const std::vector<int>& readsIn)
             }
             upload(dList_, chunk, stream_);
             const DevBatch B = View();
-            Timed(kKFill, [&] { launch_fill(B, F, dList_.ptr, (int)n, stream_); });
+            Timed(kKFillTall, [&] { launch_fill(B, F, dList_.ptr, (int)n, stream_); });
             PBCCS_HIP(hipGetLastError());
             counters_.fillLaunches += 1;
             std::vector<int> st, fl, ua, ub;

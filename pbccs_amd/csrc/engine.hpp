@@ -134,7 +134,12 @@ struct Counters {   // work counters for the roofline report (bench.py)
     long long bandTopBytes = 0, bandRegionBytes = 0, bandUsedBytes = 0;
 };
 
-enum KernelKind { kKFill = 0, kKSuffix, kKEnumerate, kKScore, kKReduce, kKQv, kKSelect, kKCompact, kKernelKinds };
+// kKFill: the 16-lane (and opt-in lane) fills of typical bands; kKFillTall: the 64-lane and lane-serial fills of
+// tall bands (launched on their own streams), reported apart so each kind's launches never overlap each other
+// within one workspace slot
+enum KernelKind {
+    kKFill = 0, kKSuffix, kKEnumerate, kKScore, kKReduce, kKQv, kKSelect, kKCompact, kKFillTall, kKernelKinds
+};
 extern const char* const kKernelNames[kKernelKinds];
 
 struct KernelStat {

@@ -855,8 +855,9 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
             F.usedB[r] = (int)ub;
             B.rStatus[r] = (mism > kAlphaBetaTol) ? kFillMismatch : kFillOk;
             if (B.stats) {   // algorithmic: 8 B per stored cell + 16 B per column per fill pass
-                atomicAdd(&B.stats[2 * kStatFill], cells);
-                atomicAdd(&B.stats[2 * kStatFill + 1], 8ull * cells + 16ull * passes * (unsigned long long)(J + 1));
+                constexpr int kind = G == 64 ? kStatFillTall : kStatFill;
+                atomicAdd(&B.stats[2 * kind], cells);
+                atomicAdd(&B.stats[2 * kind + 1], 8ull * cells + 16ull * passes * (unsigned long long)(J + 1));
                 atomicAdd(&B.stats[G == 64 ? 9 : 8], cells);   // per path (diagnostics: VALU per cell)
             }
         }

@@ -1,8 +1,9 @@
 """Multi-GPU ccs polish: ZMWs shard across ranks (one process per GPU), results gather in input order.
 
 ZMWs are independent, so the data path has no collective: each rank polishes its own
-shard on its own GPU, and only the finished per-ZMW records travel, once, to rank 0, which reassembles
-them in input order -- the ordering contract of pbccs' writer FIFO (include/pacbio/ccs/WorkQueue.h:128-167).
+shard on its own GPU, and only the finished per-ZMW records travel to rank 0, which reassembles them in
+input order -- the ordering contract of pbccs' writer FIFO (include/pacbio/ccs/WorkQueue.h:128-167).  The
+dynamic queue streams them chunk by chunk as they finish; the static plan gathers once.
 The shard assignment is a deterministic cost-balanced partition (longest-processing-time first over an
 estimate of each ZMW's DP work), so every rank computes the same plan without communicating.
 """
@@ -61,12 +62,20 @@ def dynamic_chunks(zmws, chunk):
 
 
 def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chunk=256, polish_fn=None, store=None,
-                   group=None):
+                   group=None, stats=None):
     """Polish `zmws` across ranks through a dynamic pull queue: every rank takes the next
     chunk index from one shared counter -- an atomic fetch-add on the rank-0 key-value store, host-side, not a
     device collective -- until the queue is empty, so a rank that drew slow ZMWs (tall bands, long templates)
-    simply pulls fewer chunks.  Rank 0 returns every ZMW's result in input order (one ordered gather, as
-    WorkQueue.h:128-167); the other ranks return None."""
+    simply pulls fewer chunks.
+
+    Results stream to rank 0 as chunks finish (the ordered FIFO of WorkQueue.h:128-167 fed as workers
+    complete): a rank > 0 puts each finished chunk's records under its own key on the same store; rank 0 takes
+    whatever has arrived between its own chunks, and once the queue is empty only the chunks still running
+    elsewhere are left to wait for.  Nothing is gathered in one piece at the end.  Rank 0 returns every ZMW's
+    result in input order; the other ranks return None.  `stats` (a dict, optional) receives the queue's
+    counters on rank 0: chunks per rank and `tail_ms`, the time from rank 0's last chunk to the last record."""
+    import pickle
+    import time
     import torch.distributed as dist
     if rank is None:
         rank = dist.get_rank() if dist.is_initialized() else 0
@@ -82,19 +91,57 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
     key = f"pbccs_queue_{_queue_calls[0]}"
     if world > 1 and store is None:
         store = dist.distributed_c10d._get_default_store()
-    mine, local = [], []
+    out = [None] * len(zmws) if rank == 0 else None
+    mine = []          # chunks this rank polished
+    pending = set()    # rank 0: chunks another rank took, records not yet collected
+    taken = [0] * world
+
+    def collect(c, block):
+        k = f"{key}/done/{c}"
+        if not block and not store.check([k]):
+            return False
+        who, recs = pickle.loads(store.get(k))
+        store.delete_key(k)
+        taken[who] += 1
+        for i, rec in zip(chunks[c], recs):
+            out[i] = rec
+        return True
+
     serial = 0
+    high = 0           # rank 0: chunk indices below `high` were handed out
     while True:
         if world > 1:
             c = store.add(key, 1) - 1
         else:
             c, serial = serial, serial + 1
+        if rank == 0:
+            pending.update(range(high, min(c, len(chunks))))   # handed to other ranks since our last pull
+            high = max(high, c + 1)
+            for p in sorted(pending):
+                if collect(p, block=False):
+                    pending.discard(p)
         if c >= len(chunks):
             break
-        idx = chunks[c]
-        local.extend(polish_fn([zmws[i] for i in idx]))
-        mine.extend(idx)
-    return gather_in_order(local, mine, len(zmws), rank, world, group)
+        recs = polish_fn([zmws[i] for i in chunks[c]])
+        mine.append(c)
+        if rank == 0:
+            taken[0] += 1
+            for i, rec in zip(chunks[c], recs):
+                out[i] = rec
+        else:
+            store.set(f"{key}/done/{c}", pickle.dumps((rank, recs)))
+    if rank != 0:
+        return None
+    t0 = time.perf_counter()
+    pending.update(c for c in range(high, len(chunks)) if c not in mine)
+    for p in sorted(pending):
+        collect(p, block=True)   # store.get waits for the key
+    if stats is not None:
+        stats.update({"chunks": len(chunks), "chunks_by_rank": taken, "tail_ms": (time.perf_counter() - t0) * 1e3})
+    missing = [i for i, rec in enumerate(out) if rec is None]
+    if missing:
+        raise RuntimeError(f"ZMWs missing after the queue drained: {missing[:8]}")
+    return out
 
 
 def polish_sharded(zmws, settings=None, engine=None, rank=None, world=None, polish_fn=None, group=None):

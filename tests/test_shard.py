@@ -39,14 +39,18 @@ def _stand_in(rank, slow_rank=None):
     return polish
 
 
-def _worker(rank, world, port, zmws, out_q, use_gpu, mode="static"):
+def _worker(rank, world, port, zmws, out_q, use_gpu, mode="static", chunk=2):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         if mode == "dynamic":
-            res = shard.polish_dynamic(zmws, chunk=2, polish_fn=None if use_gpu else _stand_in(rank, slow_rank=1))
+            st = {}
+            res = shard.polish_dynamic(zmws, chunk=chunk, polish_fn=None if use_gpu else _stand_in(rank, slow_rank=1),
+                                       stats=st)
+            if rank == 0:
+                res = (res, st)
         elif use_gpu:
             res = shard.polish_sharded(zmws)
         else:
@@ -57,14 +61,14 @@ def _worker(rank, world, port, zmws, out_q, use_gpu, mode="static"):
         dist.destroy_process_group()
 
 
-def _run(world, zmws, use_gpu=False, mode="static"):
+def _run(world, zmws, use_gpu=False, mode="static", chunk=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, zmws, q, use_gpu, mode)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, zmws, q, use_gpu, mode, chunk)) for r in range(world)]
     for p in procs:
         p.start()
-    res = q.get(timeout=240)
+    res = q.get(timeout=600)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -102,10 +106,12 @@ def test_gloo_world2_dynamic_queue_balances_and_keeps_order():
     """Rank 1 is slow (its stand-in sleeps per ZMW): through the pull queue rank 0 takes more chunks, and
     the gathered records still come back in input order."""
     zmws = _toy_zmws(24)
-    res = _run(2, zmws, mode="dynamic")
+    res, st = _run(2, zmws, mode="dynamic")
     assert [r["draft"] for r in res] == [z["draft"][::-1] for z in zmws]
     by_rank = [sum(1 for r in res if r["rank"] == k) for k in (0, 1)]
     assert by_rank[1] >= 2 and by_rank[0] > by_rank[1], by_rank
+    # records streamed per chunk: rank 0 saw every chunk, the other rank's through the store
+    assert st["chunks"] == 12 and sum(st["chunks_by_rank"]) == 12 and st["chunks_by_rank"][1] >= 1
 
 
 @pytest.mark.gpu
@@ -113,7 +119,7 @@ def test_two_ranks_dynamic_queue_on_one_gpu_match_unsharded():
     import pbccs_amd
     from pbccs_amd import synth
     zmws = synth.make_zmws(8, 300, 5, seed=809)
-    res = _run(2, zmws, use_gpu=True, mode="dynamic")
+    res, _ = _run(2, zmws, use_gpu=True, mode="dynamic")
     ref = pbccs_amd.polish_zmws(zmws)
     for a, b in zip(res, ref):
         assert (a["consensus"], a["n_tested"], a["n_applied"], a["status"]) == \
@@ -130,3 +136,60 @@ def test_two_ranks_on_one_gpu_match_unsharded():
     for a, b in zip(res, ref):
         assert (a["consensus"], a["n_tested"], a["n_applied"], a["status"]) == \
                (b["consensus"], b["n_tested"], b["n_applied"], b["status"])
+
+
+@pytest.mark.gpu
+def test_smrtcell_mix_two_ranks_dynamic_queue_match_oracle_and_fixtures():
+    """configs[4] reduced: an SMRT-cell mix -- 12 ZMWs of 2 kb x 10 passes, the two 10 kb x 8-pass ZMWs of
+    tests/golden/polish_10kb.json and the three configs[3] ZMWs of polish_mixed_long.json (15.2 kb x 21 passes,
+    0.7 kb x 3, 4.8 kb x 14) -- shuffled, through shard.polish_dynamic on two ranks sharing cuda:0 (records
+    streamed to rank 0 per chunk).  Every gathered record is checked against the oracle (2 kb) or the
+    committed oracle fixtures (10 kb, mixed), not only against an unsharded run."""
+    import json
+    import random
+    import sys
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    from pbccs_amd import synth
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, gold)
+    from make_polish_fixtures import digest, mixed_long_zmws
+    short = synth.make_zmws(12, 2000, 10, seed=4404)
+    fx10 = json.load(open(os.path.join(gold, "polish_10kb.json")))["zmws"]
+    fxm = json.load(open(os.path.join(gold, "polish_mixed_long.json")))["zmws"]
+    long10, mixed = synth.make_zmws(2, 10000, 8, seed=82), mixed_long_zmws()
+    cell = [("oracle", z, None) for z in short] + [("fx", z, e) for z, e in zip(long10 + mixed, fx10 + fxm)]
+    for kind, z, e in cell:
+        assert kind == "oracle" or digest(z) == e["digest"]
+    random.Random(4).shuffle(cell)
+    zmws = [z for _, z, _ in cell]
+    (res, st) = _run(2, zmws, use_gpu=True, mode="dynamic", chunk=2)
+    assert len(res) == len(cell) and sum(st["chunks_by_rank"]) == st["chunks"] and min(st["chunks_by_rank"]) >= 1
+    O.lib()
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        orc = list(ex.map(lambda z: O.polish_zmw(z["draft"], z["reads"], z["snr"]),
+                          [z for k, z, _ in cell if k == "oracle"]))
+    it = iter(orc)
+    for (kind, z, e), r in zip(cell, res):
+        if kind == "oracle":
+            o = next(it)
+            assert r["add_read_results"] == o["add_read_results"]
+            assert (r["n_tested"], r["n_applied"]) == (o["n_tested"], o["n_applied"])
+            if o["converged"]:
+                assert r["consensus"] == o["template"]
+                assert max(abs(a - b) for a, b in zip(r["qvs"], o["qvs"])) <= 1
+            continue
+        assert r["add_read_results"] == e["add_read_results"]
+        stt = e["add_read_results"]
+        if sum(1 for s in stt if s == 0) < 3:          # Consensus.h:473-490 gates before the polish
+            assert r["status"] == "TooFewPasses"
+            continue
+        if sum(1 for s in stt if s != 0) / len(stt) > 0.34:
+            assert r["status"] == "TooManyUnusable"
+            continue
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        if e["converged"]:
+            assert r["consensus"] == e["consensus"]
+            got = [min(max(q, 0), 93) for q in r["qvs"]]
+            exp = [ord(c) - 33 for c in e["qvs"]]
+            assert len(got) == len(exp) and max(abs(a - b) for a, b in zip(got, exp)) <= 1

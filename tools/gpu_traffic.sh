@@ -11,7 +11,8 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o pmc -- py
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/write -o pmc -- python3 -u bench.py $ARGS > $OUT/write.json 2> $OUT/write.err || { echo "write pass failed"; tail -5 $OUT/write.err; exit 1; }
 F=$(find $OUT/fetch -name "*counter_collection.csv" | head -1)
 W=$(find $OUT/write -name "*counter_collection.csv" | head -1)
-python3 tools/pmc_traffic.py "$F" "$W" $OUT/fetch.json $OUT/traffic_fill.json k_fill > /dev/null
-python3 tools/pmc_traffic.py "$F" "$W" $OUT/fetch.json $OUT/traffic_score.json k_score > /dev/null
-cat $OUT/traffic_fill.json
+for k in k_fill_tall k_fill k_score; do
+  python3 tools/pmc_traffic.py "$F" "$W" $OUT/fetch.json $OUT/traffic_${k#k_}.json $k > /dev/null || echo "no $k dispatches"
+done
+cat $OUT/traffic_fill_tall.json
 gzip -f "$F" "$W"
