@@ -273,7 +273,7 @@ def test_native_ccs_batch_pipelined_chunks(P):
     chunks.insert(4, {"snr": [9.0, 9.0, 9.0, 9.0], "reads": [{"seq": "ACG"}]})
     one = driver.ccs_batch(chunks, engine=eng)
     many = driver.ccs_batch(chunks, ConsensusSettings(zmws_per_batch=3), engine=eng)
-    assert many == one
+    assert json.dumps(many) == json.dumps(one)   # NaN z-scores (reads never added) compare equal as text
     assert one[4]["status"] == "NoSubreads"
 
 
