@@ -81,6 +81,7 @@ struct DevBatch {
     const long long* rValA;      // alpha value region offset in valPool
     const long long* rValB;      // beta value region offset in valPool
     const long long* rValCap;    // capacity (values) of each region
+    const int* rCkpt;            // checkpoint interval K of the read's bands (0: every column's values stored)
     const char* seqPool;
     // column slots
     int2* aRange;
@@ -110,6 +111,17 @@ struct TaskStat {
     unsigned long long cells = 0;
     unsigned long long bytes = 0;
 };
+
+// ---------------------------------------------------------------------------------------------
+// Checkpointed bands.  A read with checkpoint interval K > 0 keeps every column's range,
+// offset and log-scale, but the values of only these columns; the scorer replays the others from the
+// nearest kept column (a column depends only on the scaled column before it and on its own range, so the
+// replay is bit-identical).  Alpha keeps j % K == 0 and the last kCkptTail + 1 columns (ExtendAlpha to
+// the end reads them), beta j % K == 0, the first kCkptTail + 1 columns (ExtendBeta) and column J.
+// ---------------------------------------------------------------------------------------------
+constexpr int kCkptTail = 6;
+__host__ __device__ inline bool ckpt_col_a(int j, int J, int K) { return j % K == 0 || j >= J - kCkptTail; }
+__host__ __device__ inline bool ckpt_col_b(int j, int J, int K) { return j % K == 0 || j <= kCkptTail || j == J; }
 
 // ---------------------------------------------------------------------------------------------
 // Template views: WrappedTemplateParameterPair over a TemplateParameterPair with an optional

@@ -13,6 +13,7 @@
 //   k_qv          one lane per template position: ConsensusQVs (Consensus-inl.hpp:274-295).
 #include "arrow_device.hpp"
 #include "arrow_kernels.hpp"
+#include "coop_chain.hpp"
 
 #include <climits>
 
@@ -1005,9 +1006,10 @@ __global__ void __launch_bounds__(256) PBCCS_SCORE_OCC k_score(DevBatch B, Score
     const long long local = waveLive ? wave - W.waveStart[k] : 0;
     const int rr = W.readLo + (int)(local / chunks);
     const int mc = (int)(local % chunks) * 64 + lane;
-    const bool valid = waveLive && mc < Mc;
-    const int m = (valid && W.sel) ? (int)(W.sel[W.selBase[k] + mc] - W.mutStart[k]) : mc;
     const int r = waveLive ? B.zReadBegin[z] + rr : 0;
+    // checkpointed reads are k_score_ckpt's (their non-checkpoint columns hold no values)
+    const bool valid = waveLive && mc < Mc && !(B.rCkpt && B.rCkpt[r] != 0);
+    const int m = (valid && W.sel) ? (int)(W.sel[W.selBase[k] + mc] - W.mutStart[k]) : mc;
 
     // classify this lane's task
     int code = 0;
@@ -1133,6 +1135,300 @@ __global__ void __launch_bounds__(64) k_score_edge(DevBatch B, ScoreWork W, Scor
     if (B.stats) {
         atomicAdd(&B.stats[2 * kStatScore], st.cells);
         atomicAdd(&B.stats[2 * kStatScore + 1], st.bytes);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_score_ckpt: ScoreMutation for reads with checkpointed bands.  Such a read keeps the
+// values of every K-th column only (ckpt_col_a / ckpt_col_b); a wave replays the columns its mutations
+// read -- alpha forward from the kept column at or before them, beta backward from the kept column at or
+// after them -- into its slot of C.slots, with the 64-lane insertion chain of the fill and each column's
+// stored row range, so every replayed value is the fill's value bit for bit (a column depends only on the
+// scaled column before it, the template, the read and its own range).  Then each lane scores its mutation
+// with score_middle against the replayed columns, exactly as k_score does against stored ones.
+// Persistent grid: each wave owns one slot and pulls 64-mutation chunks (tasks) from C.counter until none
+// are left.  Lanes are scored block by block (alpha column / K), so a sparse chunk of a later scoring phase
+// replays only the blocks it touches.  A block whose columns do not fit the slot is skipped and its size
+// reported (C.need): the host grows the slots and reruns the launch.
+// ------------------------------------------------------------------------------------------------
+constexpr int kCkptCols = 3 * kCkptMaxK + 8;   // alpha <= K columns, beta <= 2K + 4 per block
+
+// One replayed column's inputs that are uniform over the wave.
+struct ReplayRead {
+    const char* rd;   // read bases
+    const char* T;    // strand template
+    int I, J, L, start;
+    const double* ctx;
+    double prNot, prThird;
+    __device__ __forceinline__ int TB(int idx) const   // TBase of fill_coop (nibble code of window base idx)
+    {
+        const int g = start + idx;
+        return (idx <= J && g < L) ? coop::base_code(T[g]) : coop::kBaseOther;
+    }
+    __device__ __forceinline__ int TC(int idx) const   // TCtx of fill_coop
+    {
+        return (start + idx + 1 < L) ? coop::ctx_code(TB(idx), TB(idx + 1)) : kCtxZero;
+    }
+    __device__ __forceinline__ int RB(int i) const { return (i >= 0 && i < I) ? coop::base_code(rd[i]) : 15; }
+};
+
+// the insertion chain over the first n (>= 1) rows of a 64-row chunk; lanes >= n are left unfinished
+__device__ __forceinline__ double replay_chain(double m, double k, double d, double carry, int n)
+{
+    double x = 0.0, up = carry;
+#pragma unroll
+    for (int q = 0; q < 64; q += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            up = coop::shift_up<64>(x, up);
+            x = (m + up * k) + d;
+        }
+        if (q + 8 >= n) break;
+    }
+    return x;
+}
+
+__device__ __forceinline__ double lane63(double x)   // the chunk-to-chunk carry (wave-uniform)
+{
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), 63),
+                            __builtin_amdgcn_readlane(__double2loint(x), 63));
+}
+
+__device__ __forceinline__ double wave_max_d(double x)
+{
+    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o, 64));
+    return x;
+}
+
+// Alpha column j (j >= 1) over its stored rows [b, e) from the scaled column j-1 (rows [pb, pe) at prev),
+// scaled into cur (top-down): coop_alpha's column step (fill_coop.hip) without the band-end logic.
+__device__ void replay_alpha(const ReplayRead& X, int j, const double* prev, int pb, int pe, double* cur, int b, int e)
+{
+    const int lane = threadIdx.x & 63;
+    const int curBase = X.TB(j - 1), nextBase = X.TB(j);
+    const double* cp = X.ctx + X.TC(j - 1) * kCtxStride;
+    const double* pp = X.ctx + (j >= 2 ? X.TC(j - 2) : kCtxZero) * kCtxStride;
+    const double pMatch = pp[kM], pDel = pp[kD], cBranch = cp[kB], cStick3 = cp[kS3];
+    double carry = 0.0, mx = 0.0;
+    for (int i0 = b; i0 < e; i0 += 64) {
+        const int i = i0 + lane;
+        const int rb = (i >= 1 && i <= X.I) ? X.RB(i - 1) : 15;
+        const double left = (i >= pb && i < pe) ? prev[i - pb] : 0.0;
+        const double diag = (i - 1 >= pb && i - 1 < pe) ? prev[i - 1 - pb] : 0.0;
+        const double mpe = diag * (rb == curBase ? X.prNot : X.prThird);
+        const double m = (i == 1 && j == 1) ? mpe : ((i != 1 && j != 1) ? mpe * pMatch : 0.0);
+        const double k = (i > 1) ? (rb == nextBase ? cBranch : cStick3) : 0.0;
+        const double d = (j > 1) ? left * pDel : 0.0;
+        const double x = replay_chain(m, k, d, carry, e - i0);
+        if (i < e) {
+            cur[i - b] = x;
+            mx = fmax(mx, x);
+        }
+        carry = lane63(x);
+    }
+    mx = wave_max_d(mx);
+    if (mx != 0.0 && mx != 1.0)   // ScaledMatrix::FinishEditingColumn
+        for (int i = b + lane; i < e; i += 64) cur[i - b] = cur[i - b] / mx;
+}
+
+// Beta column j (0 < j < J) over its stored rows [b, e), bottom-up, from the scaled column j+1 (rows [pb, pe)
+// at nxt, stored bottom-up), scaled into cur (bottom-up): coop_beta's column step.
+__device__ void replay_beta(const ReplayRead& X, int j, const double* nxt, int pb, int pe, double* cur, int b, int e)
+{
+    const int lane = threadIdx.x & 63;
+    const int nextBase = X.TB(j);
+    const double* cp = X.ctx + X.TC(j - 1) * kCtxStride;
+    const double cMatch = cp[kM], cDel = cp[kD], cBranch = cp[kB], cStick3 = cp[kS3];
+    const int I = X.I, J = X.J;
+    double carry = 0.0, mx = 0.0;
+    for (int o0 = 0; o0 < e - b; o0 += 64) {
+        const int off = o0 + lane;
+        const int i = e - 1 - off;
+        const int nb = X.RB(i);
+        const double left = (i >= pb && i < pe) ? nxt[pe - 1 - i] : 0.0;
+        const double diag = (i + 1 >= pb && i + 1 < pe) ? nxt[pe - 2 - i] : 0.0;
+        const bool same = nb == nextBase;
+        const double mpe = diag * (same ? X.prNot : X.prThird);
+        const double m = (i < I - 1) ? mpe * cMatch : ((i == I - 1 && j == J - 1) ? mpe : 0.0);
+        const double k = (i < I - 1 && i > 0) ? (same ? cBranch : cStick3) : 0.0;
+        const double d = (j < J - 1 && j > 0) ? left * cDel : 0.0;
+        const double x = replay_chain(m, k, d, carry, e - b - o0);
+        if (i >= b) {
+            cur[off] = x;
+            mx = fmax(mx, x);
+        }
+        carry = lane63(x);
+    }
+    mx = wave_max_d(mx);
+    if (mx != 0.0 && mx != 1.0)
+        for (int off = lane; off < e - b; off += 64) cur[off] = cur[off] / mx;
+}
+
+__global__ void __launch_bounds__(64) k_score_ckpt(DevBatch B, ScoreWork W, CkptWork C)
+{
+    __shared__ int sOff[kCkptCols];
+    const int lane = threadIdx.x;
+    double* slot = C.slots + (long long)blockIdx.x * C.slotCap;
+    for (;;) {
+        unsigned long long tt = 0;
+        if (lane == 0) tt = atomicAdd(C.counter, 1ull);
+        const unsigned hi32 = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(tt >> 32));
+        const unsigned lo32 = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)tt);
+        const long long t = (long long)(((unsigned long long)hi32 << 32) | lo32);
+        if (t >= C.nTasks) break;   // every wave leaves once the task list is drained
+        int lo = 0, hi = C.nPairs;   // pair of task t (wave-uniform binary search)
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (C.taskStart[mid] <= t) lo = mid; else hi = mid;
+        }
+        const int k = C.pairs[lo].x, rr = C.pairs[lo].y;
+        const int chunk = (int)(t - C.taskStart[lo]);
+        const int z = W.zmw[k];
+        const int M = W.nMut[k];
+        const int Mc = W.sel ? W.nSel[k] : M;
+        const int mc = chunk * 64 + lane;
+        const bool valid = mc < Mc;
+        const int m = (valid && W.sel) ? (int)(W.sel[W.selBase[k] + mc] - W.mutStart[k]) : mc;
+        const int r = B.zReadBegin[z] + rr;
+        int code = 0;
+        bool scored = false;
+        if (valid) {
+            code = W.codes[W.mutBase[k] + m];
+            const int type = mut_type(code), pos = mut_pos(code);
+            const int me = (type == kIns) ? pos : pos + 1;
+            scored = B.rActive[r] && read_scores(B.rTs[r], B.rTe[r], type, pos, me);
+        }
+        ScoreCtx S;
+        Oriented o;
+        o.os = o.oe = o.ld = o.type = 0;
+        bool middle = false;
+        int sc = 0, bc = 0;
+        MidGeom g;
+        g.b0 = g.e0 = g.b1 = g.e1 = g.lb = g.le = 0;
+        if (scored) {
+            o = setup_score(B, r, code, S);
+            const int J = S.Jorig;
+            middle = !(o.os < 3) && !(o.oe > J - 2);
+            if (middle) {
+                sc = (o.type == kDel) ? o.os - 1 : o.os;
+                bc = 1 + o.oe;
+                g = middle_geometry(S.a, S.b, sc, bc);
+            } else {   // ends of the window: k_score_edge (the kept tail columns hold their values)
+                const int es = atomicAdd(W.edgeCount, 1);
+                if (es < W.edgeCap) {
+                    W.edgeList[3 * es + 0] = k;
+                    W.edgeList[3 * es + 1] = rr;
+                    W.edgeList[3 * es + 2] = m;
+                }
+            }
+        }
+        if (valid && !scored) W.delta[W.deltaBase[k] + (long long)rr * M + m] = 0.0;
+        // replay + score, one alpha block (column / K) at a time
+        const int K = B.rCkpt[r];
+        const int J = B.rTe[r] - B.rTs[r];
+        const long long cbase = B.rColBase[r];
+        const int2* aR = B.aRange + cbase;
+        const int2* bR = B.bRange + cbase;
+        const int* aO = B.aOff + cbase;
+        const int* bO = B.bOff + cbase;
+        const double* aV = B.valPool + B.rValA[r];
+        const double* bV = B.valPool + B.rValB[r];
+        ReplayRead X;
+        {
+            const TplView tv = window_view(B, r);
+            X.rd = B.seqPool + B.rSeqOff[r];
+            X.T = tv.T;
+            X.I = B.rLen[r];
+            X.J = J;
+            X.L = tv.L;
+            X.start = tv.start;
+            X.ctx = B.zCtx + (long long)z * 9 * kCtxStride;
+            X.prNot = B.prNot;
+            X.prThird = B.prThird;
+        }
+        bool pending = middle;
+        TaskStat st;
+        while (__ballot(pending) != 0) {
+            const int ja = sc - 1;
+            const int q = wave_min(pending ? ja / K : INT_MAX);
+            const bool mine = pending && ja / K == q;
+            const int aHi = wave_max(mine ? ja : -1);
+            const int jbLo = wave_min(mine ? bc : INT_MAX), jbHi = wave_max(mine ? bc : -1);
+            const int ckA = q * K;                 // kept (j % K == 0)
+            int ckB = jbHi;
+            while (!ckpt_col_b(ckB, J, K)) ++ckB;   // <= the next multiple of K, or J
+            const int nA = aHi - ckA + 1, nB = ckB - jbLo + 1;
+            // slot layout: alpha columns ckA..aHi, then beta columns ckB down to jbLo, each compact
+            long long need = 0;
+            if (nA + nB <= kCkptCols) {
+                long long hsum = 0;
+                for (int c = lane; c < nA + nB; c += 64) {
+                    const int2 rg = c < nA ? aR[ckA + c] : bR[ckB - (c - nA)];
+                    hsum += max(0, rg.y - rg.x);
+                }
+                for (int w = 32; w > 0; w >>= 1) hsum += __shfl_xor(hsum, w, 64);
+                need = hsum;
+            }
+            if (nA + nB > kCkptCols || need > C.slotCap) {   // rerun with larger slots (or a bad geometry)
+                if (lane == 0) atomicMax(C.need, nA + nB > kCkptCols ? kCkptBadGeometry : (unsigned long long)need);
+                pending = pending && !mine;
+                continue;
+            }
+            if (lane == 0) {
+                int o2 = 0;
+                for (int c = 0; c < nA + nB; ++c) {
+                    const int2 rg = c < nA ? aR[ckA + c] : bR[ckB - (c - nA)];
+                    sOff[c] = o2;
+                    o2 += max(0, rg.y - rg.x);
+                }
+            }
+            __syncthreads();
+            // alpha: the kept column, then forward
+            {
+                const int2 r0 = aR[ckA];
+                const double* src = aV + aO[ckA];
+                for (int i = lane; i < r0.y - r0.x; i += 64) slot[sOff[0] + i] = src[i];
+                for (int j = ckA + 1; j <= aHi; ++j) {
+                    const int2 pr = aR[j - 1], rg = aR[j];
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                    replay_alpha(X, j, slot + sOff[j - 1 - ckA], pr.x, pr.y, slot + sOff[j - ckA], rg.x, rg.y);
+                }
+            }
+            // beta: the kept column, then backward
+            {
+                const int2 r0 = bR[ckB];
+                const double* src = bV + bO[ckB];
+                for (int i = lane; i < r0.y - r0.x; i += 64) slot[sOff[nA] + i] = src[i];
+                for (int j = ckB - 1; j >= jbLo; --j) {
+                    const int2 nr = bR[j + 1], rg = bR[j];
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                    replay_beta(X, j, slot + sOff[nA + (ckB - (j + 1))], nr.x, nr.y, slot + sOff[nA + (ckB - j)], rg.x,
+                                rg.y);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            if (mine) {
+                const int2 ar = aR[ja];
+                const int2 br = bR[bc];
+                const double* av = slot + sOff[ja - ckA] - ar.x;
+                const double* bv = slot + sOff[nA + (ckB - bc)] + (br.y - 1);
+                const double score = score_middle(S, sc, bc, g, av, ar, bv, br, S.rd, st);
+                W.delta[W.deltaBase[k] + (long long)rr * M + m] = score - B.rBaseline[r];
+            }
+            pending = pending && !mine;
+            __syncthreads();   // sOff and the slot are reused by the next block
+        }
+        if (B.stats) {
+            unsigned long long c2 = st.cells, b2 = st.bytes;
+            for (int w = 32; w > 0; w >>= 1) {
+                c2 += __shfl_xor(c2, w, 64);
+                b2 += __shfl_xor(b2, w, 64);
+            }
+            if (lane == 0) {
+                atomicAdd(&B.stats[2 * kStatScore], c2);
+                atomicAdd(&B.stats[2 * kStatScore + 1], b2);
+            }
+        }
     }
 }
 
@@ -1345,11 +1641,14 @@ void launch_enumerate(const DevBatch& B, const int* zmws, int n, const long long
     hipLaunchKernelGGL(k_enumerate, dim3(n), dim3(256), 0, s, B, zmws, mutBase, posBase, codes, posOff);
 }
 
-void launch_score(const DevBatch& B, const ScoreWork& W, long long nWaves, const ScoreScratch& scratch, hipStream_t s)
+void launch_score(const DevBatch& B, const ScoreWork& W, long long nWaves, const ScoreScratch& scratch, hipStream_t s,
+                  const CkptWork* ck)
 {
     if (nWaves <= 0) return;
     const long long blocks = (nWaves + kScoreWaves - 1) / kScoreWaves;
     hipLaunchKernelGGL(k_score, dim3((unsigned)blocks), dim3(64 * kScoreWaves), 0, s, B, W, scratch);
+    if (ck && ck->nTasks > 0 && ck->nSlots > 0)
+        hipLaunchKernelGGL(k_score_ckpt, dim3((unsigned)ck->nSlots), dim3(64), 0, s, B, W, *ck);
     if (W.edgeCap > 0)
         hipLaunchKernelGGL(k_score_edge, dim3((W.edgeCap + 63) / 64), dim3(64), 0, s, B, W, scratch);
 }

@@ -34,6 +34,24 @@ struct ScoreWork {
     const int* nSel = nullptr;
 };
 
+// Scoring of reads with checkpointed bands (k_score_ckpt): a persistent grid of nSlots waves, each with a
+// slot of slotCap doubles for the columns it replays, pulls the round's tasks -- the 64-mutation chunks of
+// the (work item, read) pairs whose read is checkpointed -- from `counter`.  `need` receives the largest
+// slot a skipped block needed (0 when every block fit); the host then grows the slots and reruns.
+constexpr int kCkptMaxK = 32;                             // largest checkpoint interval the replay supports
+constexpr unsigned long long kCkptBadGeometry = 1ull << 62;   // CkptWork::need: a block outgrew the replay tables
+struct CkptWork {
+    const int2* pairs = nullptr;           // [nPairs] (work item, read index within the ZMW)
+    const long long* taskStart = nullptr;  // [nPairs + 1] cumulative chunks
+    int nPairs = 0;
+    long long nTasks = 0;
+    unsigned long long* counter = nullptr;
+    double* slots = nullptr;
+    long long slotCap = 0;
+    int nSlots = 0;
+    unsigned long long* need = nullptr;
+};
+
 // Bump-allocated scratch for the rare whole-window refill case (tiny windows).
 struct ScoreScratch {
     double* pool = nullptr;
@@ -93,7 +111,8 @@ void launch_compact(const DevBatch& B, const FillScratch& F, const int* reads, i
 void launch_suffix(const DevBatch& B, const int* reads, int n, hipStream_t s, bool withPrefix = false);
 void launch_enumerate(const DevBatch& B, const int* zmws, int n, const long long* mutBase, const long long* posBase,
                       int* codes, int* posOff, hipStream_t s);
-void launch_score(const DevBatch& B, const ScoreWork& W, long long nWaves, const ScoreScratch& scratch, hipStream_t s);
+void launch_score(const DevBatch& B, const ScoreWork& W, long long nWaves, const ScoreScratch& scratch, hipStream_t s,
+                  const CkptWork* ck = nullptr);
 // Phased scoring helpers: alive[g] = the ordered fast-score sum of mutation g over reads [0, readHi) never
 // fell below fastThr (k_reduce's break has not happened yet); per-item ranges of the selected list.
 void launch_alive(const DevBatch& B, const ScoreWork& W, long long nMut, double fastThr, int readHi,

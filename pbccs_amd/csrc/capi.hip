@@ -807,12 +807,16 @@ static size_t slot_pool_bytes(pbccs_engine* eng)
 
 static double zmw_est_bytes(const pbccs_zmw_input& z)
 {
+    int K = 0, minLen = 0;
+    ckpt_policy(&K, &minLen);
     double b = 0.0;
     for (int k = 0; k < z.n_reads; ++k) {
         const double J = std::max(1, z.tends ? z.tends[k] - (z.tstarts ? z.tstarts[k] : 0) : z.draft_len);
         const double I = z.lens ? std::max(0, z.lens[k]) : J;
         const double typical = J * 0.5 * (2 * 32 * 8 * 1.25 + 80 + 8 * 8);
-        const double tall = std::min(0.15 * 8.0 * (I + 1) * (J + 1), 8.7e7 * std::pow(J / 1e4, 3.0));
+        double tall = std::min(0.15 * 8.0 * (I + 1) * (J + 1), 8.7e7 * std::pow(J / 1e4, 3.0));
+        // checkpointed tall bands: every K-th column plus the kept tails of both matrices
+        if (K > 0 && J >= minLen) tall = tall / K + 2.0 * 8.0 * (kCkptTail + 1) * (I + 1);
         b += typical + tall;
     }
     return std::max(b, 4096.0);

@@ -44,6 +44,16 @@ long long tall_first_div()   // PBCCS_TALL_FIRST_DIV overrides (A/B)
                                                                   : kTallFirstDivDefault;
     return d;
 }
+// Checkpointed bands: tall bands of long windows keep every K-th column's values only;
+// the scorer replays the rest.  At 10 kb a tall read's two bands are ~0.2 GB in full.
+constexpr int kCkptDefaultK = 8;
+constexpr int kCkptDefaultMinLen = 4000;
+constexpr int kCkptSlotsMax = 2048;   // k_score_ckpt persistent waves (2 per SIMD at its register budget)
+int env_int(const char* name, int dflt)
+{
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
 constexpr long long kPhasedMinTasks = 1 << 21;   // (mutation, read) tasks from which a round scores in phases
 constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
 
@@ -187,6 +197,12 @@ VmPool::~VmPool()
     (void)hipMemAddressFree(ptr, kVaBytes);
 }
 
+void ckpt_policy(int* K, int* minLen)   // read per batch: tests switch it at run time
+{
+    *K = std::min(kCkptMaxK, std::max(0, env_int("PBCCS_CKPT_K", kCkptDefaultK)));
+    *minLen = std::max(0, env_int("PBCCS_CKPT_MIN_LEN", kCkptDefaultMinLen));
+}
+
 ArrowBatch::ArrowBatch(int device, Workspace* shared)
     : device_(device),
       ownWs_(shared ? nullptr : new Workspace()),
@@ -201,6 +217,8 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared)
     // first value-region estimate per read (PBCCS_INITIAL_BAND_HEIGHT overrides it: tests use a tiny one
     // to force in-kernel band growth on every read)
     if (const char* e = std::getenv("PBCCS_INITIAL_BAND_HEIGHT")) initialBandHeight_ = std::max(1, std::atoi(e));
+    ckpt_policy(&ckptK_, &ckptMinLen_);
+    ckptAll_ = std::min(kCkptMaxK, std::max(0, env_int("PBCCS_CKPT_ALL", 0)));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream3_, hipStreamNonBlocking));
@@ -510,7 +528,7 @@ bool ArrowBatch::Relayout(const std::vector<int>& list)
         long long cap;
         if (h.filled && m > 0) cap = m + m / 8 + 64;
         else if (h.fillPath >= 2 && h.fillPath < 5)
-            cap = ((long long)h.seq.size() + 1) * (h.te - h.ts + 1) / tall_first_div() + 64;
+            cap = ((long long)h.seq.size() + 1) * (h.te - h.ts + 1) / tall_first_div() / std::max(1, h.ckpt) + 64;
         else cap = (long long)h.colCap * initialBandHeight_;
         h.valCap = cap;
         h.valA = valTop_;
@@ -540,7 +558,7 @@ void ArrowBatch::UploadDescriptors()
         std::memcpy(&zc[(size_t)i * 45], z.ctx, sizeof(z.ctx));
     }
     std::vector<long long> so(R), cb(R), va(R), vb(R), vc(R);
-    std::vector<int> rl(R), rs(R), rts(R), rte(R), ra(R), rz(R);
+    std::vector<int> rl(R), rs(R), rts(R), rte(R), ra(R), rz(R), rck(R);
     for (int i = 0; i < R; ++i) {
         const HRead& r = reads_[i];
         so[i] = r.seqOff;
@@ -554,6 +572,7 @@ void ArrowBatch::UploadDescriptors()
         rte[i] = r.te;
         ra[i] = r.active ? 1 : 0;
         rz[i] = r.zmw;
+        rck[i] = r.ckpt;
     }
     upload(dZFwd_, zf, stream_);
     upload(dZRev_, zr, stream_);
@@ -572,6 +591,7 @@ void ArrowBatch::UploadDescriptors()
     upload(dRTe_, rte, stream_);
     upload(dRActive_, ra, stream_);
     upload(dRZmw_, rz, stream_);
+    upload(dRCkpt_, rck, stream_);
     // pools (templates re-uploaded whole: they change every refine round)
     upload(dTpl_, hTpl_, stream_);
     // 32 bytes of slack at the end: the lane fill loads read bases 8 at a time (two aligned words), and
@@ -620,6 +640,7 @@ DevBatch ArrowBatch::View() const
     b.rValA = dRValA_.ptr;
     b.rValB = dRValB_.ptr;
     b.rValCap = dRValCap_.ptr;
+    b.rCkpt = dRCkpt_.ptr;
     b.seqPool = dSeq_.ptr;
     b.aRange = dARange_.ptr;
     b.aOff = dAOff_.ptr;
@@ -735,6 +756,18 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 return reads_[x].te - reads_[x].ts > reads_[y].te - reads_[y].ts;
             });
         }
+        // checkpointed bands for the tall paths' long windows (and every cooperative fill under the test hook)
+        for (int p = 0; p < kPaths; ++p)
+            for (int r : todo[p]) {
+                HRead& h = reads_[r];
+                int k = 0;
+                if (ckptAll_ > 0 && p >= 1) k = ckptAll_;
+                else if (ckptK_ > 0 && p >= 2 && h.te - h.ts >= ckptMinLen_) k = ckptK_;
+                if (h.ckpt != k) {
+                    h.ckpt = k;
+                    descDirty_ = true;
+                }
+            }
         UploadDescriptors();
         const size_t R = reads_.size();
         dUsedA_.reserve(std::max<size_t>(R, 1), true);
@@ -759,7 +792,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             for (int p = 2; p < kPaths; ++p)
                 for (int r : todo[p]) {   // tall bands use ~2-22% of the full matrix (mean ~11%)
                     const long long I = (long long)reads_[r].seq.size(), J = reads_[r].te - reads_[r].ts;
-                    want += 2 * std::max<long long>(0, (I + 1) * (J + 1) / 7 - reads_[r].valCap);
+                    const long long K = std::max(1, reads_[r].ckpt);
+                    want += 2 * std::max<long long>(0, (I + 1) * (J + 1) / 7 / K - reads_[r].valCap);
                 }
             size_t freeB = 0, totalB = 0;
             PBCCS_HIP(hipMemGetInfo(&freeB, &totalB));
@@ -870,7 +904,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                     // from the typical 16-row region inside the kernel would copy and abandon two or three.
                     if (q >= 2 && q < kPaths) {
                         const long long I = (long long)h.seq.size(), J = h.te - h.ts;
-                        const long long want = (I + 1) * (J + 1) / tall_first_div() + 64;
+                        // checkpointed: every K-th column plus the kept tails (the next launch sets h.ckpt)
+                        const bool ck = ckptAll_ > 0 || (ckptK_ > 0 && J >= ckptMinLen_);
+                        const long long K = ck ? std::max(ckptAll_, ckptK_) : 1;
+                        const long long want = (I + 1) * (J + 1) / tall_first_div() / K +
+                                               (ck ? 2 * (kCkptTail + 1) * (I + 1) : 0) + 64;
                         if (want > h.valCap) {
                             h.valCap = want;
                             h.valA = valTop_;
@@ -916,6 +954,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
 void ArrowBatch::FillReadsSerial(const std::vector<int>& readsIn)
 {
     std::vector<int> todo(readsIn);
+    for (int r : todo)   // the lane-serial fill keeps full bands
+        if (reads_[r].ckpt != 0) {
+            reads_[r].ckpt = 0;
+            descDirty_ = true;
+        }
     for (int r : todo) EnsureCapacity(r);
     int H = kFillBandHeight;
     for (int attempt = 0; !todo.empty(); ++attempt) {
@@ -1182,7 +1225,53 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
     W.edgeList = dEdge_.ptr;
     W.edgeCount = dEdgeCount_.ptr;
     W.edgeCap = (int)edgeCap;
-    // one scoring launch (k_score + k_score_edge) over W's current phase; re-run on scratch overflow
+    // Checkpointed reads are scored by k_score_ckpt from a task list of (work item, read)
+    // pairs: the phase's reads [lo, hi) of each item whose read keeps checkpoint columns only, with the chunks
+    // of the phase's mutations (all of them, or the item's survivors nSel).
+    bool anyCkpt = false;
+    for (int k = 0; k < n && !anyCkpt; ++k) {
+        const HZmw& z = zmws_[zl[k]];
+        for (int q = 0; q < z.nReads; ++q) anyCkpt = anyCkpt || reads_[z.readBegin + q].ckpt != 0;
+    }
+    CkptWork ck;
+    auto ckpt_tasks = [&](int lo, int hi, const std::vector<int>* nSelH) {
+        ck = CkptWork();
+        if (!anyCkpt) return;
+        std::vector<int2> pairs;
+        std::vector<long long> start{0};
+        long long maxI = 1;
+        int maxK = 1;
+        for (int k = 0; k < n; ++k) {
+            const HZmw& z = zmws_[zl[k]];
+            const long long mc = nSelH ? (*nSelH)[k] : rNMut_[k];
+            if (mc <= 0) continue;
+            for (int q = std::max(0, lo); q < std::min(hi, z.nReads); ++q) {
+                const HRead& h = reads_[z.readBegin + q];
+                if (h.ckpt == 0) continue;
+                pairs.push_back(make_int2(k, q));
+                start.push_back(start.back() + (mc + 63) / 64);
+                maxI = std::max<long long>(maxI, (long long)h.seq.size() + 1);
+                maxK = std::max(maxK, h.ckpt);
+            }
+        }
+        if (pairs.empty()) return;
+        upload(dCkPairs_, pairs, stream_);
+        upload(dCkStart_, start, stream_);
+        ws_->ckCounter.reserve(2, false);
+        // a block replays <= 3K + 4 columns, each at most I + 1 rows; start from 1024-row columns
+        const long long first = (3LL * maxK + 4) * std::min<long long>(maxI, 1024);
+        ckSlotCap_ = std::max(ckSlotCap_, first);
+        ck.pairs = dCkPairs_.ptr;
+        ck.taskStart = dCkStart_.ptr;
+        ck.nPairs = (int)pairs.size();
+        ck.nTasks = start.back();
+        ck.counter = ws_->ckCounter.ptr;
+        ck.need = ws_->ckCounter.ptr + 1;
+        ck.nSlots = (int)std::min<long long>(ck.nTasks, kCkptSlotsMax);
+    };
+    ckpt_tasks(0, 1 << 30, nullptr);
+    // one scoring launch (k_score + k_score_ckpt + k_score_edge) over W's current phase; re-run on scratch
+    // overflow or when a checkpoint replay outgrew its slot
     auto score_launch = [&](long long nWaves) {
         for (int attempt = 0;; ++attempt) {
             PBCCS_HIP(hipMemsetAsync(dEdgeCount_.ptr, 0, sizeof(int), stream_));
@@ -1193,11 +1282,26 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
             sc.top = dScratchTop_.ptr;
             sc.cap = dScratch_.cap;
             sc.overflow = dScratchOverflow_.ptr;
-            Timed(kKScore, [&] { launch_score(B, W, nWaves, sc, stream_); });
+            if (ck.nTasks > 0) {
+                ws_->ckSlots.reserve((size_t)ck.nSlots * ckSlotCap_, false);
+                ck.slots = ws_->ckSlots.ptr;
+                ck.slotCap = ckSlotCap_;
+                PBCCS_HIP(hipMemsetAsync(ws_->ckCounter.ptr, 0, 2 * sizeof(unsigned long long), stream_));
+            }
+            Timed(kKScore, [&] { launch_score(B, W, nWaves, sc, stream_, ck.nTasks > 0 ? &ck : nullptr); });
             PBCCS_HIP(hipGetLastError());
             int ovf = 0;
+            unsigned long long ckNeed = 0;
             PBCCS_HIP(hipMemcpyAsync(&ovf, dScratchOverflow_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
+            if (ck.nTasks > 0)
+                PBCCS_HIP(hipMemcpyAsync(&ckNeed, ck.need, sizeof(ckNeed), hipMemcpyDeviceToHost, stream_));
             PBCCS_HIP(hipStreamSynchronize(stream_));
+            if (ckNeed >= kCkptBadGeometry) throw DeviceError("checkpoint replay: block outgrew its column tables");
+            if (ckNeed > 0) {
+                if (attempt > 8) throw DeviceError("checkpoint replay slots keep overflowing");
+                ckSlotCap_ = (long long)ckNeed + (long long)ckNeed / 4 + 64;
+                continue;
+            }
             if (!ovf) break;
             if (attempt > 8) throw DeviceError("scratch overflow");
             if (ovf & 1) dScratch_.reserve(dScratch_.cap * 4, false);
@@ -1280,6 +1384,7 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
             W.readHi = hi;
             upload(dWWaveStart_, wsv, stream_);
             W.waveStart = dWWaveStart_.ptr;
+            ckpt_tasks(lo, hi, ph == 0 ? nullptr : &nSel);
             score_launch(wsv[n]);
         }
         W.sel = nullptr;

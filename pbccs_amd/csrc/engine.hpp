@@ -134,6 +134,10 @@ struct Counters {   // work counters for the roofline report (bench.py)
     long long bandTopBytes = 0, bandRegionBytes = 0, bandUsedBytes = 0;
 };
 
+// Checkpointed-band policy: interval K (0 = off) and the shortest window it applies to;
+// PBCCS_CKPT_K / PBCCS_CKPT_MIN_LEN override the defaults.
+void ckpt_policy(int* K, int* minLen);
+
 // kKFill: the 16-lane (and opt-in lane) fills of typical bands; kKFillTall: the 64-lane and lane-serial fills of
 // tall bands (launched on their own streams), reported apart so each kind's launches never overlap each other
 // within one workspace slot
@@ -164,6 +168,8 @@ struct Workspace {
     DevVec<int> fOff;
     // scoring rounds
     DevVec<int> codes, posOff, qv, list, edge, edgeCount;
+    DevVec<double> ckSlots;                    // k_score_ckpt replay slots
+    DevVec<unsigned long long> ckCounter;      // [0] task counter, [1] largest slot need
     DevVec<double> delta, score;
     DevVec<unsigned char> fav;
     DevVec<double> scratch;
@@ -267,7 +273,8 @@ private:
         long long colBase = 0;
         int colCap = 0;
         long long valA = 0, valB = 0, valCap = 0;
-        long long usedA = 0, usedB = 0;   // band cells of the last fill
+        long long usedA = 0, usedB = 0;   // band values the last fill kept (its region need)
+        int ckpt = 0;   // checkpoint interval of the bands (0: every column's values kept)
     };
 
     void EnsureZmwUploaded();
@@ -311,7 +318,13 @@ private:
     DevVec<double> dZCtx_;
     DevVec<char> dTpl_, dSeq_;
     DevVec<long long> dRSeqOff_, dRColBase_, dRValA_, dRValB_, dRValCap_;
-    DevVec<int> dRLen_, dRStrand_, dRTs_, dRTe_, dRActive_, dRZmw_;
+    DevVec<int> dRLen_, dRStrand_, dRTs_, dRTe_, dRActive_, dRZmw_, dRCkpt_;
+    DevVec<int2> dCkPairs_;        // k_score_ckpt task list of a scoring phase
+    DevVec<long long> dCkStart_;
+    // checkpointed bands: interval K for tall-path reads of windows >= ckptMinLen_; ckptAll_ (test hook
+    // PBCCS_CKPT_ALL) puts every cooperative fill on checkpoints
+    int ckptK_ = 0, ckptMinLen_ = 0, ckptAll_ = 0;
+    long long ckSlotCap_ = 0;
     DevVec<double> dRBaseline_;
     DevVec<int> dRFlips_, dRStatus_, dUsedA_, dUsedB_;
     DevVec<int> dWZmw_, dWNMut_;

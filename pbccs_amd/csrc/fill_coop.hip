@@ -20,6 +20,7 @@
 // count-only mode and reports the exact size it needs (kFillOverflow).
 #include "arrow_device.hpp"
 #include "arrow_kernels.hpp"
+#include "coop_chain.hpp"
 
 #include <cstdlib>
 #include <stdexcept>
@@ -27,154 +28,7 @@
 namespace pbccs {
 namespace {
 
-constexpr int kCtxDoubles = 9 * kCtxStride;   // 45
-constexpr int kBaseOther = 4;                 // nibble code of a non-ACGT read base (never matches)
-
-__device__ __forceinline__ int base_code(char c)
-{
-    return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : kBaseOther;
-}
-
-__device__ __forceinline__ int nib(const unsigned* w, int x) { return (w[x >> 3] >> ((x & 7) << 2)) & 15; }
-
-// ContextParameters::GetParametersForContext slot from two template base codes (ACGT only).
-__device__ __forceinline__ int ctx_code(int b1, int b2) { return b1 == b2 ? b2 : 4 + b2; }
-
-// --- cross-lane primitives (gfx9 DPP) -------------------------------------------------------------
-template <int CTRL, int ROWMASK, bool BOUND>
-__device__ __forceinline__ double dpp_d(double old, double x)
-{
-    const int xl = __double2loint(x), xh = __double2hiint(x);
-    const int ol = __double2loint(old), oh = __double2hiint(old);
-    const int rl = __builtin_amdgcn_update_dpp(ol, xl, CTRL, ROWMASK, 0xF, BOUND);
-    const int rh = __builtin_amdgcn_update_dpp(oh, xh, CTRL, ROWMASK, 0xF, BOUND);
-    return __hiloint2double(rh, rl);
-}
-
-// value of lane l-1 of the group; lane 0 receives `first`
-template <int G>
-__device__ __forceinline__ double shift_up(double x, double first)
-{
-    if constexpr (G == 16) {
-        return dpp_d<0x111, 0xF, false>(first, x);   // row_shr:1
-    } else {
-        return dpp_d<0x138, 0xF, false>(first, x);   // wave_shr:1
-    }
-}
-
-// inclusive prefix maximum over the group's lanes (values >= 0)
-template <int G>
-__device__ __forceinline__ double prefix_max(double x)
-{
-    x = fmax(x, dpp_d<0x111, 0xF, true>(0.0, x));
-    x = fmax(x, dpp_d<0x112, 0xF, true>(0.0, x));
-    x = fmax(x, dpp_d<0x114, 0xF, true>(0.0, x));
-    x = fmax(x, dpp_d<0x118, 0xF, true>(0.0, x));
-    if constexpr (G == 64) {
-        x = fmax(x, dpp_d<0x142, 0xA, false>(0.0, x));   // row_bcast:15
-        x = fmax(x, dpp_d<0x143, 0xC, false>(0.0, x));   // row_bcast:31
-    }
-    return x;
-}
-
-template <int G>
-struct Group {
-    int lane;   // lane within the group
-    int base;   // first wavefront lane of the group
-    __device__ __forceinline__ unsigned long long bits(bool p) const
-    {
-        const unsigned long long m = __ballot(p);
-        if constexpr (G == 64) return m;
-        else return (m >> base) & ((1ull << G) - 1);
-    }
-    // value of group lane `src` (uniform across the group).  G = 64: the group is the wavefront and src is
-    // wave-uniform at every call site (a loop counter, a ballot's first set bit, a constant), so the value
-    // moves through an SGPR (v_readlane, a few cycles) instead of an LDS permute (ds_bpermute) -- this sits
-    // on the insertion chain's critical path once per 64-row chunk.
-    __device__ __forceinline__ double bcast(double x, int src) const
-    {
-        if constexpr (G == 64) {
-            const int lo = __builtin_amdgcn_readlane(__double2loint(x), src);
-            const int hi = __builtin_amdgcn_readlane(__double2hiint(x), src);
-            return __hiloint2double(hi, lo);
-        } else {
-            return __shfl(x, src, G);
-        }
-    }
-    __device__ __forceinline__ int bcast(int x, int src) const
-    {
-        if constexpr (G == 64) return __builtin_amdgcn_readlane(x, src);
-        else return __shfl(x, src, G);
-    }
-    // value of the group's last lane: G = 16 is one DPP row, whose lane 15 a single v_mov_b64 row_newbcast:15
-    // hands to the whole row (instead of two LDS permutes on the chunk-to-chunk carry path)
-    __device__ __forceinline__ double bcast_last(double x) const
-    {
-        if constexpr (G == 64) {
-            return bcast(x, 63);
-        } else {
-            const long long r = __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x15F, 0xF, 0xF, false);
-            return __longlong_as_double(r);
-        }
-    }
-};
-
-// The in-column insertion chain x_i = (m_i + x_{i-1} k_i) + d_i over the G rows of a chunk (lane l = row
-// l; lane 0's predecessor is `carry`), in the reference's operation order (SimpleRecursor.cpp:117-150):
-// G serial shift-by-one DPP steps; after step q lanes <= q hold their final value.  (Jacobi sweeps for
-// G = 64 -- exact by fixed-point uniqueness -- measured 157 ms against 67 ms per tall fill and were
-// removed)
-template <int G>
-__device__ __forceinline__ double insertion_chain(double m, double k, double d, double carry)
-{
-    double x = 0.0, up = carry;   // lane 0's `up` stays the carry: DPP leaves it untouched
-#pragma unroll
-    for (int q = 0; q < G; ++q) {
-        up = shift_up<G>(x, up);
-        x = (m + up * k) + d;
-    }
-    return x;
-}
-
-// G = 64 serial chain with an early exit: after step q, lanes <= q hold their final value.  From lane
-// `first` on (the first lane the reference loop may stop at; >= G: none in this chunk) the chain is checked
-// every 8 steps with `maybe_stop`, a conservative form of the loop's stop test (it never reports a lane the
-// exact test continues at).  Once a lane <= q would stop, every lane past it is discarded by the caller, so
-// the remaining steps are skipped; the caller's exact test then finds the same stop lane among the final
-// lanes.  Narrow passes of tall reads (the first alpha / beta, bands of ~15-30 rows) and the last chunk of a
-// tall column no longer pay the full 64 steps.
-template <class MaybeStop>
-__device__ __forceinline__ double insertion_chain64_exit(double m, double k, double d, double carry, int first,
-                                                         MaybeStop maybe_stop)
-{
-    double x = 0.0, up = carry;
-    int q = 0;
-    const int check0 = max(first, 0) + 3;   // first check: a few rows past the first possible stop
-    if (check0 < 63) {
-        // fully unrolled like the check-free path below (a rolled block loop measured 4% slower end to end,
-        // profiles/r2h17_code_size_ab): the checks sit at fixed positions and only their branch is dynamic
-#pragma unroll
-        for (q = 0; q < 64; q += 8) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                up = shift_up<64>(x, up);
-                x = (m + up * k) + d;
-            }
-            const int last = q + 7;   // lanes <= last are final
-            if (last >= check0 && last < 63) {
-                const unsigned long long st = maybe_stop(x) & ((2ull << last) - 1);
-                if (st) return x;
-            }
-        }
-        return x;
-    }
-#pragma unroll
-    for (int s = 0; s < 64; ++s) {
-        up = shift_up<64>(x, up);
-        x = (m + up * k) + d;
-    }
-    return x;
-}
+using namespace coop;
 
 // Everything a group needs about its read (group-uniform values) + LDS views.
 template <int G>
@@ -188,6 +42,7 @@ struct Task {
     double* col1;
     int hcap;              // rows per column buffer
     bool gcol;             // column buffers live in global memory (CoopFill::colScratch), not LDS
+    int ckK;               // checkpoint interval: 0 keeps every column's values, else only ckpt_col_a/b columns
     bool chainExit;            // G = 64 serial steps with the early exit (insertion_chain64_exit)
     int slackDiv;              // regrow_bands slack: need / slackDiv
     double prNot, prThird, sdn;
@@ -209,7 +64,8 @@ struct Task {
 };
 
 struct PassOut {
-    long long used;   // values used by the pass (also when they did not fit)
+    long long used;   // cells the pass computed (the reference's used entries; also when they did not fit)
+    long long stored; // values it keeps (= used for a full band; checkpoint columns only otherwise)
     double last;      // alpha(I, J) or beta(0, 0)
     double sumL;      // accumulate(logScales, 0.0) left to right
     bool tall;        // a column exceeded the LDS buffer
@@ -312,7 +168,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
 {
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0.0, 0.0, false, !selfValid, false};
+    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false};
     bool counting = false;   // outgrew the region: finish the pass without stores (regrow_bands)
     (void)keepO;
     if (a.cap < 1) ovf = true;
@@ -327,7 +183,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     if (lane == 0) prev[0] = 1.0;
     col_fence(T.gcol);
     int pb = 0, pe = 1;
-    long long used = 1;
+    long long used = 1, stored = 1;   // cells computed / values kept (column 0 is always kept)
     int hb = 1, he = 1;
     int prevCtx = kCtxZero;
     int curBase = T.TBase(0), curCtx = T.TCtx(0);
@@ -419,11 +275,13 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                 carry = T.g.bcast_last(x);
             }
         }
-        if (!ovf && !counting && used + (e - b) + 1 > a.cap) {
+        const bool keep = T.ckK == 0 || ckpt_col_a(j, J, T.ckK);
+        const long long add = keep ? e - b : 0;
+        if (!ovf && !counting && stored + add + 1 > a.cap) {
             if (T.bump) counting = true;
             else ovf = true;
         }
-        const bool store = !ovf && !counting;
+        const bool store = !ovf && !counting && keep;
         // ScaledMatrix::FinishEditingColumn (ScaledMatrix-inl.hpp:35-60) + the next begin hint (:166)
         const double thrF = mx / T.sdn;
         const bool scale = (mx != 0.0 && mx != 1.0);
@@ -438,7 +296,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
             const double v = scale ? x / mx : x;
             if (ok) {
                 cur[kk] = v;
-                if (store && used + kk < a.cap) a.V(used + kk) = v;
+                if (store && stored + kk < a.cap) a.V(stored + kk) = v;
             }
             const unsigned long long hit = T.g.bits(ok && !(v < thrF));
             if (!found && hit) {
@@ -446,14 +304,15 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                 found = true;
             }
         }
-        if (!counting && used + (e - b) > a.cap) ovf = true;
+        if (!counting && stored + add > a.cap) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
         if (lane == 0 && !counting) {
             a.R(j) = make_int2(b, e);
-            a.O(j) = (int)used;
+            a.O(j) = (int)stored;
             a.L(j) = scale ? mx : 1.0;   // the scale factor; finish_log_scales takes its log
         }
         used += e - b;
+        stored += add;
         col_fence(T.gcol);   // the next column's lanes read rows this column's lanes wrote
         double* t = prev;
         prev = cur;
@@ -472,18 +331,19 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     const double c = (0.0 < lik) ? lik : 0.0;
     double v = lik, ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = lik / c; ls = log(c); }
-    if (!ovf && !counting && used + 1 > a.cap) {
+    if (!ovf && !counting && stored + 1 > a.cap) {
         if (T.bump) counting = true;
         else ovf = true;
     }
     out.regrow = counting;
     if (lane == 0 && !counting) {
-        if (!ovf) a.V(used) = v;
+        if (!ovf) a.V(stored) = v;
         a.R(J) = make_int2(I, I + 1);
-        a.O(J) = (int)used;
+        a.O(J) = (int)stored;
         a.L(J) = ls;
     }
     out.used = used + 1;
+    out.stored = stored + 1;
     out.last = v;
     if (!counting) out.sumL = finish_log_scales<G>(T, a, J);
     return out;
@@ -495,7 +355,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 {
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0.0, 0.0, false, !selfValid, false};
+    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false};
     bool counting = false;   // outgrew the region: finish the pass without stores (regrow_bands)
     (void)keepO;
     if (bm.cap < 1) ovf = true;
@@ -511,7 +371,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     if (lane == 0) nxt[0] = 1.0;
     col_fence(T.gcol);
     int pb = I, pe = I + 1;
-    long long used = 1;
+    long long used = 1, stored = 1;   // cells computed / values kept (column J is always kept)
     int hb = I, he = I;
     int nextBase = T.TBase(J - 1);
     int2 gR = make_int2(0, 0), sR = make_int2(0, 0), gN = make_int2(0, 0), sN = make_int2(0, 0);
@@ -598,11 +458,13 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                 carry = T.g.bcast_last(x);
             }
         }
-        if (!ovf && !counting && used + (e - b) + 1 > bm.cap) {
+        const bool keep = T.ckK == 0 || ckpt_col_b(j, J, T.ckK);
+        const long long add = keep ? e - b : 0;
+        if (!ovf && !counting && stored + add + 1 > bm.cap) {
             if (T.bump) counting = true;
             else ovf = true;
         }
-        const bool store = !ovf && !counting;
+        const bool store = !ovf && !counting && keep;
         const double thrF = mx / T.sdn;
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhe = b;
@@ -615,7 +477,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
             const double v = scale ? x / mx : x;
             if (ok) {
                 cur[off] = v;
-                if (store && used + off < bm.cap) bm.V(used + off) = v;
+                if (store && stored + off < bm.cap) bm.V(stored + off) = v;
             }
             const unsigned long long hit = T.g.bits(ok && !(v < thrF));
             if (!found && hit) {
@@ -623,14 +485,15 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                 found = true;
             }
         }
-        if (!counting && used + (e - b) > bm.cap) ovf = true;
+        if (!counting && stored + add > bm.cap) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
         if (lane == 0 && !counting) {
             bm.R(j) = make_int2(b, e);
-            bm.O(j) = (int)used;
+            bm.O(j) = (int)stored;
             bm.L(j) = scale ? mx : 1.0;   // the scale factor; finish_log_scales takes its log
         }
         used += e - b;
+        stored += add;
         col_fence(T.gcol);
         double* t = nxt;
         nxt = cur;
@@ -646,18 +509,19 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     const double c = (0.0 < raw) ? raw : 0.0;
     double v = raw, ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = raw / c; ls = log(c); }
-    if (!ovf && !counting && used + 1 > bm.cap) {
+    if (!ovf && !counting && stored + 1 > bm.cap) {
         if (T.bump) counting = true;
         else ovf = true;
     }
     out.regrow = counting;
     if (lane == 0 && !counting) {
-        if (!ovf) bm.V(used) = v;
+        if (!ovf) bm.V(stored) = v;
         bm.R(0) = make_int2(0, 1);
-        bm.O(0) = (int)used;
+        bm.O(0) = (int)stored;
         bm.L(0) = ls;
     }
     out.used = used + 1;
+    out.stored = stored + 1;
     out.last = v;
     if (!counting) out.sumL = finish_log_scales<G>(T, bm, J);
     return out;
@@ -743,6 +607,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     T.hcap = F.hcap;
     T.gcol = GC;
     T.chainExit = F.chainExit;
+    T.ckK = B.rCkpt ? B.rCkpt[r] : 0;
     T.slackDiv = max(1, F.regrowSlackDiv);
     T.prNot = B.prNot;
     T.prThird = B.prThird;
@@ -785,8 +650,9 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     // its own previous pass (hint), never on previous values.  Once an alpha pass and the beta pass after
     // it both reproduce their predecessors' ranges, every later pass repeats them bit for bit, so the
     // remaining flip-flops are skipped and only the count the reference reports is kept.
-    PassOut pa{0, 0.0, 0.0, false, false, false}, pb{0, 0.0, 0.0, false, false, false};
-    long long ua = 0, ub = 0;
+    PassOut pa{0, 0, 0.0, 0.0, false, false, false}, pb{0, 0, 0.0, 0.0, false, false, false};
+    long long ua = 0, ub = 0;   // cells of the last alpha / beta pass (the reband test)
+    long long sa = 0, sb = 0;   // values they keep (region sizes)
     const int maxSize = (int)(0.5 + kRebandFrac * (I + 1) * (J + 1));
     bool mismatched = false;
     int unchanged = 0;
@@ -814,7 +680,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
         if (o.tall) return fail_tall();
         if (o.regrow) {   // exact region for this pass, then run it again (count-only if the pool is full)
             if (++regrows > 8 ||
-                !regrow_bands<G>(T, doAlpha ? a : bm, doAlpha ? bm : a, doAlpha, o.used, doAlpha ? ub : ua))
+                !regrow_bands<G>(T, doAlpha ? a : bm, doAlpha ? bm : a, doAlpha, o.stored, doAlpha ? sb : sa))
                 ovf = true;
             --step;
             continue;
@@ -824,11 +690,13 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
         if (doAlpha) {
             pa = o;
             ua = o.used;
-            needA = max(needA, o.used);
+            sa = o.stored;
+            needA = max(needA, o.stored);
         } else {
             pb = o;
             ub = o.used;
-            needB = max(needB, o.used);
+            sb = o.stored;
+            needB = max(needB, o.stored);
         }
         if (step >= 2 && step <= 4) ++flips;
         if (step >= 5) {
@@ -851,8 +719,8 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
         } else {
             B.rFlips[r] = flips;
             B.rBaseline[r] = bv;
-            F.usedA[r] = (int)ua;
-            F.usedB[r] = (int)ub;
+            F.usedA[r] = (int)sa;   // region sizes: the values the bands keep
+            F.usedB[r] = (int)sb;
             B.rStatus[r] = (mism > kAlphaBetaTol) ? kFillMismatch : kFillOk;
             if (B.stats) {   // algorithmic: 8 B per stored cell + 16 B per column per fill pass
                 constexpr int kind = G == 64 ? kStatFillTall : kStatFill;
