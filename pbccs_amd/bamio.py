@@ -38,6 +38,10 @@ class BgzfWriter:
         self._buf = bytearray()
         self._level = level
 
+    def tell(self):
+        """BGZF virtual offset of the next byte written: compressed offset of its block << 16 | offset inside it."""
+        return (self._f.tell() << 16) | len(self._buf)
+
     def write(self, data):
         self._buf += data
         while len(self._buf) >= _MAX_BLOCK:
@@ -222,11 +226,15 @@ def bam_record_to_sam(rec):
 
 
 def write_bam(path, header_text, sam_lines, bin_=None):
+    """Returns each record's BGZF virtual offset (the offsets pbbam's BamWriter::Write reports)."""
+    offsets = []
     with BgzfWriter(path) as w:
         ht = header_text.encode()
         w.write(b"BAM\1" + struct.pack("<i", len(ht)) + ht + struct.pack("<i", 0))
         for line in sam_lines:
+            offsets.append(w.tell())
             w.write(sam_to_bam_record(line, bin_))
+    return offsets
 
 
 def read_bam(path):
@@ -298,10 +306,15 @@ def group_subread_bam(path, min_snr=4.0, min_passes=3, min_read_score=0.75):
                             flags_of=lambda n: by_name[n]["flags"])
 
 
-def write_ccs_bam(path, movies, sam_lines):
-    """ccs.bam: ccsio.sam_header + ccsio.ccs_sam_record lines, with Bin(0) as ccs.cpp:113 sets it."""
+def write_ccs_bam(path, movies, sam_lines, pbi=False):
+    """ccs.bam: ccsio.sam_header + ccsio.ccs_sam_record lines, with Bin(0) as ccs.cpp:113 sets it.  pbi: also
+    write path + ".pbi" from each record's virtual offset (ccs.cpp:164-169,386, pbccs_amd.pbi)."""
     from . import ccsio
-    write_bam(path, ccsio.sam_header(movies), sam_lines, bin_=0)
+    sam_lines = list(sam_lines)
+    offsets = write_bam(path, ccsio.sam_header(movies), sam_lines, bin_=0)
+    if pbi:
+        from .pbi import pbi_entry, write_pbi
+        write_pbi(path + ".pbi", [pbi_entry(line, off) for line, off in zip(sam_lines, offsets)])
 
 
 def subread_sam_line(movie, hole, qs, qe, seq, snr, flags=3, read_score=0.9, rg="00000000"):

@@ -706,6 +706,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         const long long want = p == 2 ? std::min<long long>(kCoopTallRows, full) : full;
         return room >= want ? (int)want : (p == 3 && room >= 64 ? (int)room : 0);
     };
+    // PBCCS_FILL_PATHS=1: one stderr line per launch set (reads per path, wall ms, reads re-routed / regrown)
+    static const bool pathTrace = std::getenv("PBCCS_FILL_PATHS") != nullptr;
     for (int attempt = 0;; ++attempt) {
         // route reads whose buffers do not fit this path's LDS budget to the next path
         for (int p = 0; p < kPaths; ++p) {
@@ -782,6 +784,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         // is then the slower of the two, not their sum.  Fork before the first launch (after the list
         // upload), so the tall fills do not wait for the 16-lane fill.
         const bool forked = !todo[2].empty() || !todo[3].empty() || !todo[4].empty();
+        const auto tLaunch = std::chrono::steady_clock::now();
         // Headroom for in-kernel band growth (CoopFill::valBump): reads on the tall paths grow to a few
         // percent of their full (I+1)(J+1) matrix; budgeted against the device's free memory.  Growth
         // beyond the mapped headroom falls back to count-only + relaunch below.
@@ -888,6 +891,19 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 }
             valTop_ = (long long)std::min<unsigned long long>(bump, (unsigned long long)valLimit);
             counters_.bandGrowths += 1;
+        }
+        if (pathTrace) {
+            int nt = 0, no = 0;
+            for (int p = 0; p < kPaths; ++p)
+                for (int r : todo[p]) {
+                    nt += st[r] == kFillTall;
+                    no += st[r] == kFillOverflow;
+                }
+            std::fprintf(stderr, "[fillpaths] batch=%p attempt=%d n=%zu/%zu/%zu/%zu/%zu wall=%.1fms tall=%d ovf=%d\n",
+                         (void*)this, attempt, todo[0].size(), todo[1].size(), todo[2].size(), todo[3].size(),
+                         todo[4].size(),
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tLaunch).count(),
+                         nt, no);
         }
         std::vector<int> next[kPaths];
         for (int p = 0; p < kPaths; ++p) {

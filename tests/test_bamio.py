@@ -53,6 +53,50 @@ def test_ccs_record_round_trip_and_layout(tmp_path):
     assert gzip.decompress(p.read_bytes())[:4] == b"BAM\1"
 
 
+def test_pbi_index_round_trip_and_offsets(tmp_path):
+    """ccs.bam + .pbi (ccs.cpp --pbi): the index holds one basic-data entry per record in file order (rgId from
+    the read-group hex id, qStart/qEnd -1, holeNumber = zm, readQual = rq / 1000, ctxtFlag 0), and every
+    fileOffset is a BGZF virtual offset that lands on its record -- checked across block boundaries with
+    records large enough to span several 64 KiB blocks."""
+    import zlib
+    from pbccs_amd import pbi
+    rng = random.Random(11)
+    lines = []
+    for k in range(40):
+        res = dict(_ccs_result())
+        L = rng.choice([13, 500, 9000, 70000])
+        res["consensus"] = "".join(rng.choice("ACGT") for _ in range(L))
+        res["qvs"] = [rng.randint(0, 93) for _ in range(L)]
+        res["predicted_accuracy"] = rng.uniform(0.9, 1.0)
+        lines.append(ccsio.ccs_sam_record("m140905_42", 1000 + 7 * k, res, [10.0, 7.0, 5.0, 11.5]))
+    p = tmp_path / "ccs.bam"
+    bamio.write_ccs_bam(str(p), ["m140905_42"], lines, pbi=True)
+    idx = pbi.read_pbi(str(p) + ".pbi")
+    assert idx["version"] == 0x030001 and idx["flags"] == 0 and idx["n_reads"] == len(lines)
+    rg = int(ccsio.read_group_id("m140905_42"), 16)
+    assert idx["rg_id"] == [rg - (1 << 32) if rg >= 1 << 31 else rg] * len(lines)
+    assert idx["q_start"] == [-1] * len(lines) and idx["q_end"] == [-1] * len(lines)
+    assert idx["hole_number"] == [1000 + 7 * k for k in range(len(lines))]
+    assert idx["ctxt_flag"] == [0] * len(lines)
+    for q, line in zip(idx["read_qual"], lines):
+        rq = int(line.split("rq:i:")[1].split("\t")[0])
+        assert abs(q - rq / 1000.0) < 1e-6
+    raw = p.read_bytes()
+    offs = idx["file_offset"]
+    assert offs == sorted(offs) and len(set(offs)) == len(offs)
+    for off, line in zip(offs, lines):
+        coff, uoff = off >> 16, off & 0xffff
+        # inflate from the record's block on: enough blocks for the record's 4-byte size and body
+        data, k = b"", coff
+        while len(data) < uoff + 4 or len(data) < uoff + 4 + struct.unpack_from("<i", data, uoff)[0]:
+            xlen = struct.unpack_from("<H", raw, k + 10)[0]
+            bsize = struct.unpack_from("<H", raw, k + 12 + 4)[0] + 1
+            data += zlib.decompress(raw[k + 12 + xlen:k + bsize - 8], -15)
+            k += bsize
+        size = struct.unpack_from("<i", data, uoff)[0]
+        assert bamio.bam_record_to_sam(data[uoff + 4:uoff + 4 + size]) == line
+
+
 def test_subread_bam_grouping_matches_fasta_path(tmp_path):
     """group_subread_bam applies ccs.cpp's gates (PoorSNR, read score, TooFewPasses) with the tags' values,
     exactly as group_zmws does given the same values."""
