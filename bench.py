@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--streams", type=int, default=0,
                     help="workspace slots = batches polished concurrently (0 = min(steps, 5), capped by HBM)")
+    ap.add_argument("--batch-zmws", type=int, default=0,
+                    help="queue workloads: ZMWs per device batch (0 = planned from free HBM)")
     ap.add_argument("--ccs-chunk", type=int, default=0,
                     help="ccs stage: ZMWs per POA chunk / polish batch (0 = planned from free HBM)")
     ap.add_argument("--no-profile", action="store_true")
@@ -317,6 +319,8 @@ def main():
     if not args.no_profile:
         eng.set_profiling(True)   # HIP events on the launch streams + in-kernel algorithmic counters
     settings = pbccs_amd.ConsensusSettings()
+    if args.batch_zmws and args.workload != "2kb":
+        settings.zmws_per_batch = args.batch_zmws
     seed0 = args.seed + 7919 * rank
 
     if args.stage == "poa":

@@ -95,9 +95,10 @@ struct CoopFill {
     long long* rValA = nullptr;
     long long* rValB = nullptr;
     long long* rValCap = nullptr;
-    // All-rows path for columns taller than LDS holds: 2 * hcap doubles per launch slot (64-lane groups
-    // only).  nullptr: the column buffers are in LDS.
+    // Hybrid 64-lane path: column rows past the hcap LDS rows live in 2 * gRows doubles per launch slot of
+    // colScratch, so no column is ever too tall.  nullptr: the column buffers are LDS only.
     double* colScratch = nullptr;
+    int gRows = 0;
 };
 size_t coop_group_bytes(int hcap, int readWords, int tplWords);
 // Lane fill (fill_lane.hip): one lane per read, columns of up to kFillLaneRows rows (taller: kFillTall).

@@ -221,10 +221,8 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared)
     ckptAll_ = std::min(kCkptMaxK, std::max(0, env_int("PBCCS_CKPT_ALL", 0)));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     PBCCS_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
-    PBCCS_HIP(hipStreamCreateWithFlags(&stream3_, hipStreamNonBlocking));
     PBCCS_HIP(hipEventCreateWithFlags(&evFork_, hipEventDisableTiming));
     PBCCS_HIP(hipEventCreateWithFlags(&evJoin_, hipEventDisableTiming));
-    PBCCS_HIP(hipEventCreateWithFlags(&evJoin3_, hipEventDisableTiming));
     dScratch_.reserve(kInitialScratch, false);
     dScratchTop_.reserve(1, false);
     // the read pool starts with 16 bytes of padding (see UploadDescriptors: word loads of read bases)
@@ -243,12 +241,9 @@ ArrowBatch::~ArrowBatch()
         }
         for (hipEvent_t e : eventPool_) (void)hipEventDestroy(e);
         (void)hipStreamSynchronize(stream2_);
-        (void)hipStreamSynchronize(stream3_);
         (void)hipEventDestroy(evFork_);
         (void)hipEventDestroy(evJoin_);
-        (void)hipEventDestroy(evJoin3_);
         (void)hipStreamDestroy(stream2_);
-        (void)hipStreamDestroy(stream3_);
         (void)hipStreamDestroy(stream_);
     }
 }
@@ -292,11 +287,10 @@ void ArrowBatch::Timed(KernelKind k, F&& launch, hipStream_t st)
 void ArrowBatch::ResolveEvents()
 {
     if (pending_.empty()) return;
-    // events sit on all three streams (the tall fills run on stream2_/stream3_); a batch that failed after
+    // events sit on both streams (the tall fills run on stream2_); a batch that failed after
     // the fork may not have joined them back into stream_, so wait for each
     PBCCS_HIP(hipStreamSynchronize(stream_));
     PBCCS_HIP(hipStreamSynchronize(stream2_));
-    PBCCS_HIP(hipStreamSynchronize(stream3_));
     for (const Pending& p : pending_) {
         float ms = 0.0f;
         if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) stats_[p.kind].ms += ms;
@@ -527,7 +521,7 @@ bool ArrowBatch::Relayout(const std::vector<int>& list)
         const long long m = std::max(h.usedA, h.usedB);
         long long cap;
         if (h.filled && m > 0) cap = m + m / 8 + 64;
-        else if (h.fillPath >= 2 && h.fillPath < 5)
+        else if (h.fillPath == 2 || h.fillPath == 3)
             cap = ((long long)h.seq.size() + 1) * (h.te - h.ts + 1) / tall_first_div() / std::max(1, h.ckpt) + 64;
         else cap = (long long)h.colCap * initialBandHeight_;
         h.valCap = cap;
@@ -671,9 +665,11 @@ DevBatch ArrowBatch::View() const
 void ArrowBatch::FillReads(const std::vector<int>& readsIn)
 {
     // 0: one lane per read, columns of up to kFillLaneRows rows in an LDS ring (fill_lane.hip);
-    // cooperative (fill_coop.hip): 1: 16 lanes / 64 rows; 2: 64 lanes / 1024 rows; 3: 64 lanes / as many
-    // rows as LDS holds; 4: 64 lanes / all rows, column buffers in global memory (CoopFill::colScratch)
-    constexpr int kPaths = 5;
+    // cooperative (fill_coop.hip): 1: 16 lanes / 64 rows; 2: 64 lanes / 1024 rows, LDS only; 3: 64 lanes, as
+    // many rows as LDS holds and the rest of a column in global memory (the hybrid path: never too tall, so a
+    // fill re-routes a read at most twice).  Reads whose bases do not fit LDS beside 64 rows go to the
+    // lane-serial k_fill (FillReadsSerial).
+    constexpr int kPaths = 4;
     // The lane fill is opt-in (PBCCS_FILL_LANE=1).  It issues ~2x fewer VALU instructions for the band cells it
     // takes (rocprofv3: 142 G + 149 G for the reads it passes on, against 510 G on k_fill_coop<16>), but one
     // read's fill is a single lane's serial loop -- ~3x the latency of the 16-lane group -- and a batch's refine
@@ -699,12 +695,16 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     // round's critical path and 16-row chunks pay the per-chunk band logic 4x as often.
     auto rows_for = [&](int p, int maxI, int w) -> int {
         if (p == 0) return laneFill ? kFillLaneRows : 0;
-        if (p == 4) return coop_group_bytes(0, w, 0) <= kCoopLdsBytes ? (maxI + 64) / 64 * 64 : 0;
         if (p == 1) return 4 * coop_group_bytes(kCoopNarrowRows, w, 0) <= kCoopLdsBytes ? kCoopNarrowRows : 0;
         const long long room = ((long long)kCoopLdsBytes - (long long)coop_group_bytes(0, w, 0)) / 16 / 64 * 64;
         const long long full = (maxI + 64) / 64 * 64;   // a column never exceeds I + 1 rows
-        const long long want = p == 2 ? std::min<long long>(kCoopTallRows, full) : full;
-        return room >= want ? (int)want : (p == 3 && room >= 64 ? (int)room : 0);
+        if (p == 2) {   // LDS only
+            const long long want = std::min<long long>(kCoopTallRows, full);
+            return room >= want ? (int)want : 0;
+        }
+        // hybrid: as many LDS rows as fit (the rest of a column goes to global memory)
+        const long long want = std::min(full, room);
+        return want >= 64 ? (int)want : 0;
     };
     // PBCCS_FILL_PATHS=1: one stderr line per launch set (reads per path, wall ms, reads re-routed / regrown)
     static const bool pathTrace = std::getenv("PBCCS_FILL_PATHS") != nullptr;
@@ -779,11 +779,10 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         upload(dList_, list, stream_);
         const DevBatch B = View();
         size_t off = 0;
-        int hcapOf[kPaths] = {0, 0, 0, 0, 0};
         // the 64-lane (tall) launches run on a second stream beside the 16-lane one: a round's latency
         // is then the slower of the two, not their sum.  Fork before the first launch (after the list
         // upload), so the tall fills do not wait for the 16-lane fill.
-        const bool forked = !todo[2].empty() || !todo[3].empty() || !todo[4].empty();
+        const bool forked = !todo[2].empty() || !todo[3].empty();
         const auto tLaunch = std::chrono::steady_clock::now();
         // Headroom for in-kernel band growth (CoopFill::valBump): reads on the tall paths grow to a few
         // percent of their full (I+1)(J+1) matrix; budgeted against the device's free memory.  Growth
@@ -816,7 +815,6 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         if (forked) {
             PBCCS_HIP(hipEventRecord(evFork_, stream_));
             PBCCS_HIP(hipStreamWaitEvent(stream2_, evFork_, 0));
-            PBCCS_HIP(hipStreamWaitEvent(stream3_, evFork_, 0));
         }
         for (int p = 0; p < kPaths; ++p) {
             const int n = (int)todo[p].size();
@@ -832,11 +830,12 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.readWords = (maxI + 7) / 8;
             F.tplWords = (maxJ + 8) / 8;
             F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
-            hcapOf[p] = F.hcap;
             const int G = p == 1 ? 16 : 64;
-            F.groupBytes = coop_group_bytes(p == 4 ? 0 : F.hcap, F.readWords, F.tplWords);
-            if (p == 4) {   // two column buffers of hcap rows per read, in global memory
-                dColScratch_.reserve((size_t)n * 2 * F.hcap, false);
+            F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);
+            const int full = (maxI + 64) / 64 * 64;
+            if (p == 3 && full > F.hcap) {   // hybrid: column rows past the LDS buffer, two buffers per read
+                F.gRows = full - F.hcap;
+                dColScratch_.reserve((size_t)n * 2 * F.gRows, false);
                 F.colScratch = dColScratch_.ptr;
             }
             static const char* prioEnv = std::getenv("PBCCS_TALL_PRIO");      // "0" disables
@@ -853,7 +852,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 F.rValCap = dRValCap_.ptr;
             }
             const int* lp = dList_.ptr + off;
-            const hipStream_t st = p <= 1 ? stream_ : p == 2 ? stream2_ : stream3_;
+            const hipStream_t st = p <= 1 ? stream_ : stream2_;
             if (p == 0) Timed(kKFill, [&] { launch_fill_lane(B, F, lp, n, st); }, st);
             else Timed(p == 1 ? kKFill : kKFillTall, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
             PBCCS_HIP(hipGetLastError());
@@ -863,8 +862,6 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         if (forked) {
             PBCCS_HIP(hipEventRecord(evJoin_, stream2_));
             PBCCS_HIP(hipStreamWaitEvent(stream_, evJoin_, 0));
-            PBCCS_HIP(hipEventRecord(evJoin3_, stream3_));
-            PBCCS_HIP(hipStreamWaitEvent(stream_, evJoin3_, 0));
         }
         std::vector<int> st, fl, ua, ub;
         std::vector<double> bl;
@@ -899,9 +896,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                     nt += st[r] == kFillTall;
                     no += st[r] == kFillOverflow;
                 }
-            std::fprintf(stderr, "[fillpaths] batch=%p attempt=%d n=%zu/%zu/%zu/%zu/%zu wall=%.1fms tall=%d ovf=%d\n",
+            std::fprintf(stderr, "[fillpaths] batch=%p attempt=%d n=%zu/%zu/%zu/%zu wall=%.1fms tall=%d ovf=%d\n",
                          (void*)this, attempt, todo[0].size(), todo[1].size(), todo[2].size(), todo[3].size(),
-                         todo[4].size(),
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tLaunch).count(),
                          nt, no);
         }
@@ -909,10 +905,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         for (int p = 0; p < kPaths; ++p) {
             for (int r : todo[p]) {
                 HRead& h = reads_[r];
-                if (st[r] == kFillTall) {
-                    // skip a path whose buffer would be no taller than the one that just failed
+                if (st[r] == kFillTall) {   // never from the hybrid path (3)
+                    // long windows skip the 1024-row LDS path: their tall bands mostly outgrow it (10 kb: 662 of 786
+                    // reads went on to the hybrid path), and each step is one more launch on the round's critical path
                     int q = p + 1;
-                    if (q == 3 && hcapOf[2] > 0 && rows_for(3, (int)h.seq.size(), words(r)) <= hcapOf[2]) ++q;
+                    if (q == 2 && (long long)h.seq.size() + 1 > 4LL * kCoopTallRows) q = 3;
                     h.fillPath = q;
                     if (q >= kPaths) serial.push_back(r);
                     else next[q].push_back(r);

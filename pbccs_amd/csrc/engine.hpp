@@ -268,7 +268,7 @@ private:
         double baseline = 0.0;
         int flips = 0;
         int status = 0;
-        int fillPath = 0;   // 0: k_fill_lane, 1-4: k_fill_coop paths (FillReads), 5: lane-serial k_fill
+        int fillPath = 0;   // 0: k_fill_lane, 1: k_fill_coop<16>, 2: k_fill_coop<64> (LDS), 3: hybrid, 4: lane-serial
         long long seqOff = 0;
         long long colBase = 0;
         int colCap = 0;
@@ -295,11 +295,10 @@ private:
     int device_ = 0;
     hipStream_t stream_ = nullptr;
     hipStream_t stream2_ = nullptr;      // second stream for the tall-band fill path
-    hipStream_t stream3_ = nullptr;      // third stream: the all-rows 64-lane path, beside the second
-    hipEvent_t evFork_ = nullptr, evJoin_ = nullptr, evJoin3_ = nullptr;
+    hipEvent_t evFork_ = nullptr, evJoin_ = nullptr;
     DevVec<long long> dSelBase_;          // phased scoring: per-item ranges of the surviving mutations
     DevVec<int> dNSel_;
-    DevVec<double> dColScratch_;          // column buffers of the global-memory fill path
+    DevVec<double> dColScratch_;          // the hybrid fill path's column rows past its LDS buffers
     DevVec<unsigned long long> dBump_;   // in-kernel band growth: the value pool's free top
     std::unique_ptr<Workspace> ownWs_;
     Workspace* ws_;

@@ -38,10 +38,15 @@ struct Task {
     const unsigned* rdW;   // read bases, nibble-packed
     const unsigned* tpW;   // template window bases [0, J], nibble-packed
     const double* ctx;     // 9 x kCtxStride transition parameters
-    double* col0;
-    double* col1;
-    int hcap;              // rows per column buffer
-    bool gcol;             // column buffers live in global memory (CoopFill::colScratch), not LDS
+    // two ping-pong column buffers: rows [0, hcap) in LDS, rows [hcap, hcap + gRows) in this group's slot of
+    // CoopFill::colScratch (gcol: the hybrid 64-lane path, whose columns are never too tall)
+    double* lds0;
+    double* lds1;
+    double* glob0;
+    double* glob1;
+    int hcap;              // LDS rows per column buffer
+    int rowsCap;           // rows a column may hold (hcap, or hcap + gRows for the hybrid path)
+    bool gcol;
     int ckK;               // checkpoint interval: 0 keeps every column's values, else only ckpt_col_a/b columns
     bool chainExit;            // G = 64 serial steps with the early exit (insertion_chain64_exit)
     int slackDiv;              // regrow_bands slack: need / slackDiv
@@ -56,6 +61,15 @@ struct Task {
     long long* gB;
     long long* gCap;
 
+    // buffer b (0 / 1), row k (no runtime-indexed pointer arrays: they would live in scratch).  The hybrid
+    // path selects an LDS or global address per lane and accesses it through one generic (flat) pointer.
+    __device__ __forceinline__ double* cptr(int b, int k) const
+    {
+        if (!gcol) return (b ? lds1 : lds0) + k;
+        return k < hcap ? (b ? lds1 : lds0) + k : (b ? glob1 : glob0) + (k - hcap);
+    }
+    __device__ __forceinline__ double cget(int b, int k) const { return *cptr(b, k); }
+    __device__ __forceinline__ void cset(int b, int k, double v) const { *cptr(b, k) = v; }
     __device__ __forceinline__ int TBase(int idx) const { return nib(tpW, idx); }
     __device__ __forceinline__ int TCtx(int idx) const
     {
@@ -73,10 +87,10 @@ struct PassOut {
     bool regrow;      // the pass outgrew its region and ran to its end counting only: `used` is its exact need
 };
 
-// Column buffers in global memory (the all-rows path for columns taller than LDS holds): a column's
-// rows are written by one lane and read by its neighbours in the next column, so the group's stores must
-// have completed before the next column's loads.  One workgroup-scope fence per column (the group is one
-// wavefront on one CU, whose L1 its loads and stores share).  LDS columns need nothing: a wavefront's LDS
+// Column rows in global memory (the hybrid path's rows past the LDS buffer): a column's rows are written by
+// one lane and read by its neighbours in the next column, so the group's stores must have completed before
+// the next column's loads.  One workgroup-scope fence after each column that reached global rows (the group
+// is one wavefront on one CU, whose L1 its loads and stores share).  LDS rows need nothing: a wavefront's LDS
 // operations complete in order.
 __device__ __forceinline__ void col_fence(bool gcol)
 {
@@ -178,10 +192,8 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         a.O(0) = 0;
         a.L(0) = 0.0;
     }
-    double* prev = T.col0;
-    double* cur = T.col1;
-    if (lane == 0) prev[0] = 1.0;
-    col_fence(T.gcol);
+    int prev = 0, cur = 1;   // column buffers
+    if (lane == 0) T.cset(prev, 0, 1.0);
     int pb = 0, pe = 1;
     long long used = 1, stored = 1;   // cells computed / values kept (column 0 is always kept)
     int hb = 1, he = 1;
@@ -236,11 +248,11 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         if (b < I) {
             double carry = 0.0;
             for (int i0 = b;; i0 += G) {
-                if ((nc + 1) * G > T.hcap) { out.tall = true; return out; }
+                if ((nc + 1) * G > T.rowsCap) { out.tall = true; return out; }
                 const int i = i0 + lane;
                 const int rb = (i >= 1 && i <= I) ? nib(T.rdW, i - 1) : 15;
-                const double left = (i >= pb && i < pe) ? prev[i - pb] : 0.0;
-                const double diag = (i - 1 >= pb && i - 1 < pe) ? prev[i - 1 - pb] : 0.0;
+                const double left = (i >= pb && i < pe) ? T.cget(prev, i - pb) : 0.0;
+                const double diag = (i - 1 >= pb && i - 1 < pe) ? T.cget(prev, i - 1 - pb) : 0.0;
                 const double mpe = diag * (rb == curBase ? T.prNot : T.prThird);
                 const double m = (i == 1 && j == 1) ? mpe : ((i != 1 && j != 1) ? mpe * pMatch : 0.0);
                 const double k = (i > 1) ? (rb == nextBase ? cBranch : cStick3) : 0.0;
@@ -271,7 +283,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                     aLast = x;
                     break;
                 }
-                cur[(nc - 1) * G + lane] = x;
+                T.cset(cur, (nc - 1) * G + lane, x);
                 carry = T.g.bcast_last(x);
             }
         }
@@ -292,10 +304,10 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         for (int c = 0; c < nc; ++c) {
             const int kk = c * G + lane;
             const bool ok = b + kk < e;
-            const double x = (c == nc - 1) ? aLast : cur[kk];
+            const double x = (c == nc - 1) ? aLast : T.cget(cur, kk);
             const double v = scale ? x / mx : x;
             if (ok) {
-                cur[kk] = v;
+                T.cset(cur, kk, v);
                 if (store && stored + kk < a.cap) a.V(stored + kk) = v;
             }
             const unsigned long long hit = T.g.bits(ok && !(v < thrF));
@@ -313,10 +325,9 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         }
         used += e - b;
         stored += add;
-        col_fence(T.gcol);   // the next column's lanes read rows this column's lanes wrote
-        double* t = prev;
-        prev = cur;
-        cur = t;
+        col_fence(T.gcol && nc * G > T.hcap);   // the next column's lanes read rows this column's lanes wrote
+        prev ^= 1;
+        cur ^= 1;
         pb = b;
         pe = e;
         prevCtx = curCtx;
@@ -327,7 +338,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     }
     // pinned final match (:169-179)
     const double em = (nib(T.rdW, I - 1) == T.TBase(J - 1)) ? T.prNot : T.prThird;
-    const double lik = ((I - 1 >= pb && I - 1 < pe) ? prev[I - 1 - pb] : 0.0) * em;
+    const double lik = ((I - 1 >= pb && I - 1 < pe) ? T.cget(prev, I - 1 - pb) : 0.0) * em;
     const double c = (0.0 < lik) ? lik : 0.0;
     double v = lik, ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = lik / c; ls = log(c); }
@@ -366,10 +377,8 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         bm.L(J) = 0.0;
     }
     // the next column (j + 1) holds rows [pb, pe) at index pe - 1 - row
-    double* nxt = T.col0;
-    double* cur = T.col1;
-    if (lane == 0) nxt[0] = 1.0;
-    col_fence(T.gcol);
+    int nxt = 0, cur = 1;   // column buffers
+    if (lane == 0) T.cset(nxt, 0, 1.0);
     int pb = I, pe = I + 1;
     long long used = 1, stored = 1;   // cells computed / values kept (column J is always kept)
     int hb = I, he = I;
@@ -417,12 +426,12 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         if (e - 1 > 0) {
             double carry = 0.0;
             for (int c = 0;; ++c) {
-                if ((c + 1) * G > T.hcap) { out.tall = true; return out; }
+                if ((c + 1) * G > T.rowsCap) { out.tall = true; return out; }
                 const int off = c * G + lane;
                 const int i = e - 1 - off;
                 const int nb = (i >= 0 && i < I) ? nib(T.rdW, i) : 15;
-                const double left = (i >= pb && i < pe) ? nxt[pe - 1 - i] : 0.0;
-                const double diag = (i + 1 >= pb && i + 1 < pe) ? nxt[pe - 2 - i] : 0.0;
+                const double left = (i >= pb && i < pe) ? T.cget(nxt, pe - 1 - i) : 0.0;
+                const double diag = (i + 1 >= pb && i + 1 < pe) ? T.cget(nxt, pe - 2 - i) : 0.0;
                 const bool same = nb == nextBase;
                 const double mpe = diag * (same ? T.prNot : T.prThird);
                 const double m = (i < I - 1) ? mpe * cMatch : ((i == I - 1 && j == J - 1) ? mpe : 0.0);
@@ -454,7 +463,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                     aLast = x;
                     break;
                 }
-                cur[off] = x;
+                T.cset(cur, off, x);
                 carry = T.g.bcast_last(x);
             }
         }
@@ -473,10 +482,10 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         for (int c = 0; c < nc; ++c) {
             const int off = c * G + lane;
             const bool ok = e - 1 - off >= b;
-            const double x = (c == nc - 1) ? aLast : cur[off];
+            const double x = (c == nc - 1) ? aLast : T.cget(cur, off);
             const double v = scale ? x / mx : x;
             if (ok) {
-                cur[off] = v;
+                T.cset(cur, off, v);
                 if (store && stored + off < bm.cap) bm.V(stored + off) = v;
             }
             const unsigned long long hit = T.g.bits(ok && !(v < thrF));
@@ -494,10 +503,9 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         }
         used += e - b;
         stored += add;
-        col_fence(T.gcol);
-        double* t = nxt;
-        nxt = cur;
-        cur = t;
+        col_fence(T.gcol && nc * G > T.hcap);
+        nxt ^= 1;
+        cur ^= 1;
         pb = b;
         pe = e;
         hb = b;
@@ -505,7 +513,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         nextBase = curBase;
     }
     const double em = (T.TBase(0) == nib(T.rdW, 0)) ? T.prNot : T.prThird;
-    const double raw = em * ((1 >= pb && 1 < pe) ? nxt[pe - 2] : 0.0);
+    const double raw = em * ((1 >= pb && 1 < pe) ? T.cget(nxt, pe - 2) : 0.0);
     const double c = (0.0 < raw) ? raw : 0.0;
     double v = raw, ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = raw / c; ls = log(c); }
@@ -545,9 +553,10 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     const int t = blockIdx.x * (64 / G) + grp;
     const int lane = threadIdx.x & (G - 1);
     unsigned char* gbase = smem + (size_t)grp * F.groupBytes;
-    // GC: the two column buffers are this slot's part of F.colScratch; LDS holds only ctx, read, template
-    double* col = GC ? F.colScratch + (size_t)t * 2 * F.hcap : reinterpret_cast<double*>(gbase);
-    double* ctx = GC ? reinterpret_cast<double*>(gbase) : col + 2 * F.hcap;
+    // LDS: two column buffers of hcap rows, ctx, read, template.  GC (hybrid): rows past hcap go to this
+    // slot's part of F.colScratch (2 x gRows doubles)
+    double* col = reinterpret_cast<double*>(gbase);
+    double* ctx = col + 2 * F.hcap;
     unsigned* rdW = reinterpret_cast<unsigned*>(ctx + kCtxDoubles + 1);
     unsigned* tpW = rdW + F.readWords;
 
@@ -602,9 +611,12 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     T.rdW = rdW;
     T.tpW = tpW;
     T.ctx = ctx;
-    T.col0 = col;
-    T.col1 = col + F.hcap;
+    T.lds0 = col;
+    T.lds1 = col + F.hcap;
+    T.glob0 = GC ? F.colScratch + (size_t)t * 2 * F.gRows : nullptr;
+    T.glob1 = GC ? T.glob0 + F.gRows : nullptr;
     T.hcap = F.hcap;
+    T.rowsCap = GC ? F.hcap + F.gRows : F.hcap;
     T.gcol = GC;
     T.chainExit = F.chainExit;
     T.ckK = B.rCkpt ? B.rCkpt[r] : 0;
