@@ -38,7 +38,9 @@ def test_plan_estimates_grow_with_length_and_passes():
     b = synth.make_zmws(1, 10000, 8, seed=1)[0]
     c = synth.make_zmws(1, 2000, 20, seed=1)[0]
     _, est = pbccs_amd.plan_batches([a, b, c], 1e12)
-    assert est[1] > 20 * est[0] and 1.8 * est[0] < est[2] < 2.2 * est[0]
+    # 10 kb windows keep checkpointed tall bands (every K-th column), so they grow by less
+    # than the full (I+1)(J+1) matrix would, but still well above linear in the window
+    assert est[1] > 6 * est[0] and 1.8 * est[0] < est[2] < 2.2 * est[0]
     # the one-batch budget of a 2 kb / 10-pass ZMW is within ~2x of the measured 13.5 MB
     assert 13.5e6 <= est[0] <= 30e6
 
