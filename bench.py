@@ -531,6 +531,44 @@ def quiver_stage(args, rank, world, eng, barrier, sync, seed0):
         dist.destroy_process_group()
 
 
+def ccs_cpu_baseline(args, n):
+    """Consensus.h's per-ZMW path on the host (include/pacbio/ccs/Consensus.h:395-552): FilterReads and
+    ExtractMappedRead (pbccs_amd.driver, host code), the SparsePoa restatement (oracle/poa_oracle.cpp) and the
+    polish restatement (oracle/arrow_oracle.cpp: AddRead, RefineConsensus, ConsensusQVs), one ZMW per task on
+    the host threads like `ccs --numThreads` (src/main/ccs.cpp:222-230)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    from pbccs_amd import driver, synth
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    threads = max(1, min(args.cpu_threads or share, os.cpu_count() or 1, n))
+    chunks = [{"snr": z["snr"], "reads": [{"seq": r["seq"]} for r in z["reads"]]}
+              for z in synth.make_zmws(n, args.length, args.passes, seed=args.seed + 99991)]
+    O.lib()
+
+    def one(c):
+        reads = driver.filter_reads(c["reads"], 10)
+        if not reads or all(r is None for r in reads):
+            return "NoSubreads"
+        p = O.sparse_poa([None if r is None else r["seq"] for r in reads])
+        if len(p["consensus"]) < 10:
+            return "TooShort"
+        mapped = [driver.extract_mapped_read(reads[i], p["summaries"][k], 10)
+                  for i, k in enumerate(p["keys"]) if k >= 0]
+        O.polish_zmw(p["consensus"], [m for m in mapped if m is not None], c["snr"])
+        return "Polished"
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(one, chunks))
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+            "nproc": os.cpu_count(),
+            "sample": f"{n} synthetic ZMWs of the same config (seed {args.seed + 99991}): FilterReads, "
+                      f"oracle/poa_oracle.cpp SparsePoa, ExtractMappedRead, oracle/arrow_oracle.cpp polish (AddRead, "
+                      f"RefineConsensus, ConsensusQVs; every ZMW polished, the gates not applied) one ZMW per task "
+                      f"on {threads} host threads, {dt:.1f} s wall"}
+
+
 def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
     """configs[1] end to end from raw subreads in one native call (pbccs_ccs_batch): Consensus.h's
     FilterReads, the POA draft on the GPU, TooShort, ExtractMappedRead and the polish through the ZMW work
@@ -572,6 +610,9 @@ def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
                       "slots": slots, "chunk": args.ccs_chunk or "planned", "parallelism": f"zmw-shard x{world}"},
            "zmw_status": statuses, "poa_wall_ms": round(st["total_ms"], 1),
            "poa_device_ms": round(st["device_ms"], 1), "poa_thread_ms": round(st["thread_ms"], 1)}
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        out["cpu_baseline"] = ccs_cpu_baseline(args, min(args.cpu_sample, 64))
+        out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
     if rank == 0:
         emit(out)
     if world > 1:

@@ -955,13 +955,15 @@ __device__ __forceinline__ int wave_max(int v)
 
 // LDS stage of one wave: the alpha columns sc-1 and beta columns bc its 64 lanes read (contiguous in
 // HBM because fills append columns in order) and the read bases under their rows.
+// 448 staged alpha and beta values and 448 read bases per wave: 30.5 KB per 4-wave block, so five blocks
+// (five waves per SIMD) fit the CU's 160 KB of LDS.
 #ifndef PBCCS_SCORE_STAGE
-#define PBCCS_SCORE_STAGE 512
+#define PBCCS_SCORE_STAGE 448
 #endif
 constexpr int kScoreWaves = 4;
 constexpr int kStageA = PBCCS_SCORE_STAGE;
 constexpr int kStageB = PBCCS_SCORE_STAGE;
-constexpr int kStageR = 2 * PBCCS_SCORE_STAGE;
+constexpr int kStageR = PBCCS_SCORE_STAGE;
 struct WaveStage {
     double a[kStageA];
     double b[kStageB];
@@ -970,12 +972,12 @@ struct WaveStage {
 
 // One wave per (work item, read, 64-mutation chunk): the lanes take consecutive mutations of one read,
 // i.e. adjacent template positions, so the wave shares a handful of band columns.
-// Occupancy experiment switch (off): a 384-entry stage with PBCCS_SCORE_WAVES=5 runs 5 waves per SIMD but
-// spills 12 VGPRs, and a kernel with a private segment needs scratch allocated at dispatch -- which fails
-// (HSA_STATUS_ERROR_OUT_OF_RESOURCES, process abort) when the band pools have taken the device memory.
-// The default build keeps k_score spill-free (100 VGPRs, 4 waves per SIMD).
+// Occupancy: five waves per SIMD (<= 96 VGPRs; the stage above fits five blocks per CU).  The wave index is
+// made wave-uniform (readfirstlane), so the item search and the per-item and per-read loads are scalar and
+// the VGPR budget fits without spills (a kernel with a private segment needs scratch allocated at dispatch,
+// which fails when the band pools have taken the device memory; check_resources.py refuses any).
 #ifndef PBCCS_SCORE_WAVES
-#define PBCCS_SCORE_WAVES 0
+#define PBCCS_SCORE_WAVES 5
 #endif
 #if PBCCS_SCORE_WAVES > 0
 #define PBCCS_SCORE_OCC __attribute__((amdgpu_waves_per_eu(PBCCS_SCORE_WAVES)))
@@ -985,7 +987,7 @@ struct WaveStage {
 __global__ void __launch_bounds__(256) PBCCS_SCORE_OCC k_score(DevBatch B, ScoreWork W, ScoreScratch scratch)
 {
     __shared__ WaveStage stage[kScoreWaves];
-    const int wid = threadIdx.x >> 6;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: the item search and per-item loads go scalar
     const long long wave = (long long)blockIdx.x * kScoreWaves + wid;
     const int lane = threadIdx.x & 63;
     const bool waveLive = wave < W.waveStart[W.nWork];

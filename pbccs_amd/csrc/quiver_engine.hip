@@ -370,24 +370,16 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
 
 void QuiverBatch::Deltas(int zi, const std::vector<int>& codes, std::vector<float>* out)
 {
+    // the batched scoring path (k_qscore_mid + the listed edge cases) over one item: NaN for inactive reads
+    // and for reads that do not score a mutation, as MultiReadMutationScorer::Score skips them
     const HZmw& z = zmws_.at(zi);
-    const int nr = (int)z.reads.size();
-    const long long M = (long long)codes.size();
-    out->assign((size_t)M * nr, std::numeric_limits<float>::quiet_NaN());
-    if (M == 0 || nr == 0) return;
-    std::vector<int> tr, tm;
-    std::vector<long long> slot;
-    for (long long m = 0; m < M; ++m)
-        for (int k = 0; k < nr; ++k) {
-            if (!reads_[z.reads[k]].active) continue;
-            tr.push_back(z.reads[k]);
-            tm.push_back((int)m);
-            slot.push_back(m * nr + k);
-        }
-    if (tr.empty()) return;
-    std::vector<float> d;
-    RunScore(tr, tm, codes, false, &d);
-    for (size_t t = 0; t < tr.size(); ++t) (*out)[slot[t]] = d[t];
+    const long long nt = (long long)codes.size() * (long long)z.reads.size();
+    out->assign((size_t)nt, std::numeric_limits<float>::quiet_NaN());
+    if (nt == 0) return;
+    std::vector<long long> taskStart, mutStart;
+    ScoreDeltas({zi}, {codes}, &taskStart, &mutStart);
+    get(*out, dDelta_, (size_t)nt, stream_);
+    QHIP(hipStreamSynchronize(stream_));
 }
 
 void QuiverBatch::RunScore(const std::vector<int>& tr, const std::vector<int>& tm, const std::vector<int>& codes,
@@ -603,12 +595,16 @@ std::vector<int> QuiverBatch::QVs(int zi)   // ConsensusQVs (Consensus-inl.hpp:2
 // hipCUB compaction of the favourable list and k_best_subset (BestSubset) on the device.
 constexpr long long kTaskChunk = 1LL << 21;
 
-void QuiverBatch::ScoreRound(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes, int sep,
-                             std::vector<std::vector<Scored>>* fav, std::vector<std::vector<Scored>>* picked,
-                             std::vector<std::vector<float>>* all)
+// Every (mutation, read) delta of the listed scorers into dDelta_, laid out [item][mutation][read] from
+// taskStart[w]; the item tables stay on the device for k_qreduce.
+void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes,
+                              std::vector<long long>* taskStartOut, std::vector<long long>* mutStartOut)
 {
     const int n = (int)zs.size();
-    std::vector<long long> taskStart(n + 1, 0), mutStart(n + 1, 0);
+    std::vector<long long>& taskStart = *taskStartOut;
+    std::vector<long long>& mutStart = *mutStartOut;
+    taskStart.assign(n + 1, 0);
+    mutStart.assign(n + 1, 0);
     std::vector<int> readBase(n), nReads(n), readList, flat;
     std::vector<float> fastThr(n);
     for (int w = 0; w < n; ++w) {
@@ -621,7 +617,7 @@ void QuiverBatch::ScoreRound(const std::vector<int>& zs, const std::vector<std::
         mutStart[w + 1] = mutStart[w] + (long long)codes[w].size();
         taskStart[w + 1] = taskStart[w] + (long long)codes[w].size() * nReads[w];
     }
-    const long long nMut = mutStart[n], nTask = taskStart[n];
+    const long long nTask = taskStart[n];
     std::vector<int> active(reads_.size());
     for (size_t r = 0; r < reads_.size(); ++r) active[r] = reads_[r].active ? 1 : 0;
     Upload();
@@ -635,8 +631,47 @@ void QuiverBatch::ScoreRound(const std::vector<int>& zs, const std::vector<std::
     put(dWFast_, fastThr, stream_);
     put(dCodes_, flat, stream_);
     dDelta_.reserve(std::max<long long>(nTask, 1), false);
-    for (long long t0 = 0; t0 < nTask;) {
-        const long long m = std::min(kTaskChunk, nTask - t0);
+    // middle cases: k_qscore_mid, one wave per (item, read, 64-mutation chunk); it lists the edge cases
+    std::vector<long long> waveStart(n + 1, 0), mutCount(n);
+    long long edgeCap = 1024;
+    for (int w = 0; w < n; ++w) {
+        mutCount[w] = mutStart[w + 1] - mutStart[w];
+        waveStart[w + 1] = waveStart[w] + (mutCount[w] > 0 ? (long long)nReads[w] * ((mutCount[w] + 63) / 64) : 0);
+        edgeCap += (long long)nReads[w] * std::min<long long>(mutCount[w], 160);   // ~7 edge positions per read
+    }
+    put(dWaveStart_, waveStart, stream_);
+    put(dWMutCount_, mutCount, stream_);
+    dEdgeCount_.reserve(1, false);
+    unsigned long long nEdge = 0;
+    for (int attempt = 0;; ++attempt) {
+        dEdge_.reserve(std::max<long long>(edgeCap, 1), false);
+        QHIP(hipMemsetAsync(dEdgeCount_.ptr, 0, sizeof(unsigned long long), stream_));
+        QMidWork MW;
+        MW.nWork = n;
+        MW.waveStart = dWaveStart_.ptr;
+        MW.wTaskStart = dWTaskStart_.ptr;
+        MW.wMutBase = dWMutBase_.ptr;
+        MW.wMutCount = dWMutCount_.ptr;
+        MW.wReadBase = dWReadBase_.ptr;
+        MW.wNReads = dWNReads_.ptr;
+        MW.readList = dReadList_.ptr;
+        MW.rActive = dRActive_.ptr;
+        MW.codes = dCodes_.ptr;
+        MW.delta = dDelta_.ptr;
+        MW.edgeList = dEdge_.ptr;
+        MW.edgeCount = dEdgeCount_.ptr;
+        MW.edgeCap = edgeCap;
+        launch_qscore_mid(View(), MW, waveStart[n], stream_);
+        QHIP(hipGetLastError());
+        QHIP(hipMemcpyAsync(&nEdge, dEdgeCount_.ptr, sizeof(nEdge), hipMemcpyDeviceToHost, stream_));
+        QHIP(hipStreamSynchronize(stream_));
+        if ((long long)nEdge <= edgeCap) break;
+        if (attempt > 2) throw DeviceError("quiver edge-case list overflow");
+        edgeCap = (long long)nEdge;   // the list was cut short: rerun with room for every edge case
+    }
+    // edge cases (ExtendAlpha to the end, ExtendBeta, whole fills): k_qscore over the listed tasks
+    for (long long t0 = 0; t0 < (long long)nEdge;) {
+        const long long m = std::min(kTaskChunk, (long long)nEdge - t0);
         for (int attempt = 0;; ++attempt) {
             QHIP(hipMemsetAsync(dScratchTop_.ptr, 0, sizeof(unsigned long long), stream_));
             QHIP(hipMemsetAsync(dOverflow_.ptr, 0, sizeof(int), stream_));
@@ -650,7 +685,8 @@ void QuiverBatch::ScoreRound(const std::vector<int>& zs, const std::vector<std::
             W.nTasks = m;
             W.raw = 0;
             W.nWork = n;
-            W.taskBase = t0;
+            W.taskBase = 0;
+            W.taskList = dEdge_.ptr + t0;
             W.wTaskStart = dWTaskStart_.ptr;
             W.wMutBase = dWMutBase_.ptr;
             W.wReadBase = dWReadBase_.ptr;
@@ -668,6 +704,16 @@ void QuiverBatch::ScoreRound(const std::vector<int>& zs, const std::vector<std::
         }
         t0 += m;
     }
+}
+
+void QuiverBatch::ScoreRound(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes, int sep,
+                             std::vector<std::vector<Scored>>* fav, std::vector<std::vector<Scored>>* picked,
+                             std::vector<std::vector<float>>* all)
+{
+    const int n = (int)zs.size();
+    std::vector<long long> taskStart, mutStart;
+    ScoreDeltas(zs, codes, &taskStart, &mutStart);
+    const long long nMut = mutStart[n];
     dMScore_.reserve(std::max<long long>(nMut, 1), false);
     dFav_.reserve(std::max<long long>(nMut, 1), false);
     QReduceWork R;

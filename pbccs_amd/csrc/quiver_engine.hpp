@@ -107,6 +107,8 @@ private:
         int code;
         float score;
     };
+    void ScoreDeltas(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes,
+                     std::vector<long long>* taskStart, std::vector<long long>* mutStart);
     void ScoreRound(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes, int sep,
                     std::vector<std::vector<Scored>>* fav, std::vector<std::vector<Scored>>* picked,
                     std::vector<std::vector<float>>* all);
@@ -136,6 +138,8 @@ private:
     DevVec<unsigned char> dMoves_;
     // batched rounds
     DevVec<long long> dWTaskStart_, dWMutBase_, dSel_, dSelCount_, dSelBase_;
+    DevVec<long long> dWaveStart_, dWMutCount_, dEdge_;   // k_qscore_mid work + its edge-case task list
+    DevVec<unsigned long long> dEdgeCount_;
     DevVec<int> dWReadBase_, dWNReads_, dReadList_, dRActive_, dSelCode_, dSelRank_, dNSel_;
     DevVec<float> dWFast_;
     DevVec<double> dMScore_, dSelScore_;

@@ -969,7 +969,7 @@ __global__ void __launch_bounds__(64) k_qscore(QBatch B, QScoreWork W)
 {
     const long long lt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (lt >= W.nTasks) return;
-    const long long t = W.taskBase + lt;
+    const long long t = W.taskList ? W.taskList[lt] : W.taskBase + lt;
     int r, code;
     if (W.nWork > 0) {   // batched round: decode (item, mutation, read) from the task number
         int lo = 0, hi = W.nWork;
@@ -1108,6 +1108,349 @@ __global__ void __launch_bounds__(256) k_qreduce(QReduceWork W)
     W.fav[g] = (fast && (double)sum > 0.04) ? 1 : 0;   // MIN_FAVORABLE_SCOREDIFF (:52), a double
 }
 
+// ---- k_qscore_mid: ScoreMutation's middle case, one wavefront per (item, read, 64-mutation chunk) ----------
+// MutationScorer::ScoreMutation (Quiver/MutationScorer.cpp:150-175) away from the window ends is ExtendAlpha
+// over two columns (SseRecursor.cpp:433-551 / SimpleRecursor.cpp:303-388) and LinkAlphaBeta of those with
+// beta (SseRecursor.cpp:355-431 / SimpleRecursor.cpp:232-295).  Here the three are one top-down walk over the
+// link's rows: row i of extension column 0, then of column 1, then row i's link terms.  A row only needs its
+// predecessor's values, so the extension columns never leave registers (k_qscore writes them to a bump
+// scratch and reads them back).  Every term keeps the reference's order: an extension column's scalar head
+// rows combine Inc, Extra, Merge, Del; its 4-row SSE blocks combine Inc, Merge, Del from -FLT_MAX and then the
+// Extra cascade; the link's block rows accumulate into 4 SSE lanes, its tail rows into one, and the lanes are
+// folded in lane order at the end.  The read's QV-feature rows under the wave's lanes are staged in LDS.
+namespace {
+
+struct QMidStage {   // one wave's QV-feature rows [lo, lo + kQMidStageRows)
+    float ins[kQMidStageRows], subs[kQMidStageRows], del[kQMidStageRows], tag[kQMidStageRows],
+        merge[kQMidStageRows];
+    char seq[kQMidStageRows];
+};
+
+struct QCol {   // one band column: value at row i is p[i] for i in [x, y), else -FLT_MAX
+    const float* p;
+    int x, y;
+    __device__ __forceinline__ float at(int i) const { return (i >= x && i < y) ? p[i] : kNegInf; }
+};
+
+__device__ __forceinline__ QCol qcol(const QBand& m, int j)
+{
+    QCol c;
+    const int2 r = m.range[j];
+    c.x = r.x;
+    c.y = r.y;
+    c.p = m.val + m.off[j] - r.x;
+    return c;
+}
+
+// QvEvaluator terms (QvEvaluator.hpp:150-207) from a row's features and a template base
+struct QMerge {   // Merge(i, j) for the template pair (t(j), t(j + 1)): only reads of a homopolymer base merge
+    int base;     // t(j) when t(j) == t(j + 1), else -1 (never matches a read base)
+    float c, s;
+};
+__device__ __forceinline__ QMerge qmerge(const QParams& P, char a, char b)
+{
+    QMerge m;
+    const int k = tpl_code(a);
+    m.base = (a == b) ? (int)a : -1;
+    m.c = P.Merge[k];
+    m.s = P.MergeS[k];
+    return m;
+}
+
+template <bool SIMPLE, class FEAT>
+__device__ __forceinline__ float qmid_walk(const QParams& P, bool sp, bool merge, int I, const FEAT& F, int j0,
+                                           const QCol& A1, const QCol& A2, const QCol& B0, const QCol& B1, int b0,
+                                           int e0, int b1, int e1, int lb, int le, char t0m1, char t0, char t0p1,
+                                           const QMerge& m0, const QMerge& m1, char l1, const QMerge& ml0,
+                                           const QMerge& ml1)
+{
+    auto inc = [&](int s, float subs, char tb) { return (s == tb) ? P.Match : P.Mismatch + P.MismatchS * subs; };
+    auto del = [&](int i, float tag, float d, char tb) {
+        return (i < I && (float)tb == tag) ? P.DeletionWithTag + P.DeletionWithTagS * d : P.DeletionN;
+    };
+    auto extra = [&](int s, float ins, char tb) { return (s == tb) ? P.Branch + P.BranchS * ins : P.Nce + P.NceS * ins; };
+    auto mrg = [&](int s, float mq, const QMerge& m) { return (s == m.base) ? m.c + m.s * mq : kNegInf; };
+
+    // first SSE-block row of each extension column (the head loop of SseRecursor::ExtendAlpha)
+    int p0 = b0, p1 = b1;
+    if (!SIMPLE) {
+        while (p0 < e0 && (p0 == 0 || (e0 - p0) % 4 != 0)) ++p0;
+        while (p1 < e1 && (p1 == 0 || (e1 - p1) % 4 != 0)) ++p1;
+    }
+    const int blockEnd = SIMPLE ? lb : lb + 4 * max(0, (le - 4 - lb + 3) / 4);   // link rows in 4-row blocks
+
+    // row i - 1 state
+    float e0p = kNegInf, e1p = kNegInf;
+    float a1p = (lb >= 1) ? A1.at(lb - 1) : kNegInf;
+    float a2p = (lb >= 1) ? A2.at(lb - 1) : kNegInf;
+    int sP = 0;
+    float insP = 0.f, subsP = 0.f, mergeP = 0.f;
+    if (lb >= 1) {
+        sP = F.seq(lb - 1);
+        insP = F.ins(lb - 1);
+        subsP = F.subs(lb - 1);
+        mergeP = F.merge(lb - 1);
+    }
+    float bCur = B0.at(lb);
+    float v4a = kNegInf, v4b = kNegInf, v4c = kNegInf, v4d = kNegInf, v = kNegInf;
+    for (int i = lb; i < le; ++i) {
+        int s = 0;
+        float ins = 0.f, subs = 0.f, d = 0.f, tag = 0.f, mq = 0.f;
+        if (i < I) {
+            s = F.seq(i);
+            ins = F.ins(i);
+            subs = F.subs(i);
+            d = F.del(i);
+            tag = F.tag(i);
+            mq = F.merge(i);
+        }
+        const float a1c = A1.at(i);
+        // extension column 0 (template column j0)
+        float e0c = kNegInf;
+        if (i >= b0 && i < e0) {
+            float x = kNegInf;
+            if (SIMPLE) {
+                if (i > 0) x = comb(sp, x, a1p + inc(sP, subsP, t0m1));
+                if (i > 0) x = comb(sp, x, e0p + extra(sP, insP, t0));
+                x = comb(sp, x, a1c + del(i, tag, d, t0m1));
+                if (merge && i > 0) x = comb(sp, x, a2p + mrg(sP, mergeP, m0));
+            } else if (i < p0) {
+                if (i > 0) {
+                    x = comb(sp, x, a1p + inc(sP, subsP, t0m1));
+                    x = comb(sp, x, e0p + extra(sP, insP, t0));
+                    if (merge) x = comb(sp, x, a2p + mrg(sP, mergeP, m0));
+                }
+                x = comb(sp, x, a1c + del(i, tag, d, t0m1));
+            } else {
+                x = comb4(sp, x, a1p + inc(sP, subsP, t0m1));
+                if (merge && j0 >= 2) x = comb4(sp, x, a2p + mrg(sP, mergeP, m0));
+                x = comb4(sp, x, a1c + del(i, tag, d, t0m1));
+                x = comb(sp, x, e0p + extra(sP, insP, t0));
+            }
+            e0c = x;
+        }
+        // extension column 1 (template column j0 + 1): its merge term reads alpha column j0 - 1, as the
+        // reference's ExtendAlpha does for every extension column
+        float e1c = kNegInf;
+        if (i >= b1 && i < e1) {
+            float x = kNegInf;
+            if (SIMPLE) {
+                if (i > 0) x = comb(sp, x, e0p + inc(sP, subsP, t0));
+                if (i > 0) x = comb(sp, x, e1p + extra(sP, insP, t0p1));
+                x = comb(sp, x, e0c + del(i, tag, d, t0));
+                if (merge && i > 0) x = comb(sp, x, a1p + mrg(sP, mergeP, m1));
+            } else if (i < p1) {
+                if (i > 0) {
+                    x = comb(sp, x, e0p + inc(sP, subsP, t0));
+                    x = comb(sp, x, e1p + extra(sP, insP, t0p1));
+                    if (merge) x = comb(sp, x, a1p + mrg(sP, mergeP, m1));
+                }
+                x = comb(sp, x, e0c + del(i, tag, d, t0));
+            } else {
+                x = comb4(sp, x, e0p + inc(sP, subsP, t0));
+                if (merge) x = comb4(sp, x, a1p + mrg(sP, mergeP, m1));
+                x = comb4(sp, x, e0c + del(i, tag, d, t0));
+                x = comb(sp, x, e1p + extra(sP, insP, t0p1));
+            }
+            e1c = x;
+        }
+        // LinkAlphaBeta row i: extension columns (ac - 2, ac - 1) = (0, 1) against beta (bc, bc + 1)
+        const float bN0 = B0.at(i + 1), bN1 = B1.at(i + 1);
+        if (SIMPLE) {
+            if (i < I) {
+                v = comb(sp, v, e1c + inc(s, subs, l1) + bN0);
+                v = comb(sp, v, e0c + mrg(s, mq, ml0) + bN0);
+                v = comb(sp, v, e1c + mrg(s, mq, ml1) + bN1);
+            }
+            v = comb(sp, v, e1c + del(i, tag, d, l1) + bCur);
+        } else if (i < blockEnd) {
+            float x = v4a;
+            x = comb4(sp, x, e1c + inc(s, subs, l1) + bN0);
+            if (merge) {
+                x = comb4(sp, x, e0c + mrg(s, mq, ml0) + bN0);
+                x = comb4(sp, x, e1c + mrg(s, mq, ml1) + bN1);
+            }
+            x = comb4(sp, x, e1c + del(i, tag, d, l1) + bCur);
+            v4a = v4b;   // rotate: the next row accumulates into the next SSE lane
+            v4b = v4c;
+            v4c = v4d;
+            v4d = x;
+        } else {
+            if (i < I) {
+                v = comb(sp, v, e1c + inc(s, subs, l1) + bN0);
+                if (merge) {
+                    v = comb(sp, v, e0c + mrg(s, mq, ml0) + bN0);
+                    v = comb(sp, v, e1c + mrg(s, mq, ml1) + bN1);
+                }
+            }
+            v = comb(sp, v, e1c + del(i, tag, d, l1) + bCur);
+        }
+        e0p = e0c;
+        e1p = e1c;
+        a2p = A2.at(i);
+        a1p = a1c;
+        sP = s;
+        insP = ins;
+        subsP = subs;
+        mergeP = mq;
+        bCur = bN0;
+    }
+    if (SIMPLE) return v;
+    float acc = kNegInf;   // std::accumulate over the 4 SSE lanes, then the tail
+    acc = comb(sp, acc, v4a);
+    acc = comb(sp, acc, v4b);
+    acc = comb(sp, acc, v4c);
+    acc = comb(sp, acc, v4d);
+    return comb(sp, acc, v);
+}
+
+struct QFeatLds {
+    const QMidStage* st;
+    int lo;
+    __device__ __forceinline__ int seq(int i) const { return st->seq[i - lo]; }
+    __device__ __forceinline__ float ins(int i) const { return st->ins[i - lo]; }
+    __device__ __forceinline__ float subs(int i) const { return st->subs[i - lo]; }
+    __device__ __forceinline__ float del(int i) const { return st->del[i - lo]; }
+    __device__ __forceinline__ float tag(int i) const { return st->tag[i - lo]; }
+    __device__ __forceinline__ float merge(int i) const { return st->merge[i - lo]; }
+};
+
+struct QFeatHbm {
+    QRead r;
+    __device__ __forceinline__ int seq(int i) const { return r.seq[i]; }
+    __device__ __forceinline__ float ins(int i) const { return r.ins[i]; }
+    __device__ __forceinline__ float subs(int i) const { return r.subs[i]; }
+    __device__ __forceinline__ float del(int i) const { return r.del[i]; }
+    __device__ __forceinline__ float tag(int i) const { return r.tag[i]; }
+    __device__ __forceinline__ float merge(int i) const { return r.merge[i]; }
+};
+
+}  // namespace
+
+__global__ void __launch_bounds__(64 * kQMidWaves) k_qscore_mid(QBatch B, QMidWork W)
+{
+    __shared__ QMidStage stage[kQMidWaves];
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar item search
+    const int lane = threadIdx.x & 63;
+    const long long wave = (long long)blockIdx.x * kQMidWaves + wid;
+    const bool waveLive = wave < W.waveStart[W.nWork];
+    int w = 0;
+    if (waveLive) {   // binary search of the work item (wave-uniform)
+        int lo = 0, hi = W.nWork;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (W.waveStart[mid] <= wave) lo = mid; else hi = mid;
+        }
+        w = lo;
+    }
+    w = __builtin_amdgcn_readfirstlane(w);
+    const int nr = waveLive ? W.wNReads[w] : 1;
+    const long long M = waveLive ? W.wMutCount[w] : 0;
+    const int chunks = (int)max(1LL, (M + 63) >> 6);
+    const long long local = waveLive ? wave - W.waveStart[w] : 0;
+    const int rd = (int)(local / chunks);
+    const long long m = (local % chunks) * 64 + lane;
+    const bool valid = waveLive && m < M;
+    const int r = __builtin_amdgcn_readfirstlane(waveLive ? W.readList[W.wReadBase[w] + rd] : 0);
+    const long long t = valid ? W.wTaskStart[w] + m * nr + rd : 0;
+
+    // classify the lane: not scored (NaN), middle case (here), edge case (k_qscore's listed form)
+    bool middle = false;
+    int os = 0, oe = 0, type = 0, ld = 0;
+    char ob = 'A';
+    const int ts = B.rTs[r], te = B.rTe[r];
+    const int J = te - ts;
+    if (valid) {
+        const int code = W.codes[W.wMutBase[w] + m];
+        type = (code >> 2) & 3;
+        const int pos = code >> 4, base = code & 3;
+        const int ms = pos, me = (type == 0) ? pos : pos + 1;
+        const bool scores = W.rActive[r] && ((type == 0) ? (ts < ms && me <= te) : (ts < me && ms < te));
+        if (!scores) {
+            W.delta[t] = __builtin_nanf("");
+        } else {
+            const char* kB = "ACGT";
+            if (B.rStrand[r] == 0) { os = ms - ts; oe = me - ts; ob = kB[base]; }
+            else { os = te - me; oe = te - ms; ob = kB[3 - base]; }
+            ld = (type == 0) ? 1 : (type == 1) ? -1 : 0;
+            middle = !(os < 3) && !(oe > J - 2);
+            if (!middle) {
+                const unsigned long long slot = atomicAdd(W.edgeCount, 1ULL);
+                if ((long long)slot < W.edgeCap) W.edgeList[slot] = t;
+            }
+        }
+    }
+    ReadView v = read_view(B, r);
+    const QParams& P = *v.ev.p;
+    const int I = v.ev.I();
+    const QBand a = arena(v, B.rCurA[r]);
+    const QBand b = arena(v, 2 + B.rCurB[r]);
+    const int j0 = (type == 1) ? os - 1 : os;   // ExtendAlpha's first column
+    const int bc = 1 + oe;                       // beta link column
+    int b0 = 0, e0 = 0, b1 = 0, e1 = 0, lb = 0, le = 0;
+    QCol A1{}, A2{}, B0{}, B1{};
+    if (middle) {
+        A1 = qcol(a, j0 - 1);
+        A2 = qcol(a, j0 - 2);
+        B0 = qcol(b, bc);
+        B1 = qcol(b, bc + 1);
+        const int2 r0 = a.range[j0], r1 = a.range[j0 + 1];
+        b0 = r0.x; e0 = r0.y; b1 = r1.x; e1 = r1.y;
+        lb = min(min(b0, b1), min(B0.x, B1.x));
+        le = max(max(e0, e1), max(B0.y, B1.y));
+    }
+    // the wave's feature rows [lb - 1, le) of its middle lanes, staged in LDS when they fit
+    int rLo = middle ? max(0, lb - 1) : INT_MAX, rHi = middle ? min(le, I) : -1;
+    for (int o = 32; o > 0; o >>= 1) {
+        rLo = min(rLo, __shfl_xor(rLo, o, 64));
+        rHi = max(rHi, __shfl_xor(rHi, o, 64));
+    }
+    const bool staged = rHi >= rLo && rHi - rLo <= kQMidStageRows;
+    QMidStage& st = stage[wid];
+    if (staged) {
+        const QRead& R = v.ev.r;
+        for (int q = lane; q < rHi - rLo; q += 64) {
+            const int i = rLo + q;
+            st.seq[q] = R.seq[i];
+            st.ins[q] = R.ins[i];
+            st.subs[q] = R.subs[i];
+            st.del[q] = R.del[i];
+            st.tag[q] = R.tag[i];
+            st.merge[q] = R.merge[i];
+        }
+    }
+    __syncthreads();   // every wave of the block reaches this point exactly once
+    if (!middle) return;
+
+    // template bases of the mutated window (OrientedMutation applied virtually, as k_qscore's QTpl)
+    QTpl T = v.ev.t;
+    T.editPos = os;
+    T.editType = type;
+    T.editBase = ob;
+    T.len = J + ld;
+    const int absc = 1 + oe + ld;   // absolute link column
+    const char t0m2 = T.at(j0 - 2), t0m1 = T.at(j0 - 1), t0 = T.at(j0), t0p1 = T.at(j0 + 1);
+    const char la = T.at(absc - 2), l1 = T.at(absc - 1), lc = T.at(absc);
+    const QMerge m0 = qmerge(P, t0m2, t0m1), m1 = qmerge(P, t0m1, t0);
+    const QMerge ml0 = qmerge(P, la, l1), ml1 = qmerge(P, l1, lc);
+    const bool sp = P.sumProduct != 0, mv = (P.moves & kMerge) != 0;
+    float score;
+    if (staged) {
+        const QFeatLds F{&st, rLo};
+        score = P.simple ? qmid_walk<true>(P, sp, mv, I, F, j0, A1, A2, B0, B1, b0, e0, b1, e1, lb, le, t0m1, t0, t0p1,
+                                           m0, m1, l1, ml0, ml1)
+                         : qmid_walk<false>(P, sp, mv, I, F, j0, A1, A2, B0, B1, b0, e0, b1, e1, lb, le, t0m1, t0,
+                                            t0p1, m0, m1, l1, ml0, ml1);
+    } else {
+        const QFeatHbm F{v.ev.r};
+        score = P.simple ? qmid_walk<true>(P, sp, mv, I, F, j0, A1, A2, B0, B1, b0, e0, b1, e1, lb, le, t0m1, t0, t0p1,
+                                           m0, m1, l1, ml0, ml1)
+                         : qmid_walk<false>(P, sp, mv, I, F, j0, A1, A2, B0, B1, b0, e0, b1, e1, lb, le, t0m1, t0,
+                                            t0p1, m0, m1, l1, ml0, ml1);
+    }
+    W.delta[t] = score - B.rScore[r];
+}
+
 // ---- k_qalign: RecursorBase::Alignment (detail/RecursorBase.cpp:118-264) -------------------------------
 // The Viterbi path through a read's final alpha band, one lane per read, walking back from (I, J): moves
 // tried in the order Incorporate, Delete, Extra, Merge, strict '>' against -FLT_MAX, the move score added
@@ -1180,6 +1523,13 @@ void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s)
 {
     if (W.nTasks <= 0) return;
     hipLaunchKernelGGL(k_qscore, dim3((unsigned)((W.nTasks + 63) / 64)), dim3(64), 0, s, B, W);
+}
+
+void launch_qscore_mid(const QBatch& B, const QMidWork& W, long long nWaves, hipStream_t s)
+{
+    if (nWaves <= 0) return;
+    hipLaunchKernelGGL(k_qscore_mid, dim3((unsigned)((nWaves + kQMidWaves - 1) / kQMidWaves)), dim3(64 * kQMidWaves),
+                       0, s, B, W);
 }
 
 void launch_qreduce(const QReduceWork& W, hipStream_t s)

@@ -73,6 +73,34 @@ struct QScoreWork {
     const int* wNReads = nullptr;
     const int* readList = nullptr;
     const int* rActive = nullptr;
+    // listed form (taskList != nullptr): the kernel's tasks are taskList[0 .. nTasks), global task numbers of
+    // the batched layout above (the edge-case tasks k_qscore_mid handed back)
+    const long long* taskList = nullptr;
+};
+
+// Batched middle-case scoring (k_qscore_mid): one wavefront per (item, read, 64-mutation chunk), the lanes
+// on consecutive mutations of the item's list -- adjacent template positions of one read, so the wave walks
+// a handful of neighbouring band columns and the same QV-feature rows, staged in LDS.  Item w owns waves
+// [waveStart[w], waveStart[w + 1]): read-major, wNReads[w] x ceil(M / 64).  Mutations within 3 columns of a
+// read's window ends (ScoreMutation's edge cases) are appended to edgeList as global task numbers for
+// k_qscore's listed form; the rest write delta[wTaskStart[w] + m * nReads + read] directly.
+constexpr int kQMidWaves = 4;        // waves per workgroup
+constexpr int kQMidStageRows = 320;  // staged QV-feature rows per wave (a wider span reads HBM directly)
+struct QMidWork {
+    int nWork;
+    const long long* waveStart;
+    const long long* wTaskStart;
+    const long long* wMutBase;
+    const long long* wMutCount;   // mutations of item w
+    const int* wReadBase;
+    const int* wNReads;
+    const int* readList;
+    const int* rActive;
+    const int* codes;
+    float* delta;
+    long long* edgeList;
+    unsigned long long* edgeCount;
+    long long edgeCap;
 };
 
 // MultiReadMutationScorer::Score / FastIsFavorable per mutation of a batched round (Quiver/
@@ -97,6 +125,7 @@ constexpr int kQCoopRows = 4096;
 constexpr int kQCoopCols = 8192;
 void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, int maxCols, hipStream_t s);
 void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s);
+void launch_qscore_mid(const QBatch& B, const QMidWork& W, long long nWaves, hipStream_t s);
 void launch_qreduce(const QReduceWork& W, hipStream_t s);
 // RecursorBase::Alignment per listed read: moves (from the end) at moveOff[t], nMoves[t] of them
 void launch_qalign(const QBatch& B, const int* reads, int n, const long long* moveOff, unsigned char* moves,
