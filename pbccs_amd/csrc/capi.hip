@@ -48,14 +48,23 @@ struct pbccs_engine {
     long long oomRetries = 0;   // device batches rerun after PBCCS_EOOM
     std::vector<std::unique_ptr<Workspace>> slots;
     // the POA draft step's device state (made on first use): kPoaSlices runners, one per concurrent slice
-    static constexpr int kPoaSlices = 2;
+    // PBCCS_POA_SLICES overrides the slice count (A/B): more slices overlap one slice's host graph work with
+    // the others' device rounds, with fewer host threads each
+    static constexpr int kPoaSlicesDefault = 2;
+    static int PoaSlices()
+    {
+        static const int n = std::max(1, std::min(8, std::getenv("PBCCS_POA_SLICES") ? std::atoi(std::getenv("PBCCS_POA_SLICES"))
+                                                                                      : kPoaSlicesDefault));
+        return n;
+    }
     std::vector<std::unique_ptr<poa::PoaRunner>> poa;
     std::mutex poaMu;
     poa::PoaRunner& Poa(int k = 0)
     {
         if (poa.empty()) {
             const int hw = std::max(2, std::min(16, (int)std::thread::hardware_concurrency()));
-            for (int i = 0; i < kPoaSlices; ++i) poa.emplace_back(new poa::PoaRunner(device, hw / kPoaSlices));
+            for (int i = 0; i < PoaSlices(); ++i)
+                poa.emplace_back(new poa::PoaRunner(device, std::max(1, hw / PoaSlices())));
         }
         poa[k]->profiling = profiling;
         return *poa[k];
@@ -63,7 +72,7 @@ struct pbccs_engine {
     std::vector<poa::PoaRunner*> PoaRunners()
     {
         std::vector<poa::PoaRunner*> v;
-        for (int k = 0; k < kPoaSlices; ++k) v.push_back(&Poa(k));
+        for (int k = 0; k < PoaSlices(); ++k) v.push_back(&Poa(k));
         return v;
     }
     Workspace* Slot(int s)
@@ -1754,7 +1763,8 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
         // and larger chunks keep both stages busier (2000-ZMW chunks measured 1544 ZMWs/s end to end against
         // 1384 for 1000 and 1066 for 500).
         const int slots = std::max(1, eng->concurrency);
-        constexpr size_t kPoaPoolPerSlice = 20ull << 30;   // one round of a 1000-ZMW 2 kb slice: ~17.7 GB
+        // one round of a 1000-ZMW 2 kb slice: ~17.7 GB (the default two slices of a 2000-ZMW chunk)
+        const size_t kPoaPoolPerSlice = (40ull << 30) / (size_t)pbccs_engine::PoaSlices();
         for (poa::PoaRunner* r : eng->PoaRunners()) r->SetPoolBudget(kPoaPoolPerSlice);
         std::vector<std::vector<int>> liveLens(live.size());
         std::vector<pbccs_zmw_input> est(live.size());

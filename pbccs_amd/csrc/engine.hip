@@ -32,6 +32,16 @@ constexpr double kFillScratchBudget = 24.0 * (1ull << 30);
 constexpr int kCoopNarrowRows = 64;           // LDS column rows of the 16-lane fill path
 constexpr int kCoopTallRows = 1024;           // LDS column rows of the first 64-lane fill path
 constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill block
+// LDS column rows of the hybrid path (the rest of a column in global memory).  A tall 10 kb band is at most
+// ~1500 rows; every LDS byte a wave holds beyond that only keeps other tall waves off the CU (at the 60 KB
+// budget two fit a CU, at ~35 KB four).  PBCCS_HYBRID_ROWS overrides it (A/B).
+constexpr int kHybridRowsDefault = 1536;
+int hybrid_rows()
+{
+    static const int r = std::getenv("PBCCS_HYBRID_ROWS") ? std::max(64, std::atoi(std::getenv("PBCCS_HYBRID_ROWS")) / 64 * 64)
+                                                         : kHybridRowsDefault;
+    return r;
+}
 constexpr size_t kHeadroomMargin = 24ull << 30;   // device bytes band-growth headroom leaves free
 // First region of a read that moves to the tall paths, as a fraction 1 / kTallFirstDiv of its (I+1)(J+1)
 // matrix.  Exploded bands at 2 kb hold 0.8-21% of it per matrix (oracle, mean 9.9%); a read that outgrows
@@ -702,8 +712,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             const long long want = std::min<long long>(kCoopTallRows, full);
             return room >= want ? (int)want : 0;
         }
-        // hybrid: as many LDS rows as fit (the rest of a column goes to global memory)
-        const long long want = std::min(full, room);
+        // hybrid: as many LDS rows as fit, up to hybrid_rows() (the rest of a column goes to global memory)
+        const long long want = std::min(std::min(full, room), (long long)hybrid_rows());
         return want >= 64 ? (int)want : 0;
     };
     // PBCCS_FILL_PATHS=1: one stderr line per launch set (reads per path, wall ms, reads re-routed / regrown)

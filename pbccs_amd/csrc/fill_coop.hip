@@ -148,18 +148,14 @@ __device__ bool regrow_bands(const Task<G>& T, Band& m, Band& o, bool mIsAlpha, 
     return true;
 }
 
-// Log-scales of a finished pass (ScaledMatrix::FinishEditingColumn's log, off the column path).  Columns
-// [1, J) hold their scale factor (1.0: the column was not scaled); the group's lanes turn a strided share of
-// them into log(factor) (0.0 for 1.0, as the reference's `scale ? log(max) : 0`) at once, instead of one
-// FP64 log per column on every lane.  Column 0 and J already hold their log-scales.  Then one lane sums all
-// J + 1 in column order from 0.0 -- accumulate(logScales, 0.0) -- and the group gets the sum.
+// Log-scale sum of a finished pass.  ScaledMatrix::FinishEditingColumn's log(max) (0.0 for an unscaled
+// column, as the reference's `scale ? log(max) : 0`) was taken off the column path: each lane keeps one
+// column's scale factor of a G-column block in a register and the block's logs are taken together and stored
+// at its end.  Here one lane sums all J + 1 in column order from 0.0 -- accumulate(logScales, 0.0) -- and the
+// group gets the sum.
 template <int G>
 __device__ double finish_log_scales(const Task<G>& T, const Band& m, int J)
 {
-    for (int k = 1 + T.g.lane; k < J; k += G) {
-        const double f = m.L(k);
-        m.L(k) = (f != 1.0) ? log(f) : 0.0;
-    }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the group's stores before lane 0's loads
     double s = 0.0;
     if (T.g.lane == 0) {   // loads batched 8 at a time so the serial adds, not the load latency, set the pace
@@ -199,6 +195,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     int hb = 1, he = 1;
     int prevCtx = kCtxZero;
     int curBase = T.TBase(0), curCtx = T.TCtx(0);
+    double myF = 1.0;   // the scale factor of column (block start + lane) of the current G-column block
     // ranges of the guide and of this matrix's previous pass, prefetched one G-column block ahead
     // (a.R(jj) of a later block is read before this pass overwrites it)
     // G = 64: lane l holds column (block + l) and v_readlane hands it out; G = 16 (LDS permutes would sit on
@@ -321,8 +318,12 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         if (lane == 0 && !counting) {
             a.R(j) = make_int2(b, e);
             a.O(j) = (int)stored;
-            a.L(j) = scale ? mx : 1.0;   // the scale factor; finish_log_scales takes its log
         }
+        // ScaledMatrix's log(max) off the column path: lane jb keeps this column's factor, and at the end of a
+        // G-column block every lane takes the log of its own and stores it (coalesced) -- the factors never
+        // reach memory
+        if (lane == jb) myF = scale ? mx : 1.0;
+        if ((jb == G - 1 || j == J - 1) && !counting && lane <= jb) a.L(j - jb + lane) = (myF != 1.0) ? log(myF) : 0.0;
         used += e - b;
         stored += add;
         col_fence(T.gcol && nc * G > T.hcap);   // the next column's lanes read rows this column's lanes wrote
@@ -383,6 +384,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     long long used = 1, stored = 1;   // cells computed / values kept (column J is always kept)
     int hb = I, he = I;
     int nextBase = T.TBase(J - 1);
+    double myF = 1.0;   // the scale factor of column (block start - lane) of the current G-column block
     int2 gR = make_int2(0, 0), sR = make_int2(0, 0), gN = make_int2(0, 0), sN = make_int2(0, 0);
     {
         const int jj = G == 64 ? J - 1 - lane : J - 1;
@@ -499,8 +501,9 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         if (lane == 0 && !counting) {
             bm.R(j) = make_int2(b, e);
             bm.O(j) = (int)stored;
-            bm.L(j) = scale ? mx : 1.0;   // the scale factor; finish_log_scales takes its log
         }
+        if (lane == jb) myF = scale ? mx : 1.0;   // as in coop_alpha; the block runs down from column j + jb
+        if ((jb == G - 1 || j == 1) && !counting && lane <= jb) bm.L(j + jb - lane) = (myF != 1.0) ? log(myF) : 0.0;
         used += e - b;
         stored += add;
         col_fence(T.gcol && nc * G > T.hcap);

@@ -24,7 +24,8 @@ constexpr int kMaxFlipFlops = 5;              // detail/RecursorBase.cpp:51
 // ALPHA_BETA_MISMATCH_TOLERANCE 0.2 and REBANDING_THRESHOLD 0.04 (detail/RecursorBase.cpp:52-53) are
 // double literals in the reference; quiver_kernels.hip uses them as such.
 
-enum QFillStatus : int { kQOk = 0, kQMismatch = 1, kQOverflow = 2, kQBad = 3, kQMemFail = 4 };
+// kQTall: a column outgrew k_qfill_coop's band-height LDS ring; the host reruns the read with a full-height ring
+enum QFillStatus : int { kQOk = 0, kQMismatch = 1, kQOverflow = 2, kQBad = 3, kQMemFail = 4, kQTall = 5 };
 
 // QvModelParams + QuiverConfig fields the recursion reads (QuiverConfig.hpp:79-176)
 struct QParams {

@@ -245,8 +245,18 @@ void QuiverBatch::Upload()
     put(dRValBase_, rvb, stream_);
     put(dRValCap_, rvc, stream_);
     put(dRColBuf_, rcbuf, stream_);
-    put(dSeq_, hSeq_, stream_);
-    put(dFeat_, hFeat_, stream_);
+    // the read pools only ever grow (AddRead appends): upload the new tail, not every read's bases and five
+    // feature tracks again on each refine round that edits a template
+    auto tail = [&](auto& d, const auto& h, size_t& up) {
+        if (h.size() < up) up = 0;   // never happens (append-only); re-upload if it did
+        if (h.size() == up) return;
+        d.reserve(std::max<size_t>(h.size(), 1), true);
+        QHIP(hipMemcpyAsync(d.ptr + up, h.data() + up, (h.size() - up) * sizeof(h[0]), hipMemcpyHostToDevice,
+                            stream_));
+        up = h.size();
+    };
+    tail(dSeq_, hSeq_, seqUp_);
+    tail(dFeat_, hFeat_, featUp_);
     dRange_.reserve(std::max<long long>(colTop_, 1), true);
     dOff_.reserve(std::max<long long>(colTop_, 1), true);
     dAlloc_.reserve(std::max<long long>(colTop_ / 2, 1), true);
@@ -310,26 +320,36 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         // SparseSse configs with reads below kQCoopRows rows: one wavefront per read (k_qfill_coop); the
         // Simple / Dense recursors and longer reads: one lane per read (k_qfill).  PBCCS_QFILL_LANE=1 sends
         // every read to the lane kernel.
+        // The coop kernel's LDS ring holds kQRingRows rows per column (band height, rows modulo the ring), so
+        // many read waves share a CU; a read with a taller column comes back kQTall and from then on fills with
+        // a ring of its full height (tallRing).
         static const bool laneOnly = std::getenv("PBCCS_QFILL_LANE") != nullptr;
-        std::vector<int> coop, lane;
-        int maxRows = 1, maxCols = 1;
+        std::vector<int> coop, full, lane;
+        int maxCols = 1, maxColsFull = 1, maxRowsFull = 1;
         for (int r : todo) {
             const QParams& p = configs_[reads_[r].config];
             const int cols = reads_[r].te - reads_[r].ts + 1;
             if (!laneOnly && !p.simple && !p.dense && reads_[r].len + 1 <= kQCoopRows && cols <= kQCoopCols) {
-                coop.push_back(r);
-                maxRows = std::max(maxRows, reads_[r].len + 1);
-                maxCols = std::max(maxCols, cols);
+                if (reads_[r].tallRing) {
+                    full.push_back(r);
+                    maxRowsFull = std::max(maxRowsFull, reads_[r].len + 1);
+                    maxColsFull = std::max(maxColsFull, cols);
+                } else {
+                    coop.push_back(r);
+                    maxCols = std::max(maxCols, cols);
+                }
             } else {
                 lane.push_back(r);
             }
         }
         std::vector<int> both(coop);
+        both.insert(both.end(), full.begin(), full.end());
         both.insert(both.end(), lane.begin(), lane.end());
         put(dList_, both, stream_);
         const QBatch B = View();
-        launch_qfill_coop(B, dList_.ptr, (int)coop.size(), maxRows, maxCols, stream_);
-        launch_qfill(B, dList_.ptr + coop.size(), (int)lane.size(), stream_);
+        launch_qfill_coop(B, dList_.ptr, (int)coop.size(), kQRingRows, maxCols, stream_);
+        launch_qfill_coop(B, dList_.ptr + coop.size(), (int)full.size(), maxRowsFull, maxColsFull, stream_);
+        launch_qfill(B, dList_.ptr + coop.size() + full.size(), (int)lane.size(), stream_);
         QHIP(hipGetLastError());
         const size_t R = reads_.size();
         std::vector<int> st, ca, cb, fl;
@@ -346,6 +366,11 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         std::vector<int> next;
         for (int r : todo) {
             HRead& h = reads_[r];
+            if (st[r] == kQTall) {
+                h.tallRing = true;
+                next.push_back(r);
+                continue;
+            }
             if (st[r] == kQOverflow) {
                 const long long need = std::max(used[2 * r], used[2 * r + 1]);
                 h.valCap = std::max(need + need / 4 + 64, h.valCap + 1);

@@ -92,6 +92,7 @@ private:
         int curA = 0, curB = 0, flips = 0;
         float score = 0.0f;
         long long alloc[2] = {0, 0};
+        bool tallRing = false;   // a column outgrew the band-height LDS ring: fill with the full-height one
     };
     int Register(int z, const QReadFeatures& f, int strand, int ts, int te, int config);   // a read, unfilled
     void Upload();
@@ -121,6 +122,7 @@ private:
     std::vector<char> hSeq_;
     std::vector<float> hFeat_;
     long long colTop_ = 0, valTop_ = 0;
+    size_t seqUp_ = 0, featUp_ = 0;   // host read pools already on the device (append-only)
     bool dirty_ = true;
     // device
     DevVec<long long> dZFwd_, dZRev_, dRSeq_, dRColBase_, dRValBase_, dRValCap_, dRColBuf_, dRUsed_, dRAlloc_;

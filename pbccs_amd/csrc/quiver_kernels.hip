@@ -553,10 +553,14 @@ __device__ __forceinline__ void coop_range_guide(int j, const QBand* guide, cons
     *he = e;
 }
 
+// One column of the LDS ring.  Row i lives at v[i & mask]: the ring is a power of two of rows, either the
+// read's full height (no two rows share a slot) or a band-height window -- a column's rows [b, e) are then
+// distinct modulo the ring as long as e - b fits it, which coop_column checks (kQTall otherwise).
 struct LdsCol {
     float* v;
     int b, e;   // valid rows [b, e)
-    __device__ __forceinline__ float at(int i) const { return (i >= b && i < e) ? v[i] : kNegInf; }
+    int mask;
+    __device__ __forceinline__ float at(int i) const { return (i >= b && i < e) ? v[i & mask] : kNegInf; }
 };
 
 // One column of one pass.  BETA: rows run downwards (lane l <-> row top - l), the chain from row + 1.
@@ -565,7 +569,7 @@ struct LdsCol {
 template <bool BETA>
 __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int hb, int he, const LdsCol& c1,
                                             const LdsCol& c2, float* cur, const QBand& out, long long base, QAlloc* alloc,
-                                            bool& ovf, int* ob, int* oe, float* thrOut)
+                                            bool& ovf, int* ob, int* oe, float* thrOut, int mask, bool& tall)
 {
     const int I = e.I(), J = e.J();
     const bool sp = e.p->sumProduct != 0;
@@ -591,6 +595,13 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
     bool done = empty;
     if (empty) stop = BETA ? first + 1 : first;
     for (int c = 0; !done; ++c) {
+        // rows of this chunk past the band-height ring would alias the column's first rows: the read is tall
+        if (mask < I && (BETA ? first - (chunk - 64 * c - 63) : chunk + 64 * c + 63 - first) > mask) {
+            tall = true;
+            *ob = *oe = first;
+            *thrOut = thr;
+            return;
+        }
         const int row = BETA ? chunk - 64 * c - lane : chunk + 64 * c + lane;
         const bool valid = BETA ? (row <= first && row >= 0) : (row >= first && row <= I);
         const int g = lane >> 2;
@@ -689,7 +700,7 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
         const int stopQuad = fails ? (__ffsll((long long)fails) - 1) >> 2 : 16;
         // rows of the quads before the stop are the column's
         const bool keep = valid && g < stopQuad;
-        if (keep) cur[row] = sv;
+        if (keep) cur[row & mask] = sv;
         // state after the last kept quad
         if (stopQuad > 0) {
             const int lastLane = 4 * stopQuad - 1;
@@ -711,7 +722,7 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
     // store the column top-down into the arena
     for (int r = beginRow + lane; r < endRow; r += 64) {
         const long long k = base + (r - beginRow);
-        if (k < out.cap) out.val[k] = cur[r];
+        if (k < out.cap) out.val[k] = cur[r & mask];
         else ovf = true;
     }
     *ob = beginRow;
@@ -720,23 +731,27 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
 }
 
 template <bool BETA>
-__device__ long long coop_fill(const QEval& e, const QBand* guide, const QBand* prev, const QBand& out, QAlloc* alloc,
+__device__ long long coop_fill(const QEval& e, const QBand& guideBand, bool useGuide, const QBand& prevBand, bool usePrev,
+                               const QBand& out, QAlloc* alloc,
                                bool allocExists, bool& ovf, float* lds, int ldsRows, int4* hint, int lane)
 {
+    // returns the pass's used cells, or -1 when a column outgrew the band-height ring (kQTall)
     const int I = e.I(), J = e.J();
     const float sd = e.p->scoreDiff;
     // RowRange of the guide and self matrices for every column, up front and one lane per column: both are
     // finished passes, and only RangeGuide's min / max with the running hints is sequential
     for (int j = lane; j <= J; j += 64) {
         int4 h = make_int4(-1, -1, -1, -1);
-        if (guide && !guide->Empty(j)) row_range(*guide, j, sd, &h.x, &h.y);
-        if (prev && !prev->Empty(j)) row_range(*prev, j, sd, &h.z, &h.w);
+        if (useGuide && !guideBand.Empty(j)) row_range(guideBand, j, sd, &h.x, &h.y);
+        if (usePrev && !prevBand.Empty(j)) row_range(prevBand, j, sd, &h.z, &h.w);
         hint[j] = h;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     // the LDS ring: cur (column being filled), c1 (previous), c2 (the one before), rotated by value
-    LdsCol cur{lds, 0, 0}, c1{lds + ldsRows, 0, 0}, c2{lds + 2 * ldsRows, 0, 0};
+    const int mask = ldsRows - 1;   // ldsRows is a power of two
+    LdsCol cur{lds, 0, 0, mask}, c1{lds + ldsRows, 0, 0, mask}, c2{lds + 2 * ldsRows, 0, 0, mask};
     long long used = 0;
+    bool tall = false;
     int hb = BETA ? I + 1 : 0, he = BETA ? I + 1 : 0;
     int4 hNext = hint[BETA ? J : 0];
     for (int s = 0; s <= J; ++s) {
@@ -747,7 +762,8 @@ __device__ long long coop_fill(const QEval& e, const QBand* guide, const QBand* 
         if (h.z >= 0) { hb = min(h.z, hb); he = max(h.w, he); }
         int b, en;
         float thr;
-        coop_column<BETA>(e, j, lane, hb, he, c1, c2, cur.v, out, used, nullptr, ovf, &b, &en, &thr);
+        coop_column<BETA>(e, j, lane, hb, he, c1, c2, cur.v, out, used, nullptr, ovf, &b, &en, &thr, mask, tall);
+        if (tall) return -1;
         cur.b = b;
         cur.e = en;
         if (lane == 0) {
@@ -762,7 +778,7 @@ __device__ long long coop_fill(const QEval& e, const QBand* guide, const QBand* 
             int nb = en;
             for (int i0 = b; i0 < en; i0 += 64) {
                 const int i = i0 + lane;
-                const bool hit = i < en && !(cur.v[i] < thr);
+                const bool hit = i < en && !(cur.v[i & mask] < thr);
                 const unsigned long long bal = __ballot(hit);
                 if (bal) { nb = i0 + __ffsll((long long)bal) - 1; break; }
             }
@@ -772,7 +788,7 @@ __device__ long long coop_fill(const QEval& e, const QBand* guide, const QBand* 
             int ne = b;
             for (int i1 = en; i1 > b; i1 -= 64) {
                 const int i = i1 - 1 - lane;
-                const bool hit = i >= b && !(cur.v[i] < thr);
+                const bool hit = i >= b && !(cur.v[i & mask] < thr);
                 const unsigned long long bal = __ballot(hit);
                 if (bal) { ne = i1 - (__ffsll((long long)bal) - 1); break; }
             }
@@ -815,7 +831,7 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
     const int r = reads[t];
     ReadView v = read_view(B, r);
     const int I = v.ev.I(), J = v.ev.J();
-    if (I < 1 || J < 1 || J + 1 > B.rColCap[r] || I + 1 > ldsRows || J + 1 > ldsCols) {
+    if (I < 1 || J < 1 || J + 1 > B.rColCap[r] || J + 1 > ldsCols) {
         if (lane == 0) B.rStatus[r] = kQBad;
         return;
     }
@@ -829,15 +845,16 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
         for (int j = lane; j <= J; j += 64) m.range[j] = make_int2(0, 0);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    bool ovf = false;
+    bool ovf = false, tall = false;
     long long needA = 0, needB = 0;
     int curA = 0, curB = 2;
     bool aPassed = false, bPassed = false;
     auto passA = [&](bool guided) {
         const int nxt = aPassed ? (curA ^ 1) : 0;
         const QBand g = arena(v, curB), self = arena(v, curA), out = arena(v, nxt);
-        const long long u = coop_fill<false>(e, guided ? &g : nullptr, aPassed ? &self : nullptr, out, v.allocA, aPassed,
-                                             ovf, qlds, ldsRows, v.hint, lane);
+        const long long u = coop_fill<false>(e, g, guided, self, aPassed, out, v.allocA, aPassed, ovf, qlds, ldsRows,
+                                             v.hint, lane);
+        tall = tall || u < 0;
         needA = max(needA, u);
         curA = nxt;
         aPassed = true;
@@ -846,35 +863,61 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
     auto passB = [&]() {
         const int nxt = bPassed ? (curB ^ 1) : 2;
         const QBand g = arena(v, curA), self = arena(v, curB), out = arena(v, nxt);
-        const long long u = coop_fill<true>(e, &g, bPassed ? &self : nullptr, out, v.allocB, bPassed, ovf, qlds, ldsRows,
+        const long long u = coop_fill<true>(e, g, true, self, bPassed, out, v.allocB, bPassed, ovf, qlds, ldsRows,
                                             v.hint, lane);
+        tall = tall || u < 0;
         needB = max(needB, u);
         curB = nxt;
         bPassed = true;
         return u;
     };
-    // RecursorBase::FillAlphaBeta (detail/RecursorBase.cpp:70-116)
-    const long long ua = passA(false);
-    const long long ub = passB();
-    ovf = __ballot(ovf) != 0;
-    int flips = 0;
-    const int maxSize = (int)(0.5 + 0.04 * (I + 1) * (J + 1));
-    if (!ovf && (ua >= maxSize || ub >= maxSize)) {
-        passA(true);
-        passB();
-        passA(true);
-        flips += 3;
-        ovf = __ballot(ovf) != 0;
-    }
+    // RecursorBase::FillAlphaBeta (detail/RecursorBase.cpp:70-116) as one loop over the pass schedule, so each
+    // pass kind is instantiated once: alpha, beta; the reband triple (alpha, beta, alpha) when either band
+    // reached 4% of the matrix; then the flip-flops while alpha and beta disagree.  A tall column ends the
+    // fill (kQTall).
     auto a_end = [&]() { return arena(v, curA).Get(I, J); };
     auto b_start = [&]() { return arena(v, curB).Get(0, 0); };
-    while (!ovf && (double)fabsf(a_end() - b_start()) > 0.2 && flips <= kMaxFlipFlops) {
-        if (flips % 2 == 0) passA(true);
-        else passB();
-        flips++;
-        ovf = __ballot(ovf) != 0;
+    const int maxSize = (int)(0.5 + 0.04 * (I + 1) * (J + 1));
+    long long ua = 0;
+    int flips = 0, stage = 0, pending = 0;   // stage 0: first alpha, 1: first beta, 2: reband triple, 3: flip-flops
+    for (;;) {
+        bool alpha = true, guided = true;
+        if (stage == 0) guided = false;
+        else if (stage == 1) alpha = false;
+        else if (stage == 2) alpha = pending != 2;
+        else {
+            if (ovf || !((double)fabsf(a_end() - b_start()) > 0.2) || flips > kMaxFlipFlops) break;
+            alpha = flips % 2 == 0;
+        }
+        const long long u = alpha ? passA(guided) : passB();
+        if (tall) break;
+        if (stage == 0) {
+            ua = u;
+            stage = 1;
+        } else if (stage == 1) {
+            ovf = __ballot(ovf) != 0;
+            if (!ovf && (ua >= maxSize || u >= maxSize)) {
+                stage = 2;
+                pending = 3;
+                flips += 3;
+            } else {
+                stage = 3;
+            }
+        } else if (stage == 2) {
+            if (--pending == 0) {
+                ovf = __ballot(ovf) != 0;
+                stage = 3;
+            }
+        } else {
+            flips++;
+            ovf = __ballot(ovf) != 0;
+        }
     }
     if (lane != 0) return;
+    if (tall) {
+        B.rStatus[r] = kQTall;
+        return;
+    }
     B.rUsed[2 * r] = needA;
     B.rUsed[2 * r + 1] = needB;
     if (ovf) {
@@ -1513,7 +1556,8 @@ void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s)
 void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, int maxCols, hipStream_t s)
 {
     if (n <= 0) return;
-    const int rows = (maxRows + 63) / 64 * 64;
+    int rows = 64;   // the LDS ring: a power of two (rows index it modulo its size)
+    while (rows < maxRows) rows *= 2;
     const int cols = (maxCols + 15) / 16 * 16;
     hipLaunchKernelGGL(k_qfill_coop, dim3(n), dim3(64), (size_t)3 * rows * sizeof(float) + cols, s, B, reads, n, rows,
                        cols);
