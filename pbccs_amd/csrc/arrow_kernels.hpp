@@ -78,6 +78,7 @@ struct FillScratch {
 struct CoopFill {
     int* usedA = nullptr;    // per read: values used by the final alpha / beta (or needed, on overflow)
     int* usedB = nullptr;
+    int* maxH = nullptr;     // per read: the tallest column of the fill's passes (routing of its next refill)
     int hcap = 0;            // LDS rows per column buffer
     int readWords = 0;       // nibble-packed read words per group (>= ceil(I / 8) of every read)
     int tplWords = 0;        // nibble-packed template words per group (>= ceil((J + 1) / 8))

@@ -36,6 +36,16 @@ constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill 
 // ~1500 rows; every LDS byte a wave holds beyond that only keeps other tall waves off the CU (at the 60 KB
 // budget two fit a CU, at ~35 KB four).  PBCCS_HYBRID_ROWS overrides it (A/B).
 constexpr int kHybridRowsDefault = 1536;
+// A refill on the 16-lane path whose last fill had a column of more than this many rows (of the path's 64)
+// starts on the tall paths: a read that goes tall there is only re-run after the whole 16-lane launch ends,
+// one more fill latency on its batch's round.  PBCCS_NEAR_TALL overrides it (0: off).
+constexpr int kNearTallDefault = 0;
+int near_tall()
+{
+    static const int r = std::getenv("PBCCS_NEAR_TALL") ? std::max(0, std::atoi(std::getenv("PBCCS_NEAR_TALL")))
+                                                       : kNearTallDefault;
+    return r;
+}
 int hybrid_rows()
 {
     static const int r = std::getenv("PBCCS_HYBRID_ROWS") ? std::max(64, std::atoi(std::getenv("PBCCS_HYBRID_ROWS")) / 64 * 64)
@@ -689,6 +699,39 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     const char* laneEnv = std::getenv("PBCCS_FILL_LANE");   // read per call: a test switches it at run time
     const bool laneFill = laneEnv && std::strcmp(laneEnv, "1") == 0;
     for (int r : readsIn) EnsureCapacity(r);
+    // a read moves from path p to the tall paths: long windows skip the 1024-row LDS path (their tall bands
+    // mostly outgrow it -- 10 kb: 662 of 786 reads went on to the hybrid path -- and each step is one more
+    // launch on the round's critical path); it gets a first tall region now (kTallFirstDiv): growing from the
+    // typical 16-row region inside the kernel would copy and abandon two or three.  Returns the new path.
+    auto promote = [&](int r, int p) {
+        HRead& h = reads_[r];
+        int q = p + 1;
+        if (q == 2 && (long long)h.seq.size() + 1 > 4LL * kCoopTallRows) q = 3;
+        h.fillPath = q;
+        if (q >= 2 && q < kPaths) {
+            const long long I = (long long)h.seq.size(), J = h.te - h.ts;
+            // checkpointed: every K-th column plus the kept tails (the next launch sets h.ckpt)
+            const bool ck = ckptAll_ > 0 || (ckptK_ > 0 && J >= ckptMinLen_);
+            const long long K = ck ? std::max(ckptAll_, ckptK_) : 1;
+            const long long want = (I + 1) * (J + 1) / tall_first_div() / K + (ck ? 2 * (kCkptTail + 1) * (I + 1) : 0) + 64;
+            if (want > h.valCap) {
+                h.valCap = want;
+                h.valA = valTop_;
+                h.valB = valTop_ + h.valCap;
+                valTop_ += 2 * h.valCap;
+                descDirty_ = true;
+            }
+        }
+        return q;
+    };
+    if (near_tall() > 0)
+        for (int r : readsIn) {
+            HRead& h = reads_[r];
+            if (h.fillPath == 1 && h.filled && h.maxH > near_tall()) {
+                promote(r, 1);
+                counters_.nearTall += 1;
+            }
+        }
     Relayout(readsIn);
     std::vector<int> todo[kPaths], serial, done;
     for (int r : readsIn) {
@@ -784,6 +827,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         const size_t R = reads_.size();
         dUsedA_.reserve(std::max<size_t>(R, 1), true);
         dUsedB_.reserve(std::max<size_t>(R, 1), true);
+        dMaxH_.reserve(std::max<size_t>(R, 1), true);
         std::vector<int> list;
         for (auto& v : todo) list.insert(list.end(), v.begin(), v.end());
         upload(dList_, list, stream_);
@@ -837,6 +881,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             CoopFill F;
             F.usedA = dUsedA_.ptr;
             F.usedB = dUsedB_.ptr;
+            F.maxH = dMaxH_.ptr;
             F.readWords = (maxI + 7) / 8;
             F.tplWords = (maxJ + 8) / 8;
             F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
@@ -873,8 +918,9 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             PBCCS_HIP(hipEventRecord(evJoin_, stream2_));
             PBCCS_HIP(hipStreamWaitEvent(stream_, evJoin_, 0));
         }
-        std::vector<int> st, fl, ua, ub;
+        std::vector<int> st, fl, ua, ub, mh;
         std::vector<double> bl;
+        download(mh, dMaxH_, R, stream_);
         download(st, dRStatus_, R, stream_);
         download(fl, dRFlips_, R, stream_);
         download(bl, dRBaseline_, R, stream_);
@@ -916,30 +962,9 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             for (int r : todo[p]) {
                 HRead& h = reads_[r];
                 if (st[r] == kFillTall) {   // never from the hybrid path (3)
-                    // long windows skip the 1024-row LDS path: their tall bands mostly outgrow it (10 kb: 662 of 786
-                    // reads went on to the hybrid path), and each step is one more launch on the round's critical path
-                    int q = p + 1;
-                    if (q == 2 && (long long)h.seq.size() + 1 > 4LL * kCoopTallRows) q = 3;
-                    h.fillPath = q;
+                    const int q = promote(r, p);
                     if (q >= kPaths) serial.push_back(r);
                     else next[q].push_back(r);
-                    // A read that moves to the tall paths gets a first tall region now (kTallFirstDiv): growing
-                    // from the typical 16-row region inside the kernel would copy and abandon two or three.
-                    if (q >= 2 && q < kPaths) {
-                        const long long I = (long long)h.seq.size(), J = h.te - h.ts;
-                        // checkpointed: every K-th column plus the kept tails (the next launch sets h.ckpt)
-                        const bool ck = ckptAll_ > 0 || (ckptK_ > 0 && J >= ckptMinLen_);
-                        const long long K = ck ? std::max(ckptAll_, ckptK_) : 1;
-                        const long long want = (I + 1) * (J + 1) / tall_first_div() / K +
-                                               (ck ? 2 * (kCkptTail + 1) * (I + 1) : 0) + 64;
-                        if (want > h.valCap) {
-                            h.valCap = want;
-                            h.valA = valTop_;
-                            h.valB = valTop_ + h.valCap;
-                            valTop_ += 2 * h.valCap;
-                            descDirty_ = true;
-                        }
-                    }
                     continue;
                 }
                 if (st[r] == kFillOverflow) {
@@ -958,6 +983,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 h.filled = true;
                 h.usedA = ua[r];
                 h.usedB = ub[r];
+                if (p >= 1) h.maxH = mh[r];
                 if (st[r] == kFillOk || st[r] == kFillMismatch) done.push_back(r);
             }
         }

@@ -128,6 +128,7 @@ struct Counters {   // work counters for the roofline report (bench.py)
     long long scoreTasks = 0, scoreLaunches = 0;
     long long mutations = 0;
     long long bandGrowths = 0;   // fill launch sets in which some read grew its band region in-kernel
+    long long nearTall = 0;      // refills sent to the tall paths up front (PBCCS_NEAR_TALL)
     long long relayouts = 0;     // fills that laid the band pool out afresh (ArrowBatch::Relayout)
     // band value pool of the batch, bytes (maxima over the batches merged into an engine's counters):
     // bump top (everything ever handed out), current regions (2 x capacity per read), cells in use
@@ -274,6 +275,7 @@ private:
         int colCap = 0;
         long long valA = 0, valB = 0, valCap = 0;
         long long usedA = 0, usedB = 0;   // band values the last fill kept (its region need)
+        int maxH = 0;                       // the last cooperative fill's tallest column (rows)
         int ckpt = 0;   // checkpoint interval of the bands (0: every column's values kept)
     };
 
@@ -325,7 +327,7 @@ private:
     int ckptK_ = 0, ckptMinLen_ = 0, ckptAll_ = 0;
     long long ckSlotCap_ = 0;
     DevVec<double> dRBaseline_;
-    DevVec<int> dRFlips_, dRStatus_, dUsedA_, dUsedB_;
+    DevVec<int> dRFlips_, dRStatus_, dUsedA_, dUsedB_, dMaxH_;
     DevVec<int> dWZmw_, dWNMut_;
     DevVec<long long> dWMutBase_, dWDeltaBase_, dWWaveStart_, dWMutStart_, dWPosStart_, dWPosBase_, dWQvBase_;
     // workspace pools (aliases into *ws_)

@@ -85,6 +85,7 @@ struct PassOut {
     bool tall;        // a column exceeded the LDS buffer
     bool changed;     // some column's [begin, end) differs from the previous pass of this matrix
     bool regrow;      // the pass outgrew its region and ran to its end counting only: `used` is its exact need
+    int maxH;         // the pass's tallest column (rows)
 };
 
 // Column rows in global memory (the hybrid path's rows past the LDS buffer): a column's rows are written by
@@ -178,7 +179,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
 {
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false};
+    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1};
     bool counting = false;   // outgrew the region: finish the pass without stores (regrow_bands)
     (void)keepO;
     if (a.cap < 1) ovf = true;
@@ -315,6 +316,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         }
         if (!counting && stored + add > a.cap) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
+        out.maxH = max(out.maxH, e - b);
         if (lane == 0 && !counting) {
             a.R(j) = make_int2(b, e);
             a.O(j) = (int)stored;
@@ -367,7 +369,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 {
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false};
+    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1};
     bool counting = false;   // outgrew the region: finish the pass without stores (regrow_bands)
     (void)keepO;
     if (bm.cap < 1) ovf = true;
@@ -498,6 +500,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         }
         if (!counting && stored + add > bm.cap) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
+        out.maxH = max(out.maxH, e - b);
         if (lane == 0 && !counting) {
             bm.R(j) = make_int2(b, e);
             bm.O(j) = (int)stored;
@@ -665,7 +668,8 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     // its own previous pass (hint), never on previous values.  Once an alpha pass and the beta pass after
     // it both reproduce their predecessors' ranges, every later pass repeats them bit for bit, so the
     // remaining flip-flops are skipped and only the count the reference reports is kept.
-    PassOut pa{0, 0, 0.0, 0.0, false, false, false}, pb{0, 0, 0.0, 0.0, false, false, false};
+    PassOut pa{0, 0, 0.0, 0.0, false, false, false, 0}, pb{0, 0, 0.0, 0.0, false, false, false, 0};
+    int maxH = 0;
     long long ua = 0, ub = 0;   // cells of the last alpha / beta pass (the reband test)
     long long sa = 0, sb = 0;   // values they keep (region sizes)
     const int maxSize = (int)(0.5 + kRebandFrac * (I + 1) * (J + 1));
@@ -702,6 +706,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
         }
         cells += o.used;
         passes += 1;
+        maxH = max(maxH, o.maxH);
         if (doAlpha) {
             pa = o;
             ua = o.used;
@@ -736,6 +741,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
             B.rBaseline[r] = bv;
             F.usedA[r] = (int)sa;   // region sizes: the values the bands keep
             F.usedB[r] = (int)sb;
+            if (F.maxH) F.maxH[r] = maxH;
             B.rStatus[r] = (mism > kAlphaBetaTol) ? kFillMismatch : kFillOk;
             if (B.stats) {   // algorithmic: 8 B per stored cell + 16 B per column per fill pass
                 constexpr int kind = G == 64 ? kStatFillTall : kStatFill;

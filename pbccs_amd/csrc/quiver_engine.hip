@@ -1,6 +1,8 @@
 // pbccs_amd/csrc/quiver_engine.hip -- QuiverBatch (quiver_engine.hpp).
 #include "quiver_engine.hpp"
 
+#include <cstdio>
+
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -347,7 +349,14 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         both.insert(both.end(), lane.begin(), lane.end());
         put(dList_, both, stream_);
         const QBatch B = View();
-        launch_qfill_coop(B, dList_.ptr, (int)coop.size(), kQRingRows, maxCols, stream_);
+        static const int ringRows = [] {   // PBCCS_QRING_ROWS overrides the ring (A/B; a power of two)
+            const char* e = std::getenv("PBCCS_QRING_ROWS");
+            int r = e ? std::atoi(e) : kQRingRows;
+            int p = 64;
+            while (p < r && p < kQCoopRows) p *= 2;
+            return p;
+        }();
+        launch_qfill_coop(B, dList_.ptr, (int)coop.size(), ringRows, maxCols, stream_);
         launch_qfill_coop(B, dList_.ptr + coop.size(), (int)full.size(), maxRowsFull, maxColsFull, stream_);
         launch_qfill(B, dList_.ptr + coop.size() + full.size(), (int)lane.size(), stream_);
         QHIP(hipGetLastError());
@@ -364,6 +373,13 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         get(al, dRAlloc_, 2 * R, stream_);
         QHIP(hipStreamSynchronize(stream_));
         std::vector<int> next;
+        static const bool trace = std::getenv("PBCCS_QFILL_TRACE") != nullptr;   // one stderr line per launch set
+        if (trace) {
+            int nt = 0;
+            for (int r : coop) nt += st[r] == kQTall;
+            std::fprintf(stderr, "[qfill] attempt %d ring %zu full %zu lane %zu -> tall %d\n", attempt, coop.size(),
+                         full.size(), lane.size(), nt);
+        }
         for (int r : todo) {
             HRead& h = reads_[r];
             if (st[r] == kQTall) {

@@ -553,9 +553,10 @@ __device__ __forceinline__ void coop_range_guide(int j, const QBand* guide, cons
     *he = e;
 }
 
-// One column of the LDS ring.  Row i lives at v[i & mask]: the ring is a power of two of rows, either the
-// read's full height (no two rows share a slot) or a band-height window -- a column's rows [b, e) are then
-// distinct modulo the ring as long as e - b fits it, which coop_column checks (kQTall otherwise).
+// One column of the LDS ring.  Row i lives at v[i & mask]: either the ring holds the read's full height
+// (mask = -1, every row its own slot) or it is a band-height window of a power of two of rows -- a column's
+// rows [b, e) are then distinct modulo the ring as long as e - b fits it, which coop_column checks (kQTall
+// otherwise).
 struct LdsCol {
     float* v;
     int b, e;   // valid rows [b, e)
@@ -596,7 +597,7 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
     if (empty) stop = BETA ? first + 1 : first;
     for (int c = 0; !done; ++c) {
         // rows of this chunk past the band-height ring would alias the column's first rows: the read is tall
-        if (mask < I && (BETA ? first - (chunk - 64 * c - 63) : chunk + 64 * c + 63 - first) > mask) {
+        if ((unsigned)mask < (unsigned)I && (BETA ? first - (chunk - 64 * c - 63) : chunk + 64 * c + 63 - first) > mask) {
             tall = true;
             *ob = *oe = first;
             *thrOut = thr;
@@ -748,7 +749,8 @@ __device__ long long coop_fill(const QEval& e, const QBand& guideBand, bool useG
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     // the LDS ring: cur (column being filled), c1 (previous), c2 (the one before), rotated by value
-    const int mask = ldsRows - 1;   // ldsRows is a power of two
+    // a ring shorter than the read (ldsRows a power of two): rows modulo it; else every row has its slot
+    const int mask = ldsRows >= I + 1 ? -1 : ldsRows - 1;
     LdsCol cur{lds, 0, 0, mask}, c1{lds + ldsRows, 0, 0, mask}, c2{lds + 2 * ldsRows, 0, 0, mask};
     long long used = 0;
     bool tall = false;
@@ -1556,8 +1558,9 @@ void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s)
 void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, int maxCols, hipStream_t s)
 {
     if (n <= 0) return;
-    int rows = 64;   // the LDS ring: a power of two (rows index it modulo its size)
-    while (rows < maxRows) rows *= 2;
+    // the LDS ring: a power of two of rows (a band-height ring, rows modulo its size) or, for reads that fit,
+    // their full height
+    const int rows = (maxRows & (maxRows - 1)) == 0 ? maxRows : (maxRows + 63) / 64 * 64;
     const int cols = (maxCols + 15) / 16 * 16;
     hipLaunchKernelGGL(k_qfill_coop, dim3(n), dim3(64), (size_t)3 * rows * sizeof(float) + cols, s, B, reads, n, rows,
                        cols);
