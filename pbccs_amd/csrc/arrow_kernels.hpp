@@ -102,10 +102,6 @@ struct CoopFill {
     int gRows = 0;
 };
 size_t coop_group_bytes(int hcap, int readWords, int tplWords);
-// Lane fill (fill_lane.hip): one lane per read, columns of up to kFillLaneRows rows (taller: kFillTall).
-// Uses CoopFill's usedA/usedB and band-growth fields only.
-constexpr int kFillLaneRows = 32;
-void launch_fill_lane(const DevBatch& B, const CoopFill& F, const int* reads, int n, hipStream_t s);
 void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* reads, int n, hipStream_t s);
 
 void launch_fill(const DevBatch& B, const FillScratch& F, const int* reads, int n, hipStream_t s);

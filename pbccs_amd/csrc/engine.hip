@@ -684,20 +684,14 @@ DevBatch ArrowBatch::View() const
 // the kernel reported.  Bands land directly in the compact layout; k_suffix adds the log-scale sums.
 void ArrowBatch::FillReads(const std::vector<int>& readsIn)
 {
-    // 0: one lane per read, columns of up to kFillLaneRows rows in an LDS ring (fill_lane.hip);
-    // cooperative (fill_coop.hip): 1: 16 lanes / 64 rows; 2: 64 lanes / 1024 rows, LDS only; 3: 64 lanes, as
-    // many rows as LDS holds and the rest of a column in global memory (the hybrid path: never too tall, so a
+    // Cooperative paths (fill_coop.hip): 1: 16 lanes / 64 rows; 2: 64 lanes / 1024 rows, LDS only; 3: 64 lanes,
+    // as many rows as LDS holds and the rest of a column in global memory (the hybrid path: never too tall, so a
     // fill re-routes a read at most twice).  Reads whose bases do not fit LDS beside 64 rows go to the
-    // lane-serial k_fill (FillReadsSerial).
+    // lane-serial k_fill (FillReadsSerial).  Path 0 was a one-lane-per-read fill with an LDS ring per lane
+    // (fill_lane.hip, removed in round 3): ~2x fewer VALU instructions, but a single lane's serial loop per read
+    // -- measured 2937 / 3006 ZMWs/s against 3403 / 3465 without it under the round-3 wave sorting
+    // (profiles/r3m_*; round 2: profiles/r2_lane_fill_ab.txt).
     constexpr int kPaths = 4;
-    // The lane fill is opt-in (PBCCS_FILL_LANE=1).  It issues ~2x fewer VALU instructions for the band cells it
-    // takes (rocprofv3: 142 G + 149 G for the reads it passes on, against 510 G on k_fill_coop<16>), but one
-    // read's fill is a single lane's serial loop -- ~3x the latency of the 16-lane group -- and a batch's refine
-    // rounds wait on their slowest fill: measured 2965-3095 ZMWs/s against 3194-3263 without it
-    // (profiles/r2_lane_fill_ab.txt).  Lanes idle once their read's passes end (a wave runs its slowest read's
-    // flip-flops), which is where most of the remaining instructions go.
-    const char* laneEnv = std::getenv("PBCCS_FILL_LANE");   // read per call: a test switches it at run time
-    const bool laneFill = laneEnv && std::strcmp(laneEnv, "1") == 0;
     for (int r : readsIn) EnsureCapacity(r);
     // a read moves from path p to the tall paths: long windows skip the 1024-row LDS path (their tall bands
     // mostly outgrow it -- 10 kb: 662 of 786 reads went on to the hybrid path -- and each step is one more
@@ -747,7 +741,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     // slots per chain step) measured 1290 against 2480 ZMWs/s and were removed: the tall reads are each
     // round's critical path and 16-row chunks pay the per-chunk band logic 4x as often.
     auto rows_for = [&](int p, int maxI, int w) -> int {
-        if (p == 0) return laneFill ? kFillLaneRows : 0;
+        if (p == 0) return 0;
         if (p == 1) return 4 * coop_group_bytes(kCoopNarrowRows, w, 0) <= kCoopLdsBytes ? kCoopNarrowRows : 0;
         const long long room = ((long long)kCoopLdsBytes - (long long)coop_group_bytes(0, w, 0)) / 16 / 64 * 64;
         const long long full = (maxI + 64) / 64 * 64;   // a column never exceeds I + 1 rows
@@ -908,8 +902,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             }
             const int* lp = dList_.ptr + off;
             const hipStream_t st = p <= 1 ? stream_ : stream2_;
-            if (p == 0) Timed(kKFill, [&] { launch_fill_lane(B, F, lp, n, st); }, st);
-            else Timed(p == 1 ? kKFill : kKFillTall, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
+            Timed(p == 1 ? kKFill : kKFillTall, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
             PBCCS_HIP(hipGetLastError());
             counters_.fillLaunches += 1;
             off += n;

@@ -269,7 +269,7 @@ private:
         double baseline = 0.0;
         int flips = 0;
         int status = 0;
-        int fillPath = 0;   // 0: k_fill_lane, 1: k_fill_coop<16>, 2: k_fill_coop<64> (LDS), 3: hybrid, 4: lane-serial
+        int fillPath = 1;   // 0: (unused), 1: k_fill_coop<16>, 2: k_fill_coop<64> (LDS), 3: hybrid, 4: lane-serial
         long long seqOff = 0;
         long long colBase = 0;
         int colCap = 0;

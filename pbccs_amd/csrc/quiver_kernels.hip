@@ -20,12 +20,22 @@ __device__ __forceinline__ void row_range(const QBand& m, int j, float scoreDiff
     int b = m.range[j].x, e = m.range[j].y;
     int maxRow = b;
     float maxScore = m.Get(maxRow, j);
-    for (int i = b + 1; i < e; ++i) {
+    // the first maximum, scanning down (strict '>'); loads issued 8 at a time so that one lane's serial scan
+    // waits on memory once per 8 rows, not once per row
+    int i = b + 1;
+    for (; i + 8 <= e; i += 8) {
+        float s[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[q] = m.Get(i + q, j);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (s[q] > maxScore) { maxRow = i + q; maxScore = s[q]; }
+    }
+    for (; i < e; ++i) {
         const float s = m.Get(i, j);
         if (s > maxScore) { maxRow = i; maxScore = s; }
     }
     const float thr = maxScore - scoreDiff;
-    int i;
     for (i = b; i < maxRow && m.Get(i, j) < thr; ++i) {}
     b = i;
     for (i = e - 1; i >= maxRow && m.Get(i, j) < thr; --i) {}
@@ -495,6 +505,12 @@ __device__ __forceinline__ long long allocated_entries(const QAlloc* a, int cols
 constexpr int kQCoopMaxRows = 4096;   // reads of up to 4095 bases (three LDS columns: 48 KB)
 
 __device__ __forceinline__ float rl(float x, int k) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), k)); }
+// DPP move of a float (gfx9): lanes without a source, or in rows the row mask leaves out, get `old`
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f(float old, float x)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(x), CTRL, ROWMASK, 0xF, false));
+}
 __device__ __forceinline__ float fmax_ref(float a, float b) { return b > a ? b : a; }   // keeps a on ties
 
 __device__ __forceinline__ float wave_max(float x)
@@ -648,8 +664,9 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
         }
         // band stopping rule per quad: gmin = the quad's block min (the prefix quad: its last row), gmax
         const int qb = lane & ~3;
-        const float q0 = __shfl(sv, qb, 64), q1 = __shfl(sv, qb + 1, 64), q2 = __shfl(sv, qb + 2, 64),
-                    q3 = __shfl(sv, qb + 3, 64);
+        // the quad's four values in every lane of the quad (DPP quad_perm broadcasts)
+        const float q0 = dpp_f<0x00, 0xF>(kNegInf, sv), q1 = dpp_f<0x55, 0xF>(kNegInf, sv),
+                    q2 = dpp_f<0xAA, 0xF>(kNegInf, sv), q3 = dpp_f<0xFF, 0xF>(kNegInf, sv);
         float gmin, gmax;
         if (pre) {
             // rows in processing order within the prefix quad: the valid ones, last = the quad's last valid
@@ -677,16 +694,19 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
             if (gmax < q3) gmax = q3;
             if (q3 < gmin) gmin = q3;
         }
-        // running max before each quad (exclusive scan over quads, seeded with mx)
+        // running max before each quad (exclusive scan over quads, seeded with mx): an inclusive DPP max-scan
+        // over the lanes (row_shr 1/2/4/8, then row_bcast 15/31), shifted by one lane.  Only a quad's first lane
+        // tests (the ballot below), and gmin / gmax are quad-uniform, so "the quad before" is the lane before.
         float inc = gmax;
-        for (int o = 1; o < 64; o <<= 1) {
-            const float y = __shfl_up(inc, o, 64);
-            if (lane >= o) inc = fmax_ref(inc, y);
-        }
-        const float prevInc = __shfl_up(inc, 1, 64);
-        const float mxBefore = fmax_ref(mx, lane >= 1 ? prevInc : kNegInf);
-        const float prevMin = __shfl_up(gmin, 4, 64);
-        const float scoreBefore = lane >= 4 ? prevMin : score;
+        inc = fmax_ref(inc, dpp_f<0x111, 0xF>(kNegInf, inc));
+        inc = fmax_ref(inc, dpp_f<0x112, 0xF>(kNegInf, inc));
+        inc = fmax_ref(inc, dpp_f<0x114, 0xF>(kNegInf, inc));
+        inc = fmax_ref(inc, dpp_f<0x118, 0xF>(kNegInf, inc));
+        inc = fmax_ref(inc, dpp_f<0x142, 0xA>(kNegInf, inc));   // row_bcast:15
+        inc = fmax_ref(inc, dpp_f<0x143, 0xC>(kNegInf, inc));   // row_bcast:31
+        const float mxBefore = fmax_ref(mx, dpp_f<0x138, 0xF>(kNegInf, inc));   // wave_shr:1; lane 0: -FLT_MAX
+        const float prevMin = dpp_f<0x138, 0xF>(score, gmin);                  // lane 0: the score so far
+        const float scoreBefore = prevMin;
         // the quad's block start (its lowest row) and test; the prefix quad never stops
         const int lowRow = BETA ? chunk - 64 * c - qb - 3 : chunk + 64 * c + qb;
         bool ok;
@@ -705,8 +725,8 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
         // state after the last kept quad
         if (stopQuad > 0) {
             const int lastLane = 4 * stopQuad - 1;
-            score = __shfl(gmin, lastLane, 64);
-            mx = fmax_ref(mx, __shfl(inc, lastLane, 64));
+            score = rl(gmin, lastLane);
+            mx = fmax_ref(mx, rl(inc, lastLane));
             thr = mx == kNegInf ? kNegInf : mx - sd;
         }
         if (stopQuad < 16) {

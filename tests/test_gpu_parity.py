@@ -212,26 +212,6 @@ def test_fills_2kb_match_oracle(P):
             assert _close(x, y, 1e-12, 1e-12)
 
 
-def test_lane_fill_matches_oracle(P, monkeypatch):
-    """The opt-in lane fill (PBCCS_FILL_LANE=1, fill_lane.hip): configs[1] fills (per-read LL, flip-flops;
-    the reads whose columns outgrow its 32-row ring move on to the cooperative paths) and a batch polish."""
-    from pbccs_amd import synth
-    monkeypatch.setenv("PBCCS_FILL_LANE", "1")
-    for z in synth.make_zmws(2, 2000, 10, seed=62):
-        g, o, rg, ro = _scorers(P, z["draft"], z["reads"])
-        assert rg == ro
-        assert g.NumFlipFlops() == [o.read_info(k)["flipflops"] for k in range(len(z["reads"]))]
-        for x, y in zip(g.BaselineScores(), [o.read_info(k)["ll"] for k in range(len(z["reads"]))]):
-            assert _close(x, y, 1e-12, 1e-12)
-    zs = synth.make_zmws(6, 700, 8, seed=63)
-    for z, r in zip(zs, P.polish_zmws(zs)):
-        e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
-        assert r["add_read_results"] == e["add_read_results"]
-        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
-        if e["converged"]:
-            assert r["consensus"] == e["template"]
-
-
 def test_polish_2kb_batch_matches_oracle(P):
     """configs[1] ZMWs (2 kb insert, 10 passes) through the batch entry point: bit-exact consensus,
     nTested/nApplied and AddRead results; QVs within +-1."""

@@ -22,7 +22,7 @@ import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
-KERNELS = {"k_fill": r"k_fill_coop<16|k_fill_lane", "k_fill_tall": r"k_fill_coop<64|k_fill$",
+KERNELS = {"k_fill": r"k_fill_coop<16", "k_fill_tall": r"k_fill_coop<64|k_fill$",
            "k_score": r"k_score"}   # k_score + k_score_edge (one Timed launch in the engine)
 
 
