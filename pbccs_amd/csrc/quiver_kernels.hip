@@ -580,14 +580,87 @@ struct LdsCol {
     __device__ __forceinline__ float at(int i) const { return (i >= b && i < e) ? v[i & mask] : kNegInf; }
 };
 
+// The read's QV-feature rows [lo, lo + kQWinRows) staged in LDS, row i at slot i & (kQWinRows - 1): a column's
+// chunk reads 65 consecutive rows, and the band moves about a row per column, so the window is reloaded (one
+// coalesced pass of the wave) only every few hundred columns instead of six HBM/L2 loads per cell.
+constexpr int kQWinRows = 256;
+struct QWin {
+    float* ins;
+    float* subs;
+    float* del;
+    float* tag;
+    float* merge;
+    char* seq;
+    int lo;
+};
+
+// Rows [need0, need1] (clamped to the read's [0, I)) in the window; a reload is wave-uniform.  Alpha chunks
+// move down, beta chunks up: the window is placed ahead of them.
+template <bool BETA>
+__device__ __forceinline__ void win_ensure(QWin& w, const QRead& R, int need0, int need1, int lane)
+{
+    need0 = max(need0, 0);
+    need1 = min(need1, R.I - 1);
+    if (need0 > need1 || (need0 >= w.lo && need1 < w.lo + kQWinRows)) return;
+    const int lo = BETA ? max(0, need1 + 8 - (kQWinRows - 1)) : max(0, need0 - 8);
+    __syncthreads();   // (one wave per block) earlier reads of the slots come first
+    for (int q = lane; q < kQWinRows; q += 64) {
+        const int i = lo + q;
+        if (i < R.I) {
+            const int k = i & (kQWinRows - 1);
+            w.seq[k] = R.seq[i];
+            w.ins[k] = R.ins[i];
+            w.subs[k] = R.subs[i];
+            w.del[k] = R.del[i];
+            w.tag[k] = R.tag[i];
+            w.merge[k] = R.merge[i];
+        }
+    }
+    __syncthreads();
+    w.lo = lo;
+}
+
+// QvEvaluator (QvEvaluator.hpp:150-207) over the window, the same expressions as QEval's
+struct QEvalWin {
+    const QEval& e;
+    const QWin& w;
+    __device__ __forceinline__ int K(int i) const { return i & (kQWinRows - 1); }
+    __device__ __forceinline__ float Inc(int i, int j) const
+    {
+        const QParams* p = e.p;
+        return (w.seq[K(i)] == e.t.at(j)) ? p->Match : p->Mismatch + p->MismatchS * w.subs[K(i)];
+    }
+    __device__ __forceinline__ float Del(int i, int j) const
+    {
+        const QParams* p = e.p;
+        const float tb = (float)e.t.at(j);
+        return (i < e.r.I && tb == w.tag[K(i)]) ? p->DeletionWithTag + p->DeletionWithTagS * w.del[K(i)] : p->DeletionN;
+    }
+    __device__ __forceinline__ float Extra(int i, int j) const
+    {
+        const QParams* p = e.p;
+        return (j < e.t.len && w.seq[K(i)] == e.t.at(j)) ? p->Branch + p->BranchS * w.ins[K(i)]
+                                                          : p->Nce + p->NceS * w.ins[K(i)];
+    }
+    __device__ __forceinline__ float Merge(int i, int j) const
+    {
+        const char a = e.t.at(j), b = e.t.at(j + 1), s = w.seq[K(i)];
+        if (!(s == a && s == b)) return kNegInf;
+        const int k = tpl_code(a);
+        return e.p->Merge[k] + e.p->MergeS[k] * w.merge[K(i)];
+    }
+};
+
 // One column of one pass.  BETA: rows run downwards (lane l <-> row top - l), the chain from row + 1.
 // Returns the column's [begin, end) in *ob / *oe and leaves its cells in cur.v (rows of the range) and in
 // the arena at out.off[j].  thrOut: the running threshold after the last evaluated block.
 template <bool BETA>
-__device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int hb, int he, const LdsCol& c1,
+__device__ __forceinline__ void coop_column(const QEval& e0, int j, int lane, int hb, int he, const LdsCol& c1,
                                             const LdsCol& c2, float* cur, const QBand& out, long long base, QAlloc* alloc,
-                                            bool& ovf, int* ob, int* oe, float* thrOut, int mask, bool& tall)
+                                            bool& ovf, int* ob, int* oe, float* thrOut, int mask, bool& tall, QWin& win)
 {
+    const QEval& e = e0;
+    const QEvalWin ew{e0, win};
     const int I = e.I(), J = e.J();
     const bool sp = e.p->sumProduct != 0;
     const bool merge = (e.p->moves & kMerge) != 0;
@@ -619,6 +692,9 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
             *thrOut = thr;
             return;
         }
+        // feature rows of this chunk: alpha reads rows row - 1 and row, beta row
+        if (BETA) win_ensure<true>(win, e.r, chunk - 64 * c - 63, chunk - 64 * c, lane);
+        else win_ensure<false>(win, e.r, chunk + 64 * c - 1, chunk + 64 * c + 63, lane);
         const int row = BETA ? chunk - 64 * c - lane : chunk + 64 * c + lane;
         const bool valid = BETA ? (row <= first && row >= 0) : (row >= first && row <= I);
         const int g = lane >> 2;
@@ -629,38 +705,56 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
             if (!BETA) {
                 if (pre) {
                     if (row == 0 && j == 0) v = 0.0f;
-                    if (row > 0 && j > 0) v = comb(sp, v, c1.at(row - 1) + e.Inc(row - 1, j - 1));
-                    if (merge && row > 0 && j > 1) v = comb(sp, v, c2.at(row - 1) + e.Merge(row - 1, j - 2));
-                    if (j > 0) v = comb(sp, v, c1.at(row) + e.Del(row, j - 1));
+                    if (row > 0 && j > 0) v = comb(sp, v, c1.at(row - 1) + ew.Inc(row - 1, j - 1));
+                    if (merge && row > 0 && j > 1) v = comb(sp, v, c2.at(row - 1) + ew.Merge(row - 1, j - 2));
+                    if (j > 0) v = comb(sp, v, c1.at(row) + ew.Del(row, j - 1));
                 } else {
-                    if (j > 0) v = comb4(sp, v, c1.at(row - 1) + e.Inc(row - 1, j - 1));
-                    if (merge && j >= 2) v = comb4(sp, v, c2.at(row - 1) + e.Merge(row - 1, j - 2));
-                    if (j > 0) v = comb4(sp, v, c1.at(row) + e.Del(row, j - 1));
+                    if (j > 0) v = comb4(sp, v, c1.at(row - 1) + ew.Inc(row - 1, j - 1));
+                    if (merge && j >= 2) v = comb4(sp, v, c2.at(row - 1) + ew.Merge(row - 1, j - 2));
+                    if (j > 0) v = comb4(sp, v, c1.at(row) + ew.Del(row, j - 1));
                 }
                 has = row > 0;
-                if (has) x = e.Extra(row - 1, j);
+                if (has) x = ew.Extra(row - 1, j);
             } else {
                 if (pre) {
                     if (row == I && j == J) v = 0.0f;
-                    if (row < I && j < J) v = comb(sp, v, c1.at(row + 1) + e.Inc(row, j));
-                    if (merge && j < J - 1 && row < I) v = comb(sp, v, c2.at(row + 1) + e.Merge(row, j));
-                    if (j < J) v = comb(sp, v, c1.at(row) + e.Del(row, j));
+                    if (row < I && j < J) v = comb(sp, v, c1.at(row + 1) + ew.Inc(row, j));
+                    if (merge && j < J - 1 && row < I) v = comb(sp, v, c2.at(row + 1) + ew.Merge(row, j));
+                    if (j < J) v = comb(sp, v, c1.at(row) + ew.Del(row, j));
                 } else {
-                    if (j < J) v = comb4(sp, v, c1.at(row + 1) + e.Inc(row, j));
-                    if (merge && j < J - 1) v = comb4(sp, v, c2.at(row + 1) + e.Merge(row, j));
-                    if (j < J) v = comb4(sp, v, c1.at(row) + e.Del(row, j));
+                    if (j < J) v = comb4(sp, v, c1.at(row + 1) + ew.Inc(row, j));
+                    if (merge && j < J - 1) v = comb4(sp, v, c2.at(row + 1) + ew.Merge(row, j));
+                    if (j < J) v = comb4(sp, v, c1.at(row) + ew.Del(row, j));
                 }
                 has = row < I;
-                if (has) x = e.Extra(row, j);
+                if (has) x = ew.Extra(row, j);
             }
         }
         // the Extra cascade, in processing order through the valid lanes
         float sv = valid ? v : kNegInf;
         const int k0 = BETA ? max(0, chunk - 64 * c - first) : max(0, first - (chunk + 64 * c));
         const int k1 = BETA ? min(63, chunk - 64 * c) : min(63, I - (chunk + 64 * c));
-        for (int k = k0; k <= k1; ++k) {
-            if (lane == k && has) sv = comb(sp, v, carry + x);
-            carry = rl(sv, k);
+        if (!sp) {
+            // Viterbi: the cascade sv_k = max(v_k, sv_{k-1} + x_k) (the lane before k0 reads `carry`) has exactly
+            // one solution, computed here by Jacobi sweeps from sv = v: each sweep is one DPP shift, add and max
+            // on every lane, and the sweeps only rise towards that solution, so the first sweep that changes no
+            // lane has reached it -- the same floats as the serial loop, in 1 + (the longest run of rows the
+            // Extra move wins) sweeps instead of one serial step per row.
+            // (at most k1 - k0 + 2 sweeps: the serial loop's step count bounds them, NaN inputs included)
+            for (int it = k0; it <= k1 + 1; ++it) {
+                float prev = dpp_f<0x138, 0xF>(carry, sv);   // wave_shr:1; lane 0 reads carry
+                if (lane == k0) prev = carry;
+                const float nv = has ? comb(false, v, prev + x) : sv;
+                const bool changed = nv != sv;
+                sv = nv;
+                if (__ballot(changed) == 0) break;
+            }
+            if (k1 >= k0) carry = rl(sv, k1);
+        } else {
+            for (int k = k0; k <= k1; ++k) {
+                if (lane == k && has) sv = comb(sp, v, carry + x);
+                carry = rl(sv, k);
+            }
         }
         // band stopping rule per quad: gmin = the quad's block min (the prefix quad: its last row), gmax
         const int qb = lane & ~3;
@@ -754,7 +848,7 @@ __device__ __forceinline__ void coop_column(const QEval& e, int j, int lane, int
 template <bool BETA>
 __device__ long long coop_fill(const QEval& e, const QBand& guideBand, bool useGuide, const QBand& prevBand, bool usePrev,
                                const QBand& out, QAlloc* alloc,
-                               bool allocExists, bool& ovf, float* lds, int ldsRows, int4* hint, int lane)
+                               bool allocExists, bool& ovf, float* lds, int ldsRows, int4* hint, int lane, QWin& win)
 {
     // returns the pass's used cells, or -1 when a column outgrew the band-height ring (kQTall)
     const int I = e.I(), J = e.J();
@@ -784,7 +878,7 @@ __device__ long long coop_fill(const QEval& e, const QBand& guideBand, bool useG
         if (h.z >= 0) { hb = min(h.z, hb); he = max(h.w, he); }
         int b, en;
         float thr;
-        coop_column<BETA>(e, j, lane, hb, he, c1, c2, cur.v, out, used, nullptr, ovf, &b, &en, &thr, mask, tall);
+        coop_column<BETA>(e, j, lane, hb, he, c1, c2, cur.v, out, used, nullptr, ovf, &b, &en, &thr, mask, tall, win);
         if (tall) return -1;
         cur.b = b;
         cur.e = en;
@@ -857,8 +951,11 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
         if (lane == 0) B.rStatus[r] = kQBad;
         return;
     }
-    // the template window in LDS after the column ring: every column reads its bases
-    char* tpl = reinterpret_cast<char*>(qlds + 3 * ldsRows);
+    // LDS: the column ring, the QV-feature window, the template window (every column reads its bases)
+    float* wf = qlds + 3 * ldsRows;
+    QWin win{wf, wf + kQWinRows, wf + 2 * kQWinRows, wf + 3 * kQWinRows, wf + 4 * kQWinRows,
+             reinterpret_cast<char*>(wf + 5 * kQWinRows), INT_MIN / 2};
+    char* tpl = reinterpret_cast<char*>(wf + 5 * kQWinRows) + kQWinRows;
     for (int j = lane; j < J; j += 64) tpl[j] = v.ev.t.base[j];
     v.ev.t.base = tpl;
     const QEval& e = v.ev;
@@ -875,7 +972,7 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
         const int nxt = aPassed ? (curA ^ 1) : 0;
         const QBand g = arena(v, curB), self = arena(v, curA), out = arena(v, nxt);
         const long long u = coop_fill<false>(e, g, guided, self, aPassed, out, v.allocA, aPassed, ovf, qlds, ldsRows,
-                                             v.hint, lane);
+                                             v.hint, lane, win);
         tall = tall || u < 0;
         needA = max(needA, u);
         curA = nxt;
@@ -886,7 +983,7 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
         const int nxt = bPassed ? (curB ^ 1) : 2;
         const QBand g = arena(v, curA), self = arena(v, curB), out = arena(v, nxt);
         const long long u = coop_fill<true>(e, g, true, self, bPassed, out, v.allocB, bPassed, ovf, qlds, ldsRows,
-                                            v.hint, lane);
+                                            v.hint, lane, win);
         tall = tall || u < 0;
         needB = max(needB, u);
         curB = nxt;
@@ -1582,8 +1679,8 @@ void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, in
     // their full height
     const int rows = (maxRows & (maxRows - 1)) == 0 ? maxRows : (maxRows + 63) / 64 * 64;
     const int cols = (maxCols + 15) / 16 * 16;
-    hipLaunchKernelGGL(k_qfill_coop, dim3(n), dim3(64), (size_t)3 * rows * sizeof(float) + cols, s, B, reads, n, rows,
-                       cols);
+    const size_t lds = (size_t)(3 * rows + 5 * kQWinRows) * sizeof(float) + kQWinRows + cols;
+    hipLaunchKernelGGL(k_qfill_coop, dim3(n), dim3(64), lds, s, B, reads, n, rows, cols);
 }
 
 void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s)
