@@ -1383,7 +1383,18 @@ int pbccs_quiver_polish_batch(pbccs_engine* eng, const pbccs_quiver_config* conf
                 specZmw.push_back(z);
             }
         }
+        // PBCCS_QUIVER_TRACE=1: one stderr line with the wall time of each phase (prepare, AddRead, refine, QVs)
+        static const bool qtrace = std::getenv("PBCCS_QUIVER_TRACE") != nullptr;
+        auto qt0 = std::chrono::steady_clock::now();
+        auto lap = [&]() {
+            const auto t = std::chrono::steady_clock::now();
+            const double ms = std::chrono::duration<double, std::milli>(t - qt0).count();
+            qt0 = t;
+            return ms;
+        };
+        const double msPrep = lap();
         const std::vector<char> act = qb.AddReads(&specs);
+        const double msAdd = lap();
         for (int z = 0; z < n; ++z) out[z].n_active = 0;
         for (size_t k = 0; k < act.size(); ++k) out[specZmw[k]].n_active += act[k];
         RefineOptions ro;
@@ -1395,12 +1406,16 @@ int pbccs_quiver_polish_batch(pbccs_engine* eng, const pbccs_quiver_config* conf
         std::vector<long long> nt, na;
         std::vector<char> conv, ok;
         qb.RefineMany(zs, ro, &nt, &na, &conv, &ok);
+        const double msRefine = lap();
         std::vector<int> wantQv;
         for (int z = 0; z < n; ++z)
             if (out[z].qvs && ok[z]) wantQv.push_back(z);
         std::vector<int> qz;
         for (int z : wantQv) qz.push_back(zs[z]);
         const std::vector<std::vector<int>> qv = qz.empty() ? std::vector<std::vector<int>>() : qb.QVsMany(qz);
+        if (qtrace)
+            std::fprintf(stderr, "[quiver] scorers %d prepare %.1f ms addread %.1f ms refine %.1f ms qvs %.1f ms\n", n,
+                         msPrep, msAdd, msRefine, lap());
         for (int z = 0; z < n; ++z) {
             pbccs_quiver_result& o = out[z];
             o.n_tested = nt[z];

@@ -315,12 +315,16 @@ __global__ __launch_bounds__(64) void k_poa_fill_lds(const PoaJob* __restrict__ 
 // the End move into $, then each visited cell with the move that reached it, recomputed as
 // makeAlignmentColumn chose it (candidates in order Start, per predecessor Match/Mismatch then Delete,
 // then Extra; strict '>').
+// The walk is one lane's chain of dependent loads (a column's predecessor list, then their cells); the job's
+// column program -- predStart, predCol and the column bases -- is staged in LDS first (ldsInts ints of dynamic
+// LDS; a larger program stays in HBM), so only the score cells are HBM/L2 loads on the chain.
 template <class ST>
 __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ jobs, const int* __restrict__ traceJobs,
                                                   int traceBase, PoaPools P, const ST* __restrict__ pool,
                                                   const int* __restrict__ exitCol, uint32_t* __restrict__ steps,
-                                                  TraceHeader* __restrict__ heads)
+                                                  TraceHeader* __restrict__ heads, int ldsInts)
 {
+    extern __shared__ int tprog[];
     const int t = traceBase + blockIdx.x;
     const int j = traceJobs[t];
     const PoaJob J = jobs[j];
@@ -329,6 +333,25 @@ __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ job
     const int I = J.I, stride = J.colStride, mode = J.mode, R = J.rowsPerLane;
     const int ec = exitCol[j];
     const int* vtx = P.vertexOfCol + J.progOff;
+    const int nC = J.nCols;
+    const int* psG = P.predStart + J.predStartOff;
+    const int p0 = psG[0], nPred = psG[nC] - p0;
+    const bool staged = nC + 1 + nPred + (nC + 3) / 4 <= ldsInts;
+    const int* predStartT = psG;      // absolute indices into predColT
+    const int* predColT = P.predCol;
+    const uint8_t* baseT = P.base + J.progOff;
+    if (staged) {   // rebased: predStart[c] - p0 indexes the staged predCol
+        int* ps = tprog;
+        int* pc = tprog + nC + 1;
+        uint8_t* bs = reinterpret_cast<uint8_t*>(pc + nPred);
+        for (int c = lane; c <= nC; c += 64) ps[c] = psG[c] - p0;
+        for (int q = lane; q < nPred; q += 64) pc[q] = P.predCol[p0 + q];
+        for (int c = lane; c < nC; c += 64) bs[c] = P.base[J.progOff + c];
+        predStartT = ps;
+        predColT = pc;
+        baseT = bs;
+    }
+    __syncthreads();
     // cell (column c, row i): linear rows, or lane-interleaved for the ring variants
     auto cell = [&](int c, int i) -> int {
         const int x = R ? (i % R) * 64 + i / R : i;
@@ -355,7 +378,7 @@ __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ job
     out[n++] = pack_step(kExit, kEnd);
     int k = ec, i = mode == kLocal ? prevRow : I;
     const uint8_t* rb = P.rowBase + J.readOff;
-    const int* predStart = P.predStart + J.predStartOff;
+    const int* predStart = predStartT;
     while (!(k == 0 && i == 0)) {
         if (n >= cap) {
             n = -1;
@@ -372,7 +395,7 @@ __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ job
                 mv = kInvalid;
                 pv = -1;
                 for (int p = ps; p < pe; ++p) {
-                    const int c = P.predCol[p];
+                    const int c = predColT[p];
                     const int cand = cell(c, 0) + kDeleteScore;
                     if (cand > best) {
                         best = cand;
@@ -391,9 +414,9 @@ __global__ __launch_bounds__(64) void k_poa_trace(const PoaJob* __restrict__ job
                 mv = kInvalid;
                 pv = -1;
             }
-            const bool isMatch = rb[i] == P.base[J.progOff + k];
+            const bool isMatch = rb[i] == baseT[k];
             for (int p = ps; p < pe; ++p) {
-                const int c = P.predCol[p];
+                const int c = predColT[p];
                 int cand = cell(c, i - 1) + (isMatch ? kMatchScore : kMismatchScore);
                 if (cand > best) {
                     best = cand;
@@ -492,6 +515,8 @@ void launch_fill_lds(int variant, int n, int base, size_t lds, hipStream_t s, co
     }
 #undef POA_RING_CASE
 }
+
+constexpr long long kTraceLdsBytes = 48 * 1024;   // k_poa_trace: staged column program per wave
 
 template <class F>
 void parallel_for(int threads, int n, F&& f)
@@ -770,12 +795,26 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
             dSteps_.reserve(stepTotal, false);
             dHeads_.reserve(nt, false);
             if (profiling) check(hipEventRecord(ev_[2], stream_), "event");
-            if (tn > 0)
-                hipLaunchKernelGGL(k_poa_trace<uint16_t>, dim3(tn), dim3(64), 0, stream_, dJobs_.ptr, dTraceJobs_.ptr, 0,
-                                   pools, pool16, dExitCol_.ptr, dSteps_.ptr, dHeads_.ptr);
-            if (tw > 0)
-                hipLaunchKernelGGL(k_poa_trace<int>, dim3(tw), dim3(64), 0, stream_, dJobs_.ptr, dTraceJobs_.ptr, tn,
-                                   pools, pool32, dExitCol_.ptr, dSteps_.ptr, dHeads_.ptr);
+            // LDS for the traced jobs' column programs (k_poa_trace), up to kTraceLdsBytes; larger ones walk from HBM
+            auto progInts = [&](const std::vector<int>& ks) {
+                long long m = 0;
+                for (int k : ks) {
+                    const PoaJob& Jk = gj[k];
+                    const long long np = hPredStart_.ptr[Jk.predStartOff + Jk.nCols] - hPredStart_.ptr[Jk.predStartOff];
+                    m = std::max(m, Jk.nCols + 1 + np + (Jk.nCols + 3) / 4);
+                }
+                return (int)std::min<long long>(m, kTraceLdsBytes / 4);
+            };
+            if (tn > 0) {
+                const int li = progInts(traceNarrow);
+                hipLaunchKernelGGL(k_poa_trace<uint16_t>, dim3(tn), dim3(64), (size_t)li * 4, stream_, dJobs_.ptr,
+                                   dTraceJobs_.ptr, 0, pools, pool16, dExitCol_.ptr, dSteps_.ptr, dHeads_.ptr, li);
+            }
+            if (tw > 0) {
+                const int li = progInts(traceWide);
+                hipLaunchKernelGGL(k_poa_trace<int>, dim3(tw), dim3(64), (size_t)li * 4, stream_, dJobs_.ptr,
+                                   dTraceJobs_.ptr, tn, pools, pool32, dExitCol_.ptr, dSteps_.ptr, dHeads_.ptr, li);
+            }
             check(hipGetLastError(), "k_poa_trace launch");
             if (profiling) check(hipEventRecord(ev_[3], stream_), "event");
             hSteps_.reserve(stepTotal);

@@ -1,6 +1,7 @@
 // pbccs_amd/csrc/quiver_engine.hip -- QuiverBatch (quiver_engine.hpp).
 #include "quiver_engine.hpp"
 
+#include <chrono>
 #include <cstdio>
 
 #include <hipcub/hipcub.hpp>
@@ -851,7 +852,11 @@ void QuiverBatch::RefineMany(const std::vector<int>& zs, const RefineOptions& ro
     std::vector<std::unordered_set<std::string>> history(n);
     std::vector<std::vector<int>> centers(n);
     if (ro.maxIterations <= 0) return;
-    for (;;) {
+    static const bool trace = std::getenv("PBCCS_QUIVER_TRACE") != nullptr;
+    using Clock = std::chrono::steady_clock;
+    auto msSince = [](Clock::time_point a) { return std::chrono::duration<double, std::milli>(Clock::now() - a).count(); };
+    for (int round = 0;; ++round) {
+        const Clock::time_point tr0 = Clock::now();
         std::vector<int> act, idx;
         for (int k = 0; k < n; ++k)
             if (!done[k]) { act.push_back(zs[k]); idx.push_back(k); }
@@ -865,7 +870,11 @@ void QuiverBatch::RefineMany(const std::vector<int>& zs, const RefineOptions& ro
             (*nTested)[k] += (long long)codes[a].size();
         }
         std::vector<std::vector<Scored>> fav, picked;
+        const double msEnum = msSince(tr0);
+        const Clock::time_point tr1 = Clock::now();
         ScoreRound(act, codes, ro.mutationSeparation, &fav, &picked, nullptr);
+        const double msScore = msSince(tr1);
+        const Clock::time_point tr2 = Clock::now();
         std::vector<int> refill;
         for (size_t a = 0; a < act.size(); ++a) {
             const int k = idx[a];
@@ -910,7 +919,12 @@ void QuiverBatch::RefineMany(const std::vector<int>& zs, const RefineOptions& ro
             dirty_ = true;
             if (++iter[k] >= ro.maxIterations) done[k] = 1;
         }
+        const double msApply = msSince(tr2);
+        const Clock::time_point tr3 = Clock::now();
         if (!refill.empty()) Fill(refill);   // a refill that mismatches marks the read inactive
+        if (trace)
+            std::fprintf(stderr, "[quiver] round %d scorers %zu enumerate %.1f ms score %.1f ms apply %.1f ms fill %.1f ms\n",
+                         round, act.size(), msEnum, msScore, msApply, msSince(tr3));
     }
 }
 
