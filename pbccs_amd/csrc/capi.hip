@@ -1369,17 +1369,14 @@ int pbccs_quiver_polish_batch(pbccs_engine* eng, const pbccs_quiver_config* conf
                 sp.te = q.tend < 0 ? zmws[z].tpl_len : q.tend;
                 sp.config = cfg;
                 sp.threshold = std::isnan(q.threshold) ? cfgs[pos]->add_threshold : q.threshold;
-                sp.f.seq.assign(q.seq, q.len);
-                auto track = [&](std::vector<float>& v, const float* src) {
-                    v.assign(q.len, 0.0f);
-                    if (src) std::copy(src, src + q.len, v.begin());
-                };
-                track(sp.f.ins, q.ins_qv);
-                track(sp.f.subs, q.subs_qv);
-                track(sp.f.del, q.del_qv);
-                track(sp.f.tag, q.del_tag);
-                track(sp.f.merge, q.merge_qv);
-                specs.push_back(std::move(sp));
+                sp.seq = q.seq;
+                sp.len = q.len;
+                sp.track[0] = q.ins_qv;
+                sp.track[1] = q.subs_qv;
+                sp.track[2] = q.del_qv;
+                sp.track[3] = q.del_tag;
+                sp.track[4] = q.merge_qv;
+                specs.push_back(sp);
                 specZmw.push_back(z);
             }
         }

@@ -133,16 +133,37 @@ bool QuiverBatch::AddRead(int zi, const QReadFeatures& f, int strand, int ts, in
     one[0].te = te;
     one[0].config = config;
     one[0].threshold = threshold;
-    one[0].f = f;
+    const size_t I = f.seq.size();
+    if (f.ins.size() != I || f.subs.size() != I || f.del.size() != I || f.tag.size() != I || f.merge.size() != I)
+        throw std::invalid_argument("QV feature tracks must match the read length");
+    one[0].seq = f.seq.data();
+    one[0].len = (int)I;
+    const float* const track[5] = {f.ins.data(), f.subs.data(), f.del.data(), f.tag.data(), f.merge.data()};
+    for (int k = 0; k < 5; ++k) one[0].track[k] = track[k];
     return AddReads(&one)[0] != 0;
 }
 
 std::vector<char> QuiverBatch::AddReads(std::vector<ReadSpec>* specs)
 {
+    // the host pools grow once (a 10000-scorer batch holds ~4 GB of QV tracks: no reallocation copies)
+    size_t bases = 0;
+    for (const ReadSpec& sp : *specs) bases += (size_t)std::max(0, sp.len);
+    hSeq_.reserve(hSeq_.size() + bases);
+    hFeat_.reserve(hFeat_.size() + 5 * bases);
+    static const bool trace = std::getenv("PBCCS_QUIVER_TRACE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     std::vector<int> added;
     for (ReadSpec& sp : *specs)
-        added.push_back(Register(sp.z, sp.f, sp.strand, sp.ts, sp.te, sp.config));
+        added.push_back(RegisterRaw(sp.z, sp.seq, sp.len, sp.track, sp.strand, sp.ts, sp.te, sp.config));
+    const auto t1 = std::chrono::steady_clock::now();
+    Upload();
+    const auto t2 = std::chrono::steady_clock::now();
     Fill(added);
+    if (trace)
+        std::fprintf(stderr, "[quiver] addreads %zu register %.1f ms upload %.1f ms fill %.1f ms\n", added.size(),
+                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                     std::chrono::duration<double, std::milli>(t2 - t1).count(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
     std::vector<char> act(specs->size());
     for (size_t k = 0; k < specs->size(); ++k) {
         // AddRead: a scorer whose construction threw (alpha/beta mismatch) is dropped; so is one whose
@@ -161,15 +182,14 @@ std::vector<char> QuiverBatch::AddReads(std::vector<ReadSpec>* specs)
     return act;
 }
 
-int QuiverBatch::Register(int zi, const QReadFeatures& f, int strand, int ts, int te, int config)
+int QuiverBatch::RegisterRaw(int zi, const char* seq, int len, const float* const track[5], int strand, int ts, int te,
+                             int config)
 {
     HZmw& z = zmws_.at(zi);
     const int L = (int)z.tpl.size();
-    const size_t I = f.seq.size();
-    if (ts < 0 || te > L || ts > te || I < 1 || config < 0 || config >= (int)configs_.size())
+    const size_t I = (size_t)std::max(0, len);
+    if (ts < 0 || te > L || ts > te || len < 1 || !seq || config < 0 || config >= (int)configs_.size())
         throw std::invalid_argument("read window outside the template or bad config");
-    if (f.ins.size() != I || f.subs.size() != I || f.del.size() != I || f.tag.size() != I || f.merge.size() != I)
-        throw std::invalid_argument("QV feature tracks must match the read length");
     HRead r;
     r.zmw = zi;
     r.config = config;
@@ -178,9 +198,11 @@ int QuiverBatch::Register(int zi, const QReadFeatures& f, int strand, int ts, in
     r.te = te;
     r.len = (int)I;
     r.seqOff = (long long)hSeq_.size();
-    hSeq_.insert(hSeq_.end(), f.seq.begin(), f.seq.end());
-    for (const std::vector<float>* t : {&f.ins, &f.subs, &f.del, &f.tag, &f.merge})
-        hFeat_.insert(hFeat_.end(), t->begin(), t->end());
+    hSeq_.insert(hSeq_.end(), seq, seq + I);
+    for (int k = 0; k < 5; ++k) {
+        if (track[k]) hFeat_.insert(hFeat_.end(), track[k], track[k] + I);
+        else hFeat_.resize(hFeat_.size() + I, 0.0f);
+    }
     r.colBuf = -1;
     reads_.push_back(r);
     const int ri = (int)reads_.size() - 1;
@@ -607,27 +629,9 @@ bool QuiverBatch::Alignment(int r, std::string* target, std::string* query)
     return true;
 }
 
-std::vector<int> QuiverBatch::QVs(int zi)   // ConsensusQVs (Consensus-inl.hpp:274-295)
+std::vector<int> QuiverBatch::QVs(int zi)   // ConsensusQVs (Consensus-inl.hpp:274-295), the batched device path
 {
-    const std::string tpl = zmws_[zi].tpl;
-    std::vector<int> codes, posOff;
-    for (int p = 0; p < (int)tpl.size(); ++p) {
-        posOff.push_back((int)codes.size());
-        unique_mutations(tpl, p, p + 1, &codes);
-    }
-    posOff.push_back((int)codes.size());
-    std::vector<float> d;
-    Deltas(zi, codes, &d);
-    std::vector<int> qv;
-    for (int p = 0; p < (int)tpl.size(); ++p) {
-        double sum = 0.0;
-        for (int m = posOff[p]; m < posOff[p + 1]; ++m) {
-            const double s = Score(zi, d, m, false);
-            if (s < 0.0) sum += std::exp(s);
-        }
-        qv.push_back(probability_to_qv(1.0 - 1.0 / (1.0 + sum)));
-    }
-    return qv;
+    return QVsMany({zi})[0];
 }
 
 
@@ -749,8 +753,7 @@ void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std:
 }
 
 void QuiverBatch::ScoreRound(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes, int sep,
-                             std::vector<std::vector<Scored>>* fav, std::vector<std::vector<Scored>>* picked,
-                             std::vector<std::vector<float>>* all)
+                             std::vector<std::vector<Scored>>* fav, std::vector<std::vector<Scored>>* picked)
 {
     const int n = (int)zs.size();
     std::vector<long long> taskStart, mutStart;
@@ -770,15 +773,6 @@ void QuiverBatch::ScoreRound(const std::vector<int>& zs, const std::vector<std::
     R.nMut = nMut;
     launch_qreduce(R, stream_);
     QHIP(hipGetLastError());
-    if (all) {
-        std::vector<double> sc;
-        get(sc, dMScore_, nMut, stream_);
-        QHIP(hipStreamSynchronize(stream_));
-        all->assign(n, {});
-        for (int w = 0; w < n; ++w)
-            for (long long g = mutStart[w]; g < mutStart[w + 1]; ++g) (*all)[w].push_back((float)sc[g]);
-        return;
-    }
     // favourable entries in list order, then BestSubset per scorer
     const int nm = (int)std::max<long long>(nMut, 1);
     dSel_.reserve(nm, false);
@@ -872,7 +866,7 @@ void QuiverBatch::RefineMany(const std::vector<int>& zs, const RefineOptions& ro
         std::vector<std::vector<Scored>> fav, picked;
         const double msEnum = msSince(tr0);
         const Clock::time_point tr1 = Clock::now();
-        ScoreRound(act, codes, ro.mutationSeparation, &fav, &picked, nullptr);
+        ScoreRound(act, codes, ro.mutationSeparation, &fav, &picked);
         const double msScore = msSince(tr1);
         const Clock::time_point tr2 = Clock::now();
         std::vector<int> refill;
@@ -930,31 +924,57 @@ void QuiverBatch::RefineMany(const std::vector<int>& zs, const RefineOptions& ro
 
 std::vector<std::vector<int>> QuiverBatch::QVsMany(const std::vector<int>& zs)   // ConsensusQVs (:274-295)
 {
+    // every unique single-base mutation of every position, scored over all reads (Score, no fast break), then the
+    // per-position sums and QVs on the device (k_qqv); only the QVs come back
     const int n = (int)zs.size();
-    std::vector<std::vector<int>> codes(n), posOff(n);
+    std::vector<std::vector<int>> codes(n);
+    std::vector<int> posOff;
+    std::vector<long long> posStart(n + 1, 0), posOffBase(n);
     for (int w = 0; w < n; ++w) {
         const std::string& tpl = zmws_[zs[w]].tpl;
+        posOffBase[w] = (long long)posOff.size();
         for (int p = 0; p < (int)tpl.size(); ++p) {
-            posOff[w].push_back((int)codes[w].size());
+            posOff.push_back((int)codes[w].size());
             unique_mutations(tpl, p, p + 1, &codes[w]);
         }
-        posOff[w].push_back((int)codes[w].size());
+        posOff.push_back((int)codes[w].size());
+        posStart[w + 1] = posStart[w] + (long long)tpl.size();
     }
-    std::vector<std::vector<Scored>> fav, picked;
-    std::vector<std::vector<float>> all;
-    ScoreRound(zs, codes, -1, &fav, &picked, &all);
+    std::vector<long long> taskStart, mutStart;
+    ScoreDeltas(zs, codes, &taskStart, &mutStart);
+    const long long nMut = mutStart[n], nPos = posStart[n];
+    dMScore_.reserve(std::max<long long>(nMut, 1), false);
+    dFav_.reserve(std::max<long long>(nMut, 1), false);
+    QReduceWork R;
+    R.nWork = n;
+    R.wMutStart = dWMutBase_.ptr;
+    R.wTaskStart = dWTaskStart_.ptr;
+    R.wNReads = dWNReads_.ptr;
+    R.wFastThreshold = dWFast_.ptr;
+    R.delta = dDelta_.ptr;
+    R.score = dMScore_.ptr;
+    R.fav = dFav_.ptr;
+    R.nMut = nMut;
+    launch_qreduce(R, stream_);
+    put(dPosStart_, posStart, stream_);
+    put(dPosOffBase_, posOffBase, stream_);
+    put(dPosOff_, posOff, stream_);
+    dQv_.reserve(std::max<long long>(nPos, 1), false);
+    QQvWork Q;
+    Q.nWork = n;
+    Q.posStart = dPosStart_.ptr;
+    Q.wMutStart = dWMutBase_.ptr;
+    Q.posOffBase = dPosOffBase_.ptr;
+    Q.posOff = dPosOff_.ptr;
+    Q.score = dMScore_.ptr;
+    Q.qv = dQv_.ptr;
+    launch_qqv(Q, nPos, stream_);
+    QHIP(hipGetLastError());
+    std::vector<int> all;
+    get(all, dQv_, (size_t)nPos, stream_);
+    QHIP(hipStreamSynchronize(stream_));
     std::vector<std::vector<int>> qv(n);
-    for (int w = 0; w < n; ++w) {
-        const int L = (int)posOff[w].size() - 1;
-        for (int p = 0; p < L; ++p) {
-            double sum = 0.0;
-            for (int m = posOff[w][p]; m < posOff[w][p + 1]; ++m) {
-                const double sc = all[w][m];
-                if (sc < 0.0) sum += std::exp(sc);
-            }
-            qv[w].push_back(probability_to_qv(1.0 - 1.0 / (1.0 + sum)));
-        }
-    }
+    for (int w = 0; w < n; ++w) qv[w].assign(all.begin() + posStart[w], all.begin() + posStart[w + 1]);
     return qv;
 }
 

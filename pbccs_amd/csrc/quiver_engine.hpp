@@ -48,10 +48,14 @@ public:
     std::vector<int> QVs(int z);
 
     // ---- batched forms (pbccs_quiver_polish_batch): many scorers in lock-step rounds ------------------
+    // a read of the batch path: the caller's buffers (bases and five tracks of len entries; a null track reads
+    // as zeros), copied once into the engine's host pools
     struct ReadSpec {
         int z, strand, ts, te, config;
         float threshold;
-        QReadFeatures f;
+        const char* seq;
+        int len;
+        const float* track[5];   // ins, subs, del, tag (DelTag as float(char)), merge
     };
     // AddRead for every spec, one fill launch for all; returns each read's active flag
     std::vector<char> AddReads(std::vector<ReadSpec>* specs);
@@ -94,7 +98,9 @@ private:
         long long alloc[2] = {0, 0};
         bool tallRing = false;   // a column outgrew the band-height LDS ring: fill with the full-height one
     };
-    int Register(int z, const QReadFeatures& f, int strand, int ts, int te, int config);   // a read, unfilled
+    // a read, unfilled: its bases and five tracks copied into the host pools
+    int RegisterRaw(int z, const char* seq, int len, const float* const track[5], int strand, int ts, int te,
+                    int config);
     void Upload();
     void EnsureCapacity(int r);
     QBatch View();
@@ -103,7 +109,7 @@ private:
                   bool raw, std::vector<float>* d);
     // One batched scoring round over scorers zs with their mutation lists: per scorer the favourable
     // mutations (list order, float scores) and, with sep >= 0, BestSubset's picks (pick order) from the
-    // device select; with all != nullptr every mutation's Score instead.
+    // device select.
     struct Scored {
         int code;
         float score;
@@ -111,8 +117,7 @@ private:
     void ScoreDeltas(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes,
                      std::vector<long long>* taskStart, std::vector<long long>* mutStart);
     void ScoreRound(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes, int sep,
-                    std::vector<std::vector<Scored>>* fav, std::vector<std::vector<Scored>>* picked,
-                    std::vector<std::vector<float>>* all);
+                    std::vector<std::vector<Scored>>* fav, std::vector<std::vector<Scored>>* picked);
 
     int device_ = 0;
     hipStream_t stream_ = nullptr;
@@ -142,6 +147,8 @@ private:
     DevVec<long long> dWTaskStart_, dWMutBase_, dSel_, dSelCount_, dSelBase_;
     DevVec<long long> dWaveStart_, dWMutCount_, dEdge_;   // k_qscore_mid work + its edge-case task list
     DevVec<unsigned long long> dEdgeCount_;
+    DevVec<long long> dPosStart_, dPosOffBase_;   // QVsMany: per-position QVs on the device (k_qqv)
+    DevVec<int> dPosOff_, dQv_;
     DevVec<int> dWReadBase_, dWNReads_, dReadList_, dRActive_, dSelCode_, dSelRank_, dNSel_;
     DevVec<float> dWFast_;
     DevVec<double> dMScore_, dSelScore_;

@@ -1613,6 +1613,29 @@ __global__ void __launch_bounds__(64 * kQMidWaves) k_qscore_mid(QBatch B, QMidWo
     W.delta[t] = score - B.rScore[r];
 }
 
+// ---- k_qqv: ConsensusQVs of a batched round (Consensus-inl.hpp:274-295) ------------------------------------
+__global__ void __launch_bounds__(256) k_qqv(QQvWork W, long long nPos)
+{
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nPos) return;
+    int lo = 0, hi = W.nWork;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (W.posStart[mid] <= g) lo = mid; else hi = mid;
+    }
+    const int p = (int)(g - W.posStart[lo]);
+    const int* po = W.posOff + W.posOffBase[lo];
+    const double* sc = W.score + W.wMutStart[lo];
+    double sum = 0.0;
+    for (int m = po[p]; m < po[p + 1]; ++m) {
+        const double s = (double)(float)sc[m];   // Score() is a float sum
+        if (s < 0.0) sum += exp(s);
+    }
+    double prob = 1.0 - 1.0 / (1.0 + sum);
+    if (prob == 0.0) prob = 2.2250738585072014e-308;   // std::numeric_limits<double>::min()
+    W.qv[g] = (int)round(-10.0 * log10(prob));
+}
+
 // ---- k_qalign: RecursorBase::Alignment (detail/RecursorBase.cpp:118-264) -------------------------------
 // The Viterbi path through a read's final alpha band, one lane per read, walking back from (I, J): moves
 // tried in the order Incorporate, Delete, Extra, Merge, strict '>' against -FLT_MAX, the move score added
@@ -1694,6 +1717,12 @@ void launch_qscore_mid(const QBatch& B, const QMidWork& W, long long nWaves, hip
     if (nWaves <= 0) return;
     hipLaunchKernelGGL(k_qscore_mid, dim3((unsigned)((nWaves + kQMidWaves - 1) / kQMidWaves)), dim3(64 * kQMidWaves),
                        0, s, B, W);
+}
+
+void launch_qqv(const QQvWork& W, long long nPos, hipStream_t s)
+{
+    if (nPos <= 0) return;
+    hipLaunchKernelGGL(k_qqv, dim3((unsigned)((nPos + 255) / 256)), dim3(256), 0, s, W, nPos);
 }
 
 void launch_qreduce(const QReduceWork& W, hipStream_t s)

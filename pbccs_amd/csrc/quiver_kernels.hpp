@@ -118,6 +118,19 @@ struct QReduceWork {
     long long nMut;
 };
 
+// ConsensusQVs (Consensus-inl.hpp:274-295) of a batched QV round, one lane per template position: the sum of
+// exp(score) over the position's mutations with a negative (float) score, then -10 log10(1 - 1 / (1 + sum)).
+struct QQvWork {
+    int nWork;
+    const long long* posStart;     // item w's positions [posStart[w], posStart[w + 1]) (global position index)
+    const long long* wMutStart;    // item w's mutations start in score[]
+    const long long* posOffBase;   // item w's position offsets at posOff + posOffBase[w] (L + 1 of them)
+    const int* posOff;             // mutation offset of each position within its item
+    const double* score;           // k_qreduce's per-mutation sums
+    int* qv;                       // per global position
+};
+void launch_qqv(const QQvWork& W, long long nPos, hipStream_t s);
+
 void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s);
 // FillAlphaBeta with one wavefront per read (SparseSse recursors; reads of I + 1 <= kQCoopRows rows and windows
 // of J + 1 <= kQCoopCols columns); maxRows / maxCols = the largest I + 1 / J + 1 of the listed reads

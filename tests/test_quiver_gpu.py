@@ -1,7 +1,9 @@
 """GPU parity of the Quiver family (HIP engine through the C ABI) against the reference's Quiver gtest
 known answers and against the CPU restatement (oracle/quiver_oracle.cpp) on seeded synthetic reads with
-random QV features.  Tolerance: bit-exact FP32 (every score, baseline, flip-flop count, refine outcome and
-QV), since the engine repeats the SSE recursor's single-precision operations in order."""
+random QV features.  Tolerance: bit-exact FP32 (every score, baseline, flip-flop count and refine outcome), since
+the engine repeats the SSE recursor's single-precision operations in order; ConsensusQVs within +-1 of the
+restatement (the per-position exp sums run on the device, see _qvs_within_one) and equal between the batch and
+the per-scorer calls."""
 import json
 import os
 
@@ -89,6 +91,13 @@ def _zmw(seed, length, passes):
     return z["draft"], reads
 
 
+def _qvs_within_one(got, exp):
+    """ConsensusQVs against the restatement: the per-position sums of exp(score) run on the device (k_qqv, OCML
+    exp/log10) and on the host (glibc), so a QV at a rounding boundary may differ by one -- the north_star's
+    tolerance for QVs (+-1).  Scores, templates and mutation counts stay bit-exact."""
+    return len(got) == len(exp) and all(abs(a - b) <= 1 for a, b in zip(got, exp))
+
+
 @pytest.mark.parametrize("sum_product", [False, True])
 @pytest.mark.parametrize("seed,length,passes", [(101, 80, 3), (102, 200, 5)])
 def test_quiver_scores_match_oracle(sum_product, seed, length, passes):
@@ -116,7 +125,7 @@ def test_quiver_refine_and_qvs_match_oracle(sum_product):
     ref = o.refine()
     assert (conv, nt, na) == (ref["converged"], ref["n_tested"], ref["n_applied"])
     assert g.template() == o.template()
-    assert P.ConsensusQVs(g.s) == o.qvs()
+    assert _qvs_within_one(P.ConsensusQVs(g.s), o.qvs())
 
 
 def test_quiver_add_threshold_memory_gate():
@@ -236,7 +245,7 @@ def test_quiver_polish_batch_matches_scorers(sum_product):
         ref = o.refine()
         assert (g["converged"], g["n_tested"], g["n_applied"]) == (ref["converged"], ref["n_tested"], ref["n_applied"])
         assert g["consensus"] == o.template()
-        assert g["qvs"] == o.qvs()
+        assert _qvs_within_one(g["qvs"], o.qvs())
 
 
 def test_quiver_coop_fill_long_reads_match_oracle():
@@ -269,4 +278,4 @@ def test_quiver_coop_fill_long_reads_match_oracle():
         ref = o.refine()
         assert (r["converged"], r["n_tested"], r["n_applied"]) == (ref["converged"], ref["n_tested"], ref["n_applied"])
         assert r["consensus"] == o.template()
-        assert r["qvs"] == o.qvs()
+        assert _qvs_within_one(r["qvs"], o.qvs())
