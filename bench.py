@@ -499,8 +499,8 @@ def quiver_stage(args, rank, world, eng, barrier, sync, seed0):
     import pbccs_amd as P
     from pbccs_amd import quiver, synth
     cfg = P.QuiverConfig(P.QvModelParams(**synth.QUIVER_PARAMS), score_diff=synth.QUIVER_SCORE_DIFF)
-    for w in range(args.warmup):
-        quiver.polish_batch(synth.make_quiver_zmws(min(args.zmws_per_step, 200), args.length, args.passes,
+    for w in range(args.warmup):   # full-size: the engine's device buffers reach their steady-state size untimed
+        quiver.polish_batch(synth.make_quiver_zmws(args.steps * args.zmws_per_step, args.length, args.passes,
                                                    seed=seed0 + 1000 + w), cfg, engine=eng)
     zs = synth.make_quiver_zmws(args.steps * args.zmws_per_step, args.length, args.passes, seed=seed0)
     prep = quiver.PreparedQuiverBatch(zs, cfg)   # host marshalling before the timed region (as PreparedBatch)

@@ -13,6 +13,7 @@
 #include <limits>
 #include <set>
 #include <stdexcept>
+#include <thread>
 #include <unordered_set>
 
 #include "arrow_kernels.hpp"
@@ -145,16 +146,48 @@ bool QuiverBatch::AddRead(int zi, const QReadFeatures& f, int strand, int ts, in
 
 std::vector<char> QuiverBatch::AddReads(std::vector<ReadSpec>* specs)
 {
-    // the host pools grow once (a 10000-scorer batch holds ~4 GB of QV tracks: no reallocation copies)
-    size_t bases = 0;
-    for (const ReadSpec& sp : *specs) bases += (size_t)std::max(0, sp.len);
-    hSeq_.reserve(hSeq_.size() + bases);
-    hFeat_.reserve(hFeat_.size() + 5 * bases);
+    // the host pools grow once, then the reads' bases and QV tracks (~4 GB for a 10000-scorer batch) are copied in
+    // on several host threads
     static const bool trace = std::getenv("PBCCS_QUIVER_TRACE") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
+    const size_t ns = specs->size();
+    std::vector<long long> seqOff(ns);
+    size_t bases = 0;
+    for (size_t k = 0; k < ns; ++k) {   // every spec is checked before the pools grow
+        const ReadSpec& sp = (*specs)[k];
+        const int L = (int)zmws_.at(sp.z).tpl.size();
+        if (sp.len < 1 || !sp.seq || sp.ts < 0 || sp.te > L || sp.ts > sp.te || sp.config < 0 ||
+            sp.config >= (int)configs_.size())
+            throw std::invalid_argument("read without bases, window outside the template or bad config");
+        seqOff[k] = (long long)(hSeq_.size() + bases);
+        bases += (size_t)sp.len;
+    }
+    const size_t s0 = hSeq_.grow(bases);
+    hFeat_.grow(5 * bases);
+    auto copy = [&](size_t k) {
+        const ReadSpec& sp = (*specs)[k];
+        const size_t I = (size_t)sp.len, so = (size_t)seqOff[k];
+        std::memcpy(hSeq_.data() + so, sp.seq, I);
+        for (int t = 0; t < 5; ++t) {   // track t of read k at 5 * seqOff + t * len (ReadView's layout)
+            float* dst = hFeat_.data() + 5 * so + (size_t)t * I;
+            if (sp.track[t]) std::memcpy(dst, sp.track[t], I * sizeof(float));
+            else std::memset(dst, 0, I * sizeof(float));
+        }
+    };
+    (void)s0;
+    {
+        const int nt = (int)std::max<size_t>(1, std::min<size_t>(16, std::min<size_t>(ns / 64 + 1, std::thread::hardware_concurrency())));
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t)
+            th.emplace_back([&, t] { for (size_t k = t; k < ns; k += nt) copy(k); });
+        for (size_t k = 0; k < ns; k += nt) copy(k);
+        for (std::thread& x : th) x.join();
+    }
     std::vector<int> added;
-    for (ReadSpec& sp : *specs)
-        added.push_back(RegisterRaw(sp.z, sp.seq, sp.len, sp.track, sp.strand, sp.ts, sp.te, sp.config));
+    for (size_t k = 0; k < ns; ++k) {
+        const ReadSpec& sp = (*specs)[k];
+        added.push_back(RegisterRaw(sp.z, seqOff[k], sp.len, sp.strand, sp.ts, sp.te, sp.config));
+    }
     const auto t1 = std::chrono::steady_clock::now();
     Upload();
     const auto t2 = std::chrono::steady_clock::now();
@@ -182,13 +215,12 @@ std::vector<char> QuiverBatch::AddReads(std::vector<ReadSpec>* specs)
     return act;
 }
 
-int QuiverBatch::RegisterRaw(int zi, const char* seq, int len, const float* const track[5], int strand, int ts, int te,
-                             int config)
+int QuiverBatch::RegisterRaw(int zi, long long seqOff, int len, int strand, int ts, int te, int config)
 {
     HZmw& z = zmws_.at(zi);
     const int L = (int)z.tpl.size();
     const size_t I = (size_t)std::max(0, len);
-    if (ts < 0 || te > L || ts > te || len < 1 || !seq || config < 0 || config >= (int)configs_.size())
+    if (ts < 0 || te > L || ts > te || len < 1 || config < 0 || config >= (int)configs_.size())
         throw std::invalid_argument("read window outside the template or bad config");
     HRead r;
     r.zmw = zi;
@@ -197,12 +229,7 @@ int QuiverBatch::RegisterRaw(int zi, const char* seq, int len, const float* cons
     r.ts = ts;
     r.te = te;
     r.len = (int)I;
-    r.seqOff = (long long)hSeq_.size();
-    hSeq_.insert(hSeq_.end(), seq, seq + I);
-    for (int k = 0; k < 5; ++k) {
-        if (track[k]) hFeat_.insert(hFeat_.end(), track[k], track[k] + I);
-        else hFeat_.resize(hFeat_.size() + I, 0.0f);
-    }
+    r.seqOff = seqOff;
     r.colBuf = -1;
     reads_.push_back(r);
     const int ri = (int)reads_.size() - 1;
@@ -276,7 +303,7 @@ void QuiverBatch::Upload()
         if (h.size() < up) up = 0;   // never happens (append-only); re-upload if it did
         if (h.size() == up) return;
         d.reserve(std::max<size_t>(h.size(), 1), true);
-        QHIP(hipMemcpyAsync(d.ptr + up, h.data() + up, (h.size() - up) * sizeof(h[0]), hipMemcpyHostToDevice,
+        QHIP(hipMemcpyAsync(d.ptr + up, h.data() + up, (h.size() - up) * sizeof(*h.data()), hipMemcpyHostToDevice,
                             stream_));
         up = h.size();
     };
@@ -646,6 +673,10 @@ constexpr long long kTaskChunk = 1LL << 21;
 void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes,
                               std::vector<long long>* taskStartOut, std::vector<long long>* mutStartOut)
 {
+    static const bool trace = std::getenv("PBCCS_QUIVER_TRACE") != nullptr;
+    using Clock = std::chrono::steady_clock;
+    auto msSince = [](Clock::time_point a) { return std::chrono::duration<double, std::milli>(Clock::now() - a).count(); };
+    const Clock::time_point ts0 = Clock::now();
     const int n = (int)zs.size();
     std::vector<long long>& taskStart = *taskStartOut;
     std::vector<long long>& mutStart = *mutStartOut;
@@ -677,6 +708,8 @@ void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std:
     put(dWFast_, fastThr, stream_);
     put(dCodes_, flat, stream_);
     dDelta_.reserve(std::max<long long>(nTask, 1), false);
+    const double msPrep = msSince(ts0);
+    const Clock::time_point ts1 = Clock::now();
     // middle cases: k_qscore_mid, one wave per (item, read, 64-mutation chunk); it lists the edge cases
     std::vector<long long> waveStart(n + 1, 0), mutCount(n);
     long long edgeCap = 1024;
@@ -715,6 +748,8 @@ void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std:
         if (attempt > 2) throw DeviceError("quiver edge-case list overflow");
         edgeCap = (long long)nEdge;   // the list was cut short: rerun with room for every edge case
     }
+    const double msMid = msSince(ts1);
+    const Clock::time_point ts2 = Clock::now();
     // edge cases (ExtendAlpha to the end, ExtendBeta, whole fills): k_qscore over the listed tasks
     for (long long t0 = 0; t0 < (long long)nEdge;) {
         const long long m = std::min(kTaskChunk, (long long)nEdge - t0);
@@ -750,6 +785,9 @@ void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std:
         }
         t0 += m;
     }
+    if (trace)
+        std::fprintf(stderr, "[quiver] deltas items %d mutations %lld tasks %lld: prepare %.1f ms mid %.1f ms edges %lld %.1f ms\n",
+                     n, mutStart[n], nTask, msPrep, msMid, (long long)nEdge, msSince(ts2));
 }
 
 void QuiverBatch::ScoreRound(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes, int sep,

@@ -9,6 +9,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -22,6 +24,30 @@ namespace quiver {
 struct QReadFeatures {
     std::string seq;
     std::vector<float> ins, subs, del, tag, merge;   // tag: DelTag as float(char)
+};
+
+// Append-only host buffer that grows without value-initialising (the QV tracks of a 10000-scorer batch are ~4 GB:
+// their first touch happens in AddReads' parallel copies, not in a zero fill).
+template <class T>
+struct HostPool {
+    std::unique_ptr<T[]> p;
+    size_t n = 0, cap = 0;
+    size_t size() const { return n; }
+    T* data() { return p.get(); }
+    const T* data() const { return p.get(); }
+    size_t grow(size_t add)   // returns the old size
+    {
+        const size_t at = n;
+        if (n + add > cap) {
+            const size_t nc = std::max(n + add, cap + cap / 2);
+            std::unique_ptr<T[]> q(new T[nc]);
+            if (n) std::memcpy(q.get(), p.get(), n * sizeof(T));
+            p = std::move(q);
+            cap = nc;
+        }
+        n += add;
+        return at;
+    }
 };
 
 class QuiverBatch {
@@ -98,9 +124,8 @@ private:
         long long alloc[2] = {0, 0};
         bool tallRing = false;   // a column outgrew the band-height LDS ring: fill with the full-height one
     };
-    // a read, unfilled: its bases and five tracks copied into the host pools
-    int RegisterRaw(int z, const char* seq, int len, const float* const track[5], int strand, int ts, int te,
-                    int config);
+    // a read, unfilled, whose bases and five tracks are at seqOff / 5 * seqOff of the host pools
+    int RegisterRaw(int z, long long seqOff, int len, int strand, int ts, int te, int config);
     void Upload();
     void EnsureCapacity(int r);
     QBatch View();
@@ -124,8 +149,8 @@ private:
     std::vector<QParams> configs_;
     std::vector<HZmw> zmws_;
     std::vector<HRead> reads_;
-    std::vector<char> hSeq_;
-    std::vector<float> hFeat_;
+    HostPool<char> hSeq_;
+    HostPool<float> hFeat_;
     long long colTop_ = 0, valTop_ = 0;
     size_t seqUp_ = 0, featUp_ = 0;   // host read pools already on the device (append-only)
     bool dirty_ = true;
