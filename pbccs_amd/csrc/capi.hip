@@ -23,6 +23,7 @@
 #include "engine.hpp"
 #include "driver.hpp"
 #include "poa_engine.hpp"
+#include "quiver_engine.hpp"
 
 using namespace pbccs;
 
@@ -75,6 +76,10 @@ struct pbccs_engine {
         for (int k = 0; k < PoaSlices(); ++k) v.push_back(&Poa(k));
         return v;
     }
+    // pbccs_quiver_polish_batch's scorer batch, kept between calls (Reset per call) so its device buffers and host
+    // pools are allocated once; calls on one engine take turns on it
+    std::unique_ptr<quiver::QuiverBatch> quiverBatch;
+    std::mutex quiverMu;
     Workspace* Slot(int s)
     {
         while ((int)slots.size() <= s) slots.emplace_back(new Workspace(true));
@@ -1332,7 +1337,10 @@ int pbccs_quiver_polish_batch(pbccs_engine* eng, const pbccs_quiver_config* conf
     }
     if (n == 0) return PBCCS_OK;
     return guarded([&] {
-        quiver::QuiverBatch qb(eng->device);
+        std::lock_guard<std::mutex> lock(eng->quiverMu);
+        if (!eng->quiverBatch) eng->quiverBatch.reset(new quiver::QuiverBatch(eng->device));
+        quiver::QuiverBatch& qb = *eng->quiverBatch;
+        qb.Reset();
         // the QuiverConfigTable, as pbccs_quiver_scorer_create builds it
         std::vector<std::pair<std::string, int>> table;
         std::vector<const pbccs_quiver_config*> cfgs;

@@ -87,6 +87,20 @@ QuiverBatch::~QuiverBatch()
     }
 }
 
+void QuiverBatch::Reset()
+{
+    QHIP(hipSetDevice(device_));
+    QHIP(hipStreamSynchronize(stream_));
+    configs_.clear();
+    zmws_.clear();
+    reads_.clear();
+    hSeq_.n = 0;
+    hFeat_.n = 0;
+    colTop_ = valTop_ = 0;
+    seqUp_ = featUp_ = 0;
+    dirty_ = true;
+}
+
 int QuiverBatch::AddConfig(const QParams& p)
 {
     if (!(p.scoreDiff >= 0.0f)) throw std::invalid_argument("ScoreDiff must be positive");

@@ -57,6 +57,9 @@ public:
     QuiverBatch(const QuiverBatch&) = delete;
     QuiverBatch& operator=(const QuiverBatch&) = delete;
 
+    // Drop every config, scorer and read, keeping the device buffers and host pools at their size: a long-lived
+    // batch (the engine's, for pbccs_quiver_polish_batch) reaches its steady-state allocation once.
+    void Reset();
     int AddConfig(const QParams& p);
     int AddZmw(const std::string& tpl, float fastScoreThreshold);
     // AddRead (Quiver/MultiReadMutationScorer.cpp:246-283): fills the read; returns whether it is active.
