@@ -518,34 +518,6 @@ void launch_fill_lds(int variant, int n, int base, size_t lds, hipStream_t s, co
 
 constexpr long long kTraceLdsBytes = 48 * 1024;   // k_poa_trace: staged column program per wave
 
-template <class F>
-void parallel_for(int threads, int n, F&& f)
-{
-    if (threads <= 1 || n < 2) {
-        for (int k = 0; k < n; ++k) f(k);
-        return;
-    }
-    std::atomic<int> next(0);
-    std::vector<std::thread> pool;
-    std::exception_ptr err;
-    std::atomic<bool> failed(false);
-    const int nt = std::min(threads, n);
-    for (int t = 0; t < nt; ++t)
-        pool.emplace_back([&] {
-            for (int k; (k = next.fetch_add(1)) < n;) {
-                if (failed.load()) return;
-                try {
-                    f(k);
-                } catch (...) {
-                    if (!failed.exchange(true)) err = std::current_exception();
-                    return;
-                }
-            }
-        });
-    for (auto& t : pool) t.join();
-    if (err) std::rethrow_exception(err);
-}
-
 void check(hipError_t e, const char* what)
 {
     if (e != hipSuccess) {
@@ -567,6 +539,7 @@ PoaRunner::PoaRunner(int device, int hostThreads) : device_(device)
 {
     const int hw = (int)std::thread::hardware_concurrency();
     threads_ = hostThreads > 0 ? hostThreads : std::max(1, std::min(16, hw));
+    workers_.reset(new WorkerPool(threads_));
     check(hipSetDevice(device_), "hipSetDevice");
     check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
     for (auto& e : ev_) check(hipEventCreate(&e), "hipEventCreate");
@@ -591,9 +564,10 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
 
     // ---- host: column programs, then the job layout (sizes -> prefix offsets -> parallel fill)
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<ColumnProgram> prog(n);
+    if ((int)prog_.size() < n) prog_.resize(n);
+    std::vector<ColumnProgram>& prog = prog_;
     std::vector<std::string> rcRead(n);
-    parallel_for(threads_, n, [&](int r) {
+    ParallelFor(n, [&](int r) {
         reqs[r].graph->Program(&prog[r]);
         if (reqs[r].orient) rcRead[r] = reverse_complement(reqs[r].read);
     });
@@ -642,7 +616,7 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
     hRowBase_.reserve(nRow);
     std::vector<long long> predColOff(n + 1, 0);
     for (int r = 0; r < n; ++r) predColOff[r + 1] = predColOff[r] + (long long)prog[r].predCol.size();
-    parallel_for(threads_, n, [&](int r) {
+    ParallelFor(n, [&](int r) {
         const ColumnProgram& C = prog[r];
         const PoaJob& J = jobs[firstJob[r]];
         memcpy(hBase_.ptr + J.progOff, C.base.data(), C.base.size());
@@ -847,7 +821,7 @@ void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>*
     stats.deviceMs += ms_since(t0);
     // ---- host: thread the committed reads into their graphs (CommitAdd)
     t0 = std::chrono::steady_clock::now();
-    parallel_for(threads_, n, [&](int r) {
+    ParallelFor(n, [&](int r) {
         AlignResult& R = (*out)[r];
         if (R.chosen < 0) return;
         const std::string& s = R.chosen ? rcRead[r] : reqs[r].read;
@@ -942,7 +916,7 @@ void PoaSlice(PoaRunner& R, const std::vector<std::vector<const std::string*>>& 
         }
     }
     const auto t0 = std::chrono::steady_clock::now();
-    parallel_for(R.HostThreads(), nz, [&](int z) {
+    R.ParallelFor(nz, [&](int z) {
         const int mc = minCov >= 0 ? minCov : (cov[z] < 5 ? 1 : (int)((cov[z] + 1) / 2 - 1));
         (*consensus)[z0 + z] = Z[z]->readPaths.empty() ? std::string() : Z[z]->FindConsensus(mc, &(*extents)[z0 + z]);
         (*rc)[z0 + z] = Z[z]->rc;

@@ -9,8 +9,15 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine.hpp"
@@ -64,6 +71,90 @@ struct HostVec {
     }
 };
 
+// A runner's host workers, started once: every round's column programs, staging copies and graph threading
+// are spread over them (the calling thread takes indices too) instead of spawning threads per round.
+class WorkerPool {
+public:
+    explicit WorkerPool(int threads)
+    {
+        for (int t = 1; t < threads; ++t) th_.emplace_back([this] { Loop(); });
+    }
+    ~WorkerPool()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread& t : th_) t.join();
+    }
+    WorkerPool(const WorkerPool&) = delete;
+    WorkerPool& operator=(const WorkerPool&) = delete;
+    int Size() const { return (int)th_.size() + 1; }
+    // f(k) for k in [0, n); the first exception stops the hand-out and is rethrown here
+    void Run(int n, const std::function<void(int)>& f)
+    {
+        if (n <= 0) return;
+        if (th_.empty() || n < 2) {
+            for (int k = 0; k < n; ++k) f(k);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &f;
+            n_ = n;
+            next_.store(0);
+            err_ = nullptr;
+            busy_ = (int)th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        Work();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return busy_ == 0; });
+        job_ = nullptr;
+        if (err_) std::rethrow_exception(err_);
+    }
+
+private:
+    void Work()
+    {
+        for (int k; (k = next_.fetch_add(1)) < n_;) {
+            try {
+                (*job_)(k);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (!err_) err_ = std::current_exception();
+                next_.store(n_);
+            }
+        }
+    }
+    void Loop()
+    {
+        long long seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+            }
+            Work();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--busy_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    int n_ = 0, busy_ = 0;
+    std::atomic<int> next_{0};
+    long long gen_ = 0;
+    bool quit_ = false;
+    std::exception_ptr err_;
+};
+
 struct PoaPools {
     const uint8_t* base;
     const int* vertexOfCol;
@@ -113,12 +204,15 @@ public:
     void ReleasePool() { dPool_.unmap_all(); }
     size_t PoolMappedBytes() const { return dPool_.mapped_bytes(); }
     int HostThreads() const { return threads_; }
+    void ParallelFor(int n, const std::function<void(int)>& f) { workers_->Run(n, f); }
     PoaStats stats;
     bool profiling = false;
 
 private:
     int device_;
     int threads_;
+    std::unique_ptr<WorkerPool> workers_;
+    std::vector<ColumnProgram> prog_;   // per request, reused across rounds (their vectors keep their capacity)
     size_t budget_ = 0;   // cap on the score-matrix bytes per launch group (0 = 64 GB); also <= 0.6 x free HBM
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};

@@ -102,10 +102,14 @@ public:
     void Program(ColumnProgram* P) const
     {
         const int n = (int)v_.size();
-        std::vector<int> order;
+        // scratch kept per host thread: a program is built for every read of every ZMW
+        static thread_local std::vector<int> order;
+        static thread_local std::vector<uint8_t> state;
+        static thread_local std::vector<std::pair<int, int>> stack;   // (vertex, next out-edge)
+        order.clear();
         order.reserve(n);
-        std::vector<uint8_t> state(n, 0);
-        std::vector<std::pair<int, int>> stack;   // (vertex, next out-edge)
+        state.assign(n, 0);
+        stack.clear();
         stack.emplace_back(kEnter, 0);
         state[kEnter] = 1;
         // (vertex, next out-edge): successors taken largest id first, so a vertex's oldest successor -- the

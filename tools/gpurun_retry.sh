@@ -3,7 +3,7 @@
 # reports an infrastructure-transient status -- the box was lost before the command ran, nothing executed and
 # nothing was charged.  Any other outcome (pass, fail, timeout) is final.  Usage: tools/gpurun_retry.sh LOG TIMEOUT CMD
 LOG=$1; TO=$2; shift 2
-for i in 1 2 3 4; do
+for i in $(seq 1 ${RETRIES:-4}); do
   /usr/local/graft/bin/gpurun --timeout "$TO" -- "$@" > "$LOG" 2>&1
   grep -q "status=transient\|backing off" "$LOG" || break
   echo "[retry $i: transient]" >> "$LOG.retries"
