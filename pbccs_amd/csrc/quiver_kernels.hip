@@ -583,7 +583,7 @@ struct LdsCol {
 // The read's QV-feature rows [lo, lo + kQWinRows) staged in LDS, row i at slot i & (kQWinRows - 1): a column's
 // chunk reads 65 consecutive rows, and the band moves about a row per column, so the window is reloaded (one
 // coalesced pass of the wave) only every few hundred columns instead of six HBM/L2 loads per cell.
-constexpr int kQWinRows = 256;
+constexpr int kQWinRows = 128;
 struct QWin {
     float* ins;
     float* subs;
@@ -657,8 +657,12 @@ struct QEvalWin {
 template <bool BETA>
 __device__ __forceinline__ void coop_column(const QEval& e0, int j, int lane, int hb, int he, const LdsCol& c1,
                                             const LdsCol& c2, float* cur, const QBand& out, long long base, QAlloc* alloc,
-                                            bool& ovf, int* ob, int* oe, float* thrOut, int mask, bool& tall, QWin& win)
+                                            bool& ovf, int* ob, int* oe, float* thrOut, int mask, bool& tall, QWin& win,
+                                            int* tbOut)
 {
+    // tbOut: the next column's threshold row (alpha: the first row of the range at or above the final threshold,
+    // else endRow; beta: the last such row + 1, else beginRow) when the column took one chunk -- its cells are then
+    // still in registers -- else INT_MIN and the caller scans the LDS column
     const QEval& e = e0;
     const QEvalWin ew{e0, win};
     const int I = e.I(), J = e.J();
@@ -684,7 +688,11 @@ __device__ __forceinline__ void coop_column(const QEval& e0, int j, int lane, in
     const bool empty = BETA ? (first < 0) : (first > I);
     bool done = empty;
     if (empty) stop = BETA ? first + 1 : first;
+    int nChunks = 0;
+    float lastSv = kNegInf;
+    bool lastKeep = false;
     for (int c = 0; !done; ++c) {
+        nChunks = c + 1;
         // rows of this chunk past the band-height ring would alias the column's first rows: the read is tall
         if ((unsigned)mask < (unsigned)I && (BETA ? first - (chunk - 64 * c - 63) : chunk + 64 * c + 63 - first) > mask) {
             tall = true;
@@ -816,6 +824,8 @@ __device__ __forceinline__ void coop_column(const QEval& e0, int j, int lane, in
         // rows of the quads before the stop are the column's
         const bool keep = valid && g < stopQuad;
         if (keep) cur[row & mask] = sv;
+        lastSv = sv;
+        lastKeep = keep;
         // state after the last kept quad
         if (stopQuad > 0) {
             const int lastLane = 4 * stopQuad - 1;
@@ -834,11 +844,26 @@ __device__ __forceinline__ void coop_column(const QEval& e0, int j, int lane, in
     }
     const int beginRow = BETA ? stop : first;
     const int endRow = BETA ? first + 1 : stop;
-    // store the column top-down into the arena
-    for (int r = beginRow + lane; r < endRow; r += 64) {
-        const long long k = base + (r - beginRow);
-        if (k < out.cap) out.val[k] = cur[r & mask];
-        else ovf = true;
+    if (nChunks == 1) {
+        // one chunk: its kept cells are the column's rows [beginRow, endRow), still in registers (lane l holds
+        // row chunk + l, beta chunk - l): store them and find the threshold row without re-reading LDS
+        const int row = BETA ? chunk - lane : chunk + lane;
+        if (lastKeep) {
+            const long long k = base + (row - beginRow);
+            if (k < out.cap) out.val[k] = lastSv;
+            else ovf = true;
+        }
+        const unsigned long long bal = __ballot(lastKeep && !(lastSv < thr));
+        if (!BETA) *tbOut = bal ? chunk + __ffsll((long long)bal) - 1 : endRow;
+        else *tbOut = bal ? chunk - (__ffsll((long long)bal) - 1) + 1 : beginRow;
+    } else {
+        *tbOut = INT_MIN;
+        // store the column top-down into the arena
+        for (int r = beginRow + lane; r < endRow; r += 64) {
+            const long long k = base + (r - beginRow);
+            if (k < out.cap) out.val[k] = cur[r & mask];
+            else ovf = true;
+        }
     }
     *ob = beginRow;
     *oe = endRow;
@@ -876,9 +901,10 @@ __device__ long long coop_fill(const QEval& e, const QBand& guideBand, bool useG
         if (s < J) hNext = hint[BETA ? j - 1 : j + 1];   // one column ahead: its latency hides behind this one
         if (h.x >= 0) { hb = min(h.x, hb); he = max(h.y, he); }   // RangeGuide (RecursorBase-inl.hpp:87-114)
         if (h.z >= 0) { hb = min(h.z, hb); he = max(h.w, he); }
-        int b, en;
+        int b, en, tb;
         float thr;
-        coop_column<BETA>(e, j, lane, hb, he, c1, c2, cur.v, out, used, nullptr, ovf, &b, &en, &thr, mask, tall, win);
+        coop_column<BETA>(e, j, lane, hb, he, c1, c2, cur.v, out, used, nullptr, ovf, &b, &en, &thr, mask, tall, win,
+                          &tb);
         if (tall) return -1;
         cur.b = b;
         cur.e = en;
@@ -888,7 +914,10 @@ __device__ long long coop_fill(const QEval& e, const QBand& guideBand, bool useG
             hint[j] = make_int4(hb, he, b, en);   // for the allocation bookkeeping below
         }
         used += en - b;
-        if (!BETA) {
+        if (tb != INT_MIN) {
+            if (!BETA) { he = en; hb = tb; }
+            else { hb = b; he = tb; }
+        } else if (!BETA) {
             he = en;
             // hb = first row of the column at or above the threshold (else endRow)
             int nb = en;

@@ -18,4 +18,6 @@ run ring256 PBCCS_QRING_ROWS=256 && \
 run ring512 PBCCS_QRING_ROWS=512 && \
 run w128_ring256 PBCCS_LIB=$PWD/pbccs_amd/_lib/libw128.so PBCCS_QRING_ROWS=256 && \
 run w128_ring512 PBCCS_LIB=$PWD/pbccs_amd/_lib/libw128.so PBCCS_QRING_ROWS=512 && \
+run w128_ring128 PBCCS_LIB=$PWD/pbccs_amd/_lib/libw128.so PBCCS_QRING_ROWS=128 && \
+run w128_ring64 PBCCS_LIB=$PWD/pbccs_amd/_lib/libw128.so PBCCS_QRING_ROWS=64 && \
 grep '\[quiver\]' $OUT/ring1024.err | tail -9
