@@ -1338,7 +1338,10 @@ int pbccs_quiver_polish_batch(pbccs_engine* eng, const pbccs_quiver_config* conf
     if (n == 0) return PBCCS_OK;
     return guarded([&] {
         std::lock_guard<std::mutex> lock(eng->quiverMu);
-        if (!eng->quiverBatch) eng->quiverBatch.reset(new quiver::QuiverBatch(eng->device));
+        if (!eng->quiverBatch) {
+            eng->quiverBatch.reset(new quiver::QuiverBatch(eng->device));
+            eng->quiverBatch->PinHostPools();
+        }
         quiver::QuiverBatch& qb = *eng->quiverBatch;
         qb.Reset();
         // the QuiverConfigTable, as pbccs_quiver_scorer_create builds it

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <set>
 #include <stdexcept>
 #include <thread>
@@ -43,6 +44,35 @@ void get(std::vector<T>& h, const DevVec<T>& d, size_t n, hipStream_t s)
 }
 
 constexpr int kInitialBand = 24;   // values per column per arena to start with
+
+// f(k) for k in [0, n) on up to 16 host threads, contiguous index ranges (scorers' independent host work:
+// mutation lists, list flattening, template edits); the first exception is rethrown
+template <class F>
+void par_for(int n, F&& f, int minPerThread = 32)
+{
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nt = std::max(1, std::min(std::min(16, hw), n / std::max(1, minPerThread)));
+    if (nt <= 1) {
+        for (int k = 0; k < n; ++k) f(k);
+        return;
+    }
+    std::exception_ptr err;
+    std::mutex mu;
+    auto run = [&](int t) {
+        const int a = (int)((long long)n * t / nt), b = (int)((long long)n * (t + 1) / nt);
+        try {
+            for (int k = a; k < b; ++k) f(k);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = std::current_exception();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(run, t);
+    run(0);
+    for (std::thread& x : th) x.join();
+    if (err) std::rethrow_exception(err);
+}
 
 struct ScoredMut {
     int code;
@@ -704,10 +734,13 @@ void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std:
         nReads[w] = (int)z.reads.size();
         readList.insert(readList.end(), z.reads.begin(), z.reads.end());
         fastThr[w] = z.fastThreshold;
-        flat.insert(flat.end(), codes[w].begin(), codes[w].end());
         mutStart[w + 1] = mutStart[w] + (long long)codes[w].size();
         taskStart[w + 1] = taskStart[w] + (long long)codes[w].size() * nReads[w];
     }
+    flat.resize((size_t)mutStart[n]);   // the scorers' lists back to back, copied on several threads
+    par_for(n, [&](int w) {
+        if (!codes[w].empty()) std::memcpy(flat.data() + mutStart[w], codes[w].data(), codes[w].size() * sizeof(int));
+    });
     const long long nTask = taskStart[n];
     std::vector<int> active(reads_.size());
     for (size_t r = 0; r < reads_.size(); ++r) active[r] = reads_[r].active ? 1 : 0;
@@ -908,27 +941,28 @@ void QuiverBatch::RefineMany(const std::vector<int>& zs, const RefineOptions& ro
             if (!done[k]) { act.push_back(zs[k]); idx.push_back(k); }
         if (act.empty()) break;
         std::vector<std::vector<int>> codes(act.size());
-        for (size_t a = 0; a < act.size(); ++a) {
+        par_for((int)act.size(), [&](int a) {
             const std::string& tpl = zmws_[act[a]].tpl;
             const int k = idx[a];
             if (iter[k] == 0) unique_mutations(tpl, 0, (int)tpl.size(), &codes[a]);
             else nearby_mutations(tpl, centers[k], ro.mutationNeighborhood, &codes[a]);
             (*nTested)[k] += (long long)codes[a].size();
-        }
+        });
         std::vector<std::vector<Scored>> fav, picked;
         const double msEnum = msSince(tr0);
         const Clock::time_point tr1 = Clock::now();
         ScoreRound(act, codes, ro.mutationSeparation, &fav, &picked);
         const double msScore = msSince(tr1);
         const Clock::time_point tr2 = Clock::now();
-        std::vector<int> refill;
-        for (size_t a = 0; a < act.size(); ++a) {
+        // every scorer's edit on its own (host threads), then the refilled reads' capacity in list order
+        std::vector<char> edited(act.size(), 0);
+        par_for((int)act.size(), [&](int a) {
             const int k = idx[a];
             HZmw& z = zmws_[act[a]];
             if (fav[a].empty()) {
                 (*converged)[k] = 1;
                 done[k] = 1;
-                continue;
+                return;
             }
             std::vector<Scored>& best = picked[a];
             std::vector<Mutation> muts;
@@ -950,20 +984,26 @@ void QuiverBatch::RefineMany(const std::vector<int>& zs, const RefineOptions& ro
             if (!apply_mutations(z.tpl, muts, &next, &mtp)) {   // ApplyMutations refused: Refine returns false
                 (*ok)[k] = 0;
                 done[k] = 1;
-                continue;
+                return;
             }
             z.tpl = next;
             for (int r : z.reads) {
                 HRead& h = reads_[r];
                 h.ts = mtp[h.ts];
                 h.te = mtp[h.te];
-                if (h.active) {
+            }
+            edited[a] = 1;
+            if (++iter[k] >= ro.maxIterations) done[k] = 1;
+        });
+        std::vector<int> refill;
+        for (size_t a = 0; a < act.size(); ++a) {
+            if (!edited[a]) continue;
+            for (int r : zmws_[act[a]].reads)
+                if (reads_[r].active) {
                     EnsureCapacity(r);
                     refill.push_back(r);
                 }
-            }
             dirty_ = true;
-            if (++iter[k] >= ro.maxIterations) done[k] = 1;
         }
         const double msApply = msSince(tr2);
         const Clock::time_point tr3 = Clock::now();
@@ -983,15 +1023,20 @@ std::vector<std::vector<int>> QuiverBatch::QVsMany(const std::vector<int>& zs)  
     std::vector<int> posOff;
     std::vector<long long> posStart(n + 1, 0), posOffBase(n);
     for (int w = 0; w < n; ++w) {
+        const long long L = (long long)zmws_[zs[w]].tpl.size();
+        posOffBase[w] = posStart[w] + w;   // L + 1 offsets per scorer
+        posStart[w + 1] = posStart[w] + L;
+    }
+    posOff.resize((size_t)(posStart[n] + n));
+    par_for(n, [&](int w) {   // per position's mutation list, scorers on several threads
         const std::string& tpl = zmws_[zs[w]].tpl;
-        posOffBase[w] = (long long)posOff.size();
+        int* po = posOff.data() + posOffBase[w];
         for (int p = 0; p < (int)tpl.size(); ++p) {
-            posOff.push_back((int)codes[w].size());
+            po[p] = (int)codes[w].size();
             unique_mutations(tpl, p, p + 1, &codes[w]);
         }
-        posOff.push_back((int)codes[w].size());
-        posStart[w + 1] = posStart[w] + (long long)tpl.size();
-    }
+        po[tpl.size()] = (int)codes[w].size();
+    });
     std::vector<long long> taskStart, mutStart;
     ScoreDeltas(zs, codes, &taskStart, &mutStart);
     const long long nMut = mutStart[n], nPos = posStart[n];

@@ -27,26 +27,52 @@ struct QReadFeatures {
 };
 
 // Append-only host buffer that grows without value-initialising (the QV tracks of a 10000-scorer batch are ~4 GB:
-// their first touch happens in AddReads' parallel copies, not in a zero fill).
+// their first touch happens in AddReads' parallel copies, not in a zero fill).  pinned: page-locked memory
+// (hipHostMalloc), so the append-only uploads of the pools run at DMA speed; a long-lived batch pins once.
 template <class T>
 struct HostPool {
-    std::unique_ptr<T[]> p;
+    T* p = nullptr;
     size_t n = 0, cap = 0;
+    bool pinned = false;
+    HostPool() = default;
+    HostPool(const HostPool&) = delete;
+    HostPool& operator=(const HostPool&) = delete;
+    ~HostPool() { release(); }
     size_t size() const { return n; }
-    T* data() { return p.get(); }
-    const T* data() const { return p.get(); }
+    T* data() { return p; }
+    const T* data() const { return p; }
     size_t grow(size_t add)   // returns the old size
     {
         const size_t at = n;
         if (n + add > cap) {
             const size_t nc = std::max(n + add, cap + cap / 2);
-            std::unique_ptr<T[]> q(new T[nc]);
-            if (n) std::memcpy(q.get(), p.get(), n * sizeof(T));
-            p = std::move(q);
+            T* q = nullptr;
+            bool qp = false;
+            if (pinned && hipHostMalloc((void**)&q, nc * sizeof(T), hipHostMallocDefault) == hipSuccess) qp = true;
+            else {
+                (void)hipGetLastError();
+                q = new T[nc];
+            }
+            if (n) std::memcpy(q, p, n * sizeof(T));
+            release();
+            p = q;
+            pinnedAlloc_ = qp;
             cap = nc;
         }
         n += add;
         return at;
+    }
+
+private:
+    bool pinnedAlloc_ = false;
+    void release()
+    {
+        if (p) {
+            if (pinnedAlloc_) (void)hipHostFree(p);
+            else delete[] p;
+        }
+        p = nullptr;
+        cap = 0;
     }
 };
 
@@ -60,6 +86,8 @@ public:
     // Drop every config, scorer and read, keeping the device buffers and host pools at their size: a long-lived
     // batch (the engine's, for pbccs_quiver_polish_batch) reaches its steady-state allocation once.
     void Reset();
+    // page-locked host read pools (a long-lived batch: the pinning cost is paid once)
+    void PinHostPools() { hSeq_.pinned = hFeat_.pinned = true; }
     int AddConfig(const QParams& p);
     int AddZmw(const std::string& tpl, float fastScoreThreshold);
     // AddRead (Quiver/MultiReadMutationScorer.cpp:246-283): fills the read; returns whether it is active.
