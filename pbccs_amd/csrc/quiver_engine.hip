@@ -208,6 +208,7 @@ std::vector<char> QuiverBatch::AddReads(std::vector<ReadSpec>* specs)
     }
     const size_t s0 = hSeq_.grow(bases);
     hFeat_.grow(5 * bases);
+    const auto tGrow = std::chrono::steady_clock::now();
     auto copy = [&](size_t k) {
         const ReadSpec& sp = (*specs)[k];
         const size_t I = (size_t)sp.len, so = (size_t)seqOff[k];
@@ -227,6 +228,7 @@ std::vector<char> QuiverBatch::AddReads(std::vector<ReadSpec>* specs)
         for (size_t k = 0; k < ns; k += nt) copy(k);
         for (std::thread& x : th) x.join();
     }
+    const auto tCopy = std::chrono::steady_clock::now();
     std::vector<int> added;
     for (size_t k = 0; k < ns; ++k) {
         const ReadSpec& sp = (*specs)[k];
@@ -237,8 +239,10 @@ std::vector<char> QuiverBatch::AddReads(std::vector<ReadSpec>* specs)
     const auto t2 = std::chrono::steady_clock::now();
     Fill(added);
     if (trace)
-        std::fprintf(stderr, "[quiver] addreads %zu register %.1f ms upload %.1f ms fill %.1f ms\n", added.size(),
-                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
+        std::fprintf(stderr, "[quiver] addreads %zu register %.1f ms (grow %.1f copy %.1f) upload %.1f ms fill %.1f ms\n",
+                     added.size(), std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                     std::chrono::duration<double, std::milli>(tGrow - t0).count(),
+                     std::chrono::duration<double, std::milli>(tCopy - tGrow).count(),
                      std::chrono::duration<double, std::milli>(t2 - t1).count(),
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
     std::vector<char> act(specs->size());
@@ -419,8 +423,12 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         // The coop kernel's LDS ring holds kQRingRows rows per column (band height, rows modulo the ring), so
         // many read waves share a CU; a read with a taller column comes back kQTall and from then on fills with
         // a ring of its full height (tallRing).
+        // SparseSse reads go to k_qfill_grp first (four reads per wavefront, a 64-row band ring); a read that
+        // comes back kQTall moves to k_qfill_coop's band-height ring, then to its full-height ring.
+        // PBCCS_QFILL_GRP=0 skips the grouped kernel (A/B).
         static const bool laneOnly = std::getenv("PBCCS_QFILL_LANE") != nullptr;
-        std::vector<int> coop, full, lane;
+        static const bool grpOn = !(std::getenv("PBCCS_QFILL_GRP") && std::getenv("PBCCS_QFILL_GRP")[0] == '0');
+        std::vector<int> grp, coop, full, lane;
         int maxCols = 1, maxColsFull = 1, maxRowsFull = 1;
         for (int r : todo) {
             const QParams& p = configs_[reads_[r].config];
@@ -430,15 +438,31 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
                     full.push_back(r);
                     maxRowsFull = std::max(maxRowsFull, reads_[r].len + 1);
                     maxColsFull = std::max(maxColsFull, cols);
-                } else {
+                } else if (reads_[r].grpTall || !grpOn) {
                     coop.push_back(r);
                     maxCols = std::max(maxCols, cols);
+                } else {
+                    grp.push_back(r);
                 }
             } else {
                 lane.push_back(r);
             }
         }
-        std::vector<int> both(coop);
+        // k_qfill_grp's list: each QuiverConfig's reads in whole waves of four (-1 pads), so a wave's parameters
+        // are one config's
+        std::vector<int> grpList;
+        {
+            std::stable_sort(grp.begin(), grp.end(),
+                             [&](int a, int b) { return reads_[a].config < reads_[b].config; });
+            for (size_t k = 0; k < grp.size(); ++k) {
+                if (k > 0 && reads_[grp[k]].config != reads_[grp[k - 1]].config)
+                    while (grpList.size() % 4) grpList.push_back(-1);
+                grpList.push_back(grp[k]);
+            }
+            while (grpList.size() % 4) grpList.push_back(-1);
+        }
+        std::vector<int> both(grpList);
+        both.insert(both.end(), coop.begin(), coop.end());
         both.insert(both.end(), full.begin(), full.end());
         both.insert(both.end(), lane.begin(), lane.end());
         put(dList_, both, stream_);
@@ -450,9 +474,11 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
             while (p < r && p < kQCoopRows) p *= 2;
             return p;
         }();
-        launch_qfill_coop(B, dList_.ptr, (int)coop.size(), ringRows, maxCols, stream_);
-        launch_qfill_coop(B, dList_.ptr + coop.size(), (int)full.size(), maxRowsFull, maxColsFull, stream_);
-        launch_qfill(B, dList_.ptr + coop.size() + full.size(), (int)lane.size(), stream_);
+        const size_t g0 = grpList.size();
+        launch_qfill_grp(B, dList_.ptr, (int)grpList.size(), stream_);
+        launch_qfill_coop(B, dList_.ptr + g0, (int)coop.size(), ringRows, maxCols, stream_);
+        launch_qfill_coop(B, dList_.ptr + g0 + coop.size(), (int)full.size(), maxRowsFull, maxColsFull, stream_);
+        launch_qfill(B, dList_.ptr + g0 + coop.size() + full.size(), (int)lane.size(), stream_);
         QHIP(hipGetLastError());
         const size_t R = reads_.size();
         std::vector<int> st, ca, cb, fl;
@@ -468,22 +494,25 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         QHIP(hipStreamSynchronize(stream_));
         std::vector<int> next;
         static const bool trace = std::getenv("PBCCS_QFILL_TRACE") != nullptr;   // one stderr line per launch set
-        if (trace) {
-            int nt = 0;
-            for (int r : coop) nt += st[r] == kQTall;
-            std::fprintf(stderr, "[qfill] attempt %d ring %zu full %zu lane %zu -> tall %d\n", attempt, coop.size(),
-                         full.size(), lane.size(), nt);
-        }
+        int tallG = 0, tallR = 0;
+        for (int r : grp)
+            if (st[r] == kQTall) { reads_[r].grpTall = true; tallG++; }
+        for (int r : coop)
+            if (st[r] == kQTall) { reads_[r].tallRing = true; tallR++; }
+        if (trace)
+            std::fprintf(stderr, "[qfill] attempt %d grp %zu ring %zu full %zu lane %zu -> tall %d / %d\n", attempt,
+                         grp.size(), coop.size(), full.size(), lane.size(), tallG, tallR);
         for (int r : todo) {
             HRead& h = reads_[r];
             if (st[r] == kQTall) {
-                h.tallRing = true;
                 next.push_back(r);
                 continue;
             }
             if (st[r] == kQOverflow) {
+                // the need covers the passes run before the overflow stopped the schedule; a tall read's later
+                // flip-flop passes tend to need more, so it grows by 2x (each retry is a whole refill)
                 const long long need = std::max(used[2 * r], used[2 * r + 1]);
-                h.valCap = std::max(need + need / 4 + 64, h.valCap + 1);
+                h.valCap = std::max(h.tallRing ? 2 * need + 64 : need + need / 4 + 64, h.valCap + 1);
                 h.valBase = valTop_;
                 valTop_ += 4 * h.valCap;
                 dirty_ = true;

@@ -153,6 +153,7 @@ private:
         int curA = 0, curB = 0, flips = 0;
         float score = 0.0f;
         long long alloc[2] = {0, 0};
+        bool grpTall = false;    // a column outgrew k_qfill_grp's 64-row ring: fill with k_qfill_coop
         bool tallRing = false;   // a column outgrew the band-height LDS ring: fill with the full-height one
     };
     // a read, unfilled, whose bases and five tracks are at seqOff / 5 * seqOff of the host pools

@@ -963,6 +963,394 @@ __device__ long long coop_fill(const QEval& e, const QBand& guideBand, bool useG
     return used;
 }
 
+
+// ==== grouped cooperative fill: four reads per wavefront, one 16-lane DPP row each =======================
+// At the default ScoreDiff a Quiver band column is ~10 rows (AddRead of a 2 kb read uses ~9.8 entries per
+// column), so a 64-lane wave per read leaves most lanes idle.  k_qfill_grp runs the same column recursion as
+// coop_column with a read per DPP row of 16 lanes: the Jacobi Extra cascade and the block max-scan use
+// row-local DPP (row_shr), the stopping rule a 16-bit field of the wave's ballot, and every group walks its
+// own read (its own pass schedule, divergent but barrier-free).  Per read it keeps a 64-row band ring, a
+// 64-row QV-feature window and a 64-base template window in LDS (2.2 KB); a column taller than the ring
+// returns kQTall and the host refills the read with k_qfill_coop.
+constexpr int kQG = 16;                                   // lanes per read
+constexpr int kQGRing = 64;                               // band ring rows per read
+constexpr int kQGWin = 64;                                // QV-feature window rows
+constexpr int kQGTWin = 64;                               // template window bases
+constexpr int kQGLdsFloats = 3 * kQGRing + 5 * kQGWin + (kQGWin + kQGTWin) / 4;
+
+__device__ __forceinline__ unsigned gballot(bool p, int g) { return (unsigned)((__ballot(p) >> (16 * g)) & 0xFFFFull); }
+__device__ __forceinline__ float gread(float x, int g, int k) { return __shfl(x, 16 * g + k, 64); }
+__device__ __forceinline__ void wave_lds_order()   // LDS stores of some lanes before later loads of others
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+struct QGWin {   // the group's LDS: ring (3 x 64 floats), then the five feature tracks, read bases, template bases
+    float* base;
+    int lo, tlo;
+    __device__ __forceinline__ float* ring() const { return base; }
+    __device__ __forceinline__ float* track(int t) const { return base + 3 * kQGRing + t * kQGWin; }
+    __device__ __forceinline__ char* seq() const { return reinterpret_cast<char*>(base + 3 * kQGRing + 5 * kQGWin); }
+    __device__ __forceinline__ char* tpl() const { return seq() + kQGWin; }
+};
+struct GRead {   // a read's bases and its five tracks at feat + t * I (ReadView's layout)
+    const char* seq;
+    const float* feat;
+    int I;
+};
+struct GCol {   // LdsCol with the group ring's fixed mask
+    float* v;
+    int b, e;
+    __device__ __forceinline__ float at(int i) const { return (i >= b && i < e) ? v[i & (kQGRing - 1)] : kNegInf; }
+};
+
+template <bool BETA>
+__device__ __forceinline__ void gwin_ensure(QGWin& w, const GRead& R, int need0, int need1, int gl)
+{
+    need0 = max(need0, 0);
+    need1 = min(need1, R.I - 1);
+    if (need0 > need1 || (need0 >= w.lo && need1 < w.lo + kQGWin)) return;
+    const int lo = BETA ? max(0, need1 + 8 - (kQGWin - 1)) : max(0, need0 - 8);
+    wave_lds_order();
+    for (int q = gl; q < kQGWin; q += kQG) {
+        const int i = lo + q;
+        if (i < R.I) {
+            const int k = i & (kQGWin - 1);
+            w.seq()[k] = R.seq[i];
+#pragma unroll
+            for (int tr = 0; tr < 5; ++tr) w.track(tr)[k] = R.feat[(long long)tr * R.I + i];
+        }
+    }
+    wave_lds_order();
+    w.lo = lo;
+}
+
+// template bases [need0, need1] (clamped to [0, len)) in the template window
+template <bool BETA>
+__device__ __forceinline__ void gtwin_ensure(QGWin& w, const char* base, int len, int need0, int need1, int gl)
+{
+    need0 = max(need0, 0);
+    need1 = min(need1, len - 1);
+    if (need0 > need1 || (need0 >= w.tlo && need1 < w.tlo + kQGTWin)) return;
+    const int lo = BETA ? max(0, need1 + 4 - (kQGTWin - 1)) : max(0, need0 - 4);
+    wave_lds_order();
+    for (int q = gl; q < kQGTWin; q += kQG) {
+        const int j = lo + q;
+        if (j < len) w.tpl()[j & (kQGTWin - 1)] = base[j];
+    }
+    wave_lds_order();
+    w.tlo = lo;
+}
+
+// QvEvaluator (QvEvaluator.hpp:150-207) over the group's windows, the same expressions as QEval's
+struct QEvalG {
+    const QParams* p;
+    int I, len;
+    const QGWin& w;
+    __device__ __forceinline__ int K(int i) const { return i & (kQGWin - 1); }
+    __device__ __forceinline__ char T(int j) const { return j >= len ? '\0' : w.tpl()[j & (kQGTWin - 1)]; }
+    __device__ __forceinline__ char S(int i) const { return w.seq()[K(i)]; }
+    __device__ __forceinline__ float F(int t, int i) const { return w.track(t)[K(i)]; }
+    __device__ __forceinline__ float Inc(int i, int j) const
+    {
+        return (S(i) == T(j)) ? p->Match : p->Mismatch + p->MismatchS * F(1, i);
+    }
+    __device__ __forceinline__ float Del(int i, int j) const
+    {
+        const float tb = (float)T(j);
+        return (i < I && tb == F(3, i)) ? p->DeletionWithTag + p->DeletionWithTagS * F(2, i) : p->DeletionN;
+    }
+    __device__ __forceinline__ float Extra(int i, int j) const
+    {
+        return (j < len && S(i) == T(j)) ? p->Branch + p->BranchS * F(0, i) : p->Nce + p->NceS * F(0, i);
+    }
+    __device__ __forceinline__ float Merge(int i, int j) const
+    {
+        const char a = T(j), b = T(j + 1), s = S(i);
+        if (!(s == a && s == b)) return kNegInf;
+        const int k = tpl_code(a);
+        return p->Merge[k] + p->MergeS[k] * F(4, i);
+    }
+};
+
+// coop_column for one read on its 16-lane row (chunks of 16 rows = 4 SSE quads); same outputs
+template <bool BETA>
+__device__ __forceinline__ void grp_column(const QEvalG& ew, const GRead& R, const char* tbase, int j, int g, int gl,
+                                           int hb, int he, const GCol& c1, const GCol& c2, float* cur,
+                                           const QBand& out, long long base, bool& ovf, int* ob, int* oe,
+                                           float* thrOut, int* tbOut, bool& tall, QGWin& win)
+{
+    const int I = ew.I, J = ew.len;
+    const int mask = kQGRing - 1;
+    const bool sp = ew.p->sumProduct != 0;
+    const bool merge = (ew.p->moves & kMerge) != 0;
+    const float sd = ew.p->scoreDiff;
+    const int req = BETA ? max(0, hb) : min(I + 1, he);
+    const int first = BETA ? he - 1 : hb;
+    int chunk;
+    bool prefix;
+    if (!BETA) {
+        const int gs = first - ((((first - (I + 1)) % 4) + 4) % 4);
+        chunk = gs;
+        prefix = first != gs || first == 0;
+    } else {
+        chunk = first | 3;
+        prefix = (first & 3) != 3 || first == I;
+    }
+    float carry = kNegInf;
+    float score = kNegInf, mx = kNegInf, thr = kNegInf;
+    int stop = BETA ? -1 : I + 1;
+    const bool empty = BETA ? (first < 0) : (first > I);
+    bool done = empty;
+    if (empty) stop = BETA ? first + 1 : first;
+    int nChunks = 0;
+    float lastSv = kNegInf;
+    bool lastKeep = false;
+    if (!empty) gtwin_ensure<BETA>(win, tbase, J, BETA ? j : j - 2, BETA ? j + 1 : j, gl);
+    for (int c = 0; !done; ++c) {
+        nChunks = c + 1;
+        if (mask < I && (BETA ? first - (chunk - 16 * c - 15) : chunk + 16 * c + 15 - first) > mask) {
+            tall = true;
+            *ob = *oe = first;
+            *thrOut = thr;
+            *tbOut = INT_MIN;
+            return;
+        }
+        if (BETA) gwin_ensure<true>(win, R, chunk - 16 * c - 15, chunk - 16 * c, gl);
+        else gwin_ensure<false>(win, R, chunk + 16 * c - 1, chunk + 16 * c + 15, gl);
+        const int row = BETA ? chunk - 16 * c - gl : chunk + 16 * c + gl;
+        const bool valid = BETA ? (row <= first && row >= 0) : (row >= first && row <= I);
+        const int q = gl >> 2;
+        const bool pre = prefix && c == 0 && q == 0;
+        float v = kNegInf, x = 0.0f;
+        bool has = false;
+        if (valid) {
+            if (!BETA) {
+                if (pre) {
+                    if (row == 0 && j == 0) v = 0.0f;
+                    if (row > 0 && j > 0) v = comb(sp, v, c1.at(row - 1) + ew.Inc(row - 1, j - 1));
+                    if (merge && row > 0 && j > 1) v = comb(sp, v, c2.at(row - 1) + ew.Merge(row - 1, j - 2));
+                    if (j > 0) v = comb(sp, v, c1.at(row) + ew.Del(row, j - 1));
+                } else {
+                    if (j > 0) v = comb4(sp, v, c1.at(row - 1) + ew.Inc(row - 1, j - 1));
+                    if (merge && j >= 2) v = comb4(sp, v, c2.at(row - 1) + ew.Merge(row - 1, j - 2));
+                    if (j > 0) v = comb4(sp, v, c1.at(row) + ew.Del(row, j - 1));
+                }
+                has = row > 0;
+                if (has) x = ew.Extra(row - 1, j);
+            } else {
+                if (pre) {
+                    if (row == I && j == J) v = 0.0f;
+                    if (row < I && j < J) v = comb(sp, v, c1.at(row + 1) + ew.Inc(row, j));
+                    if (merge && j < J - 1 && row < I) v = comb(sp, v, c2.at(row + 1) + ew.Merge(row, j));
+                    if (j < J) v = comb(sp, v, c1.at(row) + ew.Del(row, j));
+                } else {
+                    if (j < J) v = comb4(sp, v, c1.at(row + 1) + ew.Inc(row, j));
+                    if (merge && j < J - 1) v = comb4(sp, v, c2.at(row + 1) + ew.Merge(row, j));
+                    if (j < J) v = comb4(sp, v, c1.at(row) + ew.Del(row, j));
+                }
+                has = row < I;
+                if (has) x = ew.Extra(row, j);
+            }
+        }
+        // the Extra cascade through the group's valid lanes, in processing order
+        float sv = valid ? v : kNegInf;
+        const int k0 = BETA ? max(0, chunk - 16 * c - first) : max(0, first - (chunk + 16 * c));
+        const int k1 = BETA ? min(15, chunk - 16 * c) : min(15, I - (chunk + 16 * c));
+        if (!sp) {
+            // Viterbi: Jacobi sweeps to the cascade's one solution (coop_column), row_shr:1 within the group
+            for (int it = k0; it <= k1 + 1; ++it) {
+                float prev = dpp_f<0x111, 0xF>(carry, sv);   // row_shr:1; the group's lane 0 reads carry
+                if (gl == k0) prev = carry;
+                const float nv = has ? comb(false, v, prev + x) : sv;
+                const bool changed = nv != sv;
+                sv = nv;
+                if (gballot(changed, g) == 0) break;
+            }
+        } else {
+            // sum-product: one row per step, the previous row's value one DPP shift away
+            for (int k = k0; k <= k1; ++k) {
+                float prev = dpp_f<0x111, 0xF>(carry, sv);
+                if (gl == k0) prev = carry;
+                if (gl == k && has) sv = comb(sp, v, prev + x);
+            }
+        }
+        if (k1 >= k0) carry = gread(sv, g, k1);
+        // band stopping rule per quad (coop_column), over the group's four quads
+        const int qb = gl & ~3;
+        const float q0 = dpp_f<0x00, 0xF>(kNegInf, sv), q1 = dpp_f<0x55, 0xF>(kNegInf, sv),
+                    q2 = dpp_f<0xAA, 0xF>(kNegInf, sv), q3 = dpp_f<0xFF, 0xF>(kNegInf, sv);
+        float gmin, gmax;
+        if (pre) {
+            gmax = kNegInf;
+            gmin = kNegInf;
+            auto visit = [&](int t2, float qv) {
+                const int rr = BETA ? chunk - (qb + t2) : chunk + qb + t2;
+                const bool vv = BETA ? (rr <= first && rr >= 0) : (rr >= first && rr <= I);
+                if (vv) {
+                    if (qv > gmax) gmax = qv;
+                    gmin = qv;
+                }
+            };
+            visit(0, q0);
+            visit(1, q1);
+            visit(2, q2);
+            visit(3, q3);
+        } else {
+            gmax = q0;
+            gmin = q0;
+            if (gmax < q1) gmax = q1;
+            if (q1 < gmin) gmin = q1;
+            if (gmax < q2) gmax = q2;
+            if (q2 < gmin) gmin = q2;
+            if (gmax < q3) gmax = q3;
+            if (q3 < gmin) gmin = q3;
+        }
+        // running max before each quad: inclusive row-local DPP max-scan, shifted by one lane
+        float inc = gmax;
+        inc = fmax_ref(inc, dpp_f<0x111, 0xF>(kNegInf, inc));
+        inc = fmax_ref(inc, dpp_f<0x112, 0xF>(kNegInf, inc));
+        inc = fmax_ref(inc, dpp_f<0x114, 0xF>(kNegInf, inc));
+        inc = fmax_ref(inc, dpp_f<0x118, 0xF>(kNegInf, inc));
+        const float mxBefore = fmax_ref(mx, dpp_f<0x111, 0xF>(kNegInf, inc));   // row_shr:1; lane 0: -FLT_MAX
+        const float scoreBefore = dpp_f<0x111, 0xF>(score, gmin);               // lane 0: the score so far
+        const int lowRow = BETA ? chunk - 16 * c - qb - 3 : chunk + 16 * c + qb;
+        bool ok;
+        if (pre) ok = true;
+        else {
+            const float thrB = mxBefore == kNegInf ? kNegInf : mxBefore - sd;
+            ok = BETA ? (lowRow >= 0 && (scoreBefore >= thrB || lowRow >= req))
+                      : (lowRow <= I && (scoreBefore >= thrB || lowRow < req));
+        }
+        const unsigned fails = gballot((gl & 3) == 0 && !ok, g);
+        const int stopQuad = fails ? (__ffs((int)fails) - 1) >> 2 : 4;
+        const bool keep = valid && q < stopQuad;
+        if (keep) cur[row & mask] = sv;
+        lastSv = sv;
+        lastKeep = keep;
+        if (stopQuad > 0) {
+            const int lastLane = 4 * stopQuad - 1;
+            score = gread(gmin, g, lastLane);
+            mx = fmax_ref(mx, gread(inc, g, lastLane));
+            thr = mx == kNegInf ? kNegInf : mx - sd;
+        }
+        if (stopQuad < 4) {
+            const int lr = BETA ? chunk - 16 * c - 4 * stopQuad - 3 : chunk + 16 * c + 4 * stopQuad;
+            stop = BETA ? lr + 4 : lr;
+            done = true;
+        } else if (BETA ? (chunk - 16 * c - 15 <= 0) : (chunk + 16 * c + 15 >= I)) {
+            stop = BETA ? 0 : I + 1;
+            done = true;
+        }
+    }
+    const int beginRow = BETA ? stop : first;
+    const int endRow = BETA ? first + 1 : stop;
+    if (nChunks == 1) {
+        const int row = BETA ? chunk - gl : chunk + gl;
+        if (lastKeep) {
+            const long long k = base + (row - beginRow);
+            if (k < out.cap) out.val[k] = lastSv;
+            else ovf = true;
+        }
+        const unsigned bal = gballot(lastKeep && !(lastSv < thr), g);
+        if (!BETA) *tbOut = bal ? chunk + __ffs((int)bal) - 1 : endRow;
+        else *tbOut = bal ? chunk - (__ffs((int)bal) - 1) + 1 : beginRow;
+    } else {
+        *tbOut = INT_MIN;
+        for (int r = beginRow + gl; r < endRow; r += kQG) {
+            const long long k = base + (r - beginRow);
+            if (k < out.cap) out.val[k] = cur[r & mask];
+            else ovf = true;
+        }
+    }
+    *ob = beginRow;
+    *oe = endRow;
+    *thrOut = thr;
+}
+
+// coop_fill for one read on its 16-lane row
+template <bool BETA>
+__device__ long long grp_fill(const QEvalG& ew, const GRead& R, const char* tbase, const QBand& guideBand,
+                              bool useGuide, const QBand& prevBand, bool usePrev, const QBand& out, QAlloc* alloc,
+                              bool allocExists, bool& ovf, float* ring, int4* hint, int g, int gl, QGWin& win)
+{
+    const int I = ew.I, J = ew.len;
+    const float sd = ew.p->scoreDiff;
+    const int mask = kQGRing - 1;
+    for (int j = gl; j <= J; j += kQG) {
+        int4 h = make_int4(-1, -1, -1, -1);
+        if (useGuide && !guideBand.Empty(j)) row_range(guideBand, j, sd, &h.x, &h.y);
+        if (usePrev && !prevBand.Empty(j)) row_range(prevBand, j, sd, &h.z, &h.w);
+        hint[j] = h;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    GCol cur{ring, 0, 0}, c1{ring + kQGRing, 0, 0}, c2{ring + 2 * kQGRing, 0, 0};
+    long long used = 0;
+    bool tall = false;
+    int hb = BETA ? I + 1 : 0, he = BETA ? I + 1 : 0;
+    int4 hNext = hint[BETA ? J : 0];
+    for (int s = 0; s <= J; ++s) {
+        const int j = BETA ? J - s : s;
+        const int4 h = hNext;
+        if (s < J) hNext = hint[BETA ? j - 1 : j + 1];
+        if (h.x >= 0) { hb = min(h.x, hb); he = max(h.y, he); }
+        if (h.z >= 0) { hb = min(h.z, hb); he = max(h.w, he); }
+        int b, en, tb;
+        float thr;
+        grp_column<BETA>(ew, R, tbase, j, g, gl, hb, he, c1, c2, cur.v, out, used, ovf, &b, &en, &thr, &tb, tall, win);
+        if (tall) return -1;
+        cur.b = b;
+        cur.e = en;
+        if (gl == 0) {
+            out.off[j] = (int)min(used, (long long)0x7fffffff);
+            out.range[j] = make_int2(b, en);
+            hint[j] = make_int4(hb, he, b, en);
+        }
+        used += en - b;
+        if (tb != INT_MIN) {
+            if (!BETA) { he = en; hb = tb; }
+            else { hb = b; he = tb; }
+        } else if (!BETA) {
+            he = en;
+            int nb = en;
+            for (int i0 = b; i0 < en; i0 += kQG) {
+                const int i = i0 + gl;
+                const unsigned bal = gballot(i < en && !(cur.v[i & mask] < thr), g);
+                if (bal) { nb = i0 + __ffs((int)bal) - 1; break; }
+            }
+            hb = nb;
+        } else {
+            hb = b;
+            int ne = b;
+            for (int i1 = en; i1 > b; i1 -= kQG) {
+                const int i = i1 - 1 - gl;
+                const unsigned bal = gballot(i >= b && !(cur.v[i & mask] < thr), g);
+                if (bal) { ne = i1 - (__ffs((int)bal) - 1); break; }
+            }
+            he = ne;
+        }
+        const GCol old2 = c2;
+        c2 = c1;
+        c1 = cur;
+        cur = old2;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    if (alloc) {
+        for (int j = gl; j <= J; j += kQG) {
+            const int4 h = hint[j];
+            QAlloc a = alloc[j];
+            alloc_start(a, allocExists, h.x, h.y, I + 1);
+            if (!BETA) {
+                for (int r = max(h.z, a.ae); r < h.w; ++r) alloc_set(a, r, I + 1);
+            } else {
+                for (int r = h.w - 1; r >= h.z; --r) alloc_set(a, r, I + 1);
+            }
+            alloc[j] = a;
+        }
+    }
+    return used;
+}
 }  // namespace
 
 // ---- k_qfill_coop: FillAlphaBeta with one wavefront per read (SparseSse recursors, reads < kQCoopMaxRows) --
@@ -1061,6 +1449,19 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
             ovf = __ballot(ovf) != 0;
         }
     }
+    // AllocatedEntries of both passes: a wave-wide sum over the columns (not a serial walk on lane 0)
+    long long capA = 0, capB = 0;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the last pass's bookkeeping stores come first
+    if (!tall && !ovf) {
+        for (int j = lane; j <= J; j += 64) {
+            capA += v.allocA[j].capacity;
+            capB += v.allocB[j].capacity;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            capA += __shfl_xor(capA, o, 64);
+            capB += __shfl_xor(capB, o, 64);
+        }
+    }
     if (lane != 0) return;
     if (tall) {
         B.rStatus[r] = kQTall;
@@ -1076,12 +1477,153 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
     B.rCurB[r] = curB - 2;
     B.rFlips[r] = flips;
     B.rScore[r] = b_start();
-    B.rAlloc[2 * r] = allocated_entries(v.allocA, J + 1);
-    B.rAlloc[2 * r + 1] = allocated_entries(v.allocB, J + 1);
+    B.rAlloc[2 * r] = capA;
+    B.rAlloc[2 * r + 1] = capB;
     B.rStatus[r] = ((double)fabsf(a_end() - b_start()) > 0.2) ? kQMismatch : kQOk;
 }
 
 // ---- k_qfill: MutationScorer ctor / Template() -> FillAlphaBeta ------------------------------------------
+// ---- k_qfill_grp: FillAlphaBeta with four reads per wavefront (grp_fill; the pass schedule of k_qfill_coop) --
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_qfill_grp(QBatch B, const int* __restrict__ reads, int n)
+{
+    __shared__ float qlds[4 * kQGLdsFloats];
+    const int lane = threadIdx.x, g = lane >> 4, gl = lane & 15;
+    const int t = blockIdx.x * 4 + g;
+    if (t >= n) return;
+    const int r = reads[t];
+    if (r < 0) return;   // padding: the host lists each QuiverConfig's reads in whole waves
+    // the read as offsets from the batch's pools (the pools' bases are kernel arguments, scalar); the wave's
+    // reads share one QuiverConfig (the host's list), so its parameters are scalar loads
+    const QParams* P = B.params + __builtin_amdgcn_readfirstlane(B.rParam[r]);
+    const int z = B.rZmw[r];
+    const int I = B.rLen[r];
+    const long long so = B.rSeq[r];
+    const GRead R{B.seqPool + so, B.featPool + 5 * so, I};
+    const int ts = B.rTs[r], te = B.rTe[r], L = B.zLen[z];
+    const char* tbase = B.tplPool + (B.rStrand[r] == 0 ? B.zFwd[z] + ts : B.zRev[z] + (L - te));
+    const int J = te - ts;
+    const long long cb = B.rColBase[r], vb = B.rValBase[r], valCap = B.rValCap[r];
+    const int colCap = B.rColCap[r];
+    auto arena_k = [&](int k) {
+        QBand m;
+        m.range = B.range + cb + (long long)k * colCap;
+        m.off = B.off + cb + (long long)k * colCap;
+        m.val = B.valPool + vb + (long long)k * valCap;
+        m.cap = valCap;
+        m.cols = J + 1;
+        return m;
+    };
+    QAlloc* allocA = B.alloc + cb / 2;
+    QAlloc* allocB = allocA + colCap;
+    int4* hint = B.hint + cb / 4;
+    if (I < 1 || J < 1 || J + 1 > colCap) {
+        if (gl == 0) B.rStatus[r] = kQBad;
+        return;
+    }
+    float* my = qlds + g * kQGLdsFloats;
+    QGWin win{my, INT_MIN / 2, INT_MIN / 2};
+    const QEvalG ew{P, I, J, win};
+    for (int k = 0; k < 4; ++k) {
+        const QBand m = arena_k(k);
+        for (int j = gl; j <= J; j += kQG) m.range[j] = make_int2(0, 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    bool ovf = false, tall = false;
+    long long needA = 0, needB = 0;
+    int curA = 0, curB = 2;
+    bool aPassed = false, bPassed = false;
+    auto passA = [&](bool guided) {
+        const int nxt = aPassed ? (curA ^ 1) : 0;
+        const QBand gb = arena_k(curB), self = arena_k(curA), out = arena_k(nxt);
+        const long long u = grp_fill<false>(ew, R, tbase, gb, guided, self, aPassed, out, allocA, aPassed, ovf, my,
+                                            hint, g, gl, win);
+        tall = tall || u < 0;
+        needA = max(needA, u);
+        curA = nxt;
+        aPassed = true;
+        return u;
+    };
+    auto passB = [&]() {
+        const int nxt = bPassed ? (curB ^ 1) : 2;
+        const QBand gb = arena_k(curA), self = arena_k(curB), out = arena_k(nxt);
+        const long long u = grp_fill<true>(ew, R, tbase, gb, true, self, bPassed, out, allocB, bPassed, ovf, my,
+                                           hint, g, gl, win);
+        tall = tall || u < 0;
+        needB = max(needB, u);
+        curB = nxt;
+        bPassed = true;
+        return u;
+    };
+    auto a_end = [&]() { return arena_k(curA).Get(I, J); };
+    auto b_start = [&]() { return arena_k(curB).Get(0, 0); };
+    const int maxSize = (int)(0.5 + 0.04 * (I + 1) * (J + 1));
+    long long ua = 0;
+    int flips = 0, stage = 0, pending = 0;   // RecursorBase::FillAlphaBeta's schedule, as k_qfill_coop
+    for (;;) {
+        bool alpha = true, guided = true;
+        if (stage == 0) guided = false;
+        else if (stage == 1) alpha = false;
+        else if (stage == 2) alpha = pending != 2;
+        else {
+            if (ovf || !((double)fabsf(a_end() - b_start()) > 0.2) || flips > kMaxFlipFlops) break;
+            alpha = flips % 2 == 0;
+        }
+        const long long u = alpha ? passA(guided) : passB();
+        if (tall) break;
+        if (stage == 0) {
+            ua = u;
+            stage = 1;
+        } else if (stage == 1) {
+            ovf = gballot(ovf, g) != 0;
+            if (!ovf && (ua >= maxSize || u >= maxSize)) {
+                stage = 2;
+                pending = 3;
+                flips += 3;
+            } else {
+                stage = 3;
+            }
+        } else if (stage == 2) {
+            if (--pending == 0) {
+                ovf = gballot(ovf, g) != 0;
+                stage = 3;
+            }
+        } else {
+            flips++;
+            ovf = gballot(ovf, g) != 0;
+        }
+    }
+    long long capA = 0, capB = 0;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    if (!tall && !ovf) {
+        for (int j = gl; j <= J; j += kQG) {
+            capA += allocA[j].capacity;
+            capB += allocB[j].capacity;
+        }
+        for (int o = 8; o > 0; o >>= 1) {
+            capA += __shfl_xor(capA, o, 64);
+            capB += __shfl_xor(capB, o, 64);
+        }
+    }
+    if (gl != 0) return;
+    if (tall) {
+        B.rStatus[r] = kQTall;
+        return;
+    }
+    B.rUsed[2 * r] = needA;
+    B.rUsed[2 * r + 1] = needB;
+    if (ovf) {
+        B.rStatus[r] = kQOverflow;
+        return;
+    }
+    B.rCurA[r] = curA;
+    B.rCurB[r] = curB - 2;
+    B.rFlips[r] = flips;
+    B.rScore[r] = b_start();
+    B.rAlloc[2 * r] = capA;
+    B.rAlloc[2 * r + 1] = capB;
+    B.rStatus[r] = ((double)fabsf(a_end() - b_start()) > 0.2) ? kQMismatch : kQOk;
+}
+
 __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ reads, int n)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1733,6 +2275,12 @@ void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, in
     const int cols = (maxCols + 15) / 16 * 16;
     const size_t lds = (size_t)(3 * rows + 5 * kQWinRows) * sizeof(float) + kQWinRows + cols;
     hipLaunchKernelGGL(k_qfill_coop, dim3(n), dim3(64), lds, s, B, reads, n, rows, cols);
+}
+
+void launch_qfill_grp(const QBatch& B, const int* reads, int n, hipStream_t s)
+{
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_qfill_grp, dim3((n + 3) / 4), dim3(64), 0, s, B, reads, n);
 }
 
 void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s)

@@ -135,9 +135,12 @@ void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s);
 // FillAlphaBeta with one wavefront per read (SparseSse recursors; reads of I + 1 <= kQCoopRows rows and windows
 // of J + 1 <= kQCoopCols columns); maxRows / maxCols = the largest I + 1 / J + 1 of the listed reads
 constexpr int kQCoopRows = 4096;
-constexpr int kQRingRows = 256;   // band-height LDS ring rows (a power of two; taller columns: kQTall, ~1% of 2 kb reads); 256 / 512 / 1024 measured 1311 / 1241 / 1178 ZMWs/s with the 128-row feature window (profiles/r3t_quiver_ab.txt)
+constexpr int kQRingRows = 128;   // k_qfill_coop band-height ring rows (a power of two; taller columns: kQTall); 128 / 256 / 512 / 1024 measured 1760 / 1583-1626 / 1241 / 1178 ZMWs/s (profiles/r3t_quiver_ab.txt, r3v_quiver_ab.txt)
 constexpr int kQCoopCols = 8192;
 void launch_qfill_coop(const QBatch& B, const int* reads, int n, int maxRows, int maxCols, hipStream_t s);
+// The same with four reads per wavefront (a 16-lane DPP row each, 64-row band ring): the default first try for
+// SparseSse reads; a read with a taller column comes back kQTall and is refilled by k_qfill_coop.
+void launch_qfill_grp(const QBatch& B, const int* reads, int n, hipStream_t s);
 void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s);
 void launch_qscore_mid(const QBatch& B, const QMidWork& W, long long nWaves, hipStream_t s);
 void launch_qreduce(const QReduceWork& W, hipStream_t s);
