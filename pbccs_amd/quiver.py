@@ -370,18 +370,23 @@ class PreparedQuiverBatch:
         _lib_mod.check(load().pbccs_quiver_polish_batch(
             eng._h, carr, names, nc, ctypes.cast(cz.ctypes.data, ctypes.POINTER(_lib_mod.CQuiverZmw)), n,
             ctypes.byref(o), ctypes.cast(res.ctypes.data, ctypes.POINTER(_lib_mod.CQuiverResult))))
+        # per-field columns as Python lists once (not one structured-record access per field per ZMW)
+        lens, oks = res["consensus_len"][:n].tolist(), res["ok"][:n].tolist()
+        tested, applied = res["n_tested"][:n].tolist(), res["n_applied"][:n].tolist()
+        conv, active = res["converged"][:n].tolist(), res["n_active"][:n].tolist()
+        caps, starts = cap.tolist(), cstart.tolist()
+        cbytes = cons.tobytes()
         out = []
         for k in range(n):
-            r = res[k]
-            ln = int(r["consensus_len"])
-            if ln > int(cap[k]):
+            ln = lens[k]
+            if ln > caps[k]:
                 raise _lib_mod.PbccsError(-5, "consensus outgrew its buffer")
-            c0 = int(cstart[k])
-            ok = bool(r["ok"])
-            out.append({"consensus": cons[c0:c0 + ln].tobytes().decode(),
+            c0 = starts[k]
+            ok = bool(oks[k])
+            out.append({"consensus": cbytes[c0:c0 + ln].decode(),
                         "qvs": qvb[c0:c0 + ln].tolist() if qvs and ok else None,
-                        "n_tested": int(r["n_tested"]), "n_applied": int(r["n_applied"]),
-                        "converged": bool(r["converged"]), "ok": ok, "n_active": int(r["n_active"])})
+                        "n_tested": tested[k], "n_applied": applied[k],
+                        "converged": bool(conv[k]), "ok": ok, "n_active": active[k]})
         return out
 
 
