@@ -104,6 +104,9 @@ QuiverBatch::QuiverBatch(int device) : device_(device)
 {
     QHIP(hipSetDevice(device_));
     QHIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    QHIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    QHIP(hipEventCreateWithFlags(&evFork_, hipEventDisableTiming));
+    QHIP(hipEventCreateWithFlags(&evJoin_, hipEventDisableTiming));
     dScratchTop_.reserve(1, false);
     dOverflow_.reserve(1, false);
     dScratch_.reserve(1 << 20, false);
@@ -111,10 +114,16 @@ QuiverBatch::QuiverBatch(int device) : device_(device)
 
 QuiverBatch::~QuiverBatch()
 {
+    if (side_) {
+        (void)hipStreamSynchronize(side_);
+        (void)hipStreamDestroy(side_);
+    }
     if (stream_) {
         (void)hipStreamSynchronize(stream_);
         (void)hipStreamDestroy(stream_);
     }
+    if (evFork_) (void)hipEventDestroy(evFork_);
+    if (evJoin_) (void)hipEventDestroy(evJoin_);
 }
 
 void QuiverBatch::Reset()
@@ -475,10 +484,20 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
             return p;
         }();
         const size_t g0 = grpList.size();
+        // the coop lists (reads that were tall for k_qfill_grp) on the side stream, concurrently with the grouped
+        // launch; both streams join before the status download
+        const bool sideRun = !coop.empty() || !full.empty();
+        if (sideRun) {
+            QHIP(hipEventRecord(evFork_, stream_));   // after the uploads above
+            QHIP(hipStreamWaitEvent(side_, evFork_, 0));
+            launch_qfill_coop(B, dList_.ptr + g0, (int)coop.size(), ringRows, maxCols, side_);
+            launch_qfill_coop(B, dList_.ptr + g0 + coop.size(), (int)full.size(), maxRowsFull, maxColsFull, side_);
+            QHIP(hipGetLastError());
+            QHIP(hipEventRecord(evJoin_, side_));
+        }
         launch_qfill_grp(B, dList_.ptr, (int)grpList.size(), stream_);
-        launch_qfill_coop(B, dList_.ptr + g0, (int)coop.size(), ringRows, maxCols, stream_);
-        launch_qfill_coop(B, dList_.ptr + g0 + coop.size(), (int)full.size(), maxRowsFull, maxColsFull, stream_);
         launch_qfill(B, dList_.ptr + g0 + coop.size() + full.size(), (int)lane.size(), stream_);
+        if (sideRun) QHIP(hipStreamWaitEvent(stream_, evJoin_, 0));
         QHIP(hipGetLastError());
         const size_t R = reads_.size();
         std::vector<int> st, ca, cb, fl;

@@ -178,6 +178,10 @@ private:
 
     int device_ = 0;
     hipStream_t stream_ = nullptr;
+    // the fill's tall reads (k_qfill_coop's lists) run on a side stream beside k_qfill_grp: their long serial
+    // chains overlap the grouped launch instead of following it
+    hipStream_t side_ = nullptr;
+    hipEvent_t evFork_ = nullptr, evJoin_ = nullptr;
     std::vector<QParams> configs_;
     std::vector<HZmw> zmws_;
     std::vector<HRead> reads_;
