@@ -51,7 +51,7 @@ struct pbccs_engine {
     // the POA draft step's device state (made on first use): kPoaSlices runners, one per concurrent slice
     // PBCCS_POA_SLICES overrides the slice count (A/B): more slices overlap one slice's host graph work with
     // the others' device rounds, with fewer host threads each
-    static constexpr int kPoaSlicesDefault = 2;
+    static constexpr int kPoaSlicesDefault = 3;   // 1 / 2 / 3 / 4 slices: 1400 / 1527 / 1575 / 1571 ccs ZMWs/s (profiles/r3y_ccs_slices_ab.txt)
     static int PoaSlices()
     {
         static const int n = std::max(1, std::min(8, std::getenv("PBCCS_POA_SLICES") ? std::atoi(std::getenv("PBCCS_POA_SLICES"))
