@@ -1654,9 +1654,9 @@ struct CcsChunk {
 };
 
 // The chunk's polish outputs: the caller's pbccs_zmw_output fields, but per-read arrays owned by the chunk.
-static void bind_polish_outputs(CcsChunk* C, const pbccs_ccs_output* out, size_t q0 = 0, size_t q1 = SIZE_MAX)
+static void bind_polish_outputs(CcsChunk* C, const pbccs_ccs_output* out)
 {
-    for (size_t q = q0; q < std::min(q1, C->pinZ.size()); ++q) {
+    for (size_t q = 0; q < C->pinZ.size(); ++q) {
         C->pout[q] = out[C->pinZ[q]].polish;
         C->pout[q].add_read_results = C->arr[q].data();
         C->pout[q].zscores = C->zsc[q].data();
@@ -1830,24 +1830,10 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
         for (int s = 0; s < slots; ++s) eng->Slot(s);
         std::mutex qmu;
         std::condition_variable qcv;
+        int drafted = 0, next = 0;
         bool stop = false;
-        // polish units: each drafted chunk is cut into `split` pieces (the last chunk into `tailSplit`), so the
-        // pieces of the final chunks spread over the slots that free up instead of one slot's batch being the
-        // run's tail.  PBCCS_CCS_SPLIT / PBCCS_CCS_TAIL_SPLIT override them (A/B).
-        auto envInt = [](const char* name, int dflt) {
-            const char* e = std::getenv(name);
-            return e ? std::max(1, std::min(16, std::atoi(e))) : dflt;
-        };
-        static const int split = envInt("PBCCS_CCS_SPLIT", 1);
-        static const int tailSplit = envInt("PBCCS_CCS_TAIL_SPLIT", 1);
-        struct Unit {
-            int c, b, e;
-        };
-        std::vector<Unit> units;
-        units.reserve((size_t)nb * (size_t)std::max(split, tailSplit) + 1);
-        int ready = 0, next = 0;
-        std::vector<int> prc(units.capacity(), PBCCS_OK);
-        std::vector<std::string> perr(units.capacity());
+        std::vector<int> prc(nb, PBCCS_OK);
+        std::vector<std::string> perr(nb);
         // PBCCS_CCS_TRACE=1: one stderr line per chunk stage (ms since the call began)
         static const bool trace = std::getenv("PBCCS_CCS_TRACE") != nullptr;
         const auto tBegin = std::chrono::steady_clock::now();
@@ -1856,24 +1842,22 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
         };
         auto worker = [&](int slot) {
             for (;;) {
-                int u;
-                Unit U;
+                int c;
                 {
                     std::unique_lock<std::mutex> lk(qmu);
-                    qcv.wait(lk, [&] { return stop || next < ready; });
-                    if (next >= ready) return;   // stopped with nothing left
-                    u = next++;
-                    U = units[u];
+                    qcv.wait(lk, [&] { return stop || next < drafted; });
+                    if (next >= drafted) return;   // stopped with nothing left
+                    c = next++;
                 }
-                CcsChunk& C = chunks[U.c];
-                if (U.e <= U.b) continue;
+                CcsChunk& C = chunks[c];
+                if (C.pin.empty()) continue;
                 const double p0 = since();
-                prc[u] = polish_span(eng, slot, C.pin.data() + U.b, U.e - U.b, &o, C.pout.data() + U.b);
+                prc[c] = polish_span(eng, slot, C.pin.data(), (int)C.pin.size(), &o, C.pout.data());
                 if (trace)
-                    std::fprintf(stderr, "[ccs] chunk %d polish slot %d zmws %d %.1f-%.1f ms\n", U.c, slot, U.e - U.b,
+                    std::fprintf(stderr, "[ccs] chunk %d polish slot %d zmws %zu %.1f-%.1f ms\n", c, slot, C.pin.size(),
                                  p0, since());
-                if (prc[u] != PBCCS_OK && prc[u] != PBCCS_EOOM) {
-                    perr[u] = g_lastError;
+                if (prc[c] != PBCCS_OK && prc[c] != PBCCS_EOOM) {
+                    perr[c] = g_lastError;
                     std::lock_guard<std::mutex> lk(qmu);
                     stop = true;
                     qcv.notify_all();
@@ -1886,7 +1870,7 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
         const bool serial = serialEnv && serialEnv[0] == '1';
         std::vector<std::thread> pool;
         if (!serial)
-            for (int s = 0; s < std::min(slots, nb * std::max(split, tailSplit)); ++s) pool.emplace_back(worker, s);
+            for (int s = 0; s < std::min(slots, nb); ++s) pool.emplace_back(worker, s);
         int rcDraft = PBCCS_OK;
         std::string errDraft;
         for (int c = 0; c < nb; ++c) {
@@ -1911,22 +1895,19 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
             if (rcDraft != PBCCS_OK) {
                 stop = true;
             } else {
-                const int m = (int)chunks[c].pin.size();
-                const int k = std::max(1, std::min(c + 1 == nb ? tailSplit : split, m));
-                for (int q = 0; q < k; ++q) units.push_back(Unit{c, (int)((long long)m * q / k), (int)((long long)m * (q + 1) / k)});
-                ready = (int)units.size();
+                drafted = c + 1;
             }
             qcv.notify_all();
             if (rcDraft != PBCCS_OK) break;
         }
         {
             std::lock_guard<std::mutex> lk(qmu);
-            stop = true;   // every ready unit is still taken: workers leave once next == ready
+            stop = true;   // every drafted chunk is still taken: workers leave once next == drafted
             qcv.notify_all();
         }
         if (serial) {
             for (poa::PoaRunner* r : eng->PoaRunners()) r->ReleasePool();
-            for (int s = 0; s < std::min(slots, nb * std::max(split, tailSplit)); ++s) pool.emplace_back(worker, s);
+            for (int s = 0; s < std::min(slots, nb); ++s) pool.emplace_back(worker, s);
         }
         for (std::thread& t : pool) t.join();
         for (poa::PoaRunner* r : eng->PoaRunners()) {
@@ -1934,20 +1915,19 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
             r->SetPoolBudget(0);
         }
         if (rcDraft != PBCCS_OK) return fail(rcDraft, errDraft.c_str());
-        for (int u = 0; u < (int)units.size(); ++u)
-            if (prc[u] != PBCCS_OK && prc[u] != PBCCS_EOOM) return fail(prc[u], perr[u].c_str());
-        // units that ran the device out of memory beside the others: rerun alone once every pool is unmapped
+        for (int c = 0; c < nb; ++c)
+            if (prc[c] != PBCCS_OK && prc[c] != PBCCS_EOOM) return fail(prc[c], perr[c].c_str());
+        // chunks that ran the device out of memory beside the others: rerun alone once every pool is unmapped
         bool unmapped = false;
-        for (int u = 0; u < (int)units.size(); ++u) {
-            if (prc[u] != PBCCS_EOOM) continue;
+        for (int c = 0; c < nb; ++c) {
+            if (prc[c] != PBCCS_EOOM) continue;
             if (!unmapped) {
                 for (int s = 0; s < slots; ++s) eng->Slot(s)->val.unmap_all();
                 unmapped = true;
             }
-            const Unit U = units[u];
-            CcsChunk& C = chunks[U.c];
-            bind_polish_outputs(&C, out, (size_t)U.b, (size_t)U.e);
-            const int r = polish_retry(eng, 0, C.pin.data() + U.b, U.e - U.b, &o, C.pout.data() + U.b);
+            CcsChunk& C = chunks[c];
+            bind_polish_outputs(&C, out);
+            const int r = polish_retry(eng, 0, C.pin.data(), (int)C.pin.size(), &o, C.pout.data());
             if (r != PBCCS_OK) return r;
         }
         bool draftRange = false;

@@ -774,7 +774,7 @@ void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std:
     std::vector<long long>& mutStart = *mutStartOut;
     taskStart.assign(n + 1, 0);
     mutStart.assign(n + 1, 0);
-    std::vector<int> readBase(n), nReads(n), readList, flat;
+    std::vector<int> readBase(n), nReads(n), readList;
     std::vector<float> fastThr(n);
     for (int w = 0; w < n; ++w) {
         const HZmw& z = zmws_[zs[w]];
@@ -785,9 +785,11 @@ void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std:
         mutStart[w + 1] = mutStart[w] + (long long)codes[w].size();
         taskStart[w + 1] = taskStart[w] + (long long)codes[w].size() * nReads[w];
     }
-    flat.resize((size_t)mutStart[n]);   // the scorers' lists back to back, copied on several threads
+    hCodes_.n = 0;   // the scorers' lists back to back (the previous round's upload has completed)
+    hCodes_.grow((size_t)mutStart[n]);
     par_for(n, [&](int w) {
-        if (!codes[w].empty()) std::memcpy(flat.data() + mutStart[w], codes[w].data(), codes[w].size() * sizeof(int));
+        if (!codes[w].empty())
+            std::memcpy(hCodes_.data() + mutStart[w], codes[w].data(), codes[w].size() * sizeof(int));
     });
     const long long nTask = taskStart[n];
     std::vector<int> active(reads_.size());
@@ -801,7 +803,9 @@ void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std:
     put(dReadList_, readList, stream_);
     put(dRActive_, active, stream_);
     put(dWFast_, fastThr, stream_);
-    put(dCodes_, flat, stream_);
+    dCodes_.reserve(std::max<size_t>(hCodes_.size(), 1), false);
+    if (hCodes_.size())
+        QHIP(hipMemcpyAsync(dCodes_.ptr, hCodes_.data(), hCodes_.size() * sizeof(int), hipMemcpyHostToDevice, stream_));
     dDelta_.reserve(std::max<long long>(nTask, 1), false);
     const double msPrep = msSince(ts0);
     const Clock::time_point ts1 = Clock::now();

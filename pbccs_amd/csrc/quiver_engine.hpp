@@ -45,7 +45,9 @@ struct HostPool {
     {
         const size_t at = n;
         if (n + add > cap) {
-            const size_t nc = std::max(n + add, cap + cap / 2);
+            // 25% headroom: a pinned allocation costs ~0.1 s per GB, and the next batch of a long-lived pool is
+            // rarely exactly as large as the one that sized it
+            const size_t nc = std::max(n + add + (n + add) / 4, cap + cap / 2);
             T* q = nullptr;
             bool qp = false;
             if (pinned && hipHostMalloc((void**)&q, nc * sizeof(T), hipHostMallocDefault) == hipSuccess) qp = true;
@@ -87,7 +89,7 @@ public:
     // batch (the engine's, for pbccs_quiver_polish_batch) reaches its steady-state allocation once.
     void Reset();
     // page-locked host read pools (a long-lived batch: the pinning cost is paid once)
-    void PinHostPools() { hSeq_.pinned = hFeat_.pinned = true; }
+    void PinHostPools() { hSeq_.pinned = hFeat_.pinned = hCodes_.pinned = true; }
     int AddConfig(const QParams& p);
     int AddZmw(const std::string& tpl, float fastScoreThreshold);
     // AddRead (Quiver/MultiReadMutationScorer.cpp:246-283): fills the read; returns whether it is active.
@@ -187,6 +189,7 @@ private:
     std::vector<HRead> reads_;
     HostPool<char> hSeq_;
     HostPool<float> hFeat_;
+    HostPool<int> hCodes_;   // a scoring round's mutation lists back to back (staging for the upload)
     long long colTop_ = 0, valTop_ = 0;
     size_t seqUp_ = 0, featUp_ = 0;   // host read pools already on the device (append-only)
     bool dirty_ = true;
