@@ -279,3 +279,22 @@ def test_quiver_coop_fill_long_reads_match_oracle():
         assert (r["converged"], r["n_tested"], r["n_applied"]) == (ref["converged"], ref["n_tested"], ref["n_applied"])
         assert r["consensus"] == o.template()
         assert _qvs_within_one(r["qvs"], o.qvs())
+
+
+@pytest.mark.parametrize("score_diff,sum_product", [(60.0, False), (60.0, True), (400.0, False)])
+def test_quiver_tall_band_fill_paths_match_oracle(score_diff, sum_product):
+    """Wide bands send reads down every SparseSse fill path: at ScoreDiff 60 (~26 rows per column) some columns
+    outgrow k_qfill_grp's 64-row ring (kQTall -> k_qfill_coop), at ScoreDiff 400 (~137 rows) most outgrow the
+    coop kernel's 128-row ring too (-> its full-height ring).  Active flags, baselines, flip-flops,
+    AllocatedEntries and every unique mutation's score equal the oracle's."""
+    tpl, reads = _zmw(321, 300, 3)
+    g, o = _pair(tpl, reads, sum_product, score_diff=score_diff)
+    act = [k for k in range(len(reads)) if o.read_info(k)["active"]]
+    assert len(act) == len(reads)
+    assert g.s.BaselineScores() == [o.read_info(k)["score"] for k in act]
+    assert [g.s.NumFlipFlops()[k] for k in act] == [o.read_info(k)["flipflops"] for k in act]
+    assert [g.s.AllocatedEntries(k) for k in act] == [tuple(o.read_info(k)["allocated"]) for k in act]
+    muts = O.unique_mutations(tpl)
+    vals = g.s.ScoreMany([g.P.Mutation(t, s, b) for (t, s, b) in muts])
+    for (t, s, b), v in zip(muts, vals):
+        assert v == o.score(t, s, b), (t, s, b)
