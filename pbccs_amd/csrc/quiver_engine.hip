@@ -514,8 +514,11 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         std::vector<int> next;
         static const bool trace = std::getenv("PBCCS_QFILL_TRACE") != nullptr;   // one stderr line per launch set
         int tallG = 0, tallR = 0;
+        // a read too tall for the grouped kernel's 64-row ring goes straight to the full-height ring: most of
+        // them outgrow the 128-row band ring as well (round 0 of the Quiver bench: 43 of 46), and each step down
+        // the paths is one more serial launch on the round's critical path
         for (int r : grp)
-            if (st[r] == kQTall) { reads_[r].grpTall = true; tallG++; }
+            if (st[r] == kQTall) { reads_[r].grpTall = reads_[r].tallRing = true; tallG++; }
         for (int r : coop)
             if (st[r] == kQTall) { reads_[r].tallRing = true; tallR++; }
         if (trace)
