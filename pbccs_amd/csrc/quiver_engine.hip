@@ -517,21 +517,8 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         // a read too tall for the grouped kernel's 64-row ring goes straight to the full-height ring: most of
         // them outgrow the 128-row band ring as well (round 0 of the Quiver bench: 43 of 46), and each step down
         // the paths is one more serial launch on the round's critical path
-        // Its arenas are sized for a ~10-row band: a tall read would overflow them in its first full-ring fill
-        // and run it again (a count-only pass, then the regrown one), so they start at 1/16 of the full matrix.
         for (int r : grp)
-            if (st[r] == kQTall) {
-                HRead& h = reads_[r];
-                h.grpTall = h.tallRing = true;
-                tallG++;
-                const long long want = (long long)(h.len + 1) * (long long)(h.te - h.ts + 1) / 16 + 64;
-                if (want > h.valCap) {
-                    h.valCap = want;
-                    h.valBase = valTop_;
-                    valTop_ += 4 * h.valCap;
-                    dirty_ = true;
-                }
-            }
+            if (st[r] == kQTall) { reads_[r].grpTall = reads_[r].tallRing = true; tallG++; }
         for (int r : coop)
             if (st[r] == kQTall) { reads_[r].tallRing = true; tallR++; }
         if (trace)
