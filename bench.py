@@ -40,7 +40,7 @@ FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
 FLOP_PER_CELL = 11             # fill cell 6 mul + 3 add + <= 1 div, + the column rescale
 CHAIN_STEP_CYCLES = 29.7       # one dependent insertion-chain step (tools/ubench/chain_step.hip)
 BEST_SLOTS = 5                 # measured best split of 2 kb batches: 5 slots divide the driver's 20 steps into 4 full waves (6 slots: 2868 vs 3357 ZMWs/s at --steps 20, the last wave half empty)
-BEST_SLOTS_10KB = 8            # configs[2] through the work queue at 2000 ZMWs: 4 / 5 / 8 slots 27.5 / 26.3 / 29.1 ZMWs/s (profiles/r3ad_10kb_2000_s*.json): more, smaller batches in flight while the tall fills set each round's latency
+BEST_SLOTS_LONG = 8            # configs[2] / [3] through the work queue: 10 kb at 2000 ZMWs 4 / 5 / 8 / 10 / 12 slots 27.5 / 26.3 / 29.1-30.4 / 28.0 / 26.5 ZMWs/s (profiles/r3ad_*, r3af_*); mixed at 240 ZMWs 8 / 12 slots 7.19 / 5.09 (profiles/r3ag_*): more, smaller batches in flight while the tall fills set each round's latency
 SLOT_BYTES_PER_ZMW = 15 << 20  # measured band high-water per 2 kb / 10-pass ZMW in a slot (13.4 MB, exact regrow)
 HBM_MARGIN = 24 << 30          # device memory left to scratch, selection buffers and the runtime
 
@@ -270,7 +270,7 @@ def choose_slots(args, local):
     """Workspace slots: the measured best split, capped by the steps and by the HBM the slots' band pools
     need at their high-water mark (a 2 kb / 10-pass batch of 2000 ZMWs peaks near 27 GB)."""
     import torch
-    best = BEST_SLOTS_10KB if args.workload == "10kb" else BEST_SLOTS
+    best = BEST_SLOTS_LONG if args.workload in ("10kb", "mixed") else BEST_SLOTS
     want = args.streams or max(1, min(args.steps, best))
     if not torch.cuda.is_available():
         return want
