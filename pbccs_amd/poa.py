@@ -131,35 +131,36 @@ def poa_batch(zmw_reads, max_coverage=None, min_coverage=-1, engine=None):
     keys = np.zeros(max(1, len(enc)), dtype=np.int32)
     rc = np.zeros(max(1, len(enc)), dtype=np.int32)
     ext = np.zeros(max(4, 4 * len(enc)), dtype=np.int32)
-    ins = (_L.CPoaInput * max(1, n))()
-    outs = (_L.CPoaOutput * max(1, n))()
-    P = ctypes.POINTER
-    pbase, lbase = ptrs.ctypes.data, lens.ctypes.data
-    kbase, rbase, ebase = keys.ctypes.data, rc.ctypes.data, ext.ctypes.data
-    cb = ctypes.addressof(cbuf)
-    for z in range(n):
-        f = int(first[z])
-        ins[z].seqs = ctypes.cast(pbase + 8 * f, P(ctypes.c_char_p))
-        ins[z].lens = ctypes.cast(lbase + 4 * f, P(ctypes.c_int))
-        ins[z].n_reads = int(counts[z])
-        o = outs[z]
-        o.consensus = ctypes.cast(cb + int(cstart[z]), ctypes.c_char_p)
-        o.cap = int(zbases[z])
-        o.keys = ctypes.cast(kbase + 4 * f, P(ctypes.c_int))
-        o.rc = ctypes.cast(rbase + 4 * f, P(ctypes.c_int))
-        o.extents = ctypes.cast(ebase + 16 * f, P(ctypes.c_int))
+    # the per-ZMW structs filled column-wise through numpy views of their memory (one ctypes attribute store per
+    # field per ZMW was most of the marshalling time at thousands of ZMWs)
+    from .quiver import _struct_dtype
+    ins = np.zeros(max(1, n), dtype=_struct_dtype(_L.CPoaInput))
+    outs = np.zeros(max(1, n), dtype=_struct_dtype(_L.CPoaOutput))
+    if n:
+        f0 = first[:-1]
+        ins["seqs"][:n] = ptrs.ctypes.data + 8 * f0
+        ins["lens"][:n] = lens.ctypes.data + 4 * f0
+        ins["n_reads"][:n] = counts
+        outs["consensus"][:n] = ctypes.addressof(cbuf) + cstart[:-1]
+        outs["cap"][:n] = zbases
+        outs["keys"][:n] = keys.ctypes.data + 4 * f0
+        outs["rc"][:n] = rc.ctypes.data + 4 * f0
+        outs["extents"][:n] = ext.ctypes.data + 16 * f0
     mc = 2**62 if max_coverage is None else int(max_coverage)
-    _L.check(load().pbccs_poa_batch(eng._h, ins, n, mc, int(min_coverage), outs))
+    _L.check(load().pbccs_poa_batch(eng._h, ctypes.cast(ins.ctypes.data, ctypes.POINTER(_L.CPoaInput)), n, mc,
+                                    int(min_coverage), ctypes.cast(outs.ctypes.data, ctypes.POINTER(_L.CPoaOutput))))
     raw = cbuf.raw
+    firsts, cnts, nks = first.tolist(), counts.tolist(), outs["n_keys"][:n].tolist()
+    cs, lns = cstart.tolist(), outs["len"][:n].tolist()
+    keys_l, rc_l, ext_l = keys.tolist(), rc.tolist(), ext.tolist()
     res = []
     for z in range(n):
-        f, nr, nk = int(first[z]), int(counts[z]), outs[z].n_keys
-        e = ext[4 * f:4 * (f + nk)].reshape(-1, 4).tolist()
-        r_ = rc[f:f + nk].tolist()
-        res.append({"consensus": raw[int(cstart[z]):int(cstart[z]) + outs[z].len].decode(),
-                    "keys": keys[f:f + nr].tolist(),
-                    "summaries": [{"rc": bool(r_[k]), "read": (e[k][0], e[k][1]), "tpl": (e[k][2], e[k][3])}
-                                  for k in range(nk)]})
+        f, nr, nk = firsts[z], cnts[z], nks[z]
+        e0 = 4 * f
+        res.append({"consensus": raw[cs[z]:cs[z] + lns[z]].decode(),
+                    "keys": keys_l[f:f + nr],
+                    "summaries": [{"rc": bool(rc_l[f + k]), "read": (ext_l[e0 + 4 * k], ext_l[e0 + 4 * k + 1]),
+                                   "tpl": (ext_l[e0 + 4 * k + 2], ext_l[e0 + 4 * k + 3])} for k in range(nk)]})
     return res
 
 
