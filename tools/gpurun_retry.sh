@@ -7,6 +7,8 @@ for i in $(seq 1 ${RETRIES:-4}); do
   /usr/local/graft/bin/gpurun --timeout "$TO" -- "$@" > "$LOG" 2>&1
   grep -q "status=transient\|backing off" "$LOG" || break
   echo "[retry $i: transient]" >> "$LOG.retries"
-  sleep 45
+  # a back-off names its wait ("retry in Ns"): sleep that long (plus a margin), else 45 s
+  W=$(grep -o "retry in [0-9]*s" "$LOG" | tail -1 | grep -o "[0-9]*")
+  sleep $(( ${W:-30} + 15 ))
 done
 echo done >> "$LOG"
