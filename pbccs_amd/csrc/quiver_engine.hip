@@ -104,6 +104,9 @@ QuiverBatch::QuiverBatch(int device) : device_(device)
 {
     QHIP(hipSetDevice(device_));
     QHIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    QHIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    QHIP(hipEventCreateWithFlags(&evFork_, hipEventDisableTiming));
+    QHIP(hipEventCreateWithFlags(&evJoin_, hipEventDisableTiming));
     dScratchTop_.reserve(1, false);
     dOverflow_.reserve(1, false);
     dScratch_.reserve(1 << 20, false);
@@ -484,11 +487,6 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         // the coop lists (reads that were tall for k_qfill_grp) on the side stream, concurrently with the grouped
         // launch; both streams join before the status download
         const bool sideRun = !coop.empty() || !full.empty();
-        if (sideRun && !side_) {   // made on first use: most fine-grained scorers never have a tall read
-            QHIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-            QHIP(hipEventCreateWithFlags(&evFork_, hipEventDisableTiming));
-            QHIP(hipEventCreateWithFlags(&evJoin_, hipEventDisableTiming));
-        }
         if (sideRun) {
             QHIP(hipEventRecord(evFork_, stream_));   // after the uploads above
             QHIP(hipStreamWaitEvent(side_, evFork_, 0));
