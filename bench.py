@@ -211,19 +211,21 @@ def queue_workload(args, rank, world, eng, settings, seed0):
     n = args.steps * args.zmws_per_step
     if args.workload == "smrtcell":
         desc = (f"configs[4]: SMRT-cell mix of configs[1]-[3] (2 kb x 10, 10 kb x 8, 0.5-20 kb x 3-30 passes; "
-                f"one third each), {n} ZMWs in total over {world} GPU(s), dynamic pull queue")
+                f"one third each), {n} ZMWs in total over {world} GPU(s), dynamic pull queue; each rank generates "
+                f"only the chunks it pulls (synth.SmrtCell), inside the timed region")
         kw = None
     else:
         kw = workload_kw(args)
         desc = (f"configs[2]: synthetic 10000 bp insert, 8 full passes, {n} ZMWs per GPU" if args.workload == "10kb"
                 else f"configs[3]: synthetic 0.5-20 kb inserts, 3-30 passes, per-ZMW SNR U[4,20], {n} ZMWs per GPU")
     for w in range(args.warmup):
-        wz = synth.make_smrtcell(4, seed=seed0 + 1000 + w) if kw is None else \
+        wz = synth.SmrtCell(4, seed=seed0 + 1000 + w)[:] if kw is None else \
             synth.make_zmws(4, seed=seed0 + 1000 + w, **kw)
         pbccs_amd.polish_stream(wz, settings, eng)
     log(rank, "[bench] warmup done")
     if kw is None:
-        zs = synth.make_smrtcell(n, seed=args.seed + 3)   # the same cell on every rank; the queue splits it
+        # the same cell on every rank, generated lazily: a rank materialises only the chunks it pulls
+        zs = synth.SmrtCell(n, seed=args.seed + 3)
     else:
         zs = synth.make_zmws(n, seed=seed0, **kw)
     eng.kernel_stats(reset=True)
@@ -249,6 +251,12 @@ def queue_workload(args, rank, world, eng, settings, seed0):
         dist.barrier()
     local_time = time.perf_counter() - t0
     job_time = max_over_ranks(local_time, world)
+    if kw is None:   # host memory high-water of the ranks (the cell is generated per chunk; rank 0 holds the records)
+        import resource
+        rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20   # KiB -> GiB
+        qstats["host_rss_gb_rank0"] = round(rss, 3)
+        qstats["host_rss_gb_max"] = round(max_over_ranks(rss, world), 3)
+        qstats["gen_ms_max"] = round(max_over_ranks(qstats.get("gen_ms", 0.0), world), 1)
     if kw is None:   # rank 0 holds the whole cell's records; the count is the cell
         return job_time, local_time, (res or []), desc, "strong", n, qstats
     return job_time, local_time, res, desc + " (work queue; timed region includes the read upload)", "weak", \

@@ -420,7 +420,9 @@ int pbccs_poa_consensus(pbccs_engine* eng, const char* const* reads, const int* 
  * holds in pbccs_poa_batch and pbccs_sparse_poa_orient_and_add_read.  A NULL sequence with a positive
  * length or a negative length is PBCCS_EINVAL.  out[z].draft (optional, draft_cap bytes) receives the POA
  * consensus; a draft longer than its buffer sets draft_len and makes the call return PBCCS_ERANGE after
- * all outputs are written. */
+ * all outputs are written.  out[z].add_order (optional, n_subreads ints) receives the caller subread index of
+ * each AddRead call in the scorer's order -- FilterReads' stable order (Consensus.h:281, 451-453), which
+ * ZScores() and the ccs.bam zs tag follow -- padded with -1. */
 typedef struct {
     double snr[4];
     int n_subreads;
@@ -434,6 +436,7 @@ typedef struct {
     char* draft;
     int draft_cap;
     int draft_len;
+    int* add_order;   /* optional: AddRead order as caller subread indices, -1 padded (n_subreads ints) */
 } pbccs_ccs_output;
 
 int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long long max_poa_coverage,

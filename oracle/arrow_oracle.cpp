@@ -21,6 +21,7 @@
 //  restatement (same operation order, no FMA contraction: build with
 //  -ffp-contract=off), deliberately NOT sharing code with the HIP engine.
 // =============================================================================
+#include <array>
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -347,6 +348,24 @@ struct Recursor {
     Window tpl;
     ModelParams mp;
     double scoreDiff = 12.5;
+    // Diagnostics (orc_scorer_pass_log): per pass of the last FillAlphaBeta -- alpha?, used cells, tallest
+    // column, first column taller than 64 rows (-1: none), used cells of the columns before it.
+    mutable std::vector<std::array<long long, 5>> passLog;
+    void LogPass(bool alpha, const BandMatrix& m) const
+    {
+        long long used = 0, before = 0, firstTall = -1;
+        int mh = 0;
+        for (int j = 0; j < m.cols; ++j) {
+            const int h = std::max(0, m.ue[j] - m.ub[j]);
+            if (h > 64 && firstTall < 0) {
+                firstTall = j;
+                before = used;
+            }
+            used += h;
+            mh = std::max(mh, h);
+        }
+        passLog.push_back({alpha ? 1LL : 0LL, used, (long long)mh, firstTall, firstTall < 0 ? used : before});
+    }
 
     // RowRange + RangeGuide (:693-757).  RowRange's threshold (max - scoreDiff) lies below every
     // scaled cell, so it returns the used range unchanged; kept literal here.
@@ -618,23 +637,34 @@ struct Recursor {
     // FillAlphaBeta (:642-691); returns flip-flop count, throws AlphaBetaMismatch.
     int FillAlphaBeta(BandMatrix& a, BandMatrix& bm) const
     {
+        passLog.clear();
         FillAlpha(NullMatrix(), a);
+        LogPass(true, a);
         FillBeta(a, bm);
+        LogPass(false, bm);
         const int I = (int)read.size();
         const int J = tpl.Length();
         int flips = 0;
         const int maxSize = static_cast<int>(0.5 + kRebandFrac * (I + 1) * (J + 1));
         if (a.UsedEntries() >= maxSize || bm.UsedEntries() >= maxSize) {
             FillAlpha(bm, a);
+            LogPass(true, a);
             FillBeta(a, bm);
+            LogPass(false, bm);
             FillAlpha(bm, a);
+            LogPass(true, a);
             flips += 3;
         }
         double av = std::log(a.Get(I, J)) + a.LogProdAll();
         double bv = std::log(bm.Get(0, 0)) + bm.LogProdAll();
         while (std::fabs(av - bv) > kAlphaBetaTol && flips <= kMaxFlipFlops) {
-            if (flips % 2 == 0) FillAlpha(bm, a);
-            else FillBeta(a, bm);
+            if (flips % 2 == 0) {
+                FillAlpha(bm, a);
+                LogPass(true, a);
+            } else {
+                FillBeta(a, bm);
+                LogPass(false, bm);
+            }
             ++flips;
         }
         av = std::log(a.Get(I, J)) + a.LogProdAll();
@@ -1190,6 +1220,19 @@ void orc_context_params(const double* snr, double* out /* 8 x 4: match, stick, b
 
 }  // extern "C"
 
+// Diagnostics (test infrastructure): read r's last FillAlphaBeta, one row of 5 per pass (see Recursor::passLog).
+extern "C" int orc_scorer_pass_log(void* h, int r, long long* out, int cap)
+{
+    MultiReadScorer* s = static_cast<MultiReadScorer*>(h);
+    const ReadState& rs = s->reads.at(r);
+    if (!rs.scorer) return -1;
+    const auto& log = rs.scorer->rec.passLog;
+    const int n = (int)log.size();
+    for (int k = 0; k < n && k < cap; ++k)
+        for (int q = 0; q < 5; ++q) out[5 * k + q] = log[k][q];
+    return n;
+}
+
 // Diagnostics (test infrastructure): used-cell count and tallest column of read r's alpha and beta bands.
 extern "C" int orc_scorer_band_stats(void* h, int r, long long* aUsed, long long* bUsed, int* aMaxH, int* bMaxH)
 {
@@ -1212,6 +1255,37 @@ extern "C" int orc_scorer_band_stats(void* h, int r, long long* aUsed, long long
 
 // Diagnostics (test infrastructure): cells of read r's alpha band that are exactly zero, and cells whose
 // whole 64-row chunk (rows counted from each column's first used row) is zero.
+// Diagnostics (test infrastructure): zero structure of read r's alpha band for chunks of `chunk` rows: out[0] used
+// cells, out[1] exact zeros, out[2] cells of all-zero chunks, out[3] zeros before a column's first non-zero
+// cell, out[4] zeros after its last non-zero cell.
+extern "C" int orc_scorer_band_zero_profile(void* h, int r, int chunk, long long* out)
+{
+    MultiReadScorer* s = static_cast<MultiReadScorer*>(h);
+    const ReadState& rs = s->reads.at(r);
+    if (!rs.scorer) return -1;
+    const BandMatrix& m = rs.scorer->alpha;
+    for (int q = 0; q < 5; ++q) out[q] = 0;
+    for (int j = 0; j < m.cols; ++j) {
+        int first = -1, last = -1;
+        for (int i = m.ub[j]; i < m.ue[j]; ++i)
+            if (m.Get(i, j) != 0.0) {
+                if (first < 0) first = i;
+                last = i;
+            }
+        out[0] += std::max(0, m.ue[j] - m.ub[j]);
+        out[3] += first < 0 ? std::max(0, m.ue[j] - m.ub[j]) : first - m.ub[j];
+        out[4] += first < 0 ? 0 : m.ue[j] - 1 - last;
+        for (int c0 = m.ub[j]; c0 < m.ue[j]; c0 += chunk) {
+            const int c1 = std::min(c0 + chunk, m.ue[j]);
+            int z = 0;
+            for (int i = c0; i < c1; ++i) z += (m.Get(i, j) == 0.0);
+            out[1] += z;
+            if (z == c1 - c0) out[2] += z;
+        }
+    }
+    return 0;
+}
+
 extern "C" int orc_scorer_band_zeros(void* h, int r, long long* zeros, long long* zeroChunkCells)
 {
     MultiReadScorer* s = static_cast<MultiReadScorer*>(h);

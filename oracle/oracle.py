@@ -107,6 +107,16 @@ class Scorer:
         lib().orc_scorer_band_stats(self._h, r, ctypes.byref(au), ctypes.byref(bu), ctypes.byref(ah), ctypes.byref(bh))
         return au.value, bu.value, ah.value, bh.value
 
+    def pass_log(self, r):
+        """Diagnostics: read r's last FillAlphaBeta, per pass (alpha?, used cells, tallest column, first column
+        taller than 64 rows or -1, used cells before it)."""
+        buf = (ctypes.c_longlong * (5 * 16))()
+        f = lib().orc_scorer_pass_log
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
+        n = f(self._h, r, buf, 16)
+        return [tuple(buf[5 * k:5 * k + 5]) for k in range(max(0, min(n, 16)))]
+
     def score(self, mtype, start, base="-", fast_threshold=-1.7976931348623157e308):
         nb = b"" if mtype == DELETION else base.encode()
         return lib().orc_scorer_score(self._h, mtype, start, mutation_end(mtype, start), nb, fast_threshold)

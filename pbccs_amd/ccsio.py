@@ -147,8 +147,13 @@ def ccs_sam_record(movie, hole, result, snr):
     """
     name = f"{movie}/{hole}/ccs"
     qual = QVsToASCII(result["qvs"])
-    # zs: ZScores().second -- one entry per read the scorer took (inactive ones NaN), MultiReadMutationScorer.hpp:208-260
-    zs = [z for z, a in zip(result["zscores"], result["add_read_results"]) if a >= 0]
+    # zs: ZScores().second -- one entry per read the scorer took (inactive ones NaN), in AddRead order
+    # (MultiReadMutationScorer.hpp:208-260).  ccs_batch results index their per-read arrays by subread and carry
+    # that order ("add_order": FilterReads' stable sort, Consensus.h:281); polish results are in AddRead order.
+    if "add_order" in result:
+        zs = [result["zscores"][k] for k in result["add_order"]]
+    else:
+        zs = [z for z, a in zip(result["zscores"], result["add_read_results"]) if a >= 0]
     tags = [f"RG:Z:{read_group_id(movie)}", f"zm:i:{int(hole)}", f"np:i:{int(result['n_passes'])}",
             f"rq:i:{int(1000 * result['predicted_accuracy'])}",
             "sn:B:f," + ",".join(_f32(s) for s in snr),

@@ -1174,20 +1174,32 @@ struct ReplayRead {
     __device__ __forceinline__ int RB(int i) const { return (i >= 0 && i < I) ? coop::base_code(rd[i]) : 15; }
 };
 
-// the insertion chain over the first n (>= 1) rows of a 64-row chunk; lanes >= n are left unfinished
-__device__ __forceinline__ double replay_chain(double m, double k, double d, double carry, int n)
+// Rows per lane of the replay chain: the fill's 64-lane chain with R consecutive rows per lane and one DPP
+// hand-off per R rows (coop_chain.hpp insertion_chain_rows; 17.6 against 29.3 cycles per row at R = 4 / 1,
+// tools/ubench/chain_step.hip), each row in the reference's operation order.
+constexpr int kReplayRows = 4;
+
+// the insertion chain over the first n (>= 1) rows of a 64 R-row chunk; lanes holding only rows >= n are left
+// unfinished
+template <int R>
+__device__ __forceinline__ void replay_chain(const double (&m)[R], const double (&k)[R], const double (&d)[R],
+                                             double carry, int n, double (&x)[R])
 {
-    double x = 0.0, up = carry;
 #pragma unroll
-    for (int q = 0; q < 64; q += 8) {
+    for (int r = 0; r < R; ++r) x[r] = 0.0;
+    double up = carry;
+    const int phases = (n + R - 1) / R;   // lanes [0, phases) hold the rows below n
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            up = coop::shift_up<64>(x, up);
-            x = (m + up * k) + d;
+    for (int p = 0; p < 64; p += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            up = coop::shift_up<64>(x[R - 1], up);
+            x[0] = (m[0] + up * k[0]) + d[0];
+#pragma unroll
+            for (int r = 1; r < R; ++r) x[r] = (m[r] + x[r - 1] * k[r]) + d[r];
         }
-        if (q + 8 >= n) break;
+        if (p + 4 >= phases) break;
     }
-    return x;
 }
 
 __device__ __forceinline__ double lane63(double x)   // the chunk-to-chunk carry (wave-uniform)
@@ -1203,67 +1215,99 @@ __device__ __forceinline__ double wave_max_d(double x)
 }
 
 // Alpha column j (j >= 1) over its stored rows [b, e) from the scaled column j-1 (rows [pb, pe) at prev),
-// scaled into cur (top-down): coop_alpha's column step (fill_coop.hip) without the band-end logic.
+// scaled into cur (top-down): coop_alpha's column step (fill_coop.hip) without the band-end logic; lane l
+// takes rows i0 + l R .. i0 + l R + R - 1 of each 64 R-row chunk.
 __device__ void replay_alpha(const ReplayRead& X, int j, const double* prev, int pb, int pe, double* cur, int b, int e)
 {
+    constexpr int R = kReplayRows;
     const int lane = threadIdx.x & 63;
     const int curBase = X.TB(j - 1), nextBase = X.TB(j);
     const double* cp = X.ctx + X.TC(j - 1) * kCtxStride;
     const double* pp = X.ctx + (j >= 2 ? X.TC(j - 2) : kCtxZero) * kCtxStride;
     const double pMatch = pp[kM], pDel = pp[kD], cBranch = cp[kB], cStick3 = cp[kS3];
     double carry = 0.0, mx = 0.0;
-    for (int i0 = b; i0 < e; i0 += 64) {
-        const int i = i0 + lane;
-        const int rb = (i >= 1 && i <= X.I) ? X.RB(i - 1) : 15;
-        const double left = (i >= pb && i < pe) ? prev[i - pb] : 0.0;
-        const double diag = (i - 1 >= pb && i - 1 < pe) ? prev[i - 1 - pb] : 0.0;
-        const double mpe = diag * (rb == curBase ? X.prNot : X.prThird);
-        const double m = (i == 1 && j == 1) ? mpe : ((i != 1 && j != 1) ? mpe * pMatch : 0.0);
-        const double k = (i > 1) ? (rb == nextBase ? cBranch : cStick3) : 0.0;
-        const double d = (j > 1) ? left * pDel : 0.0;
-        const double x = replay_chain(m, k, d, carry, e - i0);
-        if (i < e) {
-            cur[i - b] = x;
-            mx = fmax(mx, x);
+    for (int i0 = b; i0 < e; i0 += 64 * R) {
+        const int ib = i0 + lane * R;
+        double pv[R + 1], m[R], k[R], d[R], x[R];
+#pragma unroll
+        for (int q = 0; q <= R; ++q) {
+            const int row = ib - 1 + q;
+            pv[q] = (row >= pb && row < pe) ? prev[row - pb] : 0.0;
         }
-        carry = lane63(x);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = ib + r;
+            const int rb = (i >= 1 && i <= X.I) ? X.RB(i - 1) : 15;
+            const double mpe = pv[r] * (rb == curBase ? X.prNot : X.prThird);
+            m[r] = (i == 1 && j == 1) ? mpe : ((i != 1 && j != 1) ? mpe * pMatch : 0.0);
+            k[r] = (i > 1) ? (rb == nextBase ? cBranch : cStick3) : 0.0;
+            d[r] = (j > 1) ? pv[r + 1] * pDel : 0.0;
+        }
+        replay_chain<R>(m, k, d, carry, e - i0, x);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (ib + r < e) {
+                cur[ib + r - b] = x[r];
+                mx = fmax(mx, x[r]);
+            }
+        carry = lane63(x[R - 1]);
     }
     mx = wave_max_d(mx);
-    if (mx != 0.0 && mx != 1.0)   // ScaledMatrix::FinishEditingColumn
-        for (int i = b + lane; i < e; i += 64) cur[i - b] = cur[i - b] / mx;
+    if (mx != 0.0 && mx != 1.0)   // ScaledMatrix::FinishEditingColumn, each row by the lane that stored it
+        for (int i0 = b; i0 < e; i0 += 64 * R)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int i = i0 + lane * R + r;
+                if (i < e) cur[i - b] = cur[i - b] / mx;
+            }
 }
 
 // Beta column j (0 < j < J) over its stored rows [b, e), bottom-up, from the scaled column j+1 (rows [pb, pe)
-// at nxt, stored bottom-up), scaled into cur (bottom-up): coop_beta's column step.
+// at nxt, stored bottom-up), scaled into cur (bottom-up): coop_beta's column step, R offsets per lane.
 __device__ void replay_beta(const ReplayRead& X, int j, const double* nxt, int pb, int pe, double* cur, int b, int e)
 {
+    constexpr int R = kReplayRows;
     const int lane = threadIdx.x & 63;
     const int nextBase = X.TB(j);
     const double* cp = X.ctx + X.TC(j - 1) * kCtxStride;
     const double cMatch = cp[kM], cDel = cp[kD], cBranch = cp[kB], cStick3 = cp[kS3];
     const int I = X.I, J = X.J;
     double carry = 0.0, mx = 0.0;
-    for (int o0 = 0; o0 < e - b; o0 += 64) {
-        const int off = o0 + lane;
-        const int i = e - 1 - off;
-        const int nb = X.RB(i);
-        const double left = (i >= pb && i < pe) ? nxt[pe - 1 - i] : 0.0;
-        const double diag = (i + 1 >= pb && i + 1 < pe) ? nxt[pe - 2 - i] : 0.0;
-        const bool same = nb == nextBase;
-        const double mpe = diag * (same ? X.prNot : X.prThird);
-        const double m = (i < I - 1) ? mpe * cMatch : ((i == I - 1 && j == J - 1) ? mpe : 0.0);
-        const double k = (i < I - 1 && i > 0) ? (same ? cBranch : cStick3) : 0.0;
-        const double d = (j < J - 1 && j > 0) ? left * cDel : 0.0;
-        const double x = replay_chain(m, k, d, carry, e - b - o0);
-        if (i >= b) {
-            cur[off] = x;
-            mx = fmax(mx, x);
+    for (int o0 = 0; o0 < e - b; o0 += 64 * R) {
+        const int ob = o0 + lane * R;
+        double pv[R + 1], m[R], k[R], d[R], x[R];
+#pragma unroll
+        for (int q = 0; q <= R; ++q) {   // rows e - ob - q: diag of offset q, left of offset q - 1
+            const int row = e - ob - q;
+            pv[q] = (row >= pb && row < pe) ? nxt[pe - 1 - row] : 0.0;
         }
-        carry = lane63(x);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = e - 1 - ob - r;
+            const int nb = X.RB(i);
+            const bool same = nb == nextBase;
+            const double mpe = pv[r] * (same ? X.prNot : X.prThird);
+            m[r] = (i < I - 1) ? mpe * cMatch : ((i == I - 1 && j == J - 1) ? mpe : 0.0);
+            k[r] = (i < I - 1 && i > 0) ? (same ? cBranch : cStick3) : 0.0;
+            d[r] = (j < J - 1 && j > 0) ? pv[r + 1] * cDel : 0.0;
+        }
+        replay_chain<R>(m, k, d, carry, e - b - o0, x);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (e - 1 - ob - r >= b) {
+                cur[ob + r] = x[r];
+                mx = fmax(mx, x[r]);
+            }
+        carry = lane63(x[R - 1]);
     }
     mx = wave_max_d(mx);
-    if (mx != 0.0 && mx != 1.0)
-        for (int off = lane; off < e - b; off += 64) cur[off] = cur[off] / mx;
+    if (mx != 0.0 && mx != 1.0)   // each offset by the lane that stored it
+        for (int o0 = 0; o0 < e - b; o0 += 64 * R)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int off = o0 + lane * R + r;
+                if (off < e - b) cur[off] = cur[off] / mx;
+            }
 }
 
 __global__ void __launch_bounds__(64) k_score_ckpt(DevBatch B, ScoreWork W, CkptWork C)

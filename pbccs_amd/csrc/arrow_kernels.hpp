@@ -85,6 +85,7 @@ struct CoopFill {
     size_t groupBytes = 0;   // coop_group_bytes(hcap, readWords, tplWords)
     bool prio = true;        // G = 64 waves at raised issue priority
     bool chainExit = true;   // G = 64 serial chain leaves a chunk early once its stop row is final
+    int rows = 1;            // G = 64: band rows per lane (1, 2 or 4; a chunk is 64 x rows rows); G = 16: 1
     int regrowSlackDiv = 16;   // regrow_bands: a re-homed region holds need + need / regrowSlackDiv + 64
     // In-kernel band growth: a read whose alpha/beta region overflows takes a larger region pair from
     // the pool's free top (valBump, in values; mapped up to valLimit), copies what it must keep, and
@@ -100,8 +101,13 @@ struct CoopFill {
     // colScratch, so no column is ever too tall.  nullptr: the column buffers are LDS only.
     double* colScratch = nullptr;
     int gRows = 0;
+    // diagnostics (PBCCS_FILL_PATHS=2): per listed read [6]: wall-clock start / end (100 MHz), shader cycles,
+    // cells, passes, columns
+    long long* trace = nullptr;
 };
 size_t coop_group_bytes(int hcap, int readWords, int tplWords);
+constexpr int kTallGroupLanes = 64;   // tall fills: lanes per read (one read per wavefront)
+constexpr int kTallRowsPerLane = 2;   // tall fills: band rows per lane (a 128-row chunk)
 void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* reads, int n, hipStream_t s);
 
 void launch_fill(const DevBatch& B, const FillScratch& F, const int* reads, int n, hipStream_t s);

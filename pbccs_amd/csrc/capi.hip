@@ -1757,6 +1757,7 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
         }
         for (int z = 0; z < n; ++z) {   // every per-read slot starts as "not added"
             for (int r = 0; r < in[z].n_subreads; ++r) {
+                if (out[z].add_order) out[z].add_order[r] = -1;
                 if (out[z].polish.add_read_results) out[z].polish.add_read_results[r] = -1;
                 if (out[z].polish.zscores) out[z].polish.zscores[r] = std::numeric_limits<double>::quiet_NaN();
             }
@@ -1786,7 +1787,8 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
         // and larger chunks keep both stages busier (2000-ZMW chunks measured 1544 ZMWs/s end to end against
         // 1384 for 1000 and 1066 for 500).
         const int slots = std::max(1, eng->concurrency);
-        // one round of a 1000-ZMW 2 kb slice: ~17.7 GB (the default two slices of a 2000-ZMW chunk)
+        // 40 GB over the slices (kPoaSlicesDefault = 3: 13.3 GB each).  One read round of a 2 kb slice costs
+        // ~17.7 MB per ZMW (17.7 GB for 1000 ZMWs), so a 2000-ZMW chunk's ~667-ZMW slices need ~11.8 GB
         const size_t kPoaPoolPerSlice = (40ull << 30) / (size_t)pbccs_engine::PoaSlices();
         for (poa::PoaRunner* r : eng->PoaRunners()) r->SetPoolBudget(kPoaPoolPerSlice);
         std::vector<std::vector<int>> liveLens(live.size());
@@ -1941,12 +1943,15 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
                 po = C.pout[q];
                 po.add_read_results = arrOut;
                 po.zscores = zsOut;
-                // polish position i is FilterReads' i-th read, i.e. caller subread order[z][i]
+                // polish position i is FilterReads' i-th read, i.e. caller subread order[z][i]; the scorer's reads
+                // (AddRead calls) are the positions with a result, in position order
+                int added = 0;
                 for (size_t i = 0; i < C.mapped[q].size(); ++i) {
                     const int k = order[z][i];
                     if (k < 0) continue;
                     if (arrOut) arrOut[k] = C.arr[q][i];
                     if (zsOut) zsOut[k] = C.zsc[q][i];
+                    if (out[z].add_order && C.arr[q][i] >= 0) out[z].add_order[added++] = k;
                 }
             }
         }

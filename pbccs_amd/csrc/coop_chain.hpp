@@ -1,5 +1,5 @@
 // pbccs_amd/csrc/coop_chain.hpp -- wavefront primitives of the cooperative band recursions, shared by the
-// fill (fill_coop.hip) and the checkpoint-replay scorer (score_ckpt.hip): nibble-packed bases, the gfx9 DPP
+// fill (fill_coop.hip) and the checkpoint-replay scorer (k_score_ckpt, arrow_kernels.hip): nibble-packed bases, the gfx9 DPP
 // shift / prefix-max / broadcast helpers of a G-lane group, and the in-column insertion chain
 // x_i = (m_i + x_{i-1} k_i) + d_i in the reference's operation order (SimpleRecursor.cpp:117-150).
 #pragma once
@@ -118,6 +118,55 @@ __device__ __forceinline__ double insertion_chain(double m, double k, double d, 
     return x;
 }
 
+// The chain over a chunk of G x R rows, R consecutive rows per lane (lane l holds rows l R .. l R + R - 1):
+// in phase p lane p takes its predecessor from lane p - 1 with one DPP hand-off and runs its R rows in
+// registers, so the dependent path per row is mul + add + add without a DPP move (tools/ubench/chain_step.hip,
+// 29.3 cycles per row with a hand-off per row, 17.6 / 15.6 with one per 4 / 8 rows).  Every
+// row keeps the reference's operation order.  After phase p lanes <= p hold their final values.  From
+// `firstLane` on (the first lane whose rows the reference loop may stop at; >= G: none) every kCheckPhases
+// phases `maybe_stop(x)` -- a conservative form of the loop's stop test over the final lanes -- may end the
+// chain early; the caller's exact test then finds the same stop row.  Blocks of phases below `startLane` are
+// skipped: the caller passes the first lane with a non-zero input when the carry is zero (every row before it
+// is exactly zero, and so is its predecessor), 0 otherwise -- the leading zero rows of tall bands, a quarter of
+// their cells at 2 kb (oracle), at 16-row granularity instead of whole chunks.
+// G < 64 (several reads per wavefront, one per G-lane group): the skip and the exit are wave decisions -- a
+// block is skipped when every active group's startLane passes it, the chain ends when every active group has a
+// final stop (a group that keeps running past its own stop recomputes its final lanes to the same values).
+template <int G, int R, class MaybeStop>
+__device__ __forceinline__ void insertion_chain_rows(const double (&m)[R], const double (&k)[R], const double (&d)[R],
+                                                     double carry, double (&x)[R], int firstLane, bool exitOn,
+                                                     int startLane, MaybeStop maybe_stop)
+{
+    constexpr int kCheckPhases = R >= 16 ? 1 : 16 / R;   // a check every 16 rows
+    double up = carry;   // lane 0's `up` stays the carry: DPP leaves it untouched
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = 0.0;
+    const int check0 = exitOn ? max(firstLane, 0) : G;
+#pragma unroll
+    for (int p = 0; p < G; p += kCheckPhases) {
+        if (G == 64 ? p + kCheckPhases <= startLane : __ballot(p + kCheckPhases > startLane) == 0)
+            continue;   // every lane of the block is exactly zero
+#pragma unroll
+        for (int u = 0; u < kCheckPhases; ++u) {
+            up = shift_up<G>(x[R - 1], up);
+            x[0] = (m[0] + up * k[0]) + d[0];
+#pragma unroll
+            for (int r = 1; r < R; ++r) x[r] = (m[r] + x[r - 1] * k[r]) + d[r];
+        }
+        const int last = p + kCheckPhases - 1;   // lanes <= last are final
+        if (G == 64) {
+            if (last >= check0 && last < G - 1) {
+                const unsigned long long st = maybe_stop(x) & ((2ull << last) - 1);
+                if (st) return;
+            }
+        } else if (last < G - 1 && __ballot(last >= check0) != 0) {
+            const unsigned long long sb = maybe_stop(x);   // cross-lane: every active lane takes part
+            const bool done = last >= check0 && (sb & ((2ull << last) - 1)) != 0;
+            if (__ballot(!done) == 0) return;
+        }
+    }
+}
+
 // G = 64 serial chain with an early exit: after step q, lanes <= q hold their final value.  From lane
 // `first` on (the first lane the reference loop may stop at; >= G: none in this chunk) the chain is checked
 // every 8 steps with `maybe_stop`, a conservative form of the loop's stop test (it never reports a lane the
@@ -127,16 +176,18 @@ __device__ __forceinline__ double insertion_chain(double m, double k, double d, 
 // tall column no longer pay the full 64 steps.
 template <class MaybeStop>
 __device__ __forceinline__ double insertion_chain64_exit(double m, double k, double d, double carry, int first,
-                                                         MaybeStop maybe_stop)
+                                                         MaybeStop maybe_stop, int startLane = 0)
 {
     double x = 0.0, up = carry;
     int q = 0;
     const int check0 = max(first, 0) + 3;   // first check: a few rows past the first possible stop
-    if (check0 < 63) {
+    if (check0 < 63 || startLane >= 8) {
         // fully unrolled like the check-free path below (a rolled block loop measured 4% slower end to end,
         // profiles/r2h17_code_size_ab): the checks sit at fixed positions and only their branch is dynamic
+        // (blocks below startLane: all-zero rows, see insertion_chain_rows)
 #pragma unroll
         for (q = 0; q < 64; q += 8) {
+            if (q + 8 <= startLane) continue;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 up = shift_up<64>(x, up);

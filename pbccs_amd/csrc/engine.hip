@@ -34,36 +34,14 @@ constexpr int kCoopTallRows = 1024;           // LDS column rows of the first 64
 constexpr size_t kCoopLdsBytes = 60 * 1024;    // LDS planning budget of a fill block
 // LDS column rows of the hybrid path (the rest of a column in global memory).  A tall 10 kb band is at most
 // ~1500 rows; every LDS byte a wave holds beyond that only keeps other tall waves off the CU (at the 60 KB
-// budget two fit a CU, at ~35 KB four).  PBCCS_HYBRID_ROWS overrides it (A/B).
-constexpr int kHybridRowsDefault = 1536;
-// A refill on the 16-lane path whose last fill had a column of more than this many rows (of the path's 64)
-// starts on the tall paths: a read that goes tall there is only re-run after the whole 16-lane launch ends,
-// one more fill latency on its batch's round.  PBCCS_NEAR_TALL overrides it (0: off).
-constexpr int kNearTallDefault = 0;
-int near_tall()
-{
-    static const int r = std::getenv("PBCCS_NEAR_TALL") ? std::max(0, std::atoi(std::getenv("PBCCS_NEAR_TALL")))
-                                                       : kNearTallDefault;
-    return r;
-}
-int hybrid_rows()
-{
-    static const int r = std::getenv("PBCCS_HYBRID_ROWS") ? std::max(64, std::atoi(std::getenv("PBCCS_HYBRID_ROWS")) / 64 * 64)
-                                                         : kHybridRowsDefault;
-    return r;
-}
+// budget two fit a CU, at ~35 KB four).
+constexpr int kHybridRows = 1536;
 constexpr size_t kHeadroomMargin = 24ull << 30;   // device bytes band-growth headroom leaves free
 // First region of a read that moves to the tall paths, as a fraction 1 / kTallFirstDiv of its (I+1)(J+1)
 // matrix.  Exploded bands at 2 kb hold 0.8-21% of it per matrix (oracle, mean 9.9%); a read that outgrows
 // its region re-runs that pass into an exact one (fill_coop.hip regrow_bands), so the first region only
 // trades the memory left behind (all of it, for the reads that outgrow it) against one extra pass.
-constexpr long long kTallFirstDivDefault = 25;
-long long tall_first_div()   // PBCCS_TALL_FIRST_DIV overrides (A/B)
-{
-    static const long long d = std::getenv("PBCCS_TALL_FIRST_DIV") ? std::max(1, std::atoi(std::getenv("PBCCS_TALL_FIRST_DIV")))
-                                                                  : kTallFirstDivDefault;
-    return d;
-}
+constexpr long long kTallFirstDiv = 25;
 // Checkpointed bands: tall bands of long windows keep every K-th column's values only;
 // the scorer replays the rest.  At 10 kb a tall read's two bands are ~0.2 GB in full.
 constexpr int kCkptDefaultK = 8;
@@ -542,7 +520,7 @@ bool ArrowBatch::Relayout(const std::vector<int>& list)
         long long cap;
         if (h.filled && m > 0) cap = m + m / 8 + 64;
         else if (h.fillPath == 2 || h.fillPath == 3)
-            cap = ((long long)h.seq.size() + 1) * (h.te - h.ts + 1) / tall_first_div() / std::max(1, h.ckpt) + 64;
+            cap = ((long long)h.seq.size() + 1) * (h.te - h.ts + 1) / kTallFirstDiv / std::max(1, h.ckpt) + 64;
         else cap = (long long)h.colCap * initialBandHeight_;
         h.valCap = cap;
         h.valA = valTop_;
@@ -707,7 +685,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             // checkpointed: every K-th column plus the kept tails (the next launch sets h.ckpt)
             const bool ck = ckptAll_ > 0 || (ckptK_ > 0 && J >= ckptMinLen_);
             const long long K = ck ? std::max(ckptAll_, ckptK_) : 1;
-            const long long want = (I + 1) * (J + 1) / tall_first_div() / K + (ck ? 2 * (kCkptTail + 1) * (I + 1) : 0) + 64;
+            const long long want = (I + 1) * (J + 1) / kTallFirstDiv / K + (ck ? 2 * (kCkptTail + 1) * (I + 1) : 0) + 64;
             if (want > h.valCap) {
                 h.valCap = want;
                 h.valA = valTop_;
@@ -718,14 +696,6 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         }
         return q;
     };
-    if (near_tall() > 0)
-        for (int r : readsIn) {
-            HRead& h = reads_[r];
-            if (h.fillPath == 1 && h.filled && h.maxH > near_tall()) {
-                promote(r, 1);
-                counters_.nearTall += 1;
-            }
-        }
     Relayout(readsIn);
     std::vector<int> todo[kPaths], serial, done;
     for (int r : readsIn) {
@@ -740,21 +710,31 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     // Tall bands run on 64 lanes (one read per wavefront).  16-lane groups for them (4x fewer VALU issue
     // slots per chain step) measured 1290 against 2480 ZMWs/s and were removed: the tall reads are each
     // round's critical path and 16-row chunks pay the per-chunk band logic 4x as often.
+    // Tall paths: lanes per read (PBCCS_TALL_G: 16 = four reads per wavefront, 64 = one) and rows per lane
+    // (PBCCS_TALL_ROWS); a column buffer holds whole chunks of G x rows rows.  Four 16-lane reads share an 80 KB
+    // block (two per CU), a 64-lane read has a 60 KB one.
+    static const int tallG = env_int("PBCCS_TALL_G", kTallGroupLanes) == 16 ? 16 : 64;
+    static const int tallRows = env_int("PBCCS_TALL_ROWS", tallG == 16 ? 4 : kTallRowsPerLane);
+    const long long chunk = (long long)tallG * tallRows;
+    const long long tallGroupLds = tallG == 16 ? 20 * 1024 : (long long)kCoopLdsBytes;
+    auto full_rows = [&](int maxI) { return ((long long)maxI + chunk) / chunk * chunk; };   // >= I + 1 rows
     auto rows_for = [&](int p, int maxI, int w) -> int {
         if (p == 0) return 0;
         if (p == 1) return 4 * coop_group_bytes(kCoopNarrowRows, w, 0) <= kCoopLdsBytes ? kCoopNarrowRows : 0;
-        const long long room = ((long long)kCoopLdsBytes - (long long)coop_group_bytes(0, w, 0)) / 16 / 64 * 64;
-        const long long full = (maxI + 64) / 64 * 64;   // a column never exceeds I + 1 rows
+        const long long room = (tallGroupLds - (long long)coop_group_bytes(0, w, 0)) / 16 / 64 * 64;
+        const long long full = full_rows(maxI);   // a column never exceeds I + 1 rows
         if (p == 2) {   // LDS only
             const long long want = std::min<long long>(kCoopTallRows, full);
             return room >= want ? (int)want : 0;
         }
-        // hybrid: as many LDS rows as fit, up to hybrid_rows() (the rest of a column goes to global memory)
-        const long long want = std::min(std::min(full, room), (long long)hybrid_rows());
+        // hybrid: as many LDS rows as fit, up to kHybridRows (the rest of a column goes to global memory)
+        const long long want = std::min(std::min(full, room), (long long)kHybridRows);
         return want >= 64 ? (int)want : 0;
     };
     // PBCCS_FILL_PATHS=1: one stderr line per launch set (reads per path, wall ms, reads re-routed / regrown)
     static const bool pathTrace = std::getenv("PBCCS_FILL_PATHS") != nullptr;
+    // PBCCS_FILL_PATHS=2: also per launch the slowest read (its wall ms, cycles per cell, cells, passes)
+    static const bool pathTrace2 = pathTrace && std::getenv("PBCCS_FILL_PATHS")[0] == '2';
     for (int attempt = 0;; ++attempt) {
         // route reads whose buffers do not fit this path's LDS budget to the next path
         for (int p = 0; p < kPaths; ++p) {
@@ -776,22 +756,17 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         // of the typical reads at 2 kb end after alpha + beta (0 flip-flops), the rest run the flip-flop loop
         // (oracle: 101 / 110 of 211) -- so reads with flip-flops last time come first, then the others, each
         // group by window length (similar lengths share a wave; LDS is sized by the launch's longest).
-        // PBCCS_FLIP_SORT=0: length only (A/B).
-        static const bool flipSort = !(std::getenv("PBCCS_FLIP_SORT") && std::strcmp(std::getenv("PBCCS_FLIP_SORT"), "0") == 0);
-        auto quick = [&](int x) { return flipSort && reads_[x].filled && reads_[x].flips == 0 ? 1 : 0; };
+        auto quick = [&](int x) { return reads_[x].filled && reads_[x].flips == 0 ? 1 : 0; };
         // Within a flip group, reads whose last band averaged more than 16 rows per column (two 16-row chunks in
         // many columns) come first (+1.4%).  The tall paths' reads go by their last band size, largest first:
-        // the longest fills start first (+2.0%; profiles/r2h10_sort_ab/).  PBCCS_HEIGHT_SORT=0 / PBCCS_TALL_LPT=0
-        // turn them off (A/B).
-        static const bool heightSort = !(std::getenv("PBCCS_HEIGHT_SORT") && std::strcmp(std::getenv("PBCCS_HEIGHT_SORT"), "0") == 0);
-        static const bool tallLpt = !(std::getenv("PBCCS_TALL_LPT") && std::strcmp(std::getenv("PBCCS_TALL_LPT"), "0") == 0);
+        // the longest fills start first (+2.0%; profiles/r2h10_sort_ab/).
         auto high = [&](int x) {
             const HRead& h = reads_[x];
-            return heightSort && h.filled && std::max(h.usedA, h.usedB) > 16LL * (h.te - h.ts + 1) ? 0 : 1;
+            return h.filled && std::max(h.usedA, h.usedB) > 16LL * (h.te - h.ts + 1) ? 0 : 1;
         };
         for (int p = 0; p < kPaths; ++p) {
             auto& v = todo[p];
-            if (p >= 2 && tallLpt) {
+            if (p >= 2) {
                 std::stable_sort(v.begin(), v.end(), [&](int x, int y) {
                     return std::max(reads_[x].usedA, reads_[x].usedB) > std::max(reads_[y].usedA, reads_[y].usedB);
                 });
@@ -879,20 +854,15 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.readWords = (maxI + 7) / 8;
             F.tplWords = (maxJ + 8) / 8;
             F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
-            const int G = p == 1 ? 16 : 64;
+            const int G = p == 1 ? 16 : tallG;
+            F.rows = p == 1 ? 1 : tallRows;
             F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);
-            const int full = (maxI + 64) / 64 * 64;
+            const int full = (int)full_rows(maxI);
             if (p == 3 && full > F.hcap) {   // hybrid: column rows past the LDS buffer, two buffers per read
                 F.gRows = full - F.hcap;
                 dColScratch_.reserve((size_t)n * 2 * F.gRows, false);
                 F.colScratch = dColScratch_.ptr;
             }
-            static const char* prioEnv = std::getenv("PBCCS_TALL_PRIO");      // "0" disables
-            F.prio = !(prioEnv && std::strcmp(prioEnv, "0") == 0);
-            static const char* exitEnv = std::getenv("PBCCS_CHAIN_EXIT");   // "0" disables (A/B)
-            F.chainExit = !(exitEnv && std::strcmp(exitEnv, "0") == 0);
-            static const int slackDiv = std::getenv("PBCCS_REGROW_SLACK_DIV") ? std::atoi(std::getenv("PBCCS_REGROW_SLACK_DIV")) : 16;
-            F.regrowSlackDiv = slackDiv;
             if (grow) {
                 F.valBump = dBump_.ptr;
                 F.valLimit = valLimit;
@@ -902,6 +872,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             }
             const int* lp = dList_.ptr + off;
             const hipStream_t st = p <= 1 ? stream_ : stream2_;
+            if (pathTrace2) {   // on the launch's own stream (the tall ones run beside stream_)
+                dCoopTrace_[p].reserve((size_t)6 * n, false);
+                PBCCS_HIP(hipMemsetAsync(dCoopTrace_[p].ptr, 0, sizeof(long long) * 6 * n, st));
+                F.trace = dCoopTrace_[p].ptr;
+            }
             Timed(p == 1 ? kKFill : kKFillTall, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
             PBCCS_HIP(hipGetLastError());
             counters_.fillLaunches += 1;
@@ -949,6 +924,29 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                          (void*)this, attempt, todo[0].size(), todo[1].size(), todo[2].size(), todo[3].size(),
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tLaunch).count(),
                          nt, no);
+            for (int p = 1; pathTrace2 && p < kPaths; ++p) {
+                const size_t n = todo[p].size();
+                if (n == 0) continue;
+                std::vector<long long> tr;
+                download(tr, dCoopTrace_[p], 6 * n, stream_);
+                PBCCS_HIP(hipStreamSynchronize(stream_));
+                long long t0 = LLONG_MAX, t1 = 0;
+                size_t slow = 0;
+                double sumCells = 0, sumCyc = 0;
+                for (size_t t = 0; t < n; ++t) {
+                    if (tr[6 * t + 1] <= 0) continue;
+                    t0 = std::min(t0, tr[6 * t]);
+                    t1 = std::max(t1, tr[6 * t + 1]);
+                    if (tr[6 * t + 1] - tr[6 * t] > tr[6 * slow + 1] - tr[6 * slow]) slow = t;
+                    sumCells += (double)tr[6 * t + 3];
+                    sumCyc += (double)tr[6 * t + 2];
+                }
+                const long long* s = &tr[6 * slow];
+                std::fprintf(stderr, "[fillread] path=%d n=%zu span=%.1fms slowest: %.1fms %.1f cyc/cell cells=%lld "
+                             "passes=%lld cols=%lld; all: %.1f cyc/cell\n", p, n, (t1 - t0) / 1e5, (s[1] - s[0]) / 1e5,
+                             s[3] ? (double)s[2] / (double)s[3] : 0.0, s[3], s[4], s[5],
+                             sumCells > 0 ? sumCyc / sumCells : 0.0);
+            }
         }
         std::vector<int> next[kPaths];
         for (int p = 0; p < kPaths; ++p) {

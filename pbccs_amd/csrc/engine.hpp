@@ -128,7 +128,6 @@ struct Counters {   // work counters for the roofline report (bench.py)
     long long scoreTasks = 0, scoreLaunches = 0;
     long long mutations = 0;
     long long bandGrowths = 0;   // fill launch sets in which some read grew its band region in-kernel
-    long long nearTall = 0;      // refills sent to the tall paths up front (PBCCS_NEAR_TALL)
     long long relayouts = 0;     // fills that laid the band pool out afresh (ArrowBatch::Relayout)
     // band value pool of the batch, bytes (maxima over the batches merged into an engine's counters):
     // bump top (everything ever handed out), current regions (2 x capacity per read), cells in use
@@ -301,6 +300,7 @@ private:
     DevVec<long long> dSelBase_;          // phased scoring: per-item ranges of the surviving mutations
     DevVec<int> dNSel_;
     DevVec<double> dColScratch_;          // the hybrid fill path's column rows past its LDS buffers
+    DevVec<long long> dCoopTrace_[4];     // PBCCS_FILL_PATHS=2 diagnostics: per-read fill timing, per path
     DevVec<unsigned long long> dBump_;   // in-kernel band growth: the value pool's free top
     std::unique_ptr<Workspace> ownWs_;
     Workspace* ws_;

@@ -22,6 +22,7 @@
 #include "arrow_kernels.hpp"
 #include "coop_chain.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 
@@ -174,9 +175,12 @@ __device__ double finish_log_scales(const Task<G>& T, const Band& m, int J)
 }
 
 // ---- FillAlpha (SimpleRecursor.cpp:60-181) --------------------------------------------------------
-template <int G>
+// A column's rows run in chunks of CH = G x R rows, R consecutive rows per lane (lane l: rows i0 + l R ..
+// i0 + l R + R - 1); R > 1 hands the chain on once per R rows (insertion_chain_rows).
+template <int G, int R>
 __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO)
 {
+    constexpr int CH = G * R;
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
     PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1};
@@ -241,48 +245,115 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         const double pMatch = pp[kM], pDel = pp[kD];
         const double cBranch = cp[kB], cStick3 = cp[kS3];
         const int b = hb;
-        double mx = 0.0, aLast = 0.0;
+        double mx = 0.0, aLast[R];
         int e = b, nc = 0;
         if (b < I) {
             double carry = 0.0;
-            for (int i0 = b;; i0 += G) {
-                if ((nc + 1) * G > T.rowsCap) { out.tall = true; return out; }
-                const int i = i0 + lane;
-                const int rb = (i >= 1 && i <= I) ? nib(T.rdW, i - 1) : 15;
-                const double left = (i >= pb && i < pe) ? T.cget(prev, i - pb) : 0.0;
-                const double diag = (i - 1 >= pb && i - 1 < pe) ? T.cget(prev, i - 1 - pb) : 0.0;
-                const double mpe = diag * (rb == curBase ? T.prNot : T.prThird);
-                const double m = (i == 1 && j == 1) ? mpe : ((i != 1 && j != 1) ? mpe * pMatch : 0.0);
-                const double k = (i > 1) ? (rb == nextBase ? cBranch : cStick3) : 0.0;
-                const double d = (j > 1) ? left * pDel : 0.0;
-                double x = 0.0;
-                // a chunk whose inputs are all exactly zero stays zero: skip its chain (bit-exact; common
-                // in the far rows of tall bands)
-                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0) {
-                    if (G == 64 && T.chainExit) {
-                        auto maybe_stop = [&](double xv) {   // x < pm * invLow implies x < pm / sdn
-                            const double pmv = fmax(mx, prefix_max<G>(xv));
-                            return T.g.bits((i + 1 >= I) || (xv < pmv * T.sdnInvLow && i + 1 >= reqEnd));
-                        };
-                        x = insertion_chain64_exit(m, k, d, carry, min(reqEnd, I) - 1 - i0, maybe_stop);
-                    } else {
-                        x = insertion_chain<G>(m, k, d, carry);
+            for (int i0 = b;; i0 += CH) {
+                if ((nc + 1) * CH > T.rowsCap) { out.tall = true; return out; }
+                const int ib = i0 + lane * R;   // the lane's first row of the chunk
+                double m[R], k[R], d[R], x[R];
+                {
+                    double pv[R + 1];   // scaled previous column at rows ib - 1 .. ib + R - 1 (diag, left)
+#pragma unroll
+                    for (int q = 0; q <= R; ++q) {
+                        const int row = ib - 1 + q;
+                        pv[q] = (row >= pb && row < pe) ? T.cget(prev, row - pb) : 0.0;
+                    }
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int i = ib + r;
+                        const int rb = (i >= 1 && i <= I) ? nib(T.rdW, i - 1) : 15;
+                        const double mpe = pv[r] * (rb == curBase ? T.prNot : T.prThird);
+                        m[r] = (i == 1 && j == 1) ? mpe : ((i != 1 && j != 1) ? mpe * pMatch : 0.0);
+                        k[r] = (i > 1) ? (rb == nextBase ? cBranch : cStick3) : 0.0;
+                        d[r] = (j > 1) ? pv[r + 1] * pDel : 0.0;
+                        x[r] = 0.0;
                     }
                 }
-                const double pm = fmax(mx, prefix_max<G>(x));
-                const double thr = pm / T.sdn;
-                const bool cont = (i + 1 < I) && (x >= thr || i + 1 < reqEnd);
-                const unsigned long long stop = T.g.bits(!cont);
+                // a chunk whose inputs are all exactly zero stays zero: skip its chain (bit-exact; common
+                // in the far rows of tall bands)
+                bool nz = false;
+#pragma unroll
+                for (int r = 0; r < R; ++r) nz = nz || m[r] != 0.0 || d[r] != 0.0;
+                const unsigned long long nzb = T.g.bits(nz);
+                if (carry != 0.0 || nzb != 0) {
+                    // the leading all-zero lanes of a chunk entered with a zero carry are exactly zero
+                    const int startLane = ((G == 64 || R > 1) && carry == 0.0) ? __ffsll((long long)nzb) - 1 : 0;
+                    if constexpr (R == 1) {
+                        const int i = ib;
+                        if (G == 64 && T.chainExit) {
+                            auto maybe_stop = [&](double xv) {   // x < pm * invLow implies x < pm / sdn
+                                const double pmv = fmax(mx, prefix_max<G>(xv));
+                                return T.g.bits((i + 1 >= I) || (xv < pmv * T.sdnInvLow && i + 1 >= reqEnd));
+                            };
+                            x[0] = insertion_chain64_exit(m[0], k[0], d[0], carry, min(reqEnd, I) - 1 - i0, maybe_stop,
+                                                          startLane);
+                        } else {
+                            x[0] = insertion_chain<G>(m[0], k[0], d[0], carry);
+                        }
+                    } else {
+                        auto maybe_stop = [&](const double (&xv)[R]) {   // x < pm * invLow implies x < pm / sdn
+                            double lp = xv[0];
+#pragma unroll
+                            for (int r = 1; r < R; ++r) lp = fmax(lp, xv[r]);
+                            const double ex = shift_up<G>(prefix_max<G>(lp), 0.0);   // max over the lanes before
+                            double run = fmax(mx, ex);
+                            bool st = false;
+#pragma unroll
+                            for (int r = 0; r < R; ++r) {
+                                run = fmax(run, xv[r]);
+                                const int i = ib + r;
+                                st = st || (i + 1 >= I) || (xv[r] < run * T.sdnInvLow && i + 1 >= reqEnd);
+                            }
+                            return T.g.bits(st);
+                        };
+                        const int firstRow = min(reqEnd, I) - 1 - i0;   // the first chunk row the loop may stop at
+                        insertion_chain_rows<G, R>(m, k, d, carry, x, firstRow < 0 ? 0 : firstRow / R, T.chainExit,
+                                                   startLane, maybe_stop);
+                    }
+                }
+                // the reference loop's running maximum at each row, its threshold and continue test (:110-112)
+                double pmR[R];
+                if constexpr (R == 1) {
+                    pmR[0] = fmax(mx, prefix_max<G>(x[0]));
+                } else {
+                    double lp = x[0];
+#pragma unroll
+                    for (int r = 1; r < R; ++r) lp = fmax(lp, x[r]);
+                    double run = fmax(mx, shift_up<G>(prefix_max<G>(lp), 0.0));
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        run = fmax(run, x[r]);
+                        pmR[r] = run;
+                    }
+                }
+                int fs = R;   // the lane's first row where the loop stops
+#pragma unroll
+                for (int r = R - 1; r >= 0; --r) {
+                    const int i = ib + r;
+                    const double thr = pmR[r] / T.sdn;
+                    const bool cont = (i + 1 < I) && (x[r] >= thr || i + 1 < reqEnd);
+                    if (!cont) fs = r;
+                }
+                const unsigned long long stop = T.g.bits(fs < R);
                 const int lastLane = stop ? (__ffsll((long long)stop) - 1) : (G - 1);
-                mx = T.g.bcast(pm, lastLane);
+                double pmAt = pmR[R - 1];
+#pragma unroll
+                for (int r = 0; r < R - 1; ++r)
+                    if (r == fs) pmAt = pmR[r];
+                mx = T.g.bcast(pmAt, lastLane);
                 ++nc;
                 if (stop) {
-                    e = i0 + lastLane + 1;
-                    aLast = x;
+                    const int rs = R == 1 ? 0 : T.g.bcast(fs, lastLane);
+                    e = i0 + lastLane * R + rs + 1;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) aLast[r] = x[r];
                     break;
                 }
-                T.cset(cur, (nc - 1) * G + lane, x);
-                carry = T.g.bcast_last(x);
+#pragma unroll
+                for (int r = 0; r < R; ++r) T.cset(cur, (nc - 1) * CH + lane * R + r, x[r]);
+                carry = T.g.bcast_last(x[R - 1]);
             }
         }
         const bool keep = T.ckK == 0 || ckpt_col_a(j, J, T.ckK);
@@ -300,17 +371,23 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         // two chunks per iteration: their divisions and LDS round trips overlap (tall columns have many chunks)
 #pragma unroll 2
         for (int c = 0; c < nc; ++c) {
-            const int kk = c * G + lane;
-            const bool ok = b + kk < e;
-            const double x = (c == nc - 1) ? aLast : T.cget(cur, kk);
-            const double v = scale ? x / mx : x;
-            if (ok) {
-                T.cset(cur, kk, v);
-                if (store && stored + kk < a.cap) a.V(stored + kk) = v;
+            int fh = R;   // the lane's first row at or above the scaled threshold
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int kk = c * CH + lane * R + r;
+                const bool ok = b + kk < e;
+                const double x = (c == nc - 1) ? aLast[r] : T.cget(cur, kk);
+                const double v = scale ? x / mx : x;
+                if (ok) {
+                    T.cset(cur, kk, v);
+                    if (store && stored + kk < a.cap) a.V(stored + kk) = v;
+                }
+                if (fh == R && ok && !(v < thrF)) fh = r;
             }
-            const unsigned long long hit = T.g.bits(ok && !(v < thrF));
+            const unsigned long long hit = T.g.bits(fh < R);
             if (!found && hit) {
-                nhb = b + c * G + __ffsll((long long)hit) - 1;
+                const int hl = __ffsll((long long)hit) - 1;
+                nhb = b + c * CH + hl * R + (R == 1 ? 0 : T.g.bcast(fh, hl));
                 found = true;
             }
         }
@@ -328,7 +405,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         if ((jb == G - 1 || j == J - 1) && !counting && lane <= jb) a.L(j - jb + lane) = (myF != 1.0) ? log(myF) : 0.0;
         used += e - b;
         stored += add;
-        col_fence(T.gcol && nc * G > T.hcap);   // the next column's lanes read rows this column's lanes wrote
+        col_fence(T.gcol && nc * CH > T.hcap);   // the next column's lanes read rows this column's lanes wrote
         prev ^= 1;
         cur ^= 1;
         pb = b;
@@ -364,9 +441,10 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
 }
 
 // ---- FillBeta (SimpleRecursor.cpp:183-296); rows run bottom-up, stored bottom-up --------------------
-template <int G>
+template <int G, int R>
 __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO)
 {
+    constexpr int CH = G * R;
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
     PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1};
@@ -425,50 +503,114 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         const double* cp = T.ctx + curCtx * kCtxStride;
         const double cMatch = cp[kM], cDel = cp[kD], cBranch = cp[kB], cStick3 = cp[kS3];
         const int e = he;
-        double mx = 0.0, aLast = 0.0;
+        double mx = 0.0, aLast[R];
         int b = e, nc = 0;
         if (e - 1 > 0) {
             double carry = 0.0;
             for (int c = 0;; ++c) {
-                if ((c + 1) * G > T.rowsCap) { out.tall = true; return out; }
-                const int off = c * G + lane;
-                const int i = e - 1 - off;
-                const int nb = (i >= 0 && i < I) ? nib(T.rdW, i) : 15;
-                const double left = (i >= pb && i < pe) ? T.cget(nxt, pe - 1 - i) : 0.0;
-                const double diag = (i + 1 >= pb && i + 1 < pe) ? T.cget(nxt, pe - 2 - i) : 0.0;
-                const bool same = nb == nextBase;
-                const double mpe = diag * (same ? T.prNot : T.prThird);
-                const double m = (i < I - 1) ? mpe * cMatch : ((i == I - 1 && j == J - 1) ? mpe : 0.0);
-                const double k = (i < I - 1 && i > 0) ? (same ? cBranch : cStick3) : 0.0;
-                const double d = (j < J - 1 && j > 0) ? left * cDel : 0.0;
-                double x = 0.0;
-                // a chunk whose inputs are all exactly zero stays zero: skip its chain (bit-exact; common
-                // in the far rows of tall bands)
-                if (carry != 0.0 || T.g.bits(m != 0.0 || d != 0.0) != 0) {
-                    if (G == 64 && T.chainExit) {
-                        auto maybe_stop = [&](double xv) {   // x < pm * invLow implies x < pm / sdn
-                            const double pmv = fmax(mx, prefix_max<G>(xv));
-                            return T.g.bits((i - 1 <= 0) || (xv < pmv * T.sdnInvLow && i - 1 < reqBegin));
-                        };
-                        x = insertion_chain64_exit(m, k, d, carry, e - 1 - max(1, reqBegin) - c * G, maybe_stop);
-                    } else {
-                        x = insertion_chain<G>(m, k, d, carry);
+                if ((c + 1) * CH > T.rowsCap) { out.tall = true; return out; }
+                const int ob = c * CH + lane * R;   // the lane's first offset (row e - 1 - ob)
+                double m[R], k[R], d[R], x[R];
+                {
+                    double pv[R + 1];   // scaled next column at rows e - ob .. e - ob - R (diag, left)
+#pragma unroll
+                    for (int q = 0; q <= R; ++q) {
+                        const int row = e - ob - q;
+                        pv[q] = (row >= pb && row < pe) ? T.cget(nxt, pe - 1 - row) : 0.0;
+                    }
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int i = e - 1 - ob - r;
+                        const int nb = (i >= 0 && i < I) ? nib(T.rdW, i) : 15;
+                        const bool same = nb == nextBase;
+                        const double mpe = pv[r] * (same ? T.prNot : T.prThird);
+                        m[r] = (i < I - 1) ? mpe * cMatch : ((i == I - 1 && j == J - 1) ? mpe : 0.0);
+                        k[r] = (i < I - 1 && i > 0) ? (same ? cBranch : cStick3) : 0.0;
+                        d[r] = (j < J - 1 && j > 0) ? pv[r + 1] * cDel : 0.0;
+                        x[r] = 0.0;
                     }
                 }
-                const double pm = fmax(mx, prefix_max<G>(x));
-                const double thr = pm / T.sdn;
-                const bool cont = (i - 1 > 0) && (x >= thr || i - 1 >= reqBegin);
-                const unsigned long long stop = T.g.bits(!cont);
+                // a chunk whose inputs are all exactly zero stays zero: skip its chain (bit-exact; common
+                // in the far rows of tall bands)
+                bool nz = false;
+#pragma unroll
+                for (int r = 0; r < R; ++r) nz = nz || m[r] != 0.0 || d[r] != 0.0;
+                const unsigned long long nzb = T.g.bits(nz);
+                if (carry != 0.0 || nzb != 0) {
+                    const int startLane = ((G == 64 || R > 1) && carry == 0.0) ? __ffsll((long long)nzb) - 1 : 0;
+                    if constexpr (R == 1) {
+                        const int i = e - 1 - ob;
+                        if (G == 64 && T.chainExit) {
+                            auto maybe_stop = [&](double xv) {   // x < pm * invLow implies x < pm / sdn
+                                const double pmv = fmax(mx, prefix_max<G>(xv));
+                                return T.g.bits((i - 1 <= 0) || (xv < pmv * T.sdnInvLow && i - 1 < reqBegin));
+                            };
+                            x[0] = insertion_chain64_exit(m[0], k[0], d[0], carry, e - 1 - max(1, reqBegin) - c * G,
+                                                          maybe_stop, startLane);
+                        } else {
+                            x[0] = insertion_chain<G>(m[0], k[0], d[0], carry);
+                        }
+                    } else {
+                        auto maybe_stop = [&](const double (&xv)[R]) {   // x < pm * invLow implies x < pm / sdn
+                            double lp = xv[0];
+#pragma unroll
+                            for (int r = 1; r < R; ++r) lp = fmax(lp, xv[r]);
+                            const double ex = shift_up<G>(prefix_max<G>(lp), 0.0);
+                            double run = fmax(mx, ex);
+                            bool st = false;
+#pragma unroll
+                            for (int r = 0; r < R; ++r) {
+                                run = fmax(run, xv[r]);
+                                const int i = e - 1 - ob - r;
+                                st = st || (i - 1 <= 0) || (xv[r] < run * T.sdnInvLow && i - 1 < reqBegin);
+                            }
+                            return T.g.bits(st);
+                        };
+                        const int firstOff = e - 1 - max(1, reqBegin) - c * CH;   // the first chunk offset that may stop
+                        insertion_chain_rows<G, R>(m, k, d, carry, x, firstOff < 0 ? 0 : firstOff / R, T.chainExit,
+                                                   startLane, maybe_stop);
+                    }
+                }
+                double pmR[R];
+                if constexpr (R == 1) {
+                    pmR[0] = fmax(mx, prefix_max<G>(x[0]));
+                } else {
+                    double lp = x[0];
+#pragma unroll
+                    for (int r = 1; r < R; ++r) lp = fmax(lp, x[r]);
+                    double run = fmax(mx, shift_up<G>(prefix_max<G>(lp), 0.0));
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        run = fmax(run, x[r]);
+                        pmR[r] = run;
+                    }
+                }
+                int fs = R;
+#pragma unroll
+                for (int r = R - 1; r >= 0; --r) {
+                    const int i = e - 1 - ob - r;
+                    const double thr = pmR[r] / T.sdn;
+                    const bool cont = (i - 1 > 0) && (x[r] >= thr || i - 1 >= reqBegin);
+                    if (!cont) fs = r;
+                }
+                const unsigned long long stop = T.g.bits(fs < R);
                 const int lastLane = stop ? (__ffsll((long long)stop) - 1) : (G - 1);
-                mx = T.g.bcast(pm, lastLane);
+                double pmAt = pmR[R - 1];
+#pragma unroll
+                for (int r = 0; r < R - 1; ++r)
+                    if (r == fs) pmAt = pmR[r];
+                mx = T.g.bcast(pmAt, lastLane);
                 ++nc;
                 if (stop) {
-                    b = e - 1 - (c * G + lastLane);
-                    aLast = x;
+                    const int rs = R == 1 ? 0 : T.g.bcast(fs, lastLane);
+                    b = e - 1 - (c * CH + lastLane * R + rs);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) aLast[r] = x[r];
                     break;
                 }
-                T.cset(cur, off, x);
-                carry = T.g.bcast_last(x);
+#pragma unroll
+                for (int r = 0; r < R; ++r) T.cset(cur, ob + r, x[r]);
+                carry = T.g.bcast_last(x[R - 1]);
             }
         }
         const bool keep = T.ckK == 0 || ckpt_col_b(j, J, T.ckK);
@@ -484,17 +626,23 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         bool found = false;
 #pragma unroll 2
         for (int c = 0; c < nc; ++c) {
-            const int off = c * G + lane;
-            const bool ok = e - 1 - off >= b;
-            const double x = (c == nc - 1) ? aLast : T.cget(cur, off);
-            const double v = scale ? x / mx : x;
-            if (ok) {
-                T.cset(cur, off, v);
-                if (store && stored + off < bm.cap) bm.V(stored + off) = v;
+            int fh = R;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int off = c * CH + lane * R + r;
+                const bool ok = e - 1 - off >= b;
+                const double x = (c == nc - 1) ? aLast[r] : T.cget(cur, off);
+                const double v = scale ? x / mx : x;
+                if (ok) {
+                    T.cset(cur, off, v);
+                    if (store && stored + off < bm.cap) bm.V(stored + off) = v;
+                }
+                if (fh == R && ok && !(v < thrF)) fh = r;
             }
-            const unsigned long long hit = T.g.bits(ok && !(v < thrF));
+            const unsigned long long hit = T.g.bits(fh < R);
             if (!found && hit) {
-                nhe = e - (c * G + __ffsll((long long)hit) - 1);
+                const int hl = __ffsll((long long)hit) - 1;
+                nhe = e - (c * CH + hl * R + (R == 1 ? 0 : T.g.bcast(fh, hl)));
                 found = true;
             }
         }
@@ -509,7 +657,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         if ((jb == G - 1 || j == 1) && !counting && lane <= jb) bm.L(j + jb - lane) = (myF != 1.0) ? log(myF) : 0.0;
         used += e - b;
         stored += add;
-        col_fence(T.gcol && nc * G > T.hcap);
+        col_fence(T.gcol && nc * CH > T.hcap);
         nxt ^= 1;
         cur ^= 1;
         pb = b;
@@ -548,13 +696,13 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 // LDS per group: 2 column buffers (hcap doubles each), the ZMW's transition table, nibble-packed read
 // and template window.
 // ------------------------------------------------------------------------------------------------
-template <int G, int MINW, bool GC>
+template <int G, int MINW, bool GC, int R>
 __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     // tall reads are the latency-critical path of every refine round: issue ahead of the 16-lane fills
     // and score waves that share the SIMD (F.prio = 0 leaves the default priority)
-    if (G == 64 && F.prio) __builtin_amdgcn_s_setprio(3);
+    if ((G == 64 || R > 1) && F.prio) __builtin_amdgcn_s_setprio(3);
     const int grp = threadIdx.x / G;
     const int t = blockIdx.x * (64 / G) + grp;
     const int lane = threadIdx.x & (G - 1);
@@ -567,6 +715,10 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     unsigned* tpW = rdW + F.readWords;
 
     const bool valid = t < n;
+    if (F.trace && valid && lane == 0) {   // start stamps go to memory: nothing stays live across the fill
+        F.trace[6LL * t] = (long long)wall_clock64();
+        F.trace[6LL * t + 2] = (long long)clock64();
+    }
     int r = 0, z = 0, I = 0, J = 0;
     TplView tv{};
     bool bad = true;
@@ -694,8 +846,8 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
         }
         const bool guided = step > 0, self = step > 1;
         PassOut o;
-        if (doAlpha) o = coop_alpha<G>(T, a, bm, guided, self, ovf, ub);
-        else o = coop_beta<G>(T, bm, a, guided, self, ovf, ua);
+        if (doAlpha) o = coop_alpha<G, R>(T, a, bm, guided, self, ovf, ub);
+        else o = coop_beta<G, R>(T, bm, a, guided, self, ovf, ua);
         if (o.tall) return fail_tall();
         if (o.regrow) {   // exact region for this pass, then run it again (count-only if the pool is full)
             if (++regrows > 8 ||
@@ -743,6 +895,14 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
             F.usedB[r] = (int)sb;
             if (F.maxH) F.maxH[r] = maxH;
             B.rStatus[r] = (mism > kAlphaBetaTol) ? kFillMismatch : kFillOk;
+            if (F.trace) {
+                long long* tr = F.trace + 6LL * t;
+                tr[1] = (long long)wall_clock64();
+                tr[2] = (long long)clock64() - tr[2];
+                tr[3] = (long long)cells;
+                tr[4] = (long long)passes;
+                tr[5] = (long long)J;
+            }
             if (B.stats) {   // algorithmic: 8 B per stored cell + 16 B per column per fill pass
                 constexpr int kind = G == 64 ? kStatFillTall : kStatFill;
                 atomicAdd(&B.stats[2 * kind], cells);
@@ -767,21 +927,35 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     if (lds > 160 * 1024) throw std::runtime_error("fill block needs more than 160 KB of LDS");
     using K = void (*)(DevBatch, CoopFill, const int*, int);
     const bool gc = F.colScratch != nullptr;
-    if (gc && G != 64) throw std::runtime_error("global column buffers need 64-lane groups");
     // two waves per SIMD: the register budget that leaves these kernels without spills (higher occupancy
     // was measured slower and needs a private segment, which the resource check in the Makefile forbids)
-    if (G != 16 && G != 64) throw std::runtime_error("fill groups are 16 or 64 lanes");
-    const K k = gc        ? (K)k_fill_coop<64, 2, true>
-                : G == 16 ? (K)k_fill_coop<16, 2, false>
-                          : (K)k_fill_coop<64, 2, false>;
-    static bool attrSet[3] = {false, false, false};   // dynamic LDS beyond 64 KB must be enabled per kernel
-    const int ak = gc ? 2 : (G == 64);
-    if (!attrSet[ak]) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attrSet[ak] = true;
+    // (G, rows per lane, hybrid): the 16-lane narrow path (16, 1), tall paths with four reads per wavefront
+    // (16, 4) or one (64, 1 / 2 / 4); the hybrid kernels at R = 4 need more than 256 registers and run R = 2 (the
+    // column buffers hold whole chunks either way)
+    const int R = gc ? std::min(F.rows, 2) : F.rows;
+    struct Entry {
+        int g, r;
+        bool gc;
+        K k;
+        bool attr;
+    };
+    static Entry ks[] = {
+        {16, 1, false, (K)k_fill_coop<16, 2, false, 1>, false}, {16, 4, false, (K)k_fill_coop<16, 2, false, 4>, false},
+        {16, 2, true, (K)k_fill_coop<16, 2, true, 2>, false},   {64, 1, false, (K)k_fill_coop<64, 2, false, 1>, false},
+        {64, 2, false, (K)k_fill_coop<64, 2, false, 2>, false}, {64, 4, false, (K)k_fill_coop<64, 2, false, 4>, false},
+        {64, 1, true, (K)k_fill_coop<64, 2, true, 1>, false},   {64, 2, true, (K)k_fill_coop<64, 2, true, 2>, false}};
+    Entry* e = nullptr;
+    for (Entry& x : ks)
+        if (x.g == G && x.r == R && x.gc == gc) e = &x;
+    if (!e) throw std::runtime_error("no fill kernel for this group size / rows per lane / column buffer");
+    if (R > 1 && (gc ? (F.hcap + F.gRows) : F.hcap) % (G * R) != 0)
+        throw std::runtime_error("fill column buffers must hold whole chunks of G x rows rows");
+    if (!e->attr) {   // dynamic LDS beyond 64 KB must be enabled per kernel
+        (void)hipFuncSetAttribute((const void*)e->k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        e->attr = true;
     }
     const dim3 grid((n + per - 1) / per);
-    hipLaunchKernelGGL(k, grid, dim3(64), lds, s, B, F, reads, n);
+    hipLaunchKernelGGL(e->k, grid, dim3(64), lds, s, B, F, reads, n);
 }
 
 }  // namespace pbccs

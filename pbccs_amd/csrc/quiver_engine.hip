@@ -130,6 +130,9 @@ void QuiverBatch::Reset()
 {
     QHIP(hipSetDevice(device_));
     QHIP(hipStreamSynchronize(stream_));
+    // a call that threw between the side stream's tall fills and the join may have left them running: they
+    // read the read list and the arenas this call is about to overwrite
+    if (side_) QHIP(hipStreamSynchronize(side_));
     configs_.clear();
     zmws_.clear();
     reads_.clear();
@@ -434,20 +437,17 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         // a ring of its full height (tallRing).
         // SparseSse reads go to k_qfill_grp first (four reads per wavefront, a 64-row band ring); a read that
         // comes back kQTall moves to k_qfill_coop's band-height ring, then to its full-height ring.
-        // PBCCS_QFILL_GRP=0 skips the grouped kernel (A/B).
-        static const bool laneOnly = std::getenv("PBCCS_QFILL_LANE") != nullptr;
-        static const bool grpOn = !(std::getenv("PBCCS_QFILL_GRP") && std::getenv("PBCCS_QFILL_GRP")[0] == '0');
         std::vector<int> grp, coop, full, lane;
         int maxCols = 1, maxColsFull = 1, maxRowsFull = 1;
         for (int r : todo) {
             const QParams& p = configs_[reads_[r].config];
             const int cols = reads_[r].te - reads_[r].ts + 1;
-            if (!laneOnly && !p.simple && !p.dense && reads_[r].len + 1 <= kQCoopRows && cols <= kQCoopCols) {
+            if (!p.simple && !p.dense && reads_[r].len + 1 <= kQCoopRows && cols <= kQCoopCols) {
                 if (reads_[r].tallRing) {
                     full.push_back(r);
                     maxRowsFull = std::max(maxRowsFull, reads_[r].len + 1);
                     maxColsFull = std::max(maxColsFull, cols);
-                } else if (reads_[r].grpTall || !grpOn) {
+                } else if (reads_[r].grpTall) {
                     coop.push_back(r);
                     maxCols = std::max(maxCols, cols);
                 } else {
@@ -476,13 +476,8 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         both.insert(both.end(), lane.begin(), lane.end());
         put(dList_, both, stream_);
         const QBatch B = View();
-        static const int ringRows = [] {   // PBCCS_QRING_ROWS overrides the ring (A/B; a power of two)
-            const char* e = std::getenv("PBCCS_QRING_ROWS");
-            int r = e ? std::atoi(e) : kQRingRows;
-            int p = 64;
-            while (p < r && p < kQCoopRows) p *= 2;
-            return p;
-        }();
+        constexpr int ringRows = kQRingRows;   // a power of two (128 / 256 / 512 / 1024 measured, quiver_kernels.hpp)
+        static_assert((kQRingRows & (kQRingRows - 1)) == 0, "the band ring is a power of two of rows");
         const size_t g0 = grpList.size();
         // the coop lists (reads that were tall for k_qfill_grp) on the side stream, concurrently with the grouped
         // launch; both streams join before the status download
@@ -1120,11 +1115,38 @@ std::vector<std::vector<int>> QuiverBatch::QVsMany(const std::vector<int>& zs)  
     Q.posOff = dPosOff_.ptr;
     Q.score = dMScore_.ptr;
     Q.qv = dQv_.ptr;
+    Q.hostAll = std::getenv("PBCCS_QQV_HOST") != nullptr;   // test hook: the host path for every position
     launch_qqv(Q, nPos, stream_);
     QHIP(hipGetLastError());
     std::vector<int> all;
     get(all, dQv_, (size_t)nPos, stream_);
     QHIP(hipStreamSynchronize(stream_));
+    // positions k_qqv left to the host (-1: the rounding of -10 log10(prob) could depend on the libm): their
+    // mutation scores come back and the sum, ProbabilityToQV and the libm are the reference's
+    std::vector<std::pair<int, int>> amb;   // (scorer, position)
+    for (int w = 0; w < n; ++w)
+        for (long long g = posStart[w]; g < posStart[w + 1]; ++g)
+            if (all[(size_t)g] < 0) amb.emplace_back(w, (int)(g - posStart[w]));
+    if (!amb.empty()) {
+        std::vector<std::vector<double>> sc(amb.size());
+        for (size_t a = 0; a < amb.size(); ++a) {
+            const int w = amb[a].first, p = amb[a].second;
+            const int* po = posOff.data() + posOffBase[w];
+            sc[a].resize((size_t)(po[p + 1] - po[p]));
+            if (!sc[a].empty())
+                QHIP(hipMemcpyAsync(sc[a].data(), dMScore_.ptr + mutStart[w] + po[p], sc[a].size() * sizeof(double),
+                                    hipMemcpyDeviceToHost, stream_));
+        }
+        QHIP(hipStreamSynchronize(stream_));
+        for (size_t a = 0; a < amb.size(); ++a) {
+            double sum = 0.0;
+            for (double s : sc[a]) {
+                const double f = (double)(float)s;   // Score() is a float sum
+                if (f < 0.0) sum += std::exp(f);
+            }
+            all[(size_t)(posStart[amb[a].first] + amb[a].second)] = probability_to_qv(1.0 - 1.0 / (1.0 + sum));
+        }
+    }
     std::vector<std::vector<int>> qv(n);
     for (int w = 0; w < n; ++w) qv[w].assign(all.begin() + posStart[w], all.begin() + posStart[w + 1]);
     return qv;

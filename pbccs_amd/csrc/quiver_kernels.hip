@@ -2204,7 +2204,14 @@ __global__ void __launch_bounds__(256) k_qqv(QQvWork W, long long nPos)
     }
     double prob = 1.0 - 1.0 / (1.0 + sum);
     if (prob == 0.0) prob = 2.2250738585072014e-308;   // std::numeric_limits<double>::min()
-    W.qv[g] = (int)round(-10.0 * log10(prob));
+    // The scores are the reference's floats bit for bit, but exp / log10 here are OCML's, the reference's
+    // glibc's: they may differ by an ulp, which can move the rounding only when -10 log10(prob) lies next to a
+    // .5 boundary or prob is tiny (1 + sum at the edge of 1.0).  Such positions are marked -1 and the host
+    // recomputes them with the host libm from the same float scores (QuiverBatch::QVsMany), so every QV is
+    // the reference's.
+    const double v = -10.0 * log10(prob);
+    const double frac = v - floor(v);
+    W.qv[g] = (W.hostAll || prob < 1e-12 || fabs(frac - 0.5) < 1e-6) ? -1 : (int)round(v);
 }
 
 // ---- k_qalign: RecursorBase::Alignment (detail/RecursorBase.cpp:118-264) -------------------------------

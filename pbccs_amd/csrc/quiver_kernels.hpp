@@ -127,7 +127,8 @@ struct QQvWork {
     const long long* posOffBase;   // item w's position offsets at posOff + posOffBase[w] (L + 1 of them)
     const int* posOff;             // mutation offset of each position within its item
     const double* score;           // k_qreduce's per-mutation sums
-    int* qv;                       // per global position
+    int* qv;                       // per global position (-1: left to the host, see k_qqv)
+    int hostAll = 0;               // test hook (PBCCS_QQV_HOST=1): every position left to the host
 };
 void launch_qqv(const QQvWork& W, long long nPos, hipStream_t s);
 

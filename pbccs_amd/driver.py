@@ -157,6 +157,8 @@ def ccs_batch(chunks, settings=None, engine=None, max_poa_coverage=None):
     polish_zmws) plus "draft"; add_read_results / zscores hold one entry per input subread, in the
     chunk's read order: -1 / NaN for a read that never reached AddRead (dropped by FilterReads, not added
     by the POA, rejected by ExtractMappedRead, past the maxPoaCov stop, or the ZMW ended earlier).
+    "add_order" lists the subread indices in AddRead order (FilterReads' stable order, Consensus.h:281):
+    the order of ZScores() and of the ccs.bam zs tag.
     Raises on a draft longer than its buffer (PBCCS_ERANGE)."""
     import ctypes
     from . import ZMW_STATUS, default_engine
@@ -181,6 +183,7 @@ def ccs_batch(chunks, settings=None, engine=None, max_poa_coverage=None):
         qv = (ctypes.c_int * cap)()
         arr = (ctypes.c_int * max(1, nr))()
         zs = (ctypes.c_double * max(1, nr))()
+        order = (ctypes.c_int * max(1, nr))()
         for k in range(4):
             ins[z].snr[k] = float(c["snr"][k])
         ins[z].n_subreads, ins[z].seqs, ins[z].lens, ins[z].flags = nr, seqs, lens, flags
@@ -190,12 +193,13 @@ def ccs_batch(chunks, settings=None, engine=None, max_poa_coverage=None):
         o.polish.qvs, o.polish.add_read_results, o.polish.zscores = qv, arr, zs
         o.draft = ctypes.cast(draft, ctypes.c_char_p)
         o.draft_cap = cap
-        keep.append((seqs, lens, flags, cons, draft, qv, arr, zs, nr))
+        o.add_order = order
+        keep.append((seqs, lens, flags, cons, draft, qv, arr, zs, order, nr))
     opts = settings._c()
     mc = 2**62 if max_poa_coverage is None else int(max_poa_coverage)
     L.check(L.load().pbccs_ccs_batch(eng._h, ins, n, mc, ctypes.byref(opts), outs))
     res = []
-    for z, (_, _, _, cons, draft, qv, arr, zs, nr) in enumerate(keep):
+    for z, (_, _, _, cons, draft, qv, arr, zs, order, nr) in enumerate(keep):
         p = outs[z].polish
         ok = p.status in (0, 6)
         ln = max(0, p.consensus_len) if ok else 0
@@ -204,6 +208,7 @@ def ccs_batch(chunks, settings=None, engine=None, max_poa_coverage=None):
                     "consensus": cons.raw[:ln].decode() if ok else "", "qvs": list(qv[:ln]) if ok else [],
                     "draft": draft.raw[:max(0, outs[z].draft_len)].decode(),
                     "add_read_results": list(arr[:nr]), "zscores": list(zs[:nr]), "polished": polished,
+                    "add_order": [k for k in order[:nr] if k >= 0],
                     "zg": p.zg, "za": p.za, "predicted_accuracy": p.predicted_accuracy, "n_tested": p.n_tested,
                     "n_applied": p.n_applied, "n_passes": p.n_passes, "status_counts": list(p.status_counts)})
     return res

@@ -118,7 +118,7 @@ class CCcsInput(ctypes.Structure):
 
 class CCcsOutput(ctypes.Structure):
     _fields_ = [("polish", CZmwOutput), ("draft", ctypes.c_char_p), ("draft_cap", ctypes.c_int),
-                ("draft_len", ctypes.c_int)]
+                ("draft_len", ctypes.c_int), ("add_order", ctypes.POINTER(ctypes.c_int))]
 
 
 class CPoaStats(ctypes.Structure):

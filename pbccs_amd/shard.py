@@ -56,8 +56,10 @@ _queue_calls = [0]
 
 def dynamic_chunks(zmws, chunk):
     """The pull queue's work items: ZMW indices in decreasing cost, cut into chunks of `chunk` ZMWs (largest
-    first, so the ranks' last pulls are the cheap chunks)."""
-    order = sorted(range(len(zmws)), key=lambda i: (-zmw_cost(zmws[i]), i))
+    first, so the ranks' last pulls are the cheap chunks).  A lazily generated cell (synth.SmrtCell) gives its
+    costs from the ZMW shapes, without materialising a sequence."""
+    costs = zmws.costs() if hasattr(zmws, "costs") else [zmw_cost(z) for z in zmws]
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
     return [order[k:k + chunk] for k in range(0, len(order), chunk)]
 
 
@@ -69,13 +71,21 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
     simply pulls fewer chunks.
 
     Results stream to rank 0 as chunks finish (the ordered FIFO of WorkQueue.h:128-167 fed as workers
-    complete): a rank > 0 puts each finished chunk's records under its own key on the same store; rank 0 takes
-    whatever has arrived between its own chunks, and once the queue is empty only the chunks still running
-    elsewhere are left to wait for.  Nothing is gathered in one piece at the end.  Rank 0 returns every ZMW's
-    result in input order; the other ranks return None.  `stats` (a dict, optional) receives the queue's
-    counters on rank 0: chunks per rank and `tail_ms`, the time from rank 0's last chunk to the last record."""
+    complete): a rank > 0 puts each finished chunk's records under its own key on the same store, and a
+    collector thread on rank 0 takes them as they arrive while rank 0's own thread keeps polishing -- a long
+    chunk on rank 0 never delays the collection.  Once the queue is empty only the chunks still running
+    elsewhere are left to wait for; nothing is gathered in one piece at the end.
+
+    `zmws` may be a list or a lazily generated cell (synth.SmrtCell): a rank then materialises only the chunks
+    it pulls, the next one on a helper thread while the current one polishes.
+
+    Rank 0 returns every ZMW's result in input order; the other ranks return None.  `stats` (a dict, optional)
+    receives the queue's counters on rank 0: chunks per rank, `tail_ms` (the time from rank 0's last chunk to
+    the last record) and `gen_ms` (this rank's time waiting for chunk generation)."""
     import pickle
+    import threading
     import time
+    from concurrent.futures import ThreadPoolExecutor
     import torch.distributed as dist
     if rank is None:
         rank = dist.get_rank() if dist.is_initialized() else 0
@@ -91,51 +101,109 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
     key = f"pbccs_queue_{_queue_calls[0]}"
     if world > 1 and store is None:
         store = dist.distributed_c10d._get_default_store()
+    lock = threading.Lock()   # one store client, used by the puller and by rank 0's collector
     out = [None] * len(zmws) if rank == 0 else None
-    mine = []          # chunks this rank polished
-    pending = set()    # rank 0: chunks another rank took, records not yet collected
+    mine = set()       # chunks this rank polished
     taken = [0] * world
+    lazy = hasattr(zmws, "costs")
 
-    def collect(c, block):
+    # ---- rank 0's collector: records of the chunks other ranks took, as soon as they are stored ----------
+    pending = set()    # chunk indices handed to other ranks whose records are not collected yet
+    final = threading.Event()
+    collector_err = []
+
+    def collect_one(c):
         k = f"{key}/done/{c}"
-        if not block and not store.check([k]):
-            return False
-        who, recs = pickle.loads(store.get(k))
-        store.delete_key(k)
+        with lock:
+            if not store.check([k]):
+                return False
+            blob = store.get(k)
+            store.delete_key(k)
+        who, recs = pickle.loads(blob)
         taken[who] += 1
         for i, rec in zip(chunks[c], recs):
             out[i] = rec
         return True
 
-    serial = 0
-    high = 0           # rank 0: chunk indices below `high` were handed out
-    while True:
+    def collector():
+        try:
+            while True:
+                with lock:
+                    todo = sorted(pending)
+                got = [c for c in todo if collect_one(c)]
+                with lock:
+                    pending.difference_update(got)
+                    empty = not pending
+                if final.is_set() and empty:
+                    return
+                if not got:
+                    time.sleep(0.005)
+        except Exception as e:   # surfaced by the main thread
+            collector_err.append(e)
+
+    coll = None
+    if rank == 0 and world > 1:
+        coll = threading.Thread(target=collector, daemon=True)
+        coll.start()
+
+    serial = [0]
+    high = [0]         # rank 0: chunk indices below `high` were handed out
+
+    def pull():
         if world > 1:
-            c = store.add(key, 1) - 1
+            with lock:
+                c = store.add(key, 1) - 1
         else:
-            c, serial = serial, serial + 1
-        if rank == 0:
-            pending.update(range(high, min(c, len(chunks))))   # handed to other ranks since our last pull
-            high = max(high, c + 1)
-            for p in sorted(pending):
-                if collect(p, block=False):
-                    pending.discard(p)
-        if c >= len(chunks):
-            break
-        recs = polish_fn([zmws[i] for i in chunks[c]])
-        mine.append(c)
-        if rank == 0:
-            taken[0] += 1
-            for i, rec in zip(chunks[c], recs):
-                out[i] = rec
-        else:
-            store.set(f"{key}/done/{c}", pickle.dumps((rank, recs)))
+            c = serial[0]
+            serial[0] += 1
+        if rank == 0 and world > 1:
+            with lock:   # handed to other ranks since our last pull
+                pending.update(range(high[0], min(c, len(chunks))))
+            high[0] = max(high[0], c + 1)
+        return c
+
+    def materialise(c):
+        return [zmws[i] for i in chunks[c]] if c < len(chunks) else None
+
+    gen = ThreadPoolExecutor(max_workers=1) if lazy else None
+    gen_ms = 0.0
+    try:
+        c = pull()
+        fut = gen.submit(materialise, c) if gen else None
+        while c < len(chunks):
+            t0 = time.perf_counter()
+            zs = fut.result() if gen else materialise(c)
+            gen_ms += (time.perf_counter() - t0) * 1e3
+            nxt = None
+            if gen:   # reserve and generate the next chunk while this one polishes
+                nxt = pull()
+                fut = gen.submit(materialise, nxt)
+            recs = polish_fn(zs)
+            mine.add(c)
+            if rank == 0:
+                taken[0] += 1
+                for i, rec in zip(chunks[c], recs):
+                    out[i] = rec
+            else:
+                blob = pickle.dumps((rank, recs))
+                with lock:
+                    store.set(f"{key}/done/{c}", blob)
+            c = nxt if gen else pull()
+    finally:
+        if gen:
+            gen.shutdown(wait=True)
+    if stats is not None:
+        stats["gen_ms"] = gen_ms
     if rank != 0:
         return None
     t0 = time.perf_counter()
-    pending.update(c for c in range(high, len(chunks)) if c not in mine)
-    for p in sorted(pending):
-        collect(p, block=True)   # store.get waits for the key
+    if coll is not None:
+        with lock:
+            pending.update(x for x in range(high[0], len(chunks)) if x not in mine)
+        final.set()
+        coll.join()
+        if collector_err:
+            raise collector_err[0]
     if stats is not None:
         stats.update({"chunks": len(chunks), "chunks_by_rank": taken, "tail_ms": (time.perf_counter() - t0) * 1e3})
     missing = [i for i, rec in enumerate(out) if rec is None]

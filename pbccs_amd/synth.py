@@ -83,6 +83,59 @@ def make_smrtcell(n, seed=4):
     return out
 
 
+class SmrtCell:
+    """configs[4] generated lazily: ZMW i of the cell is drawn from its own seeded stream (seed, i), so any rank
+    can materialise any chunk of the cell without generating the rest (150k ZMWs of strings per rank would be
+    ~14 GB of Python objects).  Shape (kind, insert length, passes, SNR) and sequences come from two separate
+    streams, so the work queue can order the whole cell by cost from the shapes alone.  One third each of the
+    configs #2-#4 shapes, as make_smrtcell.  Indexing returns make_zmw's dict plus "kind"."""
+    KINDS = ("2kb", "10kb", "mixed")
+
+    def __init__(self, n, seed=4):
+        self.n = int(n)
+        self.seed = int(seed)
+        self._shapes = None
+
+    def __len__(self):
+        return self.n
+
+    def shape(self, i):
+        if self._shapes is not None:
+            return self._shapes[i]
+        rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([self.seed, int(i), 0])))
+        kind = int(rng.integers(0, 3))
+        if kind == 0:
+            return kind, 2000, 10, (10.0, 7.0, 5.0, 11.0)
+        if kind == 1:
+            return kind, 10000, 8, (10.0, 7.0, 5.0, 11.0)
+        L = int(rng.integers(500, 20001))
+        P = int(rng.integers(3, 31))
+        return kind, L, P, tuple(float(x) for x in rng.uniform(4.0, 20.0, size=4))
+
+    def shapes(self):
+        if self._shapes is None:
+            self._shapes = [self.shape(i) for i in range(self.n)]
+        return self._shapes
+
+    def costs(self):
+        """shard.zmw_cost's estimate (draft length x read bases) from the shapes: L x (1.03 L) x passes."""
+        return [max(1, L) * max(1, int(1.03 * L) * P) for _, L, P, _ in self.shapes()]
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(self.n))]
+        if not 0 <= i < self.n:
+            raise IndexError(i)
+        kind, L, P, snr = self.shape(i)
+        rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([self.seed, int(i), 1])))
+        z = make_zmw(rng, L, P, snr)
+        z["kind"] = self.KINDS[kind]
+        return z
+
+    def __iter__(self):
+        return (self[i] for i in range(self.n))
+
+
 CONFIGS = {
     # name: (n_zmws, insert length, passes, seed) -- BASELINE.json configs[1..3]
     "2kb_10pass": dict(length=2000, passes=10, seed=1),

@@ -5,7 +5,8 @@ Reads data that the reference's own tests and demos hold (never its code):
   * ConsensusCore/src/Demos/MatrixTester.cpp:74-204 -- the 12 Arrow known-answer values (C#-derived,
     checked there at 1e-5 relative) and the template/read strings they are quoted on;
   * tests/data/m140905_..._X0.fasta -- the 10 subreads of ZMW 6251 (the only subread data in the tree);
-  * SURVEY.md §0 item 4 / Appendix C -- the reference's recorded polish outputs on that ZMW
+  * SURVEY.md §0 item 4 / Appendix C -- the survey's probe record of the polish on that ZMW (a boost-shim
+    build of the reference in the survey container: a cross-check, not a parity pin)
     (draft = subread 2, reads 1..8 mapped over the full draft, odd index REVERSE,
      SNR (10,7,5,11), MinZScore -5).
   * ConsensusCore/src/Tests/TestPoaConsensus.cpp and tests/TestSparsePoa.cpp -- the POA known answers

@@ -1,5 +1,6 @@
 """The C++ facade (include/pbccs_amd/ConsensusCore.hpp) compiles a Consensus.h-style driver unchanged in
-shape (CPU test), and that driver reproduces the reference record for ZMW 6251 on the GPU (gpu test)."""
+shape (CPU test), and that driver reproduces ZMW 6251 on the GPU (gpu test): bit for bit
+against the oracle, and against SURVEY.md §0 item 4's survey-probe record (a boost-shim build, a cross-check)."""
 import json
 import os
 import subprocess

@@ -233,7 +233,7 @@ def _check_native_ccs(chunks, cov, eng):
     """pbccs_ccs_batch against the Python driver + polish_zmws, per-read outputs in subread order."""
     import math
     import pbccs_amd
-    from pbccs_amd import driver
+    from pbccs_amd import ccsio, driver
     native = driver.ccs_batch(chunks, engine=eng, max_poa_coverage=cov)
     ins = driver.zmw_inputs_batch(chunks, max_poa_coverage=cov, engine=eng)
     pol = iter(pbccs_amd.polish_zmws([z for st, z in ins if st is None], engine=eng))
@@ -257,6 +257,12 @@ def _check_native_ccs(chunks, cov, eng):
         assert got["add_read_results"] == want_arr
         for a, b in zip(got["zscores"], want_z):
             assert (math.isnan(a) and math.isnan(b)) or a == b
+        # AddRead order (FilterReads' stable order): the ccs.bam zs tag of the native record equals the one of
+        # the polish_zmws record, whose per-read arrays are in AddRead order already
+        assert got["add_order"] == [order[i] for i, a in enumerate(exp["add_read_results"]) if a >= 0]
+        if got["status"] == "Success":
+            tag = lambda rec: [t for t in rec.split("\t") if t.startswith("zs:")]
+            assert tag(ccsio.ccs_sam_record("m", 1, got, c["snr"])) == tag(ccsio.ccs_sam_record("m", 1, exp, c["snr"]))
         if cov is not None:
             assert sum(1 for a in got["add_read_results"] if a >= 0) <= cov
     assert native[-1]["status"] == "NoSubreads"

@@ -1,9 +1,8 @@
 """GPU parity of the Quiver family (HIP engine through the C ABI) against the reference's Quiver gtest
 known answers and against the CPU restatement (oracle/quiver_oracle.cpp) on seeded synthetic reads with
 random QV features.  Tolerance: bit-exact FP32 (every score, baseline, flip-flop count and refine outcome), since
-the engine repeats the SSE recursor's single-precision operations in order; ConsensusQVs within +-1 of the
-restatement (the per-position exp sums run on the device, see _qvs_within_one) and equal between the batch and
-the per-scorer calls."""
+the engine repeats the SSE recursor's single-precision operations in order; ConsensusQVs equal to the
+restatement's (see _qvs_exact) and equal between the batch and the per-scorer calls."""
 import json
 import os
 
@@ -91,11 +90,12 @@ def _zmw(seed, length, passes):
     return z["draft"], reads
 
 
-def _qvs_within_one(got, exp):
-    """ConsensusQVs against the restatement: the per-position sums of exp(score) run on the device (k_qqv, OCML
-    exp/log10) and on the host (glibc), so a QV at a rounding boundary may differ by one -- the north_star's
-    tolerance for QVs (+-1).  Scores, templates and mutation counts stay bit-exact."""
-    return len(got) == len(exp) and all(abs(a - b) <= 1 for a, b in zip(got, exp))
+def _qvs_exact(got, exp):
+    """ConsensusQVs against the restatement, exactly (tighter than the north_star's +-1): the scores are
+    bit-exact floats, k_qqv sums exp(score) per position with the device libm, and every position whose rounding
+    could depend on the libm (-10 log10(prob) within 1e-6 of a .5 boundary, or prob < 1e-12) is recomputed on the
+    host with the host libm (QuiverBatch::QVsMany)."""
+    return list(got) == list(exp)
 
 
 @pytest.mark.parametrize("sum_product", [False, True])
@@ -125,7 +125,19 @@ def test_quiver_refine_and_qvs_match_oracle(sum_product):
     ref = o.refine()
     assert (conv, nt, na) == (ref["converged"], ref["n_tested"], ref["n_applied"])
     assert g.template() == o.template()
-    assert _qvs_within_one(P.ConsensusQVs(g.s), o.qvs())
+    assert _qvs_exact(P.ConsensusQVs(g.s), o.qvs())
+
+
+def test_quiver_qvs_host_path_matches_device_path(monkeypatch):
+    """k_qqv leaves positions whose rounding could depend on the libm to the host; PBCCS_QQV_HOST=1 sends every
+    position there: the QVs equal the device path's and the restatement's."""
+    tpl, reads = _zmw(112, 160, 5)
+    g, o = _pair(tpl, reads, True)
+    import pbccs_amd as P
+    dev = P.ConsensusQVs(g.s)
+    monkeypatch.setenv("PBCCS_QQV_HOST", "1")
+    host = P.ConsensusQVs(g.s)
+    assert host == dev and _qvs_exact(host, o.qvs())
 
 
 def test_quiver_add_threshold_memory_gate():
@@ -245,7 +257,7 @@ def test_quiver_polish_batch_matches_scorers(sum_product):
         ref = o.refine()
         assert (g["converged"], g["n_tested"], g["n_applied"]) == (ref["converged"], ref["n_tested"], ref["n_applied"])
         assert g["consensus"] == o.template()
-        assert _qvs_within_one(g["qvs"], o.qvs())
+        assert _qvs_exact(g["qvs"], o.qvs())
 
 
 def test_quiver_coop_fill_long_reads_match_oracle():
@@ -278,7 +290,7 @@ def test_quiver_coop_fill_long_reads_match_oracle():
         ref = o.refine()
         assert (r["converged"], r["n_tested"], r["n_applied"]) == (ref["converged"], ref["n_tested"], ref["n_applied"])
         assert r["consensus"] == o.template()
-        assert _qvs_within_one(r["qvs"], o.qvs())
+        assert _qvs_exact(r["qvs"], o.qvs())
 
 
 @pytest.mark.parametrize("score_diff,sum_product", [(60.0, False), (60.0, True), (400.0, False)])

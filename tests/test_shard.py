@@ -193,3 +193,34 @@ def test_smrtcell_mix_two_ranks_dynamic_queue_match_oracle_and_fixtures():
             got = [min(max(q, 0), 93) for q in r["qvs"]]
             exp = [ord(c) - 33 for c in e["qvs"]]
             assert len(got) == len(exp) and max(abs(a - b) for a, b in zip(got, exp)) <= 1
+
+
+def test_smrtcell_is_generated_per_zmw():
+    """configs[4]'s lazy cell: ZMW i depends only on (seed, i) -- any rank materialises any chunk alone -- and the
+    queue orders the cell by the shapes' cost estimate without generating a sequence."""
+    from pbccs_amd import synth
+    a, b = synth.SmrtCell(40, seed=9), synth.SmrtCell(400, seed=9)
+    for i in (0, 17, 39):
+        assert a[i] == b[i]
+        kind, L, P, snr = a.shape(i)
+        z = a[i]
+        assert z["kind"] == synth.SmrtCell.KINDS[kind] and len(z["reads"]) == P and z["snr"] == list(snr)
+        assert abs(len(z["draft"]) - L) <= 0.05 * L + 5
+    kinds = [b.shape(i)[0] for i in range(400)]
+    assert all(90 <= kinds.count(k) <= 180 for k in range(3))   # one third each
+    chunks = shard.dynamic_chunks(b, 16)
+    assert sorted(i for c in chunks for i in c) == list(range(400))
+    costs = b.costs()
+    flat = [i for c in chunks for i in c]
+    assert [costs[i] for i in flat] == sorted(costs, reverse=True)
+
+
+def test_gloo_world2_dynamic_queue_lazy_cell_keeps_order():
+    """The dynamic queue over a lazily generated cell: each rank materialises only the chunks it pulls (the next
+    one on a helper thread), rank 0's collector thread gathers the other rank's records, input order is kept."""
+    from pbccs_amd import synth
+    cell = synth.SmrtCell(12, seed=5)
+    res, st = _run(2, cell, mode="dynamic", chunk=2)
+    assert [r["draft"] for r in res] == [z["draft"][::-1] for z in cell]
+    assert st["chunks"] == 6 and sum(st["chunks_by_rank"]) == 6 and st["chunks_by_rank"][1] >= 1
+    assert st["gen_ms"] >= 0.0

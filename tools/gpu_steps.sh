@@ -1,0 +1,115 @@
+#!/bin/bash
+# GPU-box step runner (replaces the one-off per-experiment scripts).  Usage, from gpurun:
+#   TAG=r4a bash tools/gpu_steps.sh ubench prof1 trace bench ...
+# Each step has its own time limit; the first failure ends the call (no further GPU step after a fault).
+# Outputs go to gpurun_out/$TAG/.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/${TAG:-steps}
+mkdir -p $OUT
+BENCH="python3 -u bench.py"
+
+summ() {   # one line from a bench JSON
+  python3 - "$1" <<'EOF'
+import json, sys
+d = json.load(open(sys.argv[1]))
+r = d.get("roofline", {})
+print(d.get("value"), "ZMWs/s", "gcups", d.get("gcups"), "ms/step", d.get("ms_per_step"),
+      "dom", r.get("kernel"), "avg_ms", r.get("avg_launch_ms"), "frac", r.get("frac"), "in_flight", r.get("in_flight"))
+EOF
+}
+
+step() {
+  local s=$1
+  case $s in
+    ubench)   # chain-step variants (tools/ubench/chain_step.hip, built in-tree beforehand)
+      timeout -k 10 120 tools/ubench/chain_step > $OUT/ubench.txt 2>&1 && cat $OUT/ubench.txt ;;
+    tests)
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        > $OUT/pytest_gpu.log 2>&1; local rc=$?; tail -3 $OUT/pytest_gpu.log; return $rc ;;
+    smoke)
+      timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && tail -1 $OUT/smoke.log ;;
+    bench)    # the driver's command
+      timeout -k 10 400 $BENCH --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err && summ $OUT/bench.json ;;
+    bench5)
+      timeout -k 10 300 $BENCH --steps 5 --warmup 1 --cpu-sample 0 > $OUT/bench5.json 2> $OUT/bench5.err && summ $OUT/bench5.json ;;
+    prof)     # rocprofv3 kernel summary of the driver's command
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof -o run -- $BENCH --gpus 1 --steps 20 \
+        --warmup 5 --cpu-sample 0 > $OUT/bench_prof.json 2> $OUT/bench_prof.err && summ $OUT/bench_prof.json && \
+        cp "$(find $OUT/prof -name '*kernel_stats.csv' | head -1)" $OUT/kernel_stats.csv ;;
+    prof1)    # single slot: kernel durations that are not time-shared
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof1 -o run -- $BENCH --streams 1 --steps 5 \
+        --warmup 1 --cpu-sample 0 > $OUT/bench_streams1_prof.json 2> $OUT/bench_streams1_prof.err && \
+        summ $OUT/bench_streams1_prof.json && \
+        cp "$(find $OUT/prof1 -name '*kernel_stats.csv' | head -1)" $OUT/streams1_kernel_stats.csv ;;
+    bench1)   # single slot, no profiler
+      timeout -k 10 300 $BENCH --streams 1 --steps 5 --warmup 1 --cpu-sample 0 > $OUT/bench_streams1.json \
+        2> $OUT/bench_streams1.err && summ $OUT/bench_streams1.json ;;
+    trace)    # per-round trace of the driver's command (phase walls per batch round, fill launch sets)
+      PBCCS_ROUND_TRACE=1 PBCCS_FILL_PATHS=1 timeout -k 10 400 $BENCH --gpus 1 --steps 20 --warmup 5 --cpu-sample 0 \
+        > $OUT/trace.json 2> $OUT/trace.err && summ $OUT/trace.json ;;
+    trace1)   # the same, single slot
+      PBCCS_ROUND_TRACE=1 PBCCS_FILL_PATHS=1 timeout -k 10 300 $BENCH --streams 1 --steps 5 --warmup 1 --cpu-sample 0 \
+        > $OUT/trace1.json 2> $OUT/trace1.err && summ $OUT/trace1.json ;;
+    quiver)
+      timeout -k 10 400 $BENCH --stage quiver --steps 5 --warmup 1 > $OUT/quiver.json 2> $OUT/quiver.err && \
+        python3 -c "import json; d=json.load(open('$OUT/quiver.json')); print('quiver', d['value'])" ;;
+    poa)
+      timeout -k 10 400 $BENCH --stage poa --steps 5 --warmup 1 > $OUT/poa.json 2> $OUT/poa.err && \
+        python3 -c "import json; d=json.load(open('$OUT/poa.json')); print('poa', d['value'])" ;;
+    ccs)
+      timeout -k 10 500 $BENCH --stage ccs --steps 5 --warmup 1 > $OUT/ccs.json 2> $OUT/ccs.err && \
+        python3 -c "import json; d=json.load(open('$OUT/ccs.json')); print('ccs', d['value'], d['zmw_status'])" ;;
+    ab_tall)  # interleaved A/B of the tall fill's layout: "G:rows" (PBCCS_TALL_G, PBCCS_TALL_ROWS), 10 steps each
+      local k=0
+      for v in ${VARIANTS:-16:4 64:1 16:4 64:1}; do
+        k=$((k+1))
+        PBCCS_TALL_G=${v%:*} PBCCS_TALL_ROWS=${v#*:} timeout -k 10 300 $BENCH --steps 10 --warmup 2 --cpu-sample 0 \
+          > $OUT/ab_tall_$k.json 2> $OUT/ab_tall_$k.err || return 1
+        echo "tall=$v $(summ $OUT/ab_tall_$k.json)"
+      done ;;
+    tests_fill)   # the fill / checkpoint parity tests only
+      timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_ckpt_gpu.py -m gpu -x -q --timeout 300 \
+        --timeout-method thread > $OUT/pytest_fill.log 2>&1; local rc=$?; tail -3 $OUT/pytest_fill.log; return $rc ;;
+    pmc)      # SQ / GRBM counters, one rocprofv3 pass per group (counter limits per pass: MI355X_MICROARCH.md)
+      local i=0
+      for g in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
+               "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"; do
+        i=$((i+1))
+        timeout -s KILL 240 rocprofv3 --pmc $g -f csv -d $OUT/pmc$i -o pmc -- $BENCH --cpu-sample 0 --no-profile --steps 5 \
+          --warmup 1 > $OUT/pmc$i.json 2> $OUT/pmc$i.err || { echo "pmc pass $i failed"; return 1; }
+      done
+      python3 tools/pmc_summary.py $(find $OUT/pmc1 $OUT/pmc2 -name '*counter_collection.csv') > $OUT/pmc_summary.txt && \
+        head -60 $OUT/pmc_summary.txt ;;
+    traffic)  # HBM bytes of the fills and k_score: FETCH_SIZE and WRITE_SIZE passes (they do not fit one pass)
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o pmc -- $BENCH --cpu-sample 0 --steps 5 \
+        --warmup 1 > $OUT/fetch.json 2> $OUT/fetch.err || { echo "fetch pass failed"; return 1; }
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/write -o pmc -- $BENCH --cpu-sample 0 --steps 5 \
+        --warmup 1 > $OUT/write.json 2> $OUT/write.err || { echo "write pass failed"; return 1; }
+      local F W
+      F=$(find $OUT/fetch -name "*counter_collection.csv" | head -1)
+      W=$(find $OUT/write -name "*counter_collection.csv" | head -1)
+      for k in k_fill_tall k_fill k_score; do
+        python3 tools/pmc_traffic.py "$F" "$W" $OUT/fetch.json $OUT/traffic_${k#k_}.json $k > /dev/null || echo "no $k dispatches"
+      done
+      cat $OUT/traffic_fill_tall.json; gzip -f "$F" "$W" ;;
+    fillread) # per-launch slowest-read diagnostics (PBCCS_FILL_PATHS=2), single slot, per rows-per-lane setting
+      local k=0
+      for v in ${VARIANTS:-16:4 64:1}; do
+        k=$((k+1))
+        PBCCS_TALL_G=${v%:*} PBCCS_TALL_ROWS=${v#*:} PBCCS_FILL_PATHS=2 PBCCS_ROUND_TRACE=1 timeout -k 10 300 $BENCH \
+          --streams 1 --steps 2 --warmup 1 --cpu-sample 0 > $OUT/fillread_$k.json 2> $OUT/fillread_$k.err || return 1
+        echo "tall=$v $(summ $OUT/fillread_$k.json)"; grep "path=2" $OUT/fillread_$k.err | tail -12
+      done ;;
+    *)
+      echo "unknown step $s"; return 2 ;;
+  esac
+}
+
+for s in "$@"; do
+  t0=$(date +%s)
+  echo "== $s"
+  step $s || { echo "step $s failed (rc $?)"; tail -20 $OUT/*.err 2>/dev/null | tail -40; exit 1; }
+  echo "   ($(( $(date +%s) - t0 )) s)"
+done
