@@ -34,11 +34,15 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # PMC HBM bytes per launch of each fill kind (tools/gpu_traffic.sh -> tools/pmc_traffic.py); used only while
 # the kernel sources still hash to the digest the profile was taken at
-TRAFFIC_PROFILES = {"k_fill_tall": "r3_traffic_fill_tall.json", "k_fill": "r3_traffic_fill.json",
-                    "k_score": "r3_traffic_score.json"}
+TRAFFIC_PROFILES = {"k_fill_tall": "r4_traffic_fill_tall.json", "k_fill": "r4_traffic_fill.json",
+                    "k_score": "r4_traffic_score.json"}
+# the same command on one workspace slot (--streams 1): the dominant kernel's launch duration there is not
+# time-shared with other batches' launches; used only while the kernel sources hash to its digest
+SINGLE_SLOT_PROFILE = "r4_streams1_bench.json"
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
 FLOP_PER_CELL = 11             # fill cell 6 mul + 3 add + <= 1 div, + the column rescale
-CHAIN_STEP_CYCLES = 29.7       # one dependent insertion-chain step (tools/ubench/chain_step.hip)
+CHAIN_ROW_CYCLES = 21.5        # one band row of the tall fills' chain at 2 rows per lane (tools/ubench/chain_step.hip
+                               # variant C2; 29.3 with a DPP hand-off per row, profiles/r4a_chain_ubench.txt)
 BEST_SLOTS = 5                 # measured best split of 2 kb batches: 5 slots divide the driver's 20 steps into 4 full waves (6 slots: 2868 vs 3357 ZMWs/s at --steps 20, the last wave half empty)
 BEST_SLOTS_LONG = 8            # configs[2] / [3] through the work queue: 10 kb at 2000 ZMWs 4 / 5 / 8 / 10 / 12 slots 27.5 / 26.3 / 29.1-30.4 / 28.0 / 26.5 ZMWs/s (profiles/r3ad_*, r3af_*); mixed at 240 ZMWs 8 / 12 slots 7.19 / 5.09 (profiles/r3ag_*): more, smaller batches in flight while the tall fills set each round's latency
 SLOT_BYTES_PER_ZMW = 15 << 20  # measured band high-water per 2 kb / 10-pass ZMW in a slot (13.4 MB, exact regrow)
@@ -640,9 +644,12 @@ def make_roofline(stats, local_time, workload):
       time, so this duration is time-shared (`in_flight` = device time / wall time);
     - on wall time: the kernel's algorithmic bytes over the whole timed region / the region's wall time;
     - FP64 VALU: FLOP_PER_CELL x its DP cell-updates over the wall time, against the FP64 vector peak.
-    Neither roof binds: the fill is a serial insertion chain (one dependent DPP + mul + add + add step per row,
-    CHAIN_STEP_CYCLES), so its bound is latency; `binding` says so.  `traffic` = PMC HBM bytes per launch of
-    the same kernel from a committed profile, only while the kernel sources hash to the profile's digest."""
+    Neither roof binds: the fill is a serial insertion chain (per band row a dependent mul + add + add, a DPP
+    hand-off per two rows, CHAIN_ROW_CYCLES), so its bound is latency; `binding` says so.  `traffic` = PMC HBM
+    bytes per launch of the same kernel from a committed profile, only while the kernel sources hash to the
+    profile's digest.  `time_shared` is true when the launches overlap (in_flight > 1); `single_slot` then gives
+    the same kernel's per-launch figure from the committed --streams 1 run of the same sources, whose launches
+    do not overlap."""
     dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["device_ms"])
     launches = max(1, dom["launches"])
     avg_ms = dom["device_ms"] / launches
@@ -663,20 +670,36 @@ def make_roofline(stats, local_time, workload):
                                f"{t['dispatches_fetch_pass']} dispatches, sources {digest})")
             else:
                 traffic_src = f"profiles/{prof} is stale: taken at sources {t.get('source_digest')}, built {digest}"
+    single = None
+    spath = os.path.join(ROOT, "profiles", SINGLE_SLOT_PROFILE)
+    if os.path.exists(spath):
+        s = json.load(open(spath))
+        sr = s.get("roofline", {})
+        if sr.get("kernel") == dom_name and sr.get("source_digest") == digest:
+            single = {"frac": sr.get("frac"), "achieved": sr.get("achieved"), "avg_launch_ms": sr.get("avg_launch_ms"),
+                      "in_flight": sr.get("in_flight"),
+                      "source": f"profiles/{SINGLE_SLOT_PROFILE} (bench.py --streams 1, sources {digest})"}
+        else:
+            single = {"source": f"profiles/{SINGLE_SLOT_PROFILE} is stale: sources {sr.get('source_digest')}, "
+                                f"built {digest}"}
+    in_flight = dom["device_ms"] / (local_time * 1e3) if local_time > 0 else None
     return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_source": traffic_src,
             "kernel": dom_name, "avg_launch_ms": round(avg_ms, 4), "launches": dom["launches"],
             "bytes_per_launch": bytes_per_launch, "cells_per_launch": dom["cells"] / launches,
             "per_launch_note": "achieved/frac: algorithmic bytes per launch / HIP-event launch time on the "
                                "kernel's stream; time-shared when in_flight > 1",
-            "in_flight": round(dom["device_ms"] / (local_time * 1e3), 3) if local_time > 0 else None,
+            "in_flight": round(in_flight, 3) if in_flight is not None else None,
+            "time_shared": bool(in_flight is not None and in_flight > 1.0),
+            "single_slot": single,
             "wall": {"achieved": round(wall_gbs, 3), "frac": round(wall_gbs / HBM_PEAK_GBS, 6), "unit": "GB/s",
                      "note": "the kernel's algorithmic bytes over the timed region / its wall time"},
             "fp64_valu": {"achieved": round(fp64_tf, 4), "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": round(fp64_tf / FP64_VALU_PEAK_TFLOPS, 6),
                           "note": f"{FLOP_PER_CELL} FLOP per DP cell-update over the timed region's wall time"},
-            "binding": f"latency: the serial insertion chain, one dependent DPP + mul + add + add step per band "
-                       f"row (~{CHAIN_STEP_CYCLES} cycles, tools/ubench/chain_step.hip); neither HBM nor FP64 VALU",
+            "binding": f"latency: the serial insertion chain, a dependent mul + add + add per band row and a DPP "
+                       f"hand-off per two rows (~{CHAIN_ROW_CYCLES} cycles per row, tools/ubench/chain_step.hip), plus "
+                       f"the per-chunk band-end logic (DESIGN.md §6); neither HBM nor FP64 VALU",
             "source_digest": digest}
 
 

@@ -1220,6 +1220,22 @@ void orc_context_params(const double* snr, double* out /* 8 x 4: match, stick, b
 
 }  // extern "C"
 
+// Diagnostics (test infrastructure): histogram of read r's final alpha column heights, bins of 8 rows (the last
+// bin counts everything taller).
+extern "C" int orc_scorer_height_hist(void* h, int r, long long* hist, int nbins)
+{
+    MultiReadScorer* s = static_cast<MultiReadScorer*>(h);
+    const ReadState& rs = s->reads.at(r);
+    if (!rs.scorer) return -1;
+    const BandMatrix& m = rs.scorer->alpha;
+    for (int b = 0; b < nbins; ++b) hist[b] = 0;
+    for (int j = 1; j + 1 < m.cols; ++j) {
+        const int hgt = std::max(0, m.ue[j] - m.ub[j]);
+        hist[std::min(nbins - 1, hgt / 8)] += 1;
+    }
+    return 0;
+}
+
 // Diagnostics (test infrastructure): read r's last FillAlphaBeta, one row of 5 per pass (see Recursor::passLog).
 extern "C" int orc_scorer_pass_log(void* h, int r, long long* out, int cap)
 {

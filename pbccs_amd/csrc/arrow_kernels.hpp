@@ -83,9 +83,12 @@ struct CoopFill {
     int readWords = 0;       // nibble-packed read words per group (>= ceil(I / 8) of every read)
     int tplWords = 0;        // nibble-packed template words per group (>= ceil((J + 1) / 8))
     size_t groupBytes = 0;   // coop_group_bytes(hcap, readWords, tplWords)
-    bool prio = true;        // G = 64 waves at raised issue priority
+    bool prio = false;       // waves at raised issue priority (the tall paths: each round's critical path)
     bool chainExit = true;   // G = 64 serial chain leaves a chunk early once its stop row is final
-    int rows = 1;            // G = 64: band rows per lane (1, 2 or 4; a chunk is 64 x rows rows); G = 16: 1
+    int rows = 1;            // band rows per lane (a chunk is G x rows rows)
+    // relative width of the band around the row threshold pm / sdn in which the fill divides (thr_ge, 2^-50 x 3
+    // roundings); tests widen it (PBCCS_FILL_THR_MARGIN) so that the division path runs on most rows
+    double thrMargin = 0x1p-50;
     int regrowSlackDiv = 16;   // regrow_bands: a re-homed region holds need + need / regrowSlackDiv + 64
     // In-kernel band growth: a read whose alpha/beta region overflows takes a larger region pair from
     // the pool's free top (valBump, in values; mapped up to valLimit), copies what it must keep, and
@@ -106,7 +109,7 @@ struct CoopFill {
     long long* trace = nullptr;
 };
 size_t coop_group_bytes(int hcap, int readWords, int tplWords);
-constexpr int kTallGroupLanes = 64;   // tall fills: lanes per read (one read per wavefront)
+constexpr int kNarrowGroupLanes = 16;   // typical bands: lanes per read (four reads per wavefront)
 constexpr int kTallRowsPerLane = 2;   // tall fills: band rows per lane (a 128-row chunk)
 void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* reads, int n, hipStream_t s);
 

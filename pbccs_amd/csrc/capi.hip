@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -31,6 +32,7 @@ using namespace pbccs;
 // buffers, selection scratch, in-kernel growth headroom), and the largest batch (the best 2 kb batch
 // shape measured).
 constexpr double kQueueMargin = 24.0 * (1ull << 30);
+constexpr int kCcsTailPiece = 250;   // smallest piece of the last ccs chunk's polish (pbccs_ccs_batch)
 constexpr int kQueueMaxZmws = 2000;
 // readOf entry of a read the caller did not add (NULL sequence): counted in the drop fraction's
 // denominator only, as the reads Consensus.h:441-471 skips (POA rejected it, or ExtractMappedRead did)
@@ -1832,6 +1834,11 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
         for (int s = 0; s < slots; ++s) eng->Slot(s);
         std::mutex qmu;
         std::condition_variable qcv;
+        // work items (chunk, first, end) over each chunk's polish inputs: a chunk is one item, except the last
+        // one, whose polish is the run's tail with the other slots idle: it is cut into one piece per slot (a
+        // polish batch's time is its refine rounds' latency, ~1.1 s for a few hundred ZMWs against ~1.8 s for
+        // 2000, so parallel pieces shorten the tail; earlier chunks stay whole, their pieces would only queue)
+        std::vector<std::array<int, 3>> work;
         int drafted = 0, next = 0;
         bool stop = false;
         std::vector<int> prc(nb, PBCCS_OK);
@@ -1844,26 +1851,30 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
         };
         auto worker = [&](int slot) {
             for (;;) {
-                int c;
+                std::array<int, 3> w;
                 {
                     std::unique_lock<std::mutex> lk(qmu);
                     qcv.wait(lk, [&] { return stop || next < drafted; });
                     if (next >= drafted) return;   // stopped with nothing left
-                    c = next++;
+                    w = work[next++];
                 }
+                const int c = w[0], lo = w[1], hi = w[2];
                 CcsChunk& C = chunks[c];
-                if (C.pin.empty()) continue;
+                if (hi <= lo) continue;
                 const double p0 = since();
-                prc[c] = polish_span(eng, slot, C.pin.data(), (int)C.pin.size(), &o, C.pout.data());
+                const int rc = polish_span(eng, slot, C.pin.data() + lo, hi - lo, &o, C.pout.data() + lo);
                 if (trace)
-                    std::fprintf(stderr, "[ccs] chunk %d polish slot %d zmws %zu %.1f-%.1f ms\n", c, slot, C.pin.size(),
-                                 p0, since());
-                if (prc[c] != PBCCS_OK && prc[c] != PBCCS_EOOM) {
-                    perr[c] = g_lastError;
+                    std::fprintf(stderr, "[ccs] chunk %d polish slot %d zmws %d %.1f-%.1f ms\n", c, slot, hi - lo, p0,
+                                 since());
+                if (rc != PBCCS_OK) {
                     std::lock_guard<std::mutex> lk(qmu);
-                    stop = true;
-                    qcv.notify_all();
-                    return;
+                    if (prc[c] == PBCCS_OK || rc != PBCCS_EOOM) prc[c] = rc;   // EOOM: the chunk reruns whole below
+                    if (rc != PBCCS_EOOM) {
+                        perr[c] = g_lastError;
+                        stop = true;
+                        qcv.notify_all();
+                        return;
+                    }
                 }
             }
         };
@@ -1897,7 +1908,13 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
             if (rcDraft != PBCCS_OK) {
                 stop = true;
             } else {
-                drafted = c + 1;
+                const int m = (int)chunks[c].pin.size();
+                const char* pe = std::getenv("PBCCS_CCS_TAIL_PIECE");   // test hook: smaller pieces
+                const int piece = pe ? std::max(1, std::atoi(pe)) : kCcsTailPiece;
+                const int pieces = c + 1 < nb ? 1 : std::max(1, std::min(slots, m / piece));
+                for (int k = 0; k < pieces; ++k)
+                    work.push_back({c, (int)((long long)m * k / pieces), (int)((long long)m * (k + 1) / pieces)});
+                drafted = (int)work.size();
             }
             qcv.notify_all();
             if (rcDraft != PBCCS_OK) break;

@@ -36,8 +36,10 @@ template <int G>
 struct Task {
     Group<G> g;
     int I, J, L, start;
-    const unsigned* rdW;   // read bases, nibble-packed
-    const unsigned* tpW;   // template window bases [0, J], nibble-packed
+    const unsigned* rdW;   // read bases, nibble-packed (LDS; G = 4: nullptr, the bases come from rdG)
+    const unsigned* tpW;   // template window bases [0, J], nibble-packed (LDS; G = 4: nullptr, tpG)
+    const char* rdG;       // G = 4: the read's bases in the batch's sequence pool (global memory)
+    const char* tpG;       // G = 4: the strand template from the window start (global memory)
     const double* ctx;     // 9 x kCtxStride transition parameters
     // two ping-pong column buffers: rows [0, hcap) in LDS, rows [hcap, hcap + gRows) in this group's slot of
     // CoopFill::colScratch (gcol: the hybrid 64-lane path, whose columns are never too tall)
@@ -53,6 +55,7 @@ struct Task {
     int slackDiv;              // regrow_bands slack: need / slackDiv
     double prNot, prThird, sdn;
     double sdnInvLow;   // a double strictly below 1 / sdn (early-exit test of the 64-lane chain)
+    double sdnInvHigh;  // a double strictly above 1 / sdn (thr_ge)
     // in-kernel band growth (CoopFill::valBump): pool, bump pointer, mapped limit, descriptor arrays
     int r;
     double* pool;
@@ -64,17 +67,29 @@ struct Task {
 
     // buffer b (0 / 1), row k (no runtime-indexed pointer arrays: they would live in scratch).  The hybrid
     // path selects an LDS or global address per lane and accesses it through one generic (flat) pointer.
+    // (buffer 1 follows buffer 0 in both places: offsets, not a selected pointer member, keep T in registers)
     __device__ __forceinline__ double* cptr(int b, int k) const
     {
-        if (!gcol) return (b ? lds1 : lds0) + k;
-        return k < hcap ? (b ? lds1 : lds0) + k : (b ? glob1 : glob0) + (k - hcap);
+        if (!gcol) return lds0 + (b ? hcap : 0) + k;
+        return k < hcap ? lds0 + (b ? hcap : 0) + k : glob0 + (b ? glob1 - glob0 : 0) + (k - hcap);
     }
     __device__ __forceinline__ double cget(int b, int k) const { return *cptr(b, k); }
     __device__ __forceinline__ void cset(int b, int k, double v) const { *cptr(b, k) = v; }
-    __device__ __forceinline__ int TBase(int idx) const { return nib(tpW, idx); }
+    // template window base idx (nibble code; past the window or the template: kBaseOther) and its context slot
+    __device__ __forceinline__ int TBase(int idx) const
+    {
+        if constexpr (G == 4) return (idx >= 0 && idx <= J && start + idx < L) ? base_code(tpG[idx]) : kBaseOther;
+        else return nib(tpW, max(idx, 0));
+    }
     __device__ __forceinline__ int TCtx(int idx) const
     {
-        return (start + idx + 1 < L) ? ctx_code(nib(tpW, idx), nib(tpW, idx + 1)) : kCtxZero;
+        return (start + idx + 1 < L) ? ctx_code(TBase(idx), TBase(idx + 1)) : kCtxZero;
+    }
+    // read base x (0 <= x < I)
+    __device__ __forceinline__ int RB(int x) const
+    {
+        if constexpr (G == 4) return base_code(rdG[x]);
+        else return nib(rdW, x);
     }
 };
 
@@ -97,6 +112,19 @@ struct PassOut {
 __device__ __forceinline__ void col_fence(bool gcol)
 {
     if (gcol) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+}
+
+// The reference loop's `score >= threshold` with threshold = maxScore / exp(ScoreDiff) (SimpleRecursor.cpp:
+// 110-112), i.e. x >= fl(pm / sdn), without the division: for a normal pm, fl(pm * hi) lies above and fl(pm * lo)
+// below every rounding of pm / sdn (hi / lo are 1 / sdn widened by 2^-50, three roundings cost at most 3 * 2^-53),
+// so both products decide the comparison exactly unless x falls between them -- a band 2^-49 wide around the
+// threshold.  `amb` flags that case (and a pm too small for the bound); the caller divides there.
+__device__ __forceinline__ bool thr_ge(double x, double pm, double lo, double hi, bool& amb)
+{
+    const bool ge = x >= pm * hi;
+    const bool lt = x < pm * lo;
+    amb = pm != 0.0 && (pm < 0x1p-960 || (!ge && !lt));
+    return ge || pm == 0.0;
 }
 
 // ---- band growth ---------------------------------------------------------------------------------
@@ -200,6 +228,8 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     int hb = 1, he = 1;
     int prevCtx = kCtxZero;
     int curBase = T.TBase(0), curCtx = T.TCtx(0);
+    // template bases of the next two columns, loaded one column ahead (G = 4 reads them from global memory)
+    int tA = T.TBase(1), tB = T.TBase(2);
     double myF = 1.0;   // the scale factor of column (block start + lane) of the current G-column block
     // ranges of the guide and of this matrix's previous pass, prefetched one G-column block ahead
     // (a.R(jj) of a later block is read before this pass overwrites it)
@@ -239,7 +269,8 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
             if (sx < sy) { hb = min(sx, hb); he = max(sy, he); }
         }
         const int reqEnd = min(I, he);
-        const int nextBase = T.TBase(j), nextCtx = T.TCtx(j);
+        const int nextBase = tA, nextCtx = (T.start + j + 1 < T.L) ? ctx_code(tA, tB) : kCtxZero;   // TBase / TCtx(j)
+        const int tC = T.TBase(j + 2);   // for the next column
         const double* cp = T.ctx + curCtx * kCtxStride;
         const double* pp = T.ctx + prevCtx * kCtxStride;
         const double pMatch = pp[kM], pDel = pp[kD];
@@ -263,7 +294,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
                         const int i = ib + r;
-                        const int rb = (i >= 1 && i <= I) ? nib(T.rdW, i - 1) : 15;
+                        const int rb = (i >= 1 && i <= I) ? T.RB(i - 1) : 15;
                         const double mpe = pv[r] * (rb == curBase ? T.prNot : T.prThird);
                         m[r] = (i == 1 && j == 1) ? mpe : ((i != 1 && j != 1) ? mpe * pMatch : 0.0);
                         k[r] = (i > 1) ? (rb == nextBase ? cBranch : cStick3) : 0.0;
@@ -328,12 +359,23 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                         pmR[r] = run;
                     }
                 }
+                bool ge[R], amb = false;   // x >= pm / sdn where the test is read (rows past reqEnd - 1)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int i = ib + r;
+                    bool a;
+                    ge[r] = thr_ge(x[r], pmR[r], T.sdnInvLow, T.sdnInvHigh, a);
+                    amb = amb || (a && i + 1 < I && i + 1 >= reqEnd);
+                }
+                if (__ballot(amb) != 0) {   // rare: the quotient itself
+#pragma unroll
+                    for (int r = 0; r < R; ++r) ge[r] = x[r] >= pmR[r] / T.sdn;
+                }
                 int fs = R;   // the lane's first row where the loop stops
 #pragma unroll
                 for (int r = R - 1; r >= 0; --r) {
                     const int i = ib + r;
-                    const double thr = pmR[r] / T.sdn;
-                    const bool cont = (i + 1 < I) && (x[r] >= thr || i + 1 < reqEnd);
+                    const bool cont = (i + 1 < I) && (ge[r] || i + 1 < reqEnd);
                     if (!cont) fs = r;
                 }
                 const unsigned long long stop = T.g.bits(fs < R);
@@ -413,11 +455,13 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         prevCtx = curCtx;
         curBase = nextBase;
         curCtx = nextCtx;
+        tA = tB;
+        tB = tC;
         he = e;
         hb = nhb;
     }
     // pinned final match (:169-179)
-    const double em = (nib(T.rdW, I - 1) == T.TBase(J - 1)) ? T.prNot : T.prThird;
+    const double em = (T.RB(I - 1) == T.TBase(J - 1)) ? T.prNot : T.prThird;
     const double lik = ((I - 1 >= pb && I - 1 < pe) ? T.cget(prev, I - 1 - pb) : 0.0) * em;
     const double c = (0.0 < lik) ? lik : 0.0;
     double v = lik, ls = 0.0;
@@ -464,6 +508,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     long long used = 1, stored = 1;   // cells computed / values kept (column J is always kept)
     int hb = I, he = I;
     int nextBase = T.TBase(J - 1);
+    int tA = T.TBase(J - 2), tB = nextBase;   // TBase(j - 1), TBase(j) of the column ahead, loaded one column early
     double myF = 1.0;   // the scale factor of column (block start - lane) of the current G-column block
     int2 gR = make_int2(0, 0), sR = make_int2(0, 0), gN = make_int2(0, 0), sN = make_int2(0, 0);
     {
@@ -492,7 +537,8 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
             gx = gR.x; gy = gR.y; sx = sR.x; sy = sR.y;
         }
         (void)jb;
-        const int curBase = T.TBase(j - 1), curCtx = T.TCtx(j - 1);
+        const int curBase = tA, curCtx = (T.start + j < T.L) ? ctx_code(tA, tB) : kCtxZero;   // TBase / TCtx(j - 1)
+        const int tC = T.TBase(j - 2);   // for the next column
         if (guide) {
             if (gx < gy) { hb = min(gx, hb); he = max(gy, he); }
         }
@@ -521,7 +567,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
                         const int i = e - 1 - ob - r;
-                        const int nb = (i >= 0 && i < I) ? nib(T.rdW, i) : 15;
+                        const int nb = (i >= 0 && i < I) ? T.RB(i) : 15;
                         const bool same = nb == nextBase;
                         const double mpe = pv[r] * (same ? T.prNot : T.prThird);
                         m[r] = (i < I - 1) ? mpe * cMatch : ((i == I - 1 && j == J - 1) ? mpe : 0.0);
@@ -585,12 +631,23 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                         pmR[r] = run;
                     }
                 }
+                bool ge[R], amb = false;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int i = e - 1 - ob - r;
+                    bool a;
+                    ge[r] = thr_ge(x[r], pmR[r], T.sdnInvLow, T.sdnInvHigh, a);
+                    amb = amb || (a && i - 1 > 0 && i - 1 < reqBegin);
+                }
+                if (__ballot(amb) != 0) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) ge[r] = x[r] >= pmR[r] / T.sdn;
+                }
                 int fs = R;
 #pragma unroll
                 for (int r = R - 1; r >= 0; --r) {
                     const int i = e - 1 - ob - r;
-                    const double thr = pmR[r] / T.sdn;
-                    const bool cont = (i - 1 > 0) && (x[r] >= thr || i - 1 >= reqBegin);
+                    const bool cont = (i - 1 > 0) && (ge[r] || i - 1 >= reqBegin);
                     if (!cont) fs = r;
                 }
                 const unsigned long long stop = T.g.bits(fs < R);
@@ -665,8 +722,10 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         hb = b;
         he = nhe;
         nextBase = curBase;
+        tB = tA;
+        tA = tC;
     }
-    const double em = (T.TBase(0) == nib(T.rdW, 0)) ? T.prNot : T.prThird;
+    const double em = (T.TBase(0) == T.RB(0)) ? T.prNot : T.prThird;
     const double raw = em * ((1 >= pb && 1 < pe) ? T.cget(nxt, pe - 2) : 0.0);
     const double c = (0.0 < raw) ? raw : 0.0;
     double v = raw, ls = 0.0;
@@ -702,7 +761,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     extern __shared__ __align__(16) unsigned char smem[];
     // tall reads are the latency-critical path of every refine round: issue ahead of the 16-lane fills
     // and score waves that share the SIMD (F.prio = 0 leaves the default priority)
-    if ((G == 64 || R > 1) && F.prio) __builtin_amdgcn_s_setprio(3);
+    if (F.prio) __builtin_amdgcn_s_setprio(3);
     const int grp = threadIdx.x / G;
     const int t = blockIdx.x * (64 / G) + grp;
     const int lane = threadIdx.x & (G - 1);
@@ -728,10 +787,12 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
         I = B.rLen[r];
         tv = window_view(B, r);
         J = tv.Length();
-        bad = I < 1 || J < 1 || (I + 7) / 8 > F.readWords || (J + 8) / 8 > F.tplWords;
+        bad = I < 1 || J < 1 || (G != 4 && ((I + 7) / 8 > F.readWords || (J + 8) / 8 > F.tplWords));
         if (!bad) {
             const double* zc = B.zCtx + (long long)z * kCtxDoubles;
             for (int k = lane; k < kCtxDoubles; k += G) ctx[k] = zc[k];
+        }
+        if (!bad && G != 4) {   // G = 4 reads its bases from global memory (16 reads per wavefront: LDS per read is short)
             const char* rd = B.seqPool + B.rSeqOff[r];
             for (int w = lane; w < (I + 7) / 8; w += G) {
                 unsigned word = 0;
@@ -768,6 +829,8 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     T.start = tv.start;
     T.rdW = rdW;
     T.tpW = tpW;
+    T.rdG = B.seqPool + B.rSeqOff[r];
+    T.tpG = tv.T + tv.start;
     T.ctx = ctx;
     T.lds0 = col;
     T.lds1 = col + F.hcap;
@@ -782,7 +845,8 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     T.prNot = B.prNot;
     T.prThird = B.prThird;
     T.sdn = B.sdn;
-    T.sdnInvLow = (1.0 / B.sdn) * (1.0 - 0x1p-50);
+    T.sdnInvLow = (1.0 / B.sdn) * (1.0 - F.thrMargin);
+    T.sdnInvHigh = (1.0 / B.sdn) * (1.0 + F.thrMargin);
     T.r = r;
     T.pool = B.valPool;
     T.bump = F.valBump;
@@ -850,9 +914,10 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
         else o = coop_beta<G, R>(T, bm, a, guided, self, ovf, ua);
         if (o.tall) return fail_tall();
         if (o.regrow) {   // exact region for this pass, then run it again (count-only if the pool is full)
-            if (++regrows > 8 ||
-                !regrow_bands<G>(T, doAlpha ? a : bm, doAlpha ? bm : a, doAlpha, o.stored, doAlpha ? sb : sa))
-                ovf = true;
+            // (two calls, not a selected reference: the bands then stay in registers)
+            const bool moved = ++regrows <= 8 && (doAlpha ? regrow_bands<G>(T, a, bm, true, o.stored, sb)
+                                                          : regrow_bands<G>(T, bm, a, false, o.stored, sa));
+            if (!moved) ovf = true;
             --step;
             continue;
         }
@@ -915,6 +980,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
 
 size_t coop_group_bytes(int hcap, int readWords, int tplWords)
 {
+    // (G = 4 groups keep no read or template in LDS: the caller passes 0 words)
     size_t b = (size_t)(2 * hcap + kCtxDoubles + 1) * sizeof(double) + (size_t)(readWords + tplWords) * 4;
     return (b + 15) & ~(size_t)15;
 }
@@ -929,9 +995,10 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     const bool gc = F.colScratch != nullptr;
     // two waves per SIMD: the register budget that leaves these kernels without spills (higher occupancy
     // was measured slower and needs a private segment, which the resource check in the Makefile forbids)
-    // (G, rows per lane, hybrid): the 16-lane narrow path (16, 1), tall paths with four reads per wavefront
-    // (16, 4) or one (64, 1 / 2 / 4); the hybrid kernels at R = 4 need more than 256 registers and run R = 2 (the
-    // column buffers hold whole chunks either way)
+    // (G, rows per lane, hybrid): the narrow path with four reads per wavefront (16, 1) or sixteen (4, 4), the tall
+    // paths one read per wavefront (64, 1 / 2 / 4); the hybrid kernel at R = 4 needs more than 256 registers and
+    // runs R = 2 (the column buffers hold whole chunks either way).  Four tall reads per wavefront (16, 4) measured
+    // half the speed per read (profiles/r4e_tall_grouped_ab.txt) and were removed.
     const int R = gc ? std::min(F.rows, 2) : F.rows;
     struct Entry {
         int g, r;
@@ -940,8 +1007,8 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
         bool attr;
     };
     static Entry ks[] = {
-        {16, 1, false, (K)k_fill_coop<16, 2, false, 1>, false}, {16, 4, false, (K)k_fill_coop<16, 2, false, 4>, false},
-        {16, 2, true, (K)k_fill_coop<16, 2, true, 2>, false},   {64, 1, false, (K)k_fill_coop<64, 2, false, 1>, false},
+        {4, 4, false, (K)k_fill_coop<4, 2, false, 4>, false},   {16, 1, false, (K)k_fill_coop<16, 2, false, 1>, false},
+        {64, 1, false, (K)k_fill_coop<64, 2, false, 1>, false},
         {64, 2, false, (K)k_fill_coop<64, 2, false, 2>, false}, {64, 4, false, (K)k_fill_coop<64, 2, false, 4>, false},
         {64, 1, true, (K)k_fill_coop<64, 2, true, 1>, false},   {64, 2, true, (K)k_fill_coop<64, 2, true, 2>, false}};
     Entry* e = nullptr;

@@ -201,6 +201,20 @@ def test_zmw6251_survey_probe_record_on_gpu(P):
     assert r["consensus"] == o["template"]
 
 
+def test_fills_with_threshold_division_path_match_oracle(P, monkeypatch):
+    """The fill's row-threshold test (x >= pm / sdn) runs as two products with a division only in a 2^-49 band
+    around the quotient; PBCCS_FILL_THR_MARGIN widens that band to 2^-4 so the division path decides most rows:
+    per-read LL and flip-flop counts stay equal to the oracle, tall reads included."""
+    from pbccs_amd import synth
+    monkeypatch.setenv("PBCCS_FILL_THR_MARGIN", "0.0625")
+    for z in synth.make_zmws(2, 2000, 10, seed=62):
+        g, o, rg, ro = _scorers(P, z["draft"], z["reads"])
+        assert rg == ro
+        assert g.NumFlipFlops() == [o.read_info(k)["flipflops"] for k in range(len(z["reads"]))]
+        for x, y in zip(g.BaselineScores(), [o.read_info(k)["ll"] for k in range(len(z["reads"]))]):
+            assert _close(x, y, 1e-12, 1e-12)
+
+
 def test_fills_2kb_match_oracle(P):
     """Full-size (configs[1]) fills: per-read LL and flip-flop counts, including the reads whose first
     band explodes past 4% of the matrix (the 5-pass reband path, ~one read per ZMW at 2 kb) and the

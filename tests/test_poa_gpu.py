@@ -281,6 +281,16 @@ def test_native_ccs_batch_pipelined_chunks(P):
     many = driver.ccs_batch(chunks, ConsensusSettings(zmws_per_batch=3), engine=eng)
     assert json.dumps(many) == json.dumps(one)   # NaN z-scores (reads never added) compare equal as text
     assert one[4]["status"] == "NoSubreads"
+    # the last chunk's polish cut into one piece per slot (PBCCS_CCS_TAIL_PIECE: pieces of 2 ZMWs here)
+    import pbccs_amd
+    os.environ["PBCCS_CCS_TAIL_PIECE"] = "2"
+    try:
+        e3 = pbccs_amd.Engine(0)
+        e3.set_concurrency(3)
+        pieces = driver.ccs_batch(chunks, ConsensusSettings(zmws_per_batch=5), engine=e3)
+    finally:
+        del os.environ["PBCCS_CCS_TAIL_PIECE"]
+    assert json.dumps(pieces) == json.dumps(one)
 
 
 def test_poa_stats_counted(P):

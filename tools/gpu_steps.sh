@@ -63,7 +63,7 @@ step() {
         python3 -c "import json; d=json.load(open('$OUT/ccs.json')); print('ccs', d['value'], d['zmw_status'])" ;;
     ab_tall)  # interleaved A/B of the tall fill's layout: "G:rows" (PBCCS_TALL_G, PBCCS_TALL_ROWS), 10 steps each
       local k=0
-      for v in ${VARIANTS:-16:4 64:1 16:4 64:1}; do
+      for v in ${VARIANTS:-64:2 64:1 64:2 64:1}; do
         k=$((k+1))
         PBCCS_TALL_G=${v%:*} PBCCS_TALL_ROWS=${v#*:} timeout -k 10 300 $BENCH --steps 10 --warmup 2 --cpu-sample 0 \
           > $OUT/ab_tall_$k.json 2> $OUT/ab_tall_$k.err || return 1
@@ -94,9 +94,17 @@ step() {
         python3 tools/pmc_traffic.py "$F" "$W" $OUT/fetch.json $OUT/traffic_${k#k_}.json $k > /dev/null || echo "no $k dispatches"
       done
       cat $OUT/traffic_fill_tall.json; gzip -f "$F" "$W" ;;
+    ab_narrow)  # interleaved A/B of the narrow fill's layout (PBCCS_NARROW_G 16 / 4), 10 steps each
+      local k=0
+      for v in ${VARIANTS:-4 16 4 16}; do
+        k=$((k+1))
+        PBCCS_NARROW_G=$v timeout -k 10 300 $BENCH --steps 10 --warmup 2 --cpu-sample 0 > $OUT/ab_narrow_$k.json \
+          2> $OUT/ab_narrow_$k.err || return 1
+        echo "narrow=$v $(summ $OUT/ab_narrow_$k.json) fill16_ms $(python3 -c "import json; d=json.load(open('$OUT/ab_narrow_$k.json')); k=d['kernels']['k_fill']; print(round(k['device_ms']/max(1,k['launches']),2), k['launches'])")"
+      done ;;
     fillread) # per-launch slowest-read diagnostics (PBCCS_FILL_PATHS=2), single slot, per rows-per-lane setting
       local k=0
-      for v in ${VARIANTS:-16:4 64:1}; do
+      for v in ${VARIANTS:-64:2 64:1}; do
         k=$((k+1))
         PBCCS_TALL_G=${v%:*} PBCCS_TALL_ROWS=${v#*:} PBCCS_FILL_PATHS=2 PBCCS_ROUND_TRACE=1 timeout -k 10 300 $BENCH \
           --streams 1 --steps 2 --warmup 1 --cpu-sample 0 > $OUT/fillread_$k.json 2> $OUT/fillread_$k.err || return 1
