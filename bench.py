@@ -712,6 +712,13 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
         statuses[r["status"]] = statuses.get(r["status"], 0) + 1
 
     value = total_zmws / job_time
+    n_gated = sum(v for k, v in statuses.items() if k in ("TooFewPasses", "TooManyUnusable", "NoSubreads", "TooShort"))
+    n_polished = sum(statuses.values()) - n_gated
+    if world > 1 and scaling == "weak":   # each rank holds its own records: sum the counts
+        import torch
+        t = torch.tensor([n_polished, n_gated], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        n_polished, n_gated = int(t[0].item()), int(t[1].item())
     cells = sum(s["cells"] for s in stats.values())
     gcups_local = cells / local_time / 1e9 if local_time > 0 else 0.0
     gcups = gcups_local * world
@@ -748,6 +755,10 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
                    "parallelism": f"zmw-shard x{world}"},
         "gcups": round(gcups, 3),
         "zmw_status": statuses,
+        # ZMWs that reached RefineConsensus (Consensus.h:493-512) against those the AddRead gates dropped before
+        # it (TooFewPasses / TooManyUnusable): the polish rate of the configs[3] mix is the first figure
+        "polished": {"zmws": n_polished, "zmws_per_s": round(n_polished / job_time, 3) if job_time > 0 else None,
+                     "gated_zmws": n_gated},
         "roofline": roofline,
         "kernels": {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
                         "gcells": round(v["cells"] / 1e9, 4), "gbytes": round(v["bytes"] / 1e9, 4)}

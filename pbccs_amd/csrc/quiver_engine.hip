@@ -126,6 +126,12 @@ QuiverBatch::~QuiverBatch()
     if (evJoin_) (void)hipEventDestroy(evJoin_);
 }
 
+void QuiverBatch::grow_scratch(unsigned long long requested)
+{
+    size_t want = std::max<size_t>((size_t)dScratch_.cap * 2, (size_t)(requested + requested / 8));
+    dScratch_.reserve(want, false);
+}
+
 void QuiverBatch::Reset()
 {
     QHIP(hipSetDevice(device_));
@@ -588,11 +594,13 @@ void QuiverBatch::RunScore(const std::vector<int>& tr, const std::vector<int>& t
         launch_qscore(View(), W, stream_);
         QHIP(hipGetLastError());
         int ovf = 0;
+        unsigned long long top = 0;
         QHIP(hipMemcpyAsync(&ovf, dOverflow_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
+        QHIP(hipMemcpyAsync(&top, dScratchTop_.ptr, sizeof(top), hipMemcpyDeviceToHost, stream_));
         QHIP(hipStreamSynchronize(stream_));
         if (!ovf) break;
         if ((ovf & 2) || attempt > 6) throw DeviceError("quiver extend buffer exceeds 8 columns / scratch");
-        dScratch_.reserve(dScratch_.cap * 4, false);
+        grow_scratch(top);
     }
     get(*out, dDelta_, tr.size(), stream_);
     QHIP(hipStreamSynchronize(stream_));
@@ -874,11 +882,13 @@ void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std:
             launch_qscore(View(), W, stream_);
             QHIP(hipGetLastError());
             int ovf = 0;
+            unsigned long long top = 0;
             QHIP(hipMemcpyAsync(&ovf, dOverflow_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
+            QHIP(hipMemcpyAsync(&top, dScratchTop_.ptr, sizeof(top), hipMemcpyDeviceToHost, stream_));
             QHIP(hipStreamSynchronize(stream_));
             if (!ovf) break;
             if ((ovf & 2) || attempt > 6) throw DeviceError("quiver extend buffer exceeds 8 columns / scratch");
-            dScratch_.reserve(dScratch_.cap * 4, false);
+            grow_scratch(top);
         }
         t0 += m;
     }

@@ -177,6 +177,9 @@ private:
                      std::vector<long long>* taskStart, std::vector<long long>* mutStart);
     void ScoreRound(const std::vector<int>& zs, const std::vector<std::vector<int>>& codes, int sep,
                     std::vector<std::vector<Scored>>* fav, std::vector<std::vector<Scored>>* picked);
+    // after a scoring launch whose extension scratch overflowed: grow it to the floats the launch asked for
+    // (the kernel's bump counter keeps counting past the cap) plus an eighth, so the rerun fits
+    void grow_scratch(unsigned long long requested);
 
     int device_ = 0;
     hipStream_t stream_ = nullptr;
