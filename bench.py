@@ -571,19 +571,32 @@ def ccs_cpu_baseline(args, n):
             return "TooShort"
         mapped = [driver.extract_mapped_read(reads[i], p["summaries"][k], 10)
                   for i, k in enumerate(p["keys"]) if k >= 0]
-        O.polish_zmw(p["consensus"], [m for m in mapped if m is not None], c["snr"])
+        # Consensus.h:474-491's gates, as pbccs_ccs_batch applies them: reads FilterReads, the POA or
+        # ExtractMappedRead dropped count in the drop fraction's denominator only
+        sc = O.Scorer(p["consensus"], c["snr"])
+        st = [sc.add_read(m["seq"], m["strand"], m["ts"], m["te"], -5.0) for m in mapped if m is not None]
+        ok = sum(1 for x in st if x == 0)
+        if ok < 3:
+            return "TooFewPasses"
+        if (len(st) - ok) / len(c["reads"]) > 0.34:
+            return "TooManyUnusable"
+        sc.zscores()
+        if not sc.refine(40, 10, 20)["converged"]:
+            return "NonConvergent"
+        sc.qvs()
         return "Polished"
 
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=threads) as ex:
-        list(ex.map(one, chunks))
+        status = list(ex.map(one, chunks))
     dt = time.perf_counter() - t0
+    counts = {k: status.count(k) for k in sorted(set(status))}
     return {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
-            "nproc": os.cpu_count(),
+            "nproc": os.cpu_count(), "zmw_status": counts,
             "sample": f"{n} synthetic ZMWs of the same config (seed {args.seed + 99991}): FilterReads, "
-                      f"oracle/poa_oracle.cpp SparsePoa, ExtractMappedRead, oracle/arrow_oracle.cpp polish (AddRead, "
-                      f"RefineConsensus, ConsensusQVs; every ZMW polished, the gates not applied) one ZMW per task "
-                      f"on {threads} host threads, {dt:.1f} s wall"}
+                      f"oracle/poa_oracle.cpp SparsePoa, ExtractMappedRead, oracle/arrow_oracle.cpp AddRead, the "
+                      f"TooFewPasses / TooManyUnusable gates, RefineConsensus and ConsensusQVs of converged ZMWs, one "
+                      f"ZMW per task on {threads} host threads, {dt:.1f} s wall"}
 
 
 def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
@@ -628,7 +641,7 @@ def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
            "zmw_status": statuses, "poa_wall_ms": round(st["total_ms"], 1),
            "poa_device_ms": round(st["device_ms"], 1), "poa_thread_ms": round(st["thread_ms"], 1)}
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        out["cpu_baseline"] = ccs_cpu_baseline(args, min(args.cpu_sample, 64))
+        out["cpu_baseline"] = ccs_cpu_baseline(args, min(args.cpu_sample, 160))
         out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
     if rank == 0:
         emit(out)

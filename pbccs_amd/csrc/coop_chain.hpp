@@ -37,10 +37,7 @@ __device__ __forceinline__ double dpp_d(double old, double x)
 template <int G>
 __device__ __forceinline__ double shift_up(double x, double first)
 {
-    if constexpr (G == 4) {   // quad_perm [0,0,1,2]: lane q of a quad takes lane q - 1; the quad's lane 0 takes `first`
-        const double s = dpp_d<0x90, 0xF, false>(x, x);
-        return (__lane_id() & 3) == 0 ? first : s;
-    } else if constexpr (G == 16) {
+    if constexpr (G == 16) {
         return dpp_d<0x111, 0xF, false>(first, x);   // row_shr:1
     } else {
         return dpp_d<0x138, 0xF, false>(first, x);   // wave_shr:1
@@ -51,11 +48,6 @@ __device__ __forceinline__ double shift_up(double x, double first)
 template <int G>
 __device__ __forceinline__ double prefix_max(double x)
 {
-    if constexpr (G == 4) {   // within each quad: quad_perm [0,0,1,2] then [0,0,0,1] (lane 0 takes its own value)
-        x = fmax(x, dpp_d<0x90, 0xF, false>(x, x));
-        x = fmax(x, dpp_d<0x40, 0xF, false>(x, x));
-        return x;
-    }
     x = fmax(x, dpp_d<0x111, 0xF, true>(0.0, x));
     x = fmax(x, dpp_d<0x112, 0xF, true>(0.0, x));
     x = fmax(x, dpp_d<0x114, 0xF, true>(0.0, x));
@@ -87,10 +79,6 @@ struct Group {
             const int lo = __builtin_amdgcn_readlane(__double2loint(x), src);
             const int hi = __builtin_amdgcn_readlane(__double2hiint(x), src);
             return __hiloint2double(hi, lo);
-        } else if constexpr (G == 4) {   // the four quad_perm broadcasts and a select: no LDS round trip
-            const double b0 = dpp_d<0x00, 0xF, false>(x, x), b1 = dpp_d<0x55, 0xF, false>(x, x);
-            const double b2 = dpp_d<0xAA, 0xF, false>(x, x), b3 = dpp_d<0xFF, 0xF, false>(x, x);
-            return src == 0 ? b0 : src == 1 ? b1 : src == 2 ? b2 : b3;
         } else {
             return __shfl(x, src, G);
         }
@@ -99,12 +87,6 @@ struct Group {
     {
         if constexpr (G == 64) {
             return __builtin_amdgcn_readlane(x, src);
-        } else if constexpr (G == 4) {
-            const int b0 = __builtin_amdgcn_update_dpp(x, x, 0x00, 0xF, 0xF, false);
-            const int b1 = __builtin_amdgcn_update_dpp(x, x, 0x55, 0xF, 0xF, false);
-            const int b2 = __builtin_amdgcn_update_dpp(x, x, 0xAA, 0xF, 0xF, false);
-            const int b3 = __builtin_amdgcn_update_dpp(x, x, 0xFF, 0xF, 0xF, false);
-            return src == 0 ? b0 : src == 1 ? b1 : src == 2 ? b2 : b3;
         } else {
             return __shfl(x, src, G);
         }
@@ -115,8 +97,6 @@ struct Group {
     {
         if constexpr (G == 64) {
             return bcast(x, 63);
-        } else if constexpr (G == 4) {   // quad_perm [3,3,3,3]
-            return dpp_d<0xFF, 0xF, false>(x, x);
         } else {
             const long long r = __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x15F, 0xF, 0xF, false);
             return __longlong_as_double(r);

@@ -710,21 +710,22 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     // Tall bands run on 64 lanes (one read per wavefront).  16-lane groups for them (4x fewer VALU issue
     // slots per chain step) measured 1290 against 2480 ZMWs/s and were removed: the tall reads are each
     // round's critical path and 16-row chunks pay the per-chunk band logic 4x as often.
-    // Tall paths: one read per wavefront, rows per lane PBCCS_TALL_ROWS (1 / 2 / 4, A/B); a column buffer holds
-    // whole chunks of 64 x rows rows.
+    // Tall paths: one read per wavefront, rows per lane PBCCS_TALL_ROWS (1 / 2, A/B; 4 measured slowest in every
+    // A/B, profiles/r4c_tall_rows_ab.txt, and was removed); a column buffer holds whole chunks of 64 x rows rows.
     constexpr int tallG = 64;
-    static const int tallRows = env_int("PBCCS_TALL_ROWS", kTallRowsPerLane);
+    static const int tallRows = env_int("PBCCS_TALL_ROWS", kTallRowsPerLane) == 1 ? 1 : 2;
     const long long chunk = (long long)tallG * tallRows;
     const long long tallGroupLds = (long long)kCoopLdsBytes;
     auto full_rows = [&](int maxI) { return ((long long)maxI + chunk) / chunk * chunk; };   // >= I + 1 rows
-    // Narrow path: lanes per read (PBCCS_NARROW_G: 16 = four reads per wavefront, one row per lane; 4 = sixteen
-    // reads per wavefront, four rows per lane, read and template bases from global memory)
-    static const int narrowG = env_int("PBCCS_NARROW_G", kNarrowGroupLanes) == 4 ? 4 : 16;
-    static const int narrowRows = narrowG == 4 ? 4 : 1;
+    // Narrow path: 16 lanes per read (four reads per wavefront), rows per lane PBCCS_NARROW_ROWS (1 or 2: a 16- or
+    // 32-row chunk; A/B).  Sixteen reads per wavefront (4 lanes x 4 rows, bases from global memory) measured 0.68x
+    // per launch (profiles/r4g_narrow_ab.txt) and were removed.
+    constexpr int narrowG = kNarrowGroupLanes;
+    static const int narrowRows = env_int("PBCCS_NARROW_ROWS", 1) == 2 ? 2 : 1;
     auto rows_for = [&](int p, int maxI, int w) -> int {
         if (p == 0) return 0;
         if (p == 1)
-            return (64 / narrowG) * coop_group_bytes(kCoopNarrowRows, narrowG == 4 ? 0 : w, 0) <= kCoopLdsBytes
+            return (64 / narrowG) * coop_group_bytes(kCoopNarrowRows, w, 0) <= kCoopLdsBytes
                        ? kCoopNarrowRows : 0;
         const long long room = (tallGroupLds - (long long)coop_group_bytes(0, w, 0)) / 16 / 64 * 64;
         const long long full = full_rows(maxI);   // a column never exceeds I + 1 rows
@@ -862,7 +863,6 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             const int G = p == 1 ? narrowG : tallG;
             F.rows = p == 1 ? narrowRows : tallRows;
             F.prio = p >= 2;
-            if (G == 4) F.readWords = F.tplWords = 0;   // bases from global memory
             if (const char* e = std::getenv("PBCCS_FILL_THR_MARGIN"))   // test hook, read per launch
                 F.thrMargin = std::max(0x1p-50, std::atof(e));
             F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);

@@ -36,10 +36,8 @@ template <int G>
 struct Task {
     Group<G> g;
     int I, J, L, start;
-    const unsigned* rdW;   // read bases, nibble-packed (LDS; G = 4: nullptr, the bases come from rdG)
-    const unsigned* tpW;   // template window bases [0, J], nibble-packed (LDS; G = 4: nullptr, tpG)
-    const char* rdG;       // G = 4: the read's bases in the batch's sequence pool (global memory)
-    const char* tpG;       // G = 4: the strand template from the window start (global memory)
+    const unsigned* rdW;   // read bases, nibble-packed (LDS)
+    const unsigned* tpW;   // template window bases [0, J], nibble-packed (LDS)
     const double* ctx;     // 9 x kCtxStride transition parameters
     // two ping-pong column buffers: rows [0, hcap) in LDS, rows [hcap, hcap + gRows) in this group's slot of
     // CoopFill::colScratch (gcol: the hybrid 64-lane path, whose columns are never too tall)
@@ -78,8 +76,7 @@ struct Task {
     // template window base idx (nibble code; past the window or the template: kBaseOther) and its context slot
     __device__ __forceinline__ int TBase(int idx) const
     {
-        if constexpr (G == 4) return (idx >= 0 && idx <= J && start + idx < L) ? base_code(tpG[idx]) : kBaseOther;
-        else return nib(tpW, max(idx, 0));
+        return nib(tpW, max(idx, 0));
     }
     __device__ __forceinline__ int TCtx(int idx) const
     {
@@ -88,8 +85,7 @@ struct Task {
     // read base x (0 <= x < I)
     __device__ __forceinline__ int RB(int x) const
     {
-        if constexpr (G == 4) return base_code(rdG[x]);
-        else return nib(rdW, x);
+        return nib(rdW, x);
     }
 };
 
@@ -228,7 +224,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     int hb = 1, he = 1;
     int prevCtx = kCtxZero;
     int curBase = T.TBase(0), curCtx = T.TCtx(0);
-    // template bases of the next two columns, loaded one column ahead (G = 4 reads them from global memory)
+    // template bases of the next two columns, loaded one column ahead
     int tA = T.TBase(1), tB = T.TBase(2);
     double myF = 1.0;   // the scale factor of column (block start + lane) of the current G-column block
     // ranges of the guide and of this matrix's previous pass, prefetched one G-column block ahead
@@ -787,12 +783,12 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
         I = B.rLen[r];
         tv = window_view(B, r);
         J = tv.Length();
-        bad = I < 1 || J < 1 || (G != 4 && ((I + 7) / 8 > F.readWords || (J + 8) / 8 > F.tplWords));
+        bad = I < 1 || J < 1 || (I + 7) / 8 > F.readWords || (J + 8) / 8 > F.tplWords;
         if (!bad) {
             const double* zc = B.zCtx + (long long)z * kCtxDoubles;
             for (int k = lane; k < kCtxDoubles; k += G) ctx[k] = zc[k];
         }
-        if (!bad && G != 4) {   // G = 4 reads its bases from global memory (16 reads per wavefront: LDS per read is short)
+        if (!bad) {
             const char* rd = B.seqPool + B.rSeqOff[r];
             for (int w = lane; w < (I + 7) / 8; w += G) {
                 unsigned word = 0;
@@ -829,8 +825,6 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     T.start = tv.start;
     T.rdW = rdW;
     T.tpW = tpW;
-    T.rdG = B.seqPool + B.rSeqOff[r];
-    T.tpG = tv.T + tv.start;
     T.ctx = ctx;
     T.lds0 = col;
     T.lds1 = col + F.hcap;
@@ -980,7 +974,6 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
 
 size_t coop_group_bytes(int hcap, int readWords, int tplWords)
 {
-    // (G = 4 groups keep no read or template in LDS: the caller passes 0 words)
     size_t b = (size_t)(2 * hcap + kCtxDoubles + 1) * sizeof(double) + (size_t)(readWords + tplWords) * 4;
     return (b + 15) & ~(size_t)15;
 }
@@ -995,10 +988,13 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     const bool gc = F.colScratch != nullptr;
     // two waves per SIMD: the register budget that leaves these kernels without spills (higher occupancy
     // was measured slower and needs a private segment, which the resource check in the Makefile forbids)
-    // (G, rows per lane, hybrid): the narrow path with four reads per wavefront (16, 1) or sixteen (4, 4), the tall
-    // paths one read per wavefront (64, 1 / 2 / 4); the hybrid kernel at R = 4 needs more than 256 registers and
-    // runs R = 2 (the column buffers hold whole chunks either way).  Four tall reads per wavefront (16, 4) measured
-    // half the speed per read (profiles/r4e_tall_grouped_ab.txt) and were removed.
+    // (G, rows per lane, hybrid): the narrow path with four reads per wavefront (16, 1 / 2; sixteen, (4, 4) with
+    // the bases in global memory, measured 0.68x per launch, profiles/r4g_narrow_ab.txt, and was removed), the tall
+    // paths one read per wavefront (64, 1 / 2; R = 4 measured slowest, profiles/r4c_tall_rows_ab.txt, and was
+    // removed); the hybrid kernel runs R <= 2 (the column buffers hold whole chunks either way).  Four tall reads
+    // per wavefront (16, 4) measured half the speed per read (profiles/r4e_tall_grouped_ab.txt) and were removed.
+    // (Scaling by a reciprocal and two FMA corrections -- bit-identical -- instead of the division measured 4%
+    // slower, profiles/r4h_coldiv_ab.txt, and was removed.)
     const int R = gc ? std::min(F.rows, 2) : F.rows;
     struct Entry {
         int g, r;
@@ -1007,9 +1003,10 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
         bool attr;
     };
     static Entry ks[] = {
-        {4, 4, false, (K)k_fill_coop<4, 2, false, 4>, false},   {16, 1, false, (K)k_fill_coop<16, 2, false, 1>, false},
+        {16, 1, false, (K)k_fill_coop<16, 2, false, 1>, false},
+        {16, 2, false, (K)k_fill_coop<16, 2, false, 2>, false},
         {64, 1, false, (K)k_fill_coop<64, 2, false, 1>, false},
-        {64, 2, false, (K)k_fill_coop<64, 2, false, 2>, false}, {64, 4, false, (K)k_fill_coop<64, 2, false, 4>, false},
+        {64, 2, false, (K)k_fill_coop<64, 2, false, 2>, false},
         {64, 1, true, (K)k_fill_coop<64, 2, true, 1>, false},   {64, 2, true, (K)k_fill_coop<64, 2, true, 2>, false}};
     Entry* e = nullptr;
     for (Entry& x : ks)

@@ -61,6 +61,21 @@ step() {
     ccs)
       timeout -k 10 500 $BENCH --stage ccs --steps 5 --warmup 1 > $OUT/ccs.json 2> $OUT/ccs.err && \
         python3 -c "import json; d=json.load(open('$OUT/ccs.json')); print('ccs', d['value'], d['zmw_status'])" ;;
+    prof10k)  # configs[2] at 2000 ZMWs through the work queue, rocprofv3 kernel summary
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof10k -o run -- $BENCH --workload 10kb \
+        --steps 1 --zmws-per-step 2000 --warmup 0 > $OUT/bench_10kb.json 2> $OUT/bench_10kb.err && \
+        summ $OUT/bench_10kb.json && \
+        cp "$(find $OUT/prof10k -name '*kernel_stats.csv' | head -1)" $OUT/10kb_kernel_stats.csv ;;
+    bench10k) # configs[2] at ZMWS10K ZMWs (default 10000), no profiler, progress on stderr
+      timeout -k 10 1000 $BENCH --workload 10kb --steps 1 --zmws-per-step ${ZMWS10K:-10000} --warmup 0 \
+        > $OUT/bench_10kb_big.json 2> $OUT/bench_10kb_big.err && summ $OUT/bench_10kb_big.json ;;
+    mixed)    # configs[3] at 2000 ZMWs
+      timeout -k 10 900 $BENCH --workload mixed --steps 1 --zmws-per-step 2000 --warmup 0 > $OUT/bench_mixed.json \
+        2> $OUT/bench_mixed.err && summ $OUT/bench_mixed.json ;;
+    cell2)    # configs[4]: two ranks sharing the one device (a rehearsal of the multi-rank queue), CELLN ZMWs
+      PBCCS_BENCH_DEVICE=0 timeout -k 10 1000 $BENCH --gpus 2 --workload smrtcell --steps 1 \
+        --zmws-per-step ${CELLN:-10000} --warmup 0 --streams 4 > $OUT/bench_cell2.json 2> $OUT/bench_cell2.err && \
+        summ $OUT/bench_cell2.json ;;
     ab_tall)  # interleaved A/B of the tall fill's layout: "G:rows" (PBCCS_TALL_G, PBCCS_TALL_ROWS), 10 steps each
       local k=0
       for v in ${VARIANTS:-64:2 64:1 64:2 64:1}; do
@@ -94,13 +109,23 @@ step() {
         python3 tools/pmc_traffic.py "$F" "$W" $OUT/fetch.json $OUT/traffic_${k#k_}.json $k > /dev/null || echo "no $k dispatches"
       done
       cat $OUT/traffic_fill_tall.json; gzip -f "$F" "$W" ;;
-    ab_narrow)  # interleaved A/B of the narrow fill's layout (PBCCS_NARROW_G 16 / 4), 10 steps each
+    ab_lib)   # interleaved A/B of two in-tree builds (PBCCS_LIB; LIBS="a b" paths), 10 steps each, plus k_score / fill ms
       local k=0
-      for v in ${VARIANTS:-4 16 4 16}; do
+      for v in ${LIBS:-pbccs_amd/_lib/libpbccs_amd.so pbccs_amd/_lib_ab/libpbccs_amd.so} ; do
+        for rep in 1 2; do
+          k=$((k+1))
+          PBCCS_LIB=$v timeout -k 10 300 $BENCH --steps 10 --warmup 2 --cpu-sample 0 ${ABARGS:-} > $OUT/ab_lib_$k.json \
+            2> $OUT/ab_lib_$k.err || return 1
+          echo "lib=$v $(summ $OUT/ab_lib_$k.json) $(python3 -c "import json; d=json.load(open('$OUT/ab_lib_$k.json')); print({n: round(v['device_ms']/max(1,v['launches']),2) for n,v in d['kernels'].items() if n in ('k_score','k_fill','k_fill_tall','k_suffix')})")"
+        done
+      done ;;
+    ab_narrow)  # interleaved A/B of the narrow fill's rows per lane (PBCCS_NARROW_ROWS 1 / 2), 10 steps each
+      local k=0
+      for v in ${VARIANTS:-2 1 2 1}; do
         k=$((k+1))
-        PBCCS_NARROW_G=$v timeout -k 10 300 $BENCH --steps 10 --warmup 2 --cpu-sample 0 > $OUT/ab_narrow_$k.json \
+        PBCCS_NARROW_ROWS=$v timeout -k 10 300 $BENCH --steps 10 --warmup 2 --cpu-sample 0 > $OUT/ab_narrow_$k.json \
           2> $OUT/ab_narrow_$k.err || return 1
-        echo "narrow=$v $(summ $OUT/ab_narrow_$k.json) fill16_ms $(python3 -c "import json; d=json.load(open('$OUT/ab_narrow_$k.json')); k=d['kernels']['k_fill']; print(round(k['device_ms']/max(1,k['launches']),2), k['launches'])")"
+        echo "narrow_rows=$v $(summ $OUT/ab_narrow_$k.json) fill16_ms $(python3 -c "import json; d=json.load(open('$OUT/ab_narrow_$k.json')); k=d['kernels']['k_fill']; print(round(k['device_ms']/max(1,k['launches']),2), k['launches'])")"
       done ;;
     fillread) # per-launch slowest-read diagnostics (PBCCS_FILL_PATHS=2), single slot, per rows-per-lane setting
       local k=0
