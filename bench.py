@@ -282,8 +282,10 @@ def choose_slots(args, local):
     """Workspace slots: the measured best split, capped by the steps and by the HBM the slots' band pools
     need at their high-water mark (a 2 kb / 10-pass batch of 2000 ZMWs peaks near 27 GB)."""
     import torch
-    best = BEST_SLOTS_LONG if args.workload in ("10kb", "mixed") else BEST_SLOTS
-    want = args.streams or max(1, min(args.steps, best))
+    queue = args.workload in ("10kb", "mixed")
+    best = BEST_SLOTS_LONG if queue else BEST_SLOTS
+    # (the work queue splits its ZMWs into memory-sized batches whatever the step count: slots = concurrent batches)
+    want = args.streams or (best if queue else max(1, min(args.steps, best)))
     if not torch.cuda.is_available():
         return want
     free_b, _ = torch.cuda.mem_get_info(local)

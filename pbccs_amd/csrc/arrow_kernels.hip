@@ -327,29 +327,28 @@ __global__ void __launch_bounds__(256) k_suffix(DevBatch B, const int* __restric
         if (k <= ncol) suf[k] = s;
     }
     if (!withPrefix) return;
-    // aPre[k] = accumulate(aLs[0..k), 0.0) for k in [0, J+1] (GetLogProdScales(0, k))
+    // aPre[k] = accumulate(aLs[0..k), 0.0) for k in [0, J+1] (GetLogProdScales(0, k)): every prefix is a partial sum
+    // of the one left-to-right accumulation, so one thread's running sum gives them all with the reference's
+    // roundings (J adds, instead of a separate sum per k), loads batched 8 at a time off the add chain
+    if (threadIdx.x != 0) return;
     const double* als = B.aLs + cb;
     double* pre = B.aPre + cb;
-    for (int k0 = 0; k0 <= ncol; k0 += blockDim.x) {
-        const int kb = k0 + wbase;
-        const int k = kb + lane;
-        double s = 0.0;
-        const int cend = min(ncol, k0 + (int)blockDim.x);   // block-uniform: the columns any lane needs
-        for (int c0 = 0; c0 < cend; c0 += kSuffixTile) {
-            __syncthreads();
-            for (int q = threadIdx.x; q < kSuffixTile && c0 + q < ncol; q += blockDim.x) tile[q] = als[c0 + q];
-            __syncthreads();
-            const int hi = min(min(cend, kb + 64) - c0, kSuffixTile);
-            const int bodyEnd = min(hi, kb - c0);   // columns < kb: every lane of the wave adds them
-            int q = 0;
-            for (; q + 8 <= bodyEnd; q += 8) s = add8(s, tile + q);
-            for (; q < bodyEnd; ++q) s = s + tile[q];
-            for (; q < hi; ++q) {
-                const double v = tile[q];
-                if (c0 + q < k) s = s + v;
-            }
+    double run = 0.0;
+    pre[0] = 0.0;
+    int k = 0;
+    for (; k + 8 <= ncol; k += 8) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = als[k + q];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            run = run + v[q];
+            pre[k + q + 1] = run;
         }
-        if (k <= ncol) pre[k] = s;
+    }
+    for (; k < ncol; ++k) {
+        run = run + als[k];
+        pre[k + 1] = run;
     }
 }
 

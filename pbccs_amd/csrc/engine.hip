@@ -566,26 +566,67 @@ void ArrowBatch::UploadDescriptors()
         rz[i] = r.zmw;
         rck[i] = r.ckpt;
     }
-    upload(dZFwd_, zf, stream_);
-    upload(dZRev_, zr, stream_);
-    upload(dZLen_, zl, stream_);
-    upload(dZReadBegin_, zb, stream_);
-    upload(dZNReads_, zn, stream_);
-    upload(dZCtx_, zc, stream_);
-    upload(dRSeqOff_, so, stream_);
-    upload(dRColBase_, cb, stream_);
-    upload(dRValA_, va, stream_);
-    upload(dRValB_, vb, stream_);
-    upload(dRValCap_, vc, stream_);
-    upload(dRLen_, rl, stream_);
-    upload(dRStrand_, rs, stream_);
-    upload(dRTs_, rts, stream_);
-    upload(dRTe_, rte, stream_);
-    upload(dRActive_, ra, stream_);
-    upload(dRZmw_, rz, stream_);
-    upload(dRCkpt_, rck, stream_);
-    // pools (templates re-uploaded whole: they change every refine round)
-    upload(dTpl_, hTpl_, stream_);
+    // one arena: every array at a 256-byte aligned offset, packed into page-locked staging, one copy
+    size_t top = 0;
+    auto place = [&](size_t bytes) {
+        const size_t at = top;
+        top += (bytes + 255) & ~(size_t)255;
+        return at;
+    };
+    const size_t oZf = place(Z * sizeof(int)), oZr = place(Z * sizeof(int)), oZl = place(Z * sizeof(int)),
+                 oZb = place(Z * sizeof(int)), oZn = place(Z * sizeof(int)), oZc = place(zc.size() * sizeof(double));
+    const size_t oSo = place(R * sizeof(long long)), oCb = place(R * sizeof(long long)),
+                 oVa = place(R * sizeof(long long)), oVb = place(R * sizeof(long long)),
+                 oVc = place(R * sizeof(long long));
+    const size_t oRl = place(R * sizeof(int)), oRs = place(R * sizeof(int)), oRts = place(R * sizeof(int)),
+                 oRte = place(R * sizeof(int)), oRa = place(R * sizeof(int)), oRz = place(R * sizeof(int)),
+                 oRck = place(R * sizeof(int));
+    const size_t oTpl = place(hTpl_.size() + 32);   // (32 bytes of slack past the last template)
+    hDesc_.reserve(std::max<size_t>(top, 1));
+    auto put = [&](size_t at, const void* src, size_t bytes) {
+        if (bytes) std::memcpy(hDesc_.ptr + at, src, bytes);
+    };
+    put(oZf, zf.data(), Z * sizeof(int));
+    put(oZr, zr.data(), Z * sizeof(int));
+    put(oZl, zl.data(), Z * sizeof(int));
+    put(oZb, zb.data(), Z * sizeof(int));
+    put(oZn, zn.data(), Z * sizeof(int));
+    put(oZc, zc.data(), zc.size() * sizeof(double));
+    put(oSo, so.data(), R * sizeof(long long));
+    put(oCb, cb.data(), R * sizeof(long long));
+    put(oVa, va.data(), R * sizeof(long long));
+    put(oVb, vb.data(), R * sizeof(long long));
+    put(oVc, vc.data(), R * sizeof(long long));
+    put(oRl, rl.data(), R * sizeof(int));
+    put(oRs, rs.data(), R * sizeof(int));
+    put(oRts, rts.data(), R * sizeof(int));
+    put(oRte, rte.data(), R * sizeof(int));
+    put(oRa, ra.data(), R * sizeof(int));
+    put(oRz, rz.data(), R * sizeof(int));
+    put(oRck, rck.data(), R * sizeof(int));
+    put(oTpl, hTpl_.data(), hTpl_.size());
+    dDesc_.reserve(std::max<size_t>(top, 1), false);
+    PBCCS_HIP(hipMemcpyAsync(dDesc_.ptr, hDesc_.ptr, top, hipMemcpyHostToDevice, stream_));
+    char* base = dDesc_.ptr;
+    pZFwd_ = reinterpret_cast<int*>(base + oZf);
+    pZRev_ = reinterpret_cast<int*>(base + oZr);
+    pZLen_ = reinterpret_cast<int*>(base + oZl);
+    pZReadBegin_ = reinterpret_cast<int*>(base + oZb);
+    pZNReads_ = reinterpret_cast<int*>(base + oZn);
+    pZCtx_ = reinterpret_cast<double*>(base + oZc);
+    pRSeqOff_ = reinterpret_cast<long long*>(base + oSo);
+    pRColBase_ = reinterpret_cast<long long*>(base + oCb);
+    pRValA_ = reinterpret_cast<long long*>(base + oVa);
+    pRValB_ = reinterpret_cast<long long*>(base + oVb);
+    pRValCap_ = reinterpret_cast<long long*>(base + oVc);
+    pRLen_ = reinterpret_cast<int*>(base + oRl);
+    pRStrand_ = reinterpret_cast<int*>(base + oRs);
+    pRTs_ = reinterpret_cast<int*>(base + oRts);
+    pRTe_ = reinterpret_cast<int*>(base + oRte);
+    pRActive_ = reinterpret_cast<int*>(base + oRa);
+    pRZmw_ = reinterpret_cast<int*>(base + oRz);
+    pRCkpt_ = reinterpret_cast<int*>(base + oRck);
+    pTpl_ = base + oTpl;
     // 32 bytes of slack at the end: the lane fill loads read bases 8 at a time (two aligned words), and
     // its prefetch of the rows past a band may reach 24 bytes beyond a read
     dSeq_.reserve(hSeq_.size() + 32, true);
@@ -614,25 +655,25 @@ void ArrowBatch::UploadDescriptors()
 DevBatch ArrowBatch::View() const
 {
     DevBatch b;
-    b.zFwdOff = dZFwd_.ptr;
-    b.zRevOff = dZRev_.ptr;
-    b.zLen = dZLen_.ptr;
-    b.zCtx = dZCtx_.ptr;
-    b.zReadBegin = dZReadBegin_.ptr;
-    b.zNReads = dZNReads_.ptr;
-    b.tplPool = dTpl_.ptr;
-    b.rSeqOff = dRSeqOff_.ptr;
-    b.rLen = dRLen_.ptr;
-    b.rStrand = dRStrand_.ptr;
-    b.rTs = dRTs_.ptr;
-    b.rTe = dRTe_.ptr;
-    b.rActive = dRActive_.ptr;
-    b.rZmw = dRZmw_.ptr;
-    b.rColBase = dRColBase_.ptr;
-    b.rValA = dRValA_.ptr;
-    b.rValB = dRValB_.ptr;
-    b.rValCap = dRValCap_.ptr;
-    b.rCkpt = dRCkpt_.ptr;
+    b.zFwdOff = pZFwd_;
+    b.zRevOff = pZRev_;
+    b.zLen = pZLen_;
+    b.zCtx = pZCtx_;
+    b.zReadBegin = pZReadBegin_;
+    b.zNReads = pZNReads_;
+    b.tplPool = pTpl_;
+    b.rSeqOff = pRSeqOff_;
+    b.rLen = pRLen_;
+    b.rStrand = pRStrand_;
+    b.rTs = pRTs_;
+    b.rTe = pRTe_;
+    b.rActive = pRActive_;
+    b.rZmw = pRZmw_;
+    b.rColBase = pRColBase_;
+    b.rValA = pRValA_;
+    b.rValB = pRValB_;
+    b.rValCap = pRValCap_;
+    b.rCkpt = pRCkpt_;
     b.seqPool = dSeq_.ptr;
     b.aRange = dARange_.ptr;
     b.aOff = dAOff_.ptr;
@@ -717,11 +758,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     const long long chunk = (long long)tallG * tallRows;
     const long long tallGroupLds = (long long)kCoopLdsBytes;
     auto full_rows = [&](int maxI) { return ((long long)maxI + chunk) / chunk * chunk; };   // >= I + 1 rows
-    // Narrow path: 16 lanes per read (four reads per wavefront), rows per lane PBCCS_NARROW_ROWS (1 or 2: a 16- or
-    // 32-row chunk; A/B).  Sixteen reads per wavefront (4 lanes x 4 rows, bases from global memory) measured 0.68x
-    // per launch (profiles/r4g_narrow_ab.txt) and were removed.
+    // Narrow path: 16 lanes per read (four reads per wavefront), one row per lane.  Two rows per lane and sixteen
+    // reads per wavefront (4 lanes x 4 rows, bases from global memory) measured slower and were removed
+    // (profiles/r4i_narrow_rows_ab.txt, r4g_narrow_ab.txt).
     constexpr int narrowG = kNarrowGroupLanes;
-    static const int narrowRows = env_int("PBCCS_NARROW_ROWS", 1) == 2 ? 2 : 1;
+    constexpr int narrowRows = 1;
     auto rows_for = [&](int p, int maxI, int w) -> int {
         if (p == 0) return 0;
         if (p == 1)
@@ -862,7 +903,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             F.hcap = rows_for(p, maxI, F.readWords + F.tplWords);
             const int G = p == 1 ? narrowG : tallG;
             F.rows = p == 1 ? narrowRows : tallRows;
-            F.prio = p >= 2;
+            F.prio = p >= 2;   // (neutral in an A/B against no priority, profiles/r4k_tall_prio_slots.txt)
             if (const char* e = std::getenv("PBCCS_FILL_THR_MARGIN"))   // test hook, read per launch
                 F.thrMargin = std::max(0x1p-50, std::atof(e));
             F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);
@@ -875,9 +916,9 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             if (grow) {
                 F.valBump = dBump_.ptr;
                 F.valLimit = valLimit;
-                F.rValA = dRValA_.ptr;
-                F.rValB = dRValB_.ptr;
-                F.rValCap = dRValCap_.ptr;
+                F.rValA = pRValA_;
+                F.rValB = pRValB_;
+                F.rValCap = pRValCap_;
             }
             const int* lp = dList_.ptr + off;
             const hipStream_t st = p <= 1 ? stream_ : stream2_;
@@ -909,9 +950,12 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         if (grow && bump != (unsigned long long)valTop_) {
             // some reads moved to larger regions: adopt the device's descriptors (host mirrors stay exact)
             std::vector<long long> va, vb, vc;
-            download(va, dRValA_, R, stream_);
-            download(vb, dRValB_, R, stream_);
-            download(vc, dRValCap_, R, stream_);
+            va.resize(R);
+            vb.resize(R);
+            vc.resize(R);
+            PBCCS_HIP(hipMemcpyAsync(va.data(), pRValA_, R * sizeof(long long), hipMemcpyDeviceToHost, stream_));
+            PBCCS_HIP(hipMemcpyAsync(vb.data(), pRValB_, R * sizeof(long long), hipMemcpyDeviceToHost, stream_));
+            PBCCS_HIP(hipMemcpyAsync(vc.data(), pRValCap_, R * sizeof(long long), hipMemcpyDeviceToHost, stream_));
             PBCCS_HIP(hipStreamSynchronize(stream_));
             for (auto& v : todo)
                 for (int r : v) {

@@ -93,6 +93,33 @@ struct DevVec {
     ~DevVec() { release(); }
 };
 
+// Page-locked host staging (grow-only): copies from it go to the DMA engines asynchronously, where a copy from
+// pageable memory is staged by the runtime through a copy kernel that has to find room on the CUs.
+struct PinnedBuf {
+    char* ptr = nullptr;
+    size_t cap = 0;
+    void reserve(size_t n)
+    {
+        if (n <= cap) return;
+        const size_t nc = std::max(n, cap + cap / 2 + 4096);
+        char* p = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void**>(&p), nc, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            throw DeviceError("hipHostMalloc failed (" + std::to_string(nc >> 20) + " MB)");
+        }
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = p;
+        cap = nc;
+    }
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf()
+    {
+        if (ptr) (void)hipHostFree(ptr);
+    }
+};
+
 // Band value pool: a large virtual-address reservation whose physical backing is mapped in 1 GB
 // granules as the batch's bands grow (hipMemAddressReserve / hipMemCreate / hipMemMap).  Growth never
 // copies and never needs old + new copies side by side, so several batches can keep tens of GB of bands
@@ -314,12 +341,17 @@ private:
 
     // host mirrors of pools
     std::vector<char> hTpl_, hSeq_;
-    // device state owned by the batch (inputs + descriptors)
-    DevVec<int> dZFwd_, dZRev_, dZLen_, dZReadBegin_, dZNReads_;
-    DevVec<double> dZCtx_;
-    DevVec<char> dTpl_, dSeq_;
-    DevVec<long long> dRSeqOff_, dRColBase_, dRValA_, dRValB_, dRValCap_;
-    DevVec<int> dRLen_, dRStrand_, dRTs_, dRTe_, dRActive_, dRZmw_, dRCkpt_;
+    // device state owned by the batch (inputs + descriptors).  The per-ZMW and per-read descriptors and the
+    // template pool live in one device arena, filled by one copy from a page-locked staging buffer per
+    // UploadDescriptors (UploadDescriptors sets the typed views below).
+    DevVec<char> dDesc_, dSeq_;
+    PinnedBuf hDesc_;
+    int *pZFwd_ = nullptr, *pZRev_ = nullptr, *pZLen_ = nullptr, *pZReadBegin_ = nullptr, *pZNReads_ = nullptr;
+    double* pZCtx_ = nullptr;
+    char* pTpl_ = nullptr;
+    long long *pRSeqOff_ = nullptr, *pRColBase_ = nullptr, *pRValA_ = nullptr, *pRValB_ = nullptr, *pRValCap_ = nullptr;
+    int *pRLen_ = nullptr, *pRStrand_ = nullptr, *pRTs_ = nullptr, *pRTe_ = nullptr, *pRActive_ = nullptr,
+        *pRZmw_ = nullptr, *pRCkpt_ = nullptr;
     DevVec<int2> dCkPairs_;        // k_score_ckpt task list of a scoring phase
     DevVec<long long> dCkStart_;
     // checkpointed bands: interval K for tall-path reads of windows >= ckptMinLen_; ckptAll_ (test hook

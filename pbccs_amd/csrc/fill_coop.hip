@@ -978,6 +978,9 @@ size_t coop_group_bytes(int hcap, int readWords, int tplWords)
     return (b + 15) & ~(size_t)15;
 }
 
+#ifndef PBCCS_NARROW_MINW   // A/B builds: waves per SIMD the 16-lane kernels are compiled for
+#define PBCCS_NARROW_MINW 2
+#endif
 void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* reads, int n, hipStream_t s)
 {
     if (n <= 0) return;
@@ -988,8 +991,8 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     const bool gc = F.colScratch != nullptr;
     // two waves per SIMD: the register budget that leaves these kernels without spills (higher occupancy
     // was measured slower and needs a private segment, which the resource check in the Makefile forbids)
-    // (G, rows per lane, hybrid): the narrow path with four reads per wavefront (16, 1 / 2; sixteen, (4, 4) with
-    // the bases in global memory, measured 0.68x per launch, profiles/r4g_narrow_ab.txt, and was removed), the tall
+    // (G, rows per lane, hybrid): the narrow path with four reads per wavefront (16, 1; 2 rows per lane and sixteen
+    // reads per wavefront measured slower, profiles/r4i_narrow_rows_ab.txt, r4g_narrow_ab.txt, and were removed), the tall
     // paths one read per wavefront (64, 1 / 2; R = 4 measured slowest, profiles/r4c_tall_rows_ab.txt, and was
     // removed); the hybrid kernel runs R <= 2 (the column buffers hold whole chunks either way).  Four tall reads
     // per wavefront (16, 4) measured half the speed per read (profiles/r4e_tall_grouped_ab.txt) and were removed.
@@ -1003,8 +1006,7 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
         bool attr;
     };
     static Entry ks[] = {
-        {16, 1, false, (K)k_fill_coop<16, 2, false, 1>, false},
-        {16, 2, false, (K)k_fill_coop<16, 2, false, 2>, false},
+        {16, 1, false, (K)k_fill_coop<16, PBCCS_NARROW_MINW, false, 1>, false},
         {64, 1, false, (K)k_fill_coop<64, 2, false, 1>, false},
         {64, 2, false, (K)k_fill_coop<64, 2, false, 2>, false},
         {64, 1, true, (K)k_fill_coop<64, 2, true, 1>, false},   {64, 2, true, (K)k_fill_coop<64, 2, true, 2>, false}};

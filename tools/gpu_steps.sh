@@ -111,21 +111,23 @@ step() {
       cat $OUT/traffic_fill_tall.json; gzip -f "$F" "$W" ;;
     ab_lib)   # interleaved A/B of two in-tree builds (PBCCS_LIB; LIBS="a b" paths), 10 steps each, plus k_score / fill ms
       local k=0
-      for v in ${LIBS:-pbccs_amd/_lib/libpbccs_amd.so pbccs_amd/_lib_ab/libpbccs_amd.so} ; do
-        for rep in 1 2; do
+      for rep in 1 2; do
+        for v in ${LIBS:-pbccs_amd/_lib/libpbccs_amd.so pbccs_amd/_lib_ab/libpbccs_amd.so} ; do
           k=$((k+1))
           PBCCS_LIB=$v timeout -k 10 300 $BENCH --steps 10 --warmup 2 --cpu-sample 0 ${ABARGS:-} > $OUT/ab_lib_$k.json \
             2> $OUT/ab_lib_$k.err || return 1
           echo "lib=$v $(summ $OUT/ab_lib_$k.json) $(python3 -c "import json; d=json.load(open('$OUT/ab_lib_$k.json')); print({n: round(v['device_ms']/max(1,v['launches']),2) for n,v in d['kernels'].items() if n in ('k_score','k_fill','k_fill_tall','k_suffix')})")"
         done
       done ;;
-    ab_narrow)  # interleaved A/B of the narrow fill's rows per lane (PBCCS_NARROW_ROWS 1 / 2), 10 steps each
+    ab_env)   # interleaved A/B of environment settings: ENVS="A=1 A=0" (one KEY=VALUE per variant; "-" = none), 2 runs each
       local k=0
-      for v in ${VARIANTS:-2 1 2 1}; do
-        k=$((k+1))
-        PBCCS_NARROW_ROWS=$v timeout -k 10 300 $BENCH --steps 10 --warmup 2 --cpu-sample 0 > $OUT/ab_narrow_$k.json \
-          2> $OUT/ab_narrow_$k.err || return 1
-        echo "narrow_rows=$v $(summ $OUT/ab_narrow_$k.json) fill16_ms $(python3 -c "import json; d=json.load(open('$OUT/ab_narrow_$k.json')); k=d['kernels']['k_fill']; print(round(k['device_ms']/max(1,k['launches']),2), k['launches'])")"
+      for rep in 1 2; do
+        for v in ${ENVS:-PBCCS_TALL_PRIO=1 PBCCS_TALL_PRIO=0}; do
+          k=$((k+1))
+          env ${v/#-/PBCCS_NONE=1} timeout -k 10 300 $BENCH --steps ${ABSTEPS:-10} --warmup 2 --cpu-sample 0 ${ABARGS:-} \
+            > $OUT/ab_env_$k.json 2> $OUT/ab_env_$k.err || return 1
+          echo "$v $(summ $OUT/ab_env_$k.json) $(python3 -c "import json; d=json.load(open('$OUT/ab_env_$k.json')); print({n: round(v['device_ms']/max(1,v['launches']),2) for n,v in d['kernels'].items() if n in ('k_score','k_fill','k_fill_tall')})")"
+        done
       done ;;
     fillread) # per-launch slowest-read diagnostics (PBCCS_FILL_PATHS=2), single slot, per rows-per-lane setting
       local k=0
