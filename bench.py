@@ -286,7 +286,7 @@ def choose_slots(args, local):
     best = BEST_SLOTS_LONG if queue else BEST_SLOTS
     # (the work queue splits its ZMWs into memory-sized batches whatever the step count: slots = concurrent batches)
     want = args.streams or (best if queue else max(1, min(args.steps, best)))
-    if not torch.cuda.is_available():
+    if queue or not torch.cuda.is_available():   # the queue plans its own batches from free HBM and the slots
         return want
     free_b, _ = torch.cuda.mem_get_info(local)
     per_slot = max(1, args.zmws_per_step) * SLOT_BYTES_PER_ZMW
@@ -515,9 +515,14 @@ def quiver_stage(args, rank, world, eng, barrier, sync, seed0):
     import pbccs_amd as P
     from pbccs_amd import quiver, synth
     cfg = P.QuiverConfig(P.QvModelParams(**synth.QUIVER_PARAMS), score_diff=synth.QUIVER_SCORE_DIFF)
+    warm_ms = []   # the first call's extra cost (buffer growth) against the next ones
     for w in range(args.warmup):   # full-size: the engine's device buffers reach their steady-state size untimed
-        quiver.polish_batch(synth.make_quiver_zmws(args.steps * args.zmws_per_step, args.length, args.passes,
-                                                   seed=seed0 + 1000 + w), cfg, engine=eng)
+        wz = synth.make_quiver_zmws(args.steps * args.zmws_per_step, args.length, args.passes, seed=seed0 + 1000 + w)
+        sync()
+        tw = time.perf_counter()
+        quiver.polish_batch(wz, cfg, engine=eng)
+        sync()
+        warm_ms.append(round((time.perf_counter() - tw) * 1e3, 1))
     zs = synth.make_quiver_zmws(args.steps * args.zmws_per_step, args.length, args.passes, seed=seed0)
     prep = quiver.PreparedQuiverBatch(zs, cfg)   # host marshalling before the timed region (as PreparedBatch)
     eng.kernel_stats(reset=True)
@@ -540,7 +545,8 @@ def quiver_stage(args, rank, world, eng, barrier, sync, seed0):
                                   f"{len(zs)} scorers in one pbccs_quiver_polish_batch",
                       "parallelism": f"zmw-shard x{world}"},
            "converged": sum(r["converged"] for r in res), "mean_iterations_applied":
-               round(sum(r["n_applied"] for r in res) / max(1, len(res)), 2)}
+               round(sum(r["n_applied"] for r in res) / max(1, len(res)), 2), "warmup_call_ms": warm_ms,
+           "timed_call_ms": round(local_time * 1e3, 1)}
     if rank == 0 and args.cpu_sample:
         out["cpu_baseline"] = quiver_cpu_baseline(args, args.cpu_sample)
     if rank == 0:
