@@ -123,10 +123,28 @@ def launch_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    # a rank that fails ends the job: the others would wait on it (the queue's collector, the final barrier), so
+    # they are terminated -- the processes this launcher started, by PID
     rc = 0
-    for p in procs:
-        c = p.wait()
-        rc = rc or c
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            rc = rc or c
+            if c != 0:
+                for q in live:
+                    q.terminate()
+                for q in live:
+                    try:
+                        q.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                return c
+        time.sleep(0.2)
     return rc
 
 
@@ -718,9 +736,12 @@ def make_roofline(stats, local_time, workload):
             "fp64_valu": {"achieved": round(fp64_tf, 4), "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": round(fp64_tf / FP64_VALU_PEAK_TFLOPS, 6),
                           "note": f"{FLOP_PER_CELL} FLOP per DP cell-update over the timed region's wall time"},
-            "binding": f"latency: the serial insertion chain, a dependent mul + add + add per band row and a DPP "
-                       f"hand-off per two rows (~{CHAIN_ROW_CYCLES} cycles per row, tools/ubench/chain_step.hip), plus "
-                       f"the per-chunk band-end logic (DESIGN.md §6); neither HBM nor FP64 VALU",
+            "binding": f"device-wide: at five slots the device is saturated (five and six slots run at the same rate, "
+                       f"profiles/r4k_tall_prio_slots.txt), so the line follows the device's total work per ZMW; the "
+                       f"tall fill itself is latency-bound on the serial insertion chain (a dependent mul + add + add per "
+                       f"band row, a DPP hand-off per two rows, ~{CHAIN_ROW_CYCLES} cycles per row, "
+                       f"tools/ubench/chain_step.hip) and its per-chunk band-end logic (DESIGN.md §6); neither HBM nor "
+                       f"FP64 VALU",
             "source_digest": digest}
 
 

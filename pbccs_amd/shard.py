@@ -63,6 +63,9 @@ def dynamic_chunks(zmws, chunk):
     return [order[k:k + chunk] for k in range(0, len(order), chunk)]
 
 
+STORE_PART = 4 << 20   # bytes per value put on the rank-0 key-value store (whose values are capped at 8 MB)
+
+
 def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chunk=256, polish_fn=None, store=None,
                    group=None, stats=None):
     """Polish `zmws` across ranks through a dynamic pull queue: every rank takes the next
@@ -117,9 +120,13 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
         with lock:
             if not store.check([k]):
                 return False
-            blob = store.get(k)
+            nparts = int(store.get(k))
+            parts = []
+            for q in range(nparts):
+                parts.append(store.get(f"{k}/p{q}"))
+                store.delete_key(f"{k}/p{q}")
             store.delete_key(k)
-        who, recs = pickle.loads(blob)
+        who, recs = pickle.loads(b"".join(parts))
         taken[who] += 1
         for i, rec in zip(chunks[c], recs):
             out[i] = rec
@@ -186,8 +193,13 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
                     out[i] = rec
             else:
                 blob = pickle.dumps((rank, recs))
+                # the store takes values of up to 8 MB: the records go in parts, the part count last (the
+                # collector reads a chunk once its count key exists)
+                nparts = max(1, (len(blob) + STORE_PART - 1) // STORE_PART)
                 with lock:
-                    store.set(f"{key}/done/{c}", blob)
+                    for q in range(nparts):
+                        store.set(f"{key}/done/{c}/p{q}", blob[q * STORE_PART:(q + 1) * STORE_PART])
+                    store.set(f"{key}/done/{c}", str(nparts))
             c = nxt if gen else pull()
     finally:
         if gen:

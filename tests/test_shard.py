@@ -29,13 +29,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _stand_in(rank, slow_rank=None):
+def _stand_in(rank, slow_rank=None, pad=0):
     import time
 
     def polish(zs):
         if rank == slow_rank:
             time.sleep(0.05 * len(zs))
-        return [{"rank": rank, "draft": z["draft"][::-1]} for z in zs]
+        return [{"rank": rank, "draft": z["draft"][::-1], "pad": "A" * pad} for z in zs]
     return polish
 
 
@@ -45,10 +45,11 @@ def _worker(rank, world, port, zmws, out_q, use_gpu, mode="static", chunk=2):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        if mode == "dynamic":
+        if mode in ("dynamic", "dynamic_big"):
             st = {}
-            res = shard.polish_dynamic(zmws, chunk=chunk, polish_fn=None if use_gpu else _stand_in(rank, slow_rank=1),
-                                       stats=st)
+            pad = (3 << 20) if mode == "dynamic_big" else 0   # 3 MB per record: chunks beyond the store's 8 MB values
+            res = shard.polish_dynamic(zmws, chunk=chunk,
+                                       polish_fn=None if use_gpu else _stand_in(rank, slow_rank=1, pad=pad), stats=st)
             if rank == 0:
                 res = (res, st)
         elif use_gpu:
@@ -112,6 +113,16 @@ def test_gloo_world2_dynamic_queue_balances_and_keeps_order():
     assert by_rank[1] >= 2 and by_rank[0] > by_rank[1], by_rank
     # records streamed per chunk: rank 0 saw every chunk, the other rank's through the store
     assert st["chunks"] == 12 and sum(st["chunks_by_rank"]) == 12 and st["chunks_by_rank"][1] >= 1
+
+
+def test_gloo_world2_dynamic_queue_records_larger_than_a_store_value():
+    """A chunk's records beyond the key-value store's 8 MB value limit (a 2500-ZMW chunk of a SMRT cell is ~55 MB)
+    travel in parts and are reassembled in input order."""
+    zmws = _toy_zmws(12)
+    res, st = _run(2, zmws, mode="dynamic_big", chunk=4)
+    assert [r["draft"] for r in res] == [z["draft"][::-1] for z in zmws]
+    assert all(len(r["pad"]) == 3 << 20 for r in res)
+    assert st["chunks_by_rank"][1] >= 1
 
 
 @pytest.mark.gpu

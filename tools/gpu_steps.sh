@@ -59,7 +59,7 @@ step() {
       timeout -k 10 400 $BENCH --stage poa --steps 5 --warmup 1 > $OUT/poa.json 2> $OUT/poa.err && \
         python3 -c "import json; d=json.load(open('$OUT/poa.json')); print('poa', d['value'])" ;;
     ccs)
-      timeout -k 10 500 $BENCH --stage ccs --steps 5 --warmup 1 > $OUT/ccs.json 2> $OUT/ccs.err && \
+      PBCCS_CCS_TRACE=1 timeout -k 10 500 $BENCH --stage ccs --steps 5 --warmup 1 > $OUT/ccs.json 2> $OUT/ccs.err && \
         python3 -c "import json; d=json.load(open('$OUT/ccs.json')); print('ccs', d['value'], d['zmw_status'])" ;;
     prof10k)  # configs[2] at 2000 ZMWs through the work queue, rocprofv3 kernel summary
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof10k -o run -- $BENCH --workload 10kb \
@@ -73,7 +73,7 @@ step() {
       timeout -k 10 900 $BENCH --workload mixed --steps 1 --zmws-per-step 2000 --warmup 0 > $OUT/bench_mixed.json \
         2> $OUT/bench_mixed.err && summ $OUT/bench_mixed.json ;;
     cell2)    # configs[4]: two ranks sharing the one device (a rehearsal of the multi-rank queue), CELLN ZMWs
-      PBCCS_BENCH_DEVICE=0 timeout -k 10 1000 $BENCH --gpus 2 --workload smrtcell --steps 1 \
+      PBCCS_BENCH_DEVICE=0 timeout -k 10 ${CELLTO:-1000} $BENCH --gpus 2 --workload smrtcell --steps 1 \
         --zmws-per-step ${CELLN:-10000} --warmup 0 --streams 4 > $OUT/bench_cell2.json 2> $OUT/bench_cell2.err && \
         summ $OUT/bench_cell2.json ;;
     ab_tall)  # interleaved A/B of the tall fill's layout: "G:rows" (PBCCS_TALL_G, PBCCS_TALL_ROWS), 10 steps each
