@@ -43,7 +43,12 @@ FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
 FLOP_PER_CELL = 11             # fill cell 6 mul + 3 add + <= 1 div, + the column rescale
 CHAIN_ROW_CYCLES = 21.5        # one band row of the tall fills' chain at 2 rows per lane (tools/ubench/chain_step.hip
                                # variant C2; 29.3 with a DPP hand-off per row, profiles/r4a_chain_ubench.txt)
-BEST_SLOTS = 5                 # measured best split of 2 kb batches: 5 slots divide the driver's 20 steps into 4 full waves (6 slots: 2868 vs 3357 ZMWs/s at --steps 20, the last wave half empty)
+BEST_SLOTS = 8                 # 2 kb: eight slots of 1000-ZMW device batches (each 2000-ZMW step polished as two batches,
+                               # BATCH_SPLIT): 3677 / 3665 ZMWs/s against 3538 / 3525 for five slots of whole steps and
+                               # 3094 / 3049 for ten of halves (twenty streams on sixteen hardware queues),
+                               # profiles/r4u_batch_shape.txt; 40 half-steps fill the eight slots in five full waves
+BATCH_SPLIT = 2                # device batches per 2 kb step
+BEST_SLOTS_CCS = 5             # ccs: 2000-ZMW polish chunks beside the POA (five fit the device with the POA's pools)
 BEST_SLOTS_LONG = 8            # configs[2] / [3] through the work queue: 10 kb at 2000 ZMWs 4 / 5 / 8 / 10 / 12 slots 27.5 / 26.3 / 29.1-30.4 / 28.0 / 26.5 ZMWs/s (profiles/r3ad_*, r3af_*); mixed at 240 ZMWs 8 / 12 slots 7.19 / 5.09 (profiles/r3ag_*): more, smaller batches in flight while the tall fills set each round's latency
 SLOT_BYTES_PER_ZMW = 15 << 20  # measured band high-water per 2 kb / 10-pass ZMW in a slot (13.4 MB, exact regrow)
 HBM_MARGIN = 24 << 30          # device memory left to scratch, selection buffers and the runtime
@@ -69,6 +74,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--streams", type=int, default=0,
                     help="workspace slots = batches polished concurrently (0 = min(steps, 5), capped by HBM)")
+    ap.add_argument("--batch-split", type=int, default=BATCH_SPLIT,
+                    help="2 kb: device batches per step (each step's ZMWs polished as this many batches)")
     ap.add_argument("--batch-zmws", type=int, default=0,
                     help="queue workloads: ZMWs per device batch (0 = planned from free HBM)")
     ap.add_argument("--ccs-chunk", type=int, default=0,
@@ -261,8 +268,11 @@ def queue_workload(args, rank, world, eng, settings, seed0):
     qstats = {}
     try:
         if kw is None:
-            res = shard.polish_dynamic(zs, settings, eng, rank, world, chunk=max(1, args.zmws_per_step // 4),
-                                       stats=qstats)
+            # chunks of at most 512 ZMWs, at least four per rank: the cost-ordered pull queue balances the ranks only
+            # when the last chunks are small (four 1500-ZMW chunks left a 156 s tail on two ranks), and a chunk must
+            # still hold enough ZMWs of each shape to fill the rank's workspace slots
+            res = shard.polish_dynamic(zs, settings, eng, rank, world,
+                                       chunk=max(1, min(512, n // (4 * world))), stats=qstats)
         else:
             res = pbccs_amd.polish_stream(zs, settings, eng)
     finally:
@@ -300,14 +310,19 @@ def choose_slots(args, local):
     """Workspace slots: the measured best split, capped by the steps and by the HBM the slots' band pools
     need at their high-water mark (a 2 kb / 10-pass batch of 2000 ZMWs peaks near 27 GB)."""
     import torch
-    queue = args.workload in ("10kb", "mixed")
-    best = BEST_SLOTS_LONG if queue else BEST_SLOTS
+    queue = args.workload in ("10kb", "mixed", "smrtcell") and args.stage == "polish"
+    if args.stage == "ccs":
+        best, batches, batch_zmws = BEST_SLOTS_CCS, args.steps, args.zmws_per_step
+    else:
+        best, batches, batch_zmws = BEST_SLOTS, args.steps * args.batch_split, max(1, args.zmws_per_step // args.batch_split)
+    if queue:
+        best = BEST_SLOTS_LONG
     # (the work queue splits its ZMWs into memory-sized batches whatever the step count: slots = concurrent batches)
-    want = args.streams or (best if queue else max(1, min(args.steps, best)))
+    want = args.streams or (best if queue else max(1, min(batches, best)))
     if queue or not torch.cuda.is_available():   # the queue plans its own batches from free HBM and the slots
         return want
     free_b, _ = torch.cuda.mem_get_info(local)
-    per_slot = max(1, args.zmws_per_step) * SLOT_BYTES_PER_ZMW
+    per_slot = batch_zmws * SLOT_BYTES_PER_ZMW
     fit = max(1, int((free_b - HBM_MARGIN) // per_slot))
     return max(1, min(want, fit))
 
@@ -368,10 +383,14 @@ def main():
                                                                                      seed0)
         return report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total, qstats)
 
+    # a step's ZMWs as BATCH_SPLIT device batches (the step is the workload's unit; the batch, the engine's)
+    def split(zs):
+        per = -(-len(zs) // max(1, args.batch_split))
+        return [zs[i:i + per] for i in range(0, len(zs), per)]
+
     # ---- warmup (untimed): W steps, concurrently over the slots like the timed ones ------------------
-    wb = [pbccs_amd.PreparedBatch(synth.make_zmws(args.zmws_per_step, args.length, args.passes,
-                                                  seed=seed0 + 1000 + w), settings, eng)
-          for w in range(args.warmup)]
+    wb = [pbccs_amd.PreparedBatch(part, settings, eng) for w in range(args.warmup)
+          for part in split(synth.make_zmws(args.zmws_per_step, args.length, args.passes, seed=seed0 + 1000 + w))]
     pbccs_amd.polish_many(wb)
     for b in wb:
         b.close()
@@ -389,7 +408,7 @@ def main():
     batches = []
     for k in range(args.steps):
         zs = synth.make_zmws(args.zmws_per_step, args.length, args.passes, seed=seed0 + k)
-        batches.append(pbccs_amd.PreparedBatch(zs, settings, eng))
+        batches.extend(pbccs_amd.PreparedBatch(part, settings, eng) for part in split(zs))
     log(rank, f"[bench] prepared {args.steps} steps x {args.zmws_per_step} ZMWs in {time.perf_counter() - t_prep:.1f}s")
     eng.kernel_stats(reset=True)
     eng.counters(reset=True)
@@ -794,6 +813,8 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
                    "passes": args.passes if args.workload == "2kb" else
                    {"10kb": 8, "mixed": "3-30", "smrtcell": "mix"}[args.workload],
                    "slots": slots,
+                   "device_batch_zmws": (max(1, args.zmws_per_step // max(1, args.batch_split))
+                                         if args.workload == "2kb" else "planned"),
                    "parallelism": f"zmw-shard x{world}"},
         "gcups": round(gcups, 3),
         "zmw_status": statuses,
