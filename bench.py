@@ -48,7 +48,7 @@ BEST_SLOTS = 8                 # 2 kb: eight slots of 1000-ZMW device batches (e
                                # 3094 / 3049 for ten of halves (twenty streams on sixteen hardware queues),
                                # profiles/r4u_batch_shape.txt; 40 half-steps fill the eight slots in five full waves
 BATCH_SPLIT = 2                # device batches per 2 kb step
-BEST_SLOTS_CCS = 5             # ccs: 2000-ZMW polish chunks beside the POA (five fit the device with the POA's pools)
+BEST_SLOTS_CCS = 8             # ccs: polish chunks planned from free HBM beside the POA (profiles/r4y_ccs_shape_ab.txt: 8 > 5)
 BEST_SLOTS_LONG = 8            # configs[2] / [3] through the work queue: 10 kb at 2000 ZMWs 4 / 5 / 8 / 10 / 12 slots 27.5 / 26.3 / 29.1-30.4 / 28.0 / 26.5 ZMWs/s (profiles/r3ad_*, r3af_*); mixed at 240 ZMWs 8 / 12 slots 7.19 / 5.09 (profiles/r3ag_*): more, smaller batches in flight while the tall fills set each round's latency
 SLOT_BYTES_PER_ZMW = 15 << 20  # measured band high-water per 2 kb / 10-pass ZMW in a slot (13.4 MB, exact regrow)
 HBM_MARGIN = 24 << 30          # device memory left to scratch, selection buffers and the runtime
@@ -73,7 +73,7 @@ def parse():
                     help="ZMWs polished by the CPU baseline (0 = skip; default 256 for 2kb, 0 otherwise)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--streams", type=int, default=0,
-                    help="workspace slots = batches polished concurrently (0 = min(steps, 5), capped by HBM)")
+                    help="workspace slots = batches polished concurrently (0 = the measured best for the stage, capped by HBM)")
     ap.add_argument("--batch-split", type=int, default=BATCH_SPLIT,
                     help="2 kb: device batches per step (each step's ZMWs polished as this many batches)")
     ap.add_argument("--batch-zmws", type=int, default=0,

@@ -129,6 +129,16 @@ step() {
           echo "$v $(summ $OUT/ab_env_$k.json) $(python3 -c "import json; d=json.load(open('$OUT/ab_env_$k.json')); print({n: round(v['device_ms']/max(1,v['launches']),2) for n,v in d['kernels'].items() if n in ('k_score','k_fill','k_fill_tall')})")"
         done
       done ;;
+    ab_ccs)   # interleaved A/B of the ccs stage's shape: CCSV="slots:chunk ..." (0 = the defaults), 2 runs each
+      local k=0
+      for rep in 1 2; do
+        for v in ${CCSV:-0:0 8:1000}; do
+          k=$((k+1))
+          timeout -k 10 300 $BENCH --stage ccs --steps 5 --warmup 1 --cpu-sample 0 --streams ${v%:*} \
+            --ccs-chunk ${v#*:} > $OUT/ab_ccs_$k.json 2> $OUT/ab_ccs_$k.err || return 1
+          echo "ccs slots:chunk=$v $(python3 -c "import json; d=json.load(open('$OUT/ab_ccs_$k.json')); print(d['value'], d['config']['slots'], d['poa_wall_ms'], d['poa_device_ms'])")"
+        done
+      done ;;
     fillread) # per-launch slowest-read diagnostics (PBCCS_FILL_PATHS=2), single slot, per rows-per-lane setting
       local k=0
       for v in ${VARIANTS:-64:2 64:1}; do
