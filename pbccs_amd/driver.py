@@ -159,56 +159,88 @@ def ccs_batch(chunks, settings=None, engine=None, max_poa_coverage=None):
     by the POA, rejected by ExtractMappedRead, past the maxPoaCov stop, or the ZMW ended earlier).
     "add_order" lists the subread indices in AddRead order (FilterReads' stable order, Consensus.h:281):
     the order of ZScores() and of the ccs.bam zs tag.
-    Raises on a draft longer than its buffer (PBCCS_ERANGE)."""
+    Raises on a draft longer than its buffer (PBCCS_ERANGE).
+
+    Marshalling is flat, as poa.poa_batch's: every subread in one buffer behind one pointer table, every
+    output in shared arrays, the per-ZMW structs written column-wise through numpy views (per-ZMW ctypes
+    arrays were ~3 s of Python per 10,000 ZMWs, half the ccs stage's wall time)."""
     import ctypes
     from . import ZMW_STATUS, default_engine
     from . import lib as L
     from .polish import ConsensusSettings
+    from .quiver import _struct_dtype
     eng = engine or default_engine()
     settings = settings or ConsensusSettings()
     n = len(chunks)
-    ins = (L.CCcsInput * max(1, n))()
-    outs = (L.CCcsOutput * max(1, n))()
-    keep = []
-    for z, c in enumerate(chunks):
-        reads = c["reads"]
-        nr = len(reads)
-        enc = [r["seq"].encode() for r in reads]
-        seqs = (ctypes.c_char_p * max(1, nr))(*enc)
-        lens = (ctypes.c_int * max(1, nr))(*[len(e) for e in enc])
-        flags = (ctypes.c_ubyte * max(1, nr))(*[int(r.get("flags", FULL_PASS)) for r in reads])
-        # a POA consensus never exceeds the bases of the reads it was built from
-        cap = sum(len(e) for e in enc) + 64
-        cons, draft = ctypes.create_string_buffer(cap), ctypes.create_string_buffer(cap)
-        qv = (ctypes.c_int * cap)()
-        arr = (ctypes.c_int * max(1, nr))()
-        zs = (ctypes.c_double * max(1, nr))()
-        order = (ctypes.c_int * max(1, nr))()
-        for k in range(4):
-            ins[z].snr[k] = float(c["snr"][k])
-        ins[z].n_subreads, ins[z].seqs, ins[z].lens, ins[z].flags = nr, seqs, lens, flags
-        o = outs[z]
-        o.polish.consensus = ctypes.cast(cons, ctypes.c_char_p)
-        o.polish.consensus_cap = cap
-        o.polish.qvs, o.polish.add_read_results, o.polish.zscores = qv, arr, zs
-        o.draft = ctypes.cast(draft, ctypes.c_char_p)
-        o.draft_cap = cap
-        o.add_order = order
-        keep.append((seqs, lens, flags, cons, draft, qv, arr, zs, order, nr))
+    counts = np.fromiter((len(c["reads"]) for c in chunks), dtype=np.int64, count=n)
+    flat = [r for c in chunks for r in c["reads"]]
+    nr_all = len(flat)
+    seqs = [r["seq"] for r in flat]
+    joined = "".join(seqs).encode()   # one encode: per-read lengths in characters are bytes for ACGT text
+    lens = np.fromiter(map(len, seqs), dtype=np.int32, count=nr_all)
+    if len(joined) != int(lens.sum()):   # non-ASCII text: lengths in bytes, read by read
+        enc = [s.encode() for s in seqs]
+        joined = b"".join(enc)
+        lens = np.fromiter(map(len, enc), dtype=np.int32, count=nr_all)
+    flags = np.fromiter((int(r.get("flags", FULL_PASS)) for r in flat), dtype=np.uint8, count=nr_all)
+    bases = np.zeros(nr_all + 1, dtype=np.int64)
+    np.cumsum(lens, out=bases[1:])
+    blob = np.frombuffer(joined, dtype=np.uint8) if joined else np.zeros(1, dtype=np.uint8)   # read-only view
+    ptrs = (blob.ctypes.data + bases[:-1]).astype(np.uint64)
+    first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(counts, out=first[1:])
+    f0 = first[:-1]
+    # a POA consensus never exceeds the bases of the reads it was built from: per-ZMW capacity read bases + 64
+    caps = bases[first[1:]] - bases[f0] + 64
+    cstart = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(caps, out=cstart[1:])
+    cons = np.zeros(max(1, int(cstart[-1])), dtype=np.uint8)     # calloc'd: pages past a draft's length untouched
+    draft = np.zeros(max(1, int(cstart[-1])), dtype=np.uint8)
+    qv = np.zeros(max(1, int(cstart[-1])), dtype=np.int32)
+    arr = np.zeros(max(1, nr_all), dtype=np.int32)
+    zs = np.zeros(max(1, nr_all), dtype=np.float64)
+    order = np.zeros(max(1, nr_all), dtype=np.int32)
+    ins = np.zeros(max(1, n), dtype=_struct_dtype(L.CCcsInput))
+    outs = np.zeros(max(1, n), dtype=_struct_dtype(L.CCcsOutput))
+    if n:
+        ins["snr"][:n] = np.array([[float(v) for v in c["snr"][:4]] for c in chunks], dtype=np.float64)
+        ins["n_subreads"][:n] = counts
+        ins["seqs"][:n] = ptrs.ctypes.data + 8 * f0
+        ins["lens"][:n] = lens.ctypes.data + 4 * f0
+        ins["flags"][:n] = flags.ctypes.data + f0
+        pol = outs["polish"]
+        pol["consensus"][:n] = cons.ctypes.data + cstart[:-1]
+        pol["consensus_cap"][:n] = caps
+        pol["qvs"][:n] = qv.ctypes.data + 4 * cstart[:-1]
+        pol["add_read_results"][:n] = arr.ctypes.data + 4 * f0
+        pol["zscores"][:n] = zs.ctypes.data + 8 * f0
+        outs["draft"][:n] = draft.ctypes.data + cstart[:-1]
+        outs["draft_cap"][:n] = caps
+        outs["add_order"][:n] = order.ctypes.data + 4 * f0
     opts = settings._c()
     mc = 2**62 if max_poa_coverage is None else int(max_poa_coverage)
-    L.check(L.load().pbccs_ccs_batch(eng._h, ins, n, mc, ctypes.byref(opts), outs))
+    L.check(L.load().pbccs_ccs_batch(eng._h, ctypes.cast(ins.ctypes.data, ctypes.POINTER(L.CCcsInput)), n, mc,
+                                     ctypes.byref(opts), ctypes.cast(outs.ctypes.data, ctypes.POINTER(L.CCcsOutput))))
+    del blob, joined, ptrs, lens, flags   # the inputs lived until the call returned
+    pol = outs["polish"]
+    status, clen = pol["status"][:n].tolist(), pol["consensus_len"][:n].tolist()
+    zg, za, pacc = pol["zg"][:n].tolist(), pol["za"][:n].tolist(), pol["predicted_accuracy"][:n].tolist()
+    ntest, nappl, npass = pol["n_tested"][:n].tolist(), pol["n_applied"][:n].tolist(), pol["n_passes"][:n].tolist()
+    scounts, dlen = pol["status_counts"][:n].tolist(), outs["draft_len"][:n].tolist()
+    cs, fs, cnt = cstart.tolist(), first.tolist(), counts.tolist()
+    arr_l, zs_l, order_l = arr.tolist(), zs.tolist(), order.tolist()
     res = []
-    for z, (_, _, _, cons, draft, qv, arr, zs, order, nr) in enumerate(keep):
-        p = outs[z].polish
-        ok = p.status in (0, 6)
-        ln = max(0, p.consensus_len) if ok else 0
-        polished = p.status not in (1, 2)   # NoSubreads / TooShort end before the polish
-        res.append({"status": ZMW_STATUS[p.status], "status_code": p.status,
-                    "consensus": cons.raw[:ln].decode() if ok else "", "qvs": list(qv[:ln]) if ok else [],
-                    "draft": draft.raw[:max(0, outs[z].draft_len)].decode(),
-                    "add_read_results": list(arr[:nr]), "zscores": list(zs[:nr]), "polished": polished,
-                    "add_order": [k for k in order[:nr] if k >= 0],
-                    "zg": p.zg, "za": p.za, "predicted_accuracy": p.predicted_accuracy, "n_tested": p.n_tested,
-                    "n_applied": p.n_applied, "n_passes": p.n_passes, "status_counts": list(p.status_counts)})
+    for z in range(n):
+        st, c, f, nr = status[z], cs[z], fs[z], cnt[z]
+        ok = st in (0, 6)
+        ln = max(0, clen[z]) if ok else 0
+        res.append({"status": ZMW_STATUS[st], "status_code": st,
+                    "consensus": cons[c:c + ln].tobytes().decode() if ok else "",
+                    "qvs": qv[c:c + ln].tolist() if ok else [],
+                    "draft": draft[c:c + max(0, dlen[z])].tobytes().decode(),
+                    "add_read_results": arr_l[f:f + nr], "zscores": zs_l[f:f + nr],
+                    "polished": st not in (1, 2),   # NoSubreads / TooShort end before the polish
+                    "add_order": [k for k in order_l[f:f + nr] if k >= 0],
+                    "zg": zg[z], "za": za[z], "predicted_accuracy": pacc[z], "n_tested": ntest[z],
+                    "n_applied": nappl[z], "n_passes": npass[z], "status_counts": scounts[z]})
     return res

@@ -123,8 +123,7 @@ def poa_batch(zmw_reads, max_coverage=None, min_coverage=-1, engine=None):
     first = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(counts, out=first[1:])
     # per-ZMW consensus capacity: its read bases + 16; per-read outputs shared
-    zbases = np.add.reduceat(lens.astype(np.int64), first[:-1]) if len(enc) else np.zeros(n, np.int64)
-    zbases = np.where(counts > 0, zbases, 0) + 16
+    zbases = starts[first[1:]] - starts[first[:-1]] + 16   # (reduceat would fail on a trailing read-less ZMW)
     cstart = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(zbases, out=cstart[1:])
     cbuf = ctypes.create_string_buffer(max(1, int(cstart[-1])))

@@ -246,20 +246,24 @@ def _struct_dtype(ctype):
     """numpy dtype with the memory layout of a ctypes Structure (pointers as uint64): lets the batch entry point's
     input arrays be filled column-wise instead of one ctypes attribute at a time."""
     import numpy as np
+    scalars = {ctypes.c_int: np.int32, ctypes.c_float: np.float32, ctypes.c_longlong: np.int64,
+               ctypes.c_double: np.float64, ctypes.c_ubyte: np.uint8}
+
+    def field(ft):
+        if isinstance(ft, type) and issubclass(ft, ctypes.Structure):   # nested struct (CCcsOutput.polish)
+            return _struct_dtype(ft)
+        if isinstance(ft, type) and issubclass(ft, ctypes.Array):       # fixed array (snr[4], status_counts[5])
+            return (field(ft._type_), (ft._length_,))
+        if ft in scalars:
+            return scalars[ft]
+        assert ctypes.sizeof(ft) == 8   # pointers and char*
+        return np.uint64
+
     names, formats, offsets = [], [], []
     for name, ft in ctype._fields_:
-        f = getattr(ctype, name)
         names.append(name)
-        offsets.append(f.offset)
-        if ft in (ctypes.c_int,):
-            formats.append(np.int32)
-        elif ft in (ctypes.c_float,):
-            formats.append(np.float32)
-        elif ft in (ctypes.c_longlong,):
-            formats.append(np.int64)
-        else:   # pointers and char*
-            assert ctypes.sizeof(ft) == 8
-            formats.append(np.uint64)
+        offsets.append(getattr(ctype, name).offset)
+        formats.append(field(ft))
     return np.dtype({"names": names, "formats": formats, "offsets": offsets, "itemsize": ctypes.sizeof(ctype)})
 
 

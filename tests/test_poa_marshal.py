@@ -39,7 +39,7 @@ class _Eng:
 def test_poa_batch_marshalling_round_trip(monkeypatch):
     monkeypatch.setattr(poa, "load", lambda: _FakeLib())
     monkeypatch.setattr(poa, "_engine", lambda e: _Eng())
-    zmws = [["ACGT", None, "GG"], [], ["T"], [None], ["AC" * 50, "G", "TT"]]
+    zmws = [["ACGT", None, "GG"], [], ["T"], [None], ["AC" * 50, "G", "TT"], []]   # a read-less ZMW last
     got = poa.poa_batch(zmws)
     assert len(got) == len(zmws)
     for reads, g in zip(zmws, got):
