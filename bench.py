@@ -311,8 +311,9 @@ def choose_slots(args, local):
     need at their high-water mark (a 2 kb / 10-pass batch of 2000 ZMWs peaks near 27 GB)."""
     import torch
     queue = args.workload in ("10kb", "mixed", "smrtcell") and args.stage == "polish"
-    if args.stage == "ccs":
-        best, batches, batch_zmws = BEST_SLOTS_CCS, args.steps, args.zmws_per_step
+    if args.stage == "ccs":   # pbccs_ccs_batch plans its own chunks: the step count does not bound the slots
+        best, batches = BEST_SLOTS_CCS, BEST_SLOTS_CCS
+        batch_zmws = args.ccs_chunk or max(1, args.zmws_per_step // 2)
     else:
         best, batches, batch_zmws = BEST_SLOTS, args.steps * args.batch_split, max(1, args.zmws_per_step // args.batch_split)
     if queue:

@@ -84,6 +84,9 @@ step() {
           > $OUT/ab_tall_$k.json 2> $OUT/ab_tall_$k.err || return 1
         echo "tall=$v $(summ $OUT/ab_tall_$k.json)"
       done ;;
+    tests_sel)    # the GPU tests of the files in TESTS only
+      timeout -k 10 600 python3 -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread \
+        > $OUT/pytest_sel.log 2>&1; local rc=$?; tail -3 $OUT/pytest_sel.log; return $rc ;;
     tests_fill)   # the fill / checkpoint parity tests only
       timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_ckpt_gpu.py -m gpu -x -q --timeout 300 \
         --timeout-method thread > $OUT/pytest_fill.log 2>&1; local rc=$?; tail -3 $OUT/pytest_fill.log; return $rc ;;
