@@ -756,8 +756,9 @@ def make_roofline(stats, local_time, workload):
             "fp64_valu": {"achieved": round(fp64_tf, 4), "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": round(fp64_tf / FP64_VALU_PEAK_TFLOPS, 6),
                           "note": f"{FLOP_PER_CELL} FLOP per DP cell-update over the timed region's wall time"},
-            "binding": f"device-wide: at five slots the device is saturated (five and six slots run at the same rate, "
-                       f"profiles/r4k_tall_prio_slots.txt), so the line follows the device's total work per ZMW; the "
+            "binding": f"device-wide: with eight slots of 1000-ZMW batches the device is saturated (five and six slots "
+                       f"ran at the same rate, profiles/r4k_tall_prio_slots.txt; ten and twelve slots lose, "
+                       f"profiles/r4u_batch_shape.txt), so the line follows the device's total work per ZMW; the "
                        f"tall fill itself is latency-bound on the serial insertion chain (a dependent mul + add + add per "
                        f"band row, a DPP hand-off per two rows, ~{CHAIN_ROW_CYCLES} cycles per row, "
                        f"tools/ubench/chain_step.hip) and its per-chunk band-end logic (DESIGN.md §6); neither HBM nor "
