@@ -132,6 +132,17 @@ step() {
           echo "$v $(summ $OUT/ab_env_$k.json) $(python3 -c "import json; d=json.load(open('$OUT/ab_env_$k.json')); print({n: round(v['device_ms']/max(1,v['launches']),2) for n,v in d['kernels'].items() if n in ('k_score','k_fill','k_fill_tall')})")"
         done
       done ;;
+    ab_args)  # interleaved A/B of bench arguments: ARGV="--streams 7;--streams 8" (';' between variants), 2 runs each
+      local k=0
+      IFS=';' read -ra VS <<< "${ARGV:---streams 8;--streams 7}"
+      for rep in 1 2; do
+        for v in "${VS[@]}"; do
+          k=$((k+1))
+          timeout -k 10 300 $BENCH --steps ${ABSTEPS:-20} --warmup 3 --cpu-sample 0 $v > $OUT/ab_args_$k.json \
+            2> $OUT/ab_args_$k.err || return 1
+          echo "[$v] $(summ $OUT/ab_args_$k.json)"
+        done
+      done ;;
     ab_ccs)   # interleaved A/B of the ccs stage's shape: CCSV="slots:chunk ..." (0 = the defaults), 2 runs each
       local k=0
       for rep in 1 2; do
