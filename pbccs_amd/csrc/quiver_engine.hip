@@ -1137,25 +1137,33 @@ std::vector<std::vector<int>> QuiverBatch::QVsMany(const std::vector<int>& zs)  
     for (int w = 0; w < n; ++w)
         for (long long g = posStart[w]; g < posStart[w + 1]; ++g)
             if (all[(size_t)g] < 0) amb.emplace_back(w, (int)(g - posStart[w]));
-    if (!amb.empty()) {
-        std::vector<std::vector<double>> sc(amb.size());
-        for (size_t a = 0; a < amb.size(); ++a) {
+    static const bool qtrace = std::getenv("PBCCS_QUIVER_TRACE") != nullptr;
+    if (qtrace) std::fprintf(stderr, "[quiver] qvs positions %lld host-recomputed %zu\n", nPos, amb.size());
+    if (!amb.empty()) {   // packed on the device (k_qgather), one download
+        const int na = (int)amb.size();
+        std::vector<long long> src(na), dst(na + 1, 0);
+        for (int a = 0; a < na; ++a) {
             const int w = amb[a].first, p = amb[a].second;
             const int* po = posOff.data() + posOffBase[w];
-            sc[a].resize((size_t)(po[p + 1] - po[p]));
-            if (!sc[a].empty())
-                QHIP(hipMemcpyAsync(sc[a].data(), dMScore_.ptr + mutStart[w] + po[p], sc[a].size() * sizeof(double),
-                                    hipMemcpyDeviceToHost, stream_));
+            src[a] = mutStart[w] + po[p];
+            dst[a + 1] = dst[a] + (po[p + 1] - po[p]);
         }
+        put(dAmbSrc_, src, stream_);
+        put(dAmbDst_, dst, stream_);
+        dAmbScore_.reserve(std::max<long long>(dst[na], 1), false);
+        launch_qgather(dMScore_.ptr, dAmbSrc_.ptr, dAmbDst_.ptr, na, dAmbScore_.ptr, stream_);
+        QHIP(hipGetLastError());
+        std::vector<double> sc;
+        get(sc, dAmbScore_, (size_t)dst[na], stream_);
         QHIP(hipStreamSynchronize(stream_));
-        for (size_t a = 0; a < amb.size(); ++a) {
+        par_for(na, [&](int a) {   // (a fifth of the positions at 10 passes: the high QVs sit near prob ~ eps)
             double sum = 0.0;
-            for (double s : sc[a]) {
-                const double f = (double)(float)s;   // Score() is a float sum
+            for (long long m = dst[a]; m < dst[a + 1]; ++m) {
+                const double f = (double)(float)sc[(size_t)m];   // Score() is a float sum
                 if (f < 0.0) sum += std::exp(f);
             }
             all[(size_t)(posStart[amb[a].first] + amb[a].second)] = probability_to_qv(1.0 - 1.0 / (1.0 + sum));
-        }
+        }, 4096);
     }
     std::vector<std::vector<int>> qv(n);
     for (int w = 0; w < n; ++w) qv[w].assign(all.begin() + posStart[w], all.begin() + posStart[w + 1]);

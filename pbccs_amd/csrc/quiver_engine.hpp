@@ -215,6 +215,8 @@ private:
     DevVec<long long> dWaveStart_, dWMutCount_, dEdge_;   // k_qscore_mid work + its edge-case task list
     DevVec<unsigned long long> dEdgeCount_;
     DevVec<long long> dPosStart_, dPosOffBase_;   // QVsMany: per-position QVs on the device (k_qqv)
+    DevVec<long long> dAmbSrc_, dAmbDst_;         // QVsMany: the positions left to the host (k_qgather)
+    DevVec<double> dAmbScore_;
     DevVec<int> dPosOff_, dQv_;
     DevVec<int> dWReadBase_, dWNReads_, dReadList_, dRActive_, dSelCode_, dSelRank_, dNSel_;
     DevVec<float> dWFast_;

@@ -2202,16 +2202,36 @@ __global__ void __launch_bounds__(256) k_qqv(QQvWork W, long long nPos)
         const double s = (double)(float)sc[m];   // Score() is a float sum
         if (s < 0.0) sum += exp(s);
     }
-    double prob = 1.0 - 1.0 / (1.0 + sum);
-    if (prob == 0.0) prob = 2.2250738585072014e-308;   // std::numeric_limits<double>::min()
     // The scores are the reference's floats bit for bit, but exp / log10 here are OCML's, the reference's
-    // glibc's: they may differ by an ulp, which can move the rounding only when -10 log10(prob) lies next to a
-    // .5 boundary or prob is tiny (1 + sum at the edge of 1.0).  Such positions are marked -1 and the host
-    // recomputes them with the host libm from the same float scores (QuiverBatch::QVsMany), so every QV is
-    // the reference's.
+    // glibc's: they may differ by an ulp.  That moves prob by at most err (a few ulps of 1 from the roundings of
+    // 1 + sum and its reciprocal, and of sum from its terms), so -10 log10(prob) by at most 4.343 err / prob: a
+    // position whose value lies that close to a .5 rounding boundary, or whose 1 + sum sits near the edge of
+    // 1.0, is marked -1 and the host recomputes it with the host libm from the same float scores
+    // (QuiverBatch::QVsMany), so every QV is the reference's.
+    constexpr double eps = 2.220446049250313e-16;
+    double prob = 1.0 - 1.0 / (1.0 + sum);
+    bool amb = W.hostAll != 0;
+    double rel = 0.0;
+    if (prob == 0.0) {
+        amb = amb || sum > 0.4 * eps;   // 1 + sum rounded to 1.0 here; near 2^-53 the host's sum may not
+        prob = 2.2250738585072014e-308;   // std::numeric_limits<double>::min()
+    } else {
+        rel = (4.0 * eps + 16.0 * eps * sum) / prob;   // (sum: up to ~9 terms, an ulp each and per partial sum)
+    }
     const double v = -10.0 * log10(prob);
     const double frac = v - floor(v);
-    W.qv[g] = (W.hostAll || prob < 1e-12 || fabs(frac - 0.5) < 1e-6) ? -1 : (int)round(v);
+    amb = amb || fabs(frac - 0.5) < 4.35 * rel + 1e-6;
+    W.qv[g] = amb ? -1 : (int)round(v);
+}
+
+// ---- k_qgather: the mutation scores of the positions k_qqv left to the host, packed for one download ---------
+__global__ void __launch_bounds__(256) k_qgather(const double* __restrict__ score, const long long* __restrict__ src,
+                                                 const long long* __restrict__ dst, int n, double* __restrict__ out)
+{
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= n) return;
+    const long long s = src[a], d0 = dst[a], d1 = dst[a + 1];
+    for (long long m = d0; m < d1; ++m) out[m] = score[s + (m - d0)];
 }
 
 // ---- k_qalign: RecursorBase::Alignment (detail/RecursorBase.cpp:118-264) -------------------------------
@@ -2307,6 +2327,12 @@ void launch_qqv(const QQvWork& W, long long nPos, hipStream_t s)
 {
     if (nPos <= 0) return;
     hipLaunchKernelGGL(k_qqv, dim3((unsigned)((nPos + 255) / 256)), dim3(256), 0, s, W, nPos);
+}
+
+void launch_qgather(const double* score, const long long* src, const long long* dst, int n, double* out, hipStream_t s)
+{
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_qgather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, score, src, dst, n, out);
 }
 
 void launch_qreduce(const QReduceWork& W, hipStream_t s)

@@ -131,6 +131,8 @@ struct QQvWork {
     int hostAll = 0;               // test hook (PBCCS_QQV_HOST=1): every position left to the host
 };
 void launch_qqv(const QQvWork& W, long long nPos, hipStream_t s);
+// QVsMany's host path: out[dst[a] .. dst[a + 1]) = score[src[a] ..], one thread per position a (n positions)
+void launch_qgather(const double* score, const long long* src, const long long* dst, int n, double* out, hipStream_t s);
 
 void launch_qfill(const QBatch& B, const int* reads, int n, hipStream_t s);
 // FillAlphaBeta with one wavefront per read (SparseSse recursors; reads of I + 1 <= kQCoopRows rows and windows

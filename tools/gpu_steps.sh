@@ -53,7 +53,7 @@ step() {
       PBCCS_ROUND_TRACE=1 PBCCS_FILL_PATHS=1 timeout -k 10 300 $BENCH --streams 1 --steps 5 --warmup 1 --cpu-sample 0 \
         > $OUT/trace1.json 2> $OUT/trace1.err && summ $OUT/trace1.json ;;
     quiver)
-      timeout -k 10 400 $BENCH --stage quiver --steps 5 --warmup 2 > $OUT/quiver.json 2> $OUT/quiver.err && \
+      PBCCS_QUIVER_TRACE=1 timeout -k 10 300 $BENCH --stage quiver --steps 5 --warmup 2 > $OUT/quiver.json 2> $OUT/quiver.err && \
         python3 -c "import json; d=json.load(open('$OUT/quiver.json')); print('quiver', d['value'], 'warmup_call_ms', d.get('warmup_call_ms'), 'timed_call_ms', d.get('timed_call_ms'))" ;;
     poa)
       timeout -k 10 400 $BENCH --stage poa --steps 5 --warmup 1 > $OUT/poa.json 2> $OUT/poa.err && \
