@@ -14,7 +14,7 @@ grid) to the last kernel end.  Every instant of it is assigned to exactly one cl
 
 Prints one JSON object: seconds per class over the timed region and per timed step, plus the tall fills' wave
 counts (grid blocks) by launch.
-Usage: critical_path.py <kernel_trace.csv> <steps> [warmup]
+Usage: critical_path.py <kernel_trace.csv> <steps> [warmup] [batches_per_step]
 """
 import csv
 import json
@@ -34,6 +34,7 @@ def kind(name):
 def main():
     path, steps = sys.argv[1], int(sys.argv[2])
     warmup = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    split = int(sys.argv[4]) if len(sys.argv) > 4 else 1   # device batches per step (bench.py --batch-split)
     rows = list(csv.DictReader(open(path)))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind(r["Kernel_Name"]), r["Kernel_Name"],
            int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))) for r in rows]
@@ -42,7 +43,8 @@ def main():
     g16 = [k for k in ks if k[2] == "fill16"]
     big = max(k[4] for k in g16)
     starts = [k[0] for k in g16 if k[4] == big]
-    t0 = starts[warmup] if len(starts) > warmup else starts[0]
+    skip = warmup * split
+    t0 = starts[skip] if len(starts) > skip else starts[0]
     t1 = max(k[1] for k in ks)
     events = []
     for s, e, kd, _, _ in ks:
