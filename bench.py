@@ -8,7 +8,8 @@ per-ZMW polish that pbccs' Consensus.h runs after the POA.  Inputs are copied to
 torch.cuda.synchronize() on both sides; the job time is the max over ranks.  The K steps are pipelined over
 S workspace slots (pbccs_batch_polish_many: one host thread + HIP stream per slot), so one batch's
 convergence tail -- the last refine rounds of its few slow ZMWs -- overlaps the others' work, the way ccs's
-ZMW thread pool overlaps ZMWs.  S is the measured best split (5) capped by what fits in HBM.
+ZMW thread pool overlaps ZMWs.  Each step's ZMWs are polished as BATCH_SPLIT device batches on S = 8 slots (the
+measured best shape, profiles/r4u_batch_shape.txt), capped by what fits in HBM.
 
 Multi-GPU: `--gpus N` without a launcher spawns N ranks itself (one process per GPU, RANK/LOCAL_RANK/
 WORLD_SIZE set before any HIP call; the parent never touches the GPU); under torch.distributed.run the
@@ -779,9 +780,12 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
     n_polished = sum(statuses.values()) - n_gated
     if world > 1 and scaling == "weak":   # each rank holds its own records: sum the counts
         import torch
-        t = torch.tensor([n_polished, n_gated], dtype=torch.float64)
+        from pbccs_amd import ZMW_STATUS
+        names = list(ZMW_STATUS)   # the same list on every rank (a record's status is one of these)
+        t = torch.tensor([n_polished, n_gated] + [statuses.get(k, 0) for k in names], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         n_polished, n_gated = int(t[0].item()), int(t[1].item())
+        statuses = {k: int(v) for k, v in zip(names, t[2:].tolist()) if v}
     cells = sum(s["cells"] for s in stats.values())
     gcups_local = cells / local_time / 1e9 if local_time > 0 else 0.0
     gcups = gcups_local * world
