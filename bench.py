@@ -33,7 +33,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# PMC HBM bytes per launch of each fill kind (tools/gpu_traffic.sh -> tools/pmc_traffic.py); used only while
+# PMC HBM bytes per launch of each fill kind (tools/gpu_steps.sh traffic -> tools/pmc_traffic.py); used only while
 # the kernel sources still hash to the digest the profile was taken at
 TRAFFIC_PROFILES = {"k_fill_tall": "r4_traffic_fill_tall.json", "k_fill": "r4_traffic_fill.json",
                     "k_score": "r4_traffic_score.json"}
