@@ -35,6 +35,8 @@ def _stand_in(rank, slow_rank=None, pad=0):
     def polish(zs):
         if rank == slow_rank:
             time.sleep(0.05 * len(zs))
+        elif slow_rank is not None:   # the fast rank takes a little time too, so the slow one's first pull is not
+            time.sleep(0.01 * len(zs))  # raced by the whole queue draining during its start-up
         return [{"rank": rank, "draft": z["draft"][::-1], "pad": "A" * pad} for z in zs]
     return polish
 
