@@ -169,30 +169,182 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(args):
-    """The oracle (bit-faithful CPU restatement of the reference's polish, test infrastructure) on host
-    cores, one ZMW per task on a thread pool like `ccs --numThreads` (src/main/ccs.cpp:222-230).  The thread
-    count is this process's CPU share: the GPU boxes give one GPU's job 16 cores of a larger machine
-    (OMP_NUM_THREADS), so hardware_concurrency() would oversubscribe."""
-    from concurrent.futures import ThreadPoolExecutor
-    from oracle import oracle as O
-    from pbccs_amd import synth
-
-    n = args.cpu_sample
+def cpu_threads(args, n):
+    """This process's CPU share: the GPU boxes give one GPU's job 16 cores of a larger machine (OMP_NUM_THREADS),
+    so hardware_concurrency() would oversubscribe."""
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
     threads = args.cpu_threads or max(1, min(share, os.cpu_count() or 1))
-    threads = max(1, min(threads, n))
-    zmws = synth.make_zmws(n, seed=args.seed + 99991, **workload_kw(args))
+    return max(1, min(threads, n))
+
+
+def oracle_record(z, settings):
+    """Consensus.h:436-512 for one ZMW on the CPU restatement (oracle/arrow_oracle.cpp), with the gates the batch
+    polish applies (capi.hip polish_one): AddRead of every read, MinPasses / MaxDropFraction, ZScores,
+    RefineConsensus, ConsensusQVs and the predicted-accuracy gate.  Returns the fields a GPU record carries."""
+    from oracle import oracle as O
+    rec = {"status": "Other", "consensus": "", "qvs": [], "n_tested": 0, "n_applied": 0, "add_read_results": []}
+    reads = z["reads"]
+    if not reads:
+        rec["status"] = "NoSubreads"
+        return rec
+    if len(z["draft"]) < settings.min_length:
+        rec["status"] = "TooShort"
+        return rec
+    sc = O.Scorer(z["draft"], z["snr"], score_diff=settings.score_diff)
+    st = [sc.add_read(r["seq"], r["strand"], r["ts"], r["te"], settings.min_zscore) for r in reads]
+    rec["add_read_results"] = st
+    n_passes = sum(1 for r, s in zip(reads, st) if s == 0 and r.get("full_pass", True))
+    if n_passes < settings.min_passes:
+        rec["status"] = "TooFewPasses"
+        return rec
+    if sum(1 for s in st if s != 0) / len(reads) > settings.max_drop_fraction:
+        rec["status"] = "TooManyUnusable"
+        return rec
+    sc.zscores()
+    ref = sc.refine(settings.max_iterations, settings.mutation_separation, settings.mutation_neighborhood)
+    rec["n_tested"], rec["n_applied"] = ref["n_tested"], ref["n_applied"]
+    if not ref["converged"]:
+        rec["status"] = "Other" if ref["error"] else "NonConvergent"
+        return rec
+    q = sc.qvs()
+    acc = 1.0 - sum(10.0 ** (v / -10.0) for v in q) / max(1, len(q))
+    rec.update(consensus=sc.template(), qvs=q,
+               status="PoorQuality" if acc < settings.min_predicted_accuracy else "Success")
+    return rec
+
+
+def zmw_cost(z):
+    """Cost model of one ZMW's CPU polish: template length x read bases (the scoring rounds dominate: every
+    unique mutation of the template against every read's band)."""
+    return float(len(z["draft"])) * float(sum(len(r["seq"]) for r in z["reads"] if r["seq"]))
+
+
+def sampled_cpu_baseline(args, settings, zs, res, idx, costs=None):
+    """The CPU baseline and the parity check of the timed run, on the same ZMWs.
+
+    idx: indices into the timed ZMWs `zs` (a list, or synth.SmrtCell) whose GPU records `res` the run produced.
+    Each sampled ZMW is polished by the CPU restatement (oracle_record) one ZMW per task on the host threads, as
+    `ccs --numThreads` runs the reference (src/main/ccs.cpp:222-230), and its record is compared with the GPU's:
+    status, AddRead results, nTested / nApplied, consensus (bit-exact) and QVs (+-1).
+    costs: the cost model of every timed ZMW (queue workloads): the CPU rate of the whole workload is then
+    extrapolated from the sample by the ratio estimator (CPU seconds per unit of cost on the sample x the
+    workload's mean cost), since a small subsample of heterogeneous ZMWs is not their mean.
+    Returns (cpu_baseline, parity_sample)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    n = len(idx)
+    threads = cpu_threads(args, n)
     O.lib()
+    sample = [zs[i] for i in idx]
+
+    def one(z):
+        t = time.perf_counter()
+        r = oracle_record(z, settings)
+        return r, time.perf_counter() - t
+
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=threads) as ex:   # ctypes releases the GIL: native threads in parallel
-        list(ex.map(lambda z: O.polish_zmw(z["draft"], z["reads"], z["snr"]), zmws))
+        out = list(ex.map(one, sample))
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port",
-            "cpu": cpu_model(), "nproc": os.cpu_count(),
-            "sample": f"{n} synthetic ZMWs of the same config ({args.workload}, seed {args.seed + 99991}), "
-                      f"oracle/arrow_oracle.cpp polish (AddRead, RefineConsensus, ConsensusQVs) one ZMW per task "
-                      f"on {threads} host threads, {dt:.1f} s wall"}
+    # ---- parity of the timed run's records against the restatement ----
+    bad, counts_eq, cons_eq, arr_eq, status_eq, max_qv = [], 0, 0, 0, 0, 0
+    for i, (e, _), g in zip(idx, out, [res[i] for i in idx]):
+        ok_status = g["status"] == e["status"]
+        ok_arr = list(g["add_read_results"]) == list(e["add_read_results"])
+        refined = e["status"] in ("Success", "PoorQuality", "NonConvergent")
+        ok_counts = (not refined) or (g["n_tested"], g["n_applied"]) == (e["n_tested"], e["n_applied"])
+        ok_cons = g["consensus"] == e["consensus"]
+        qd = 0
+        if e["qvs"] or g["qvs"]:
+            qd = max(abs(a - b) for a, b in zip(g["qvs"], e["qvs"])) if len(g["qvs"]) == len(e["qvs"]) else 999
+        max_qv = max(max_qv, qd)
+        status_eq += ok_status
+        arr_eq += ok_arr
+        counts_eq += ok_counts
+        cons_eq += ok_cons
+        if not (ok_status and ok_arr and ok_counts and ok_cons and qd <= 1):
+            bad.append(i)
+    parity = {"n": n, "status_equal": status_eq, "add_read_equal": arr_eq, "counts_equal": counts_eq,
+              "consensus_equal": cons_eq, "max_qv_diff": max_qv, "mismatched_zmws": bad[:16],
+              "ok": not bad,
+              "checked": "GPU records of the timed run against oracle/arrow_oracle.cpp on the same ZMWs: status, "
+                         "AddRead results, nTested/nApplied, consensus bit-exact, QVs within +-1"}
+    # ---- CPU rate ----
+    secs = [t for _, t in out]
+    cb = {"unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(), "nproc": os.cpu_count(),
+          "sample_wall_s": round(dt, 2), "sample_rate": round(n / dt, 4)}
+    desc = (f"{n} of the timed ZMWs ({args.workload}; indices {idx[0]}..{idx[-1]}), oracle/arrow_oracle.cpp "
+            f"restatement of Consensus.h:436-512 (AddRead, gates, RefineConsensus, ConsensusQVs) one ZMW per task on "
+            f"{threads} host threads, {dt:.1f} s wall")
+    if costs is None:
+        cb["value"] = round(n / dt, 4)
+    else:
+        c_s = sum(costs[i] for i in idx)
+        mean_all = sum(costs) / len(costs)
+        core_s_per_zmw = (sum(secs) / c_s) * mean_all   # ratio estimator x the workload's mean cost
+        cb["value"] = round(threads / core_s_per_zmw, 4)
+        cb["extrapolated"] = {"core_s_per_zmw": round(core_s_per_zmw, 3), "sample_core_s": round(sum(secs), 2),
+                              "cost_sample_mean": c_s / n, "cost_workload_mean": mean_all,
+                              "method": "ratio estimator: the sample's CPU seconds per unit of cost (template length "
+                                        "x read bases) times the workload's mean cost, on `cores` threads"}
+        desc += "; the workload's rate extrapolated from it (BASELINE.md CPU-baseline plan)"
+    cb["sample"] = desc
+    # the host's whole thread count, if the pool scaled linearly to it (an upper bound: SMT threads share cores)
+    cb["full_host_value"] = round(cb["value"] * (os.cpu_count() or threads) / threads, 4)
+    return cb, parity
+
+
+SAMPLE_COST_CAP = 8.5e8   # zmw_cost of a 10 kb / 8-pass ZMW: the largest ZMW a bounded CPU sample polishes
+
+
+def sample_indices(args, n_timed, costs=None):
+    """Which timed ZMWs the CPU leg polishes: every (N/n)-th ZMW of a homogeneous workload; for a heterogeneous
+    one a seeded simple random sample of the ZMWs no costlier than a 10 kb / 8-pass ZMW (a 20 kb / 30-pass ZMW
+    alone takes ~15 core-minutes on the restatement), the rest reached by the ratio estimator."""
+    import random
+    n = max(1, min(args.cpu_sample, n_timed))
+    if costs is None:
+        step = max(1, n_timed // n)
+        return list(range(0, n_timed, step))[:n]
+    elig = [i for i in range(n_timed) if costs[i] <= SAMPLE_COST_CAP]
+    rng = random.Random(args.seed + 99991)
+    return sorted(rng.sample(elig, min(n, len(elig))))
+
+
+def coverage(costs, idx_pool_cap=SAMPLE_COST_CAP):
+    elig = [c for c in costs if c <= idx_pool_cap]
+    return {"eligible_zmws_frac": round(len(elig) / max(1, len(costs)), 4),
+            "eligible_cost_frac": round(sum(elig) / max(1.0, sum(costs)), 4),
+            "cap": f"ZMWs with template length x read bases <= {idx_pool_cap:.3g} (a 10 kb / 8-pass ZMW)"}
+
+
+class HostUsage:
+    """The rank's host cost over a timed region: CPU seconds of all its threads (getrusage RUSAGE_SELF: the
+    engine's slot threads, the POA workers and Python) and the process's peak RSS."""
+
+    def __init__(self):
+        import resource
+        self._r = resource
+        u = resource.getrusage(resource.RUSAGE_SELF)
+        self.t0 = u.ru_utime + u.ru_stime
+
+    def report(self, zmws_local, world):
+        u = self._r.getrusage(self._r.RUSAGE_SELF)
+        cpu = u.ru_utime + u.ru_stime - self.t0
+        rss = u.ru_maxrss / 2**20   # KiB -> GiB
+        out = {"cpu_s": round(cpu, 3), "cpu_ms_per_zmw": round(1e3 * cpu / max(1, zmws_local), 4),
+               "rss_gb": round(rss, 3)}
+        if world > 1:
+            out["cpu_s_max_rank"] = round(max_over_ranks(cpu, world), 3)
+            out["rss_gb_max_rank"] = round(max_over_ranks(rss, world), 3)
+        out["note"] = ("rank 0's host CPU seconds (user + system, every thread) over the timed region, per ZMW it "
+                       "polished, and its peak resident set")
+        return out
+
+
+def cpu_share_note():
+    return ("vs_cpu: against the CPU restatement on this job's CPU share (`cpu_baseline.cores` threads); "
+            "vs_cpu_full_host: against that rate scaled linearly to all `nproc` hardware threads of the node")
 
 
 def kernel_source_digest():
@@ -254,8 +406,10 @@ def queue_workload(args, rank, world, eng, settings, seed0):
         pbccs_amd.polish_stream(wz, settings, eng)
     log(rank, "[bench] warmup done")
     if kw is None:
-        # the same cell on every rank, generated lazily: a rank materialises only the chunks it pulls
+        # the same cell on every rank, generated lazily: a rank materialises only the chunks it pulls.  The
+        # shapes (length, passes) are drawn before the timed region, as ccs would know them from the .pbi index
         zs = synth.SmrtCell(n, seed=args.seed + 3)
+        zs.shapes()
     else:
         zs = synth.make_zmws(n, seed=seed0, **kw)
     eng.kernel_stats(reset=True)
@@ -264,6 +418,7 @@ def queue_workload(args, rank, world, eng, settings, seed0):
         dist.barrier()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
+    host = HostUsage()
     t0 = time.perf_counter()
     done = heartbeat(rank, t0)
     qstats = {}
@@ -284,16 +439,18 @@ def queue_workload(args, rank, world, eng, settings, seed0):
         dist.barrier()
     local_time = time.perf_counter() - t0
     job_time = max_over_ranks(local_time, world)
+    local_n = qstats.pop("zmws_local", n) if kw is None else n
+    hostu = host.report(local_n, world)
     if kw is None:   # host memory high-water of the ranks (the cell is generated per chunk; rank 0 holds the records)
-        import resource
-        rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20   # KiB -> GiB
-        qstats["host_rss_gb_rank0"] = round(rss, 3)
-        qstats["host_rss_gb_max"] = round(max_over_ranks(rss, world), 3)
+        qstats["host_rss_gb_rank0"] = hostu["rss_gb"]
+        qstats["host_rss_gb_max"] = hostu.get("rss_gb_max_rank", hostu["rss_gb"])
         qstats["gen_ms_max"] = round(max_over_ranks(qstats.get("gen_ms", 0.0), world), 1)
+    costs = zs.costs() if kw is None else [zmw_cost(z) for z in zs]
+    extra = {"host": hostu, "zs": zs, "costs": costs}
     if kw is None:   # rank 0 holds the whole cell's records; the count is the cell
-        return job_time, local_time, (res or []), desc, "strong", n, qstats
+        return job_time, local_time, (res or []), desc, "strong", n, qstats, extra
     return job_time, local_time, res, desc + " (work queue; timed region includes the read upload)", "weak", \
-        n * world, None
+        n * world, None, extra
 
 
 def max_over_ranks(t, world):
@@ -333,8 +490,8 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
-    if args.cpu_sample is None:
-        args.cpu_sample = 256 if args.workload == "2kb" else 0
+    if args.cpu_sample is None:   # ~10-60 s of the restatement on the box's 16 threads
+        args.cpu_sample = {"2kb": 256, "10kb": 16, "mixed": 32, "smrtcell": 32}[args.workload]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -381,9 +538,10 @@ def main():
     if args.stage == "quiver":
         return quiver_stage(args, rank, world, eng, barrier, sync, seed0)
     if args.workload != "2kb":
-        job_time, local_time, res, workload, scaling, total, qstats = queue_workload(args, rank, world, eng, settings,
-                                                                                     seed0)
-        return report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total, qstats)
+        job_time, local_time, res, workload, scaling, total, qstats, extra = queue_workload(args, rank, world, eng,
+                                                                                            settings, seed0)
+        return report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total, qstats,
+                      extra=extra, settings=settings)
 
     # a step's ZMWs as BATCH_SPLIT device batches (the step is the workload's unit; the batch, the engine's)
     def split(zs):
@@ -406,18 +564,32 @@ def main():
         log(rank, f"[bench] band pools: {per_slot / 2**30:.1f} GB mapped per slot x {slots}")
 
     # ---- inputs resident in HBM before the timed region ------------------------------------------
+    # split three ways: the synthetic generation (Python strings: the stand-in for reading the subreads), the
+    # marshalling into the C structs of the boundary, and pbccs_batch_create (per ZMW the ArrowConfig's
+    # transition tables and expectations, the reverse-complement template, then the one-copy upload)
+    eng.counters(reset=True)
     t_prep = time.perf_counter()
+    synth_s = 0.0
     batches = []
     for k in range(args.steps):
+        ts = time.perf_counter()
         zs = synth.make_zmws(args.zmws_per_step, args.length, args.passes, seed=seed0 + k)
+        synth_s += time.perf_counter() - ts
         batches.extend(pbccs_amd.PreparedBatch(part, settings, eng) for part in split(zs))
-    log(rank, f"[bench] prepared {args.steps} steps x {args.zmws_per_step} ZMWs in {time.perf_counter() - t_prep:.1f}s")
+    sync()
+    prep = {"synth_s": round(synth_s, 3), "marshal_s": round(sum(b.marshal_s for b in batches), 3),
+            "create_s": round(sum(b.create_s for b in batches), 3)}
+    log(rank, f"[bench] prepared {args.steps} steps x {args.zmws_per_step} ZMWs in {time.perf_counter() - t_prep:.1f}s "
+              f"{prep}")
+    c0 = eng.counters(reset=True)
+    prep["create_host_s"] = round(c0["create_host_ns"] / 1e9, 3)
+    prep["create_upload_s"] = round(c0["create_upload_ns"] / 1e9, 3)
     eng.kernel_stats(reset=True)
-    eng.counters(reset=True)
 
     # ---- timed region: exactly K steps --------------------------------------------------------
     barrier()
     sync()
+    host = HostUsage()
     t0 = time.perf_counter()
     pbccs_amd.polish_many(batches)   # the K steps, pipelined over the slots' HIP streams / host threads
     sync()
@@ -427,32 +599,54 @@ def main():
     job_time = max_over_ranks(local_time, world)
 
     res = [r for b in batches for r in b.results()]
+    zs_all = [z for b in batches for z in b.zmws]
+    hostu = host.report(len(res), world)
     for b in batches:
         b.close()
+    prep["create_frac_of_timed"] = round(prep["create_s"] / local_time, 4)
+    prep["note"] = ("outside the timed region (inputs resident in HBM when it starts): synth_s the synthetic "
+                    "subreads, marshal_s the C structs, create_s pbccs_batch_create (create_host_s of it the per-ZMW "
+                    "setup of Consensus.h:437-453 -- transition tables, expectations, reverse complement -- and "
+                    "create_upload_s the descriptor arena and read uploads)")
     workload = (f"configs[1]: synthetic {args.length} bp insert, {args.passes} full passes, "
                 f"{args.zmws_per_step} ZMWs per step")
-    report(args, rank, world, eng, slots, job_time, local_time, res, workload, "weak", len(res) * world)
+    report(args, rank, world, eng, slots, job_time, local_time, res, workload, "weak", len(res) * world,
+           extra={"host": hostu, "zs": zs_all, "costs": None, "prepare": prep}, settings=settings)
 
 
-def poa_cpu_baseline(args, n):
+def poa_cpu_baseline(args, steps_in, res, n):
     """The POA restatement (oracle/poa_oracle.cpp, SparsePoa as Consensus.h drives it) one ZMW per task on the
-    host threads, like the polish baseline."""
+    host threads, like the polish baseline, on every (N/n)-th ZMW of the timed steps; each draft, read key and
+    extent is checked against the GPU's record of the timed run (bit-exact)."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
-    from pbccs_amd import synth
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    threads = max(1, min(args.cpu_threads or share, os.cpu_count() or 1, n))
-    zr = [[r["seq"] for r in z["reads"]] for z in synth.make_zmws(n, args.length, args.passes, seed=args.seed + 99991)]
+    flat_in = [z for step in steps_in for z in step]
+    flat_res = [r for step in res for r in step]
+    args_n = argparse.Namespace(**vars(args))
+    args_n.cpu_sample = n
+    idx = sample_indices(args_n, len(flat_in))
+    threads = cpu_threads(args, len(idx))
     O.lib()
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=threads) as ex:
-        list(ex.map(O.sparse_poa, zr))
+        exp = list(ex.map(O.sparse_poa, [flat_in[i] for i in idx]))
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
-            "nproc": os.cpu_count(),
-            "sample": f"{n} synthetic ZMWs of the same config (seed {args.seed + 99991}), oracle/poa_oracle.cpp "
-                      f"SparsePoa (OrientAndAddRead per subread, FindConsensus) one ZMW per task on {threads} host "
-                      f"threads, {dt:.1f} s wall"}
+    bad = []
+    for i, e in zip(idx, exp):
+        g = flat_res[i]
+        if (g["consensus"], list(g["keys"]), g["summaries"]) != (e["consensus"], e["keys"], e["summaries"]):
+            bad.append(i)
+    n = len(idx)
+    cb = {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+          "nproc": os.cpu_count(),
+          "sample": f"{n} of the timed ZMWs (every {max(1, len(flat_in) // n)}-th), oracle/poa_oracle.cpp SparsePoa "
+                    f"(OrientAndAddRead per subread, FindConsensus) one ZMW per task on {threads} host threads, "
+                    f"{dt:.1f} s wall"}
+    cb["full_host_value"] = round(cb["value"] * (os.cpu_count() or threads) / threads, 4)
+    parity = {"n": n, "draft_equal": n - len(bad), "mismatched_zmws": bad[:16], "ok": not bad,
+              "checked": "GPU drafts, read keys and PoaAlignmentSummary extents of the timed run against "
+                         "oracle/poa_oracle.cpp on the same subreads, bit-exact"}
+    return cb, parity
 
 
 def poa_stage(args, rank, world, eng, barrier, sync, seed0):
@@ -473,12 +667,14 @@ def poa_stage(args, rank, world, eng, barrier, sync, seed0):
     poa.poa_stats(eng, reset=True)
     barrier()
     sync()
+    host = HostUsage()
     t0 = time.perf_counter()
     res = [poa.poa_batch(x, engine=eng) for x in steps_in]
     sync()
     barrier()
     local_time = time.perf_counter() - t0
     job_time = max_over_ranks(local_time, world)
+    hostu = host.report(args.steps * args.zmws_per_step, world)
     st = poa.poa_stats(eng, reset=True)
     total = args.steps * args.zmws_per_step * world
     launches = max(1, st["launches"])
@@ -506,43 +702,97 @@ def poa_stage(args, rank, world, eng, barrier, sync, seed0):
                                                              "total_ms")},
                 "draft_len_mean": round(sum(len(r["consensus"]) for b in res for r in b) / max(1, total // world), 1)},
     }
+    out["host"] = hostu
+    parity_ok = True
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        out["cpu_baseline"] = poa_cpu_baseline(args, min(args.cpu_sample, 48))
-        out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
+        cb, parity = poa_cpu_baseline(args, steps_in, res, min(args.cpu_sample, 48))
+        out["cpu_baseline"], out["parity_sample"] = cb, parity
+        out["vs_cpu"] = round(out["value"] / cb["value"], 2)
+        out["vs_cpu_full_host"] = round(out["value"] / cb["full_host_value"], 3)
+        out["vs_cpu_note"] = cpu_share_note()
+        parity_ok = parity["ok"]
     if rank == 0:
         emit(out)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    if not parity_ok:
+        log(rank, f"[bench] PARITY FAILURE on the timed POA run's sample: {out['parity_sample']}")
+        sys.exit(3)
 
 
-def quiver_cpu_baseline(args, n):
+def quiver_cpu_baseline(args, zs, res):
     """The Quiver CPU restatement (oracle/quiver_oracle.cpp: the SSE recursor's single-precision operations
-    in order) on host threads, one ZMW per task: AddRead, RefineConsensus, ConsensusQVs."""
+    in order) on host threads, one ZMW per task -- AddRead, RefineConsensus, ConsensusQVs -- on every (N/n)-th of
+    the timed scorers, whose GPU records it checks: converged, nTested / nApplied, consensus and QVs, all exact."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
     from pbccs_amd import synth
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    threads = max(1, min(args.cpu_threads or share, n))
-    zs = synth.make_quiver_zmws(n, args.length, args.passes, seed=args.seed + 99991)
+    idx = sample_indices(args, len(zs))
+    n = len(idx)
+    threads = cpu_threads(args, n)
     O.lib()
 
     def one(z):
         o = O.QuiverScorer(z["tpl"], synth.QUIVER_PARAMS, score_diff=synth.QUIVER_SCORE_DIFF)
         for r in z["reads"]:
             o.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["features"])
-        o.refine()
-        o.qvs()
+        ref = o.refine()
+        return {"converged": ref["converged"], "n_tested": ref["n_tested"], "n_applied": ref["n_applied"],
+                "consensus": o.template(), "qvs": o.qvs()}
 
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=threads) as ex:
-        list(ex.map(one, zs))
+        exp = list(ex.map(one, [zs[i] for i in idx]))
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
-            "nproc": os.cpu_count(),
-            "sample": f"{n} synthetic Quiver ZMWs of the same config (seed {args.seed + 99991}), "
-                      f"oracle/quiver_oracle.cpp AddRead + RefineConsensus + ConsensusQVs one ZMW per task on "
-                      f"{threads} host threads, {dt:.1f} s wall"}
+    bad, cons_eq, counts_eq, qv_eq = [], 0, 0, 0
+    for i, e in zip(idx, exp):
+        g = res[i]
+        ok_c = g["consensus"] == e["consensus"]
+        ok_n = (bool(g["converged"]), g["n_tested"], g["n_applied"]) == (e["converged"], e["n_tested"], e["n_applied"])
+        ok_q = list(g["qvs"] or []) == list(e["qvs"])
+        cons_eq += ok_c
+        counts_eq += ok_n
+        qv_eq += ok_q
+        if not (ok_c and ok_n and ok_q):
+            bad.append(i)
+    cb = {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+          "nproc": os.cpu_count(),
+          "sample": f"{n} of the timed Quiver ZMWs (every {max(1, len(zs) // n)}-th), oracle/quiver_oracle.cpp AddRead + "
+                    f"RefineConsensus + ConsensusQVs one ZMW per task on {threads} host threads, {dt:.1f} s wall"}
+    cb["full_host_value"] = round(cb["value"] * (os.cpu_count() or threads) / threads, 4)
+    parity = {"n": n, "consensus_equal": cons_eq, "counts_equal": counts_eq, "qvs_equal": qv_eq,
+              "mismatched_zmws": bad[:16], "ok": not bad,
+              "checked": "GPU records of the timed run against oracle/quiver_oracle.cpp on the same scorers: "
+                         "converged, nTested/nApplied, consensus and QVs exact"}
+    return cb, parity
+
+
+def quiver_roofline(stats, local_time):
+    """The Quiver stage's dominant kernel (by device time) priced against HBM: the fills store every pass's FP32
+    band (4 B per cell) and column metadata (12 B per column), counted in-kernel over the completed fills."""
+    fills = {k: v for k, v in stats.items() if k.startswith("k_qfill") and v["launches"]}
+    if not fills:
+        return None
+    dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["device_ms"])
+    fk, fv = max(fills.items(), key=lambda kv: kv[1]["device_ms"])
+    launches = max(1, fv["launches"])
+    avg_ms = fv["device_ms"] / launches
+    bpl = fv["bytes"] / launches
+    achieved = bpl / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
+    in_flight = fv["device_ms"] / (local_time * 1e3) if local_time > 0 else None
+    return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None, "kernel": fk,
+            "dominant_kernel": dom_name, "avg_launch_ms": round(avg_ms, 4), "launches": fv["launches"],
+            "bytes_per_launch": bpl, "cells_per_launch": fv["cells"] / launches,
+            "in_flight": round(in_flight, 3) if in_flight is not None else None,
+            "wall": {"achieved": round(fv["bytes"] / local_time / 1e9, 3),
+                     "frac": round(fv["bytes"] / local_time / 1e9 / HBM_PEAK_GBS, 6), "unit": "GB/s"},
+            "per_launch_note": "achieved/frac: algorithmic bytes per launch (4 B per stored FP32 band cell + 12 B per "
+                               "column per pass, counted in-kernel) / HIP-event launch time on the kernel's stream",
+            "binding": "latency: a band column is a chain of dependent LDS round trips (Inc/Merge/Del, then the "
+                       "serial Extra cascade and the block band-end test); ~10 rows per column use 16 lanes of "
+                       "four reads per wavefront (DESIGN.md §3.8); neither HBM nor FP32 VALU"}
 
 
 def quiver_stage(args, rank, world, eng, barrier, sync, seed0):
@@ -567,12 +817,15 @@ def quiver_stage(args, rank, world, eng, barrier, sync, seed0):
     eng.kernel_stats(reset=True)
     barrier()
     sync()
+    host = HostUsage()
     t0 = time.perf_counter()
     res = prep.run(engine=eng)
     sync()
     barrier()
     local_time = time.perf_counter() - t0
     job_time = max_over_ranks(local_time, world)
+    hostu = host.report(len(zs), world)
+    stats = eng.kernel_stats(reset=True)
     total = len(zs) * world
     out = {"metric": "Quiver ZMWs/sec (AddRead, RefineConsensus, ConsensusQVs per scorer) on MI355X",
            "value": round(total / job_time, 3), "unit": "ZMWs/s", "n_gpus": world, "steps": args.steps,
@@ -585,65 +838,110 @@ def quiver_stage(args, rank, world, eng, barrier, sync, seed0):
                       "parallelism": f"zmw-shard x{world}"},
            "converged": sum(r["converged"] for r in res), "mean_iterations_applied":
                round(sum(r["n_applied"] for r in res) / max(1, len(res)), 2), "warmup_call_ms": warm_ms,
-           "timed_call_ms": round(local_time * 1e3, 1)}
+           "timed_call_ms": round(local_time * 1e3, 1),
+           "gcups": round(sum(v["cells"] for k, v in stats.items() if k.startswith("k_qfill")) / local_time / 1e9, 3),
+           "roofline": quiver_roofline(stats, local_time),
+           "kernels": {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
+                           "gcells": round(v["cells"] / 1e9, 4), "gbytes": round(v["bytes"] / 1e9, 4)}
+                       for k, v in stats.items() if v["launches"]},
+           "host": hostu}
+    parity_ok = True
     if rank == 0 and args.cpu_sample:
-        out["cpu_baseline"] = quiver_cpu_baseline(args, args.cpu_sample)
+        cb, parity = quiver_cpu_baseline(args, zs, res)
+        out["cpu_baseline"], out["parity_sample"] = cb, parity
+        out["vs_cpu"] = round(out["value"] / cb["value"], 2)
+        out["vs_cpu_full_host"] = round(out["value"] / cb["full_host_value"], 3)
+        out["vs_cpu_note"] = cpu_share_note()
+        parity_ok = parity["ok"]
     if rank == 0:
         emit(out)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    if not parity_ok:
+        log(rank, f"[bench] PARITY FAILURE on the timed Quiver run's sample: {out['parity_sample']}")
+        sys.exit(3)
 
 
-def ccs_cpu_baseline(args, n):
+def ccs_cpu_baseline(args, settings, work, res, n):
     """Consensus.h's per-ZMW path on the host (include/pacbio/ccs/Consensus.h:395-552): FilterReads and
     ExtractMappedRead (pbccs_amd.driver, host code), the SparsePoa restatement (oracle/poa_oracle.cpp) and the
-    polish restatement (oracle/arrow_oracle.cpp: AddRead, RefineConsensus, ConsensusQVs), one ZMW per task on
-    the host threads like `ccs --numThreads` (src/main/ccs.cpp:222-230)."""
+    polish restatement (oracle/arrow_oracle.cpp: AddRead, the gates, RefineConsensus, ConsensusQVs), one ZMW per
+    task on the host threads like `ccs --numThreads` (src/main/ccs.cpp:222-230), on every (N/n)-th ZMW of the timed
+    run; each record (status, consensus, nTested / nApplied, QVs +-1) is checked against the GPU's."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
-    from pbccs_amd import driver, synth
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    threads = max(1, min(args.cpu_threads or share, os.cpu_count() or 1, n))
-    chunks = [{"snr": z["snr"], "reads": [{"seq": r["seq"]} for r in z["reads"]]}
-              for z in synth.make_zmws(n, args.length, args.passes, seed=args.seed + 99991)]
+    from pbccs_amd import driver
+    args_n = argparse.Namespace(**vars(args))
+    args_n.cpu_sample = n
+    idx = sample_indices(args_n, len(work))
+    threads = cpu_threads(args, len(idx))
     O.lib()
 
     def one(c):
-        reads = driver.filter_reads(c["reads"], 10)
+        rec = {"status": "Other", "consensus": "", "qvs": [], "n_tested": 0, "n_applied": 0}
+        reads = driver.filter_reads(c["reads"], settings.min_length)
         if not reads or all(r is None for r in reads):
-            return "NoSubreads"
+            rec["status"] = "NoSubreads"
+            return rec
         p = O.sparse_poa([None if r is None else r["seq"] for r in reads])
-        if len(p["consensus"]) < 10:
-            return "TooShort"
-        mapped = [driver.extract_mapped_read(reads[i], p["summaries"][k], 10)
+        if len(p["consensus"]) < settings.min_length:
+            rec["status"] = "TooShort"
+            return rec
+        mapped = [driver.extract_mapped_read(reads[i], p["summaries"][k], settings.min_length)
                   for i, k in enumerate(p["keys"]) if k >= 0]
         # Consensus.h:474-491's gates, as pbccs_ccs_batch applies them: reads FilterReads, the POA or
         # ExtractMappedRead dropped count in the drop fraction's denominator only
-        sc = O.Scorer(p["consensus"], c["snr"])
-        st = [sc.add_read(m["seq"], m["strand"], m["ts"], m["te"], -5.0) for m in mapped if m is not None]
+        sc = O.Scorer(p["consensus"], c["snr"], score_diff=settings.score_diff)
+        st = [sc.add_read(m["seq"], m["strand"], m["ts"], m["te"], settings.min_zscore) for m in mapped if m is not None]
         ok = sum(1 for x in st if x == 0)
-        if ok < 3:
-            return "TooFewPasses"
-        if (len(st) - ok) / len(c["reads"]) > 0.34:
-            return "TooManyUnusable"
+        if ok < settings.min_passes:
+            rec["status"] = "TooFewPasses"
+            return rec
+        if (len(st) - ok) / len(c["reads"]) > settings.max_drop_fraction:
+            rec["status"] = "TooManyUnusable"
+            return rec
         sc.zscores()
-        if not sc.refine(40, 10, 20)["converged"]:
-            return "NonConvergent"
-        sc.qvs()
-        return "Polished"
+        ref = sc.refine(settings.max_iterations, settings.mutation_separation, settings.mutation_neighborhood)
+        rec["n_tested"], rec["n_applied"] = ref["n_tested"], ref["n_applied"]
+        if not ref["converged"]:
+            rec["status"] = "NonConvergent"
+            return rec
+        q = sc.qvs()
+        acc = 1.0 - sum(10.0 ** (v / -10.0) for v in q) / max(1, len(q))
+        rec.update(consensus=sc.template(), qvs=q,
+                   status="PoorQuality" if acc < settings.min_predicted_accuracy else "Success")
+        return rec
 
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=threads) as ex:
-        status = list(ex.map(one, chunks))
+        exp = list(ex.map(one, [work[i] for i in idx]))
     dt = time.perf_counter() - t0
-    counts = {k: status.count(k) for k in sorted(set(status))}
-    return {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
-            "nproc": os.cpu_count(), "zmw_status": counts,
-            "sample": f"{n} synthetic ZMWs of the same config (seed {args.seed + 99991}): FilterReads, "
-                      f"oracle/poa_oracle.cpp SparsePoa, ExtractMappedRead, oracle/arrow_oracle.cpp AddRead, the "
-                      f"TooFewPasses / TooManyUnusable gates, RefineConsensus and ConsensusQVs of converged ZMWs, one "
-                      f"ZMW per task on {threads} host threads, {dt:.1f} s wall"}
+    bad, max_qv = [], 0
+    for i, e in zip(idx, exp):
+        g = res[i]
+        qd = 0
+        if e["qvs"] or g["qvs"]:
+            qd = max(abs(a - b) for a, b in zip(g["qvs"], e["qvs"])) if len(g["qvs"]) == len(e["qvs"]) else 999
+        max_qv = max(max_qv, qd)
+        refined = e["status"] in ("Success", "PoorQuality", "NonConvergent")
+        if g["status"] != e["status"] or g["consensus"] != e["consensus"] or qd > 1 or \
+                (refined and (g["n_tested"], g["n_applied"]) != (e["n_tested"], e["n_applied"])):
+            bad.append(i)
+    n = len(idx)
+    statuses = [e["status"] for e in exp]
+    cb = {"value": round(n / dt, 4), "unit": "ZMWs/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+          "nproc": os.cpu_count(), "zmw_status": {k: statuses.count(k) for k in sorted(set(statuses))},
+          "sample": f"{n} of the timed ZMWs (every {max(1, len(work) // n)}-th): FilterReads, oracle/poa_oracle.cpp "
+                    f"SparsePoa, ExtractMappedRead, oracle/arrow_oracle.cpp AddRead, the TooFewPasses / "
+                    f"TooManyUnusable gates, RefineConsensus and ConsensusQVs of converged ZMWs, one ZMW per task on "
+                    f"{threads} host threads, {dt:.1f} s wall"}
+    cb["full_host_value"] = round(cb["value"] * (os.cpu_count() or threads) / threads, 4)
+    parity = {"n": n, "record_equal": n - len(bad), "max_qv_diff": max_qv, "mismatched_zmws": bad[:16],
+              "ok": not bad,
+              "checked": "GPU records of the timed run against the CPU pipeline on the same subreads: status, "
+                         "consensus bit-exact, nTested/nApplied, QVs within +-1"}
+    return cb, parity
 
 
 def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
@@ -665,12 +963,15 @@ def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
     eng.kernel_stats(reset=True)
     barrier()
     sync()
+    host = HostUsage()
     t0 = time.perf_counter()
     res = driver.ccs_batch(work, settings, eng)
     sync()
     barrier()
     local_time = time.perf_counter() - t0
     job_time = max_over_ranks(local_time, world)
+    hostu = host.report(len(work), world)
+    kstats = eng.kernel_stats(reset=True)
     statuses = {}
     for r in res:
         statuses[r["status"]] = statuses.get(r["status"], 0) + 1
@@ -686,15 +987,30 @@ def ccs_stage(args, rank, world, eng, slots, settings, barrier, sync, seed0):
                                   f"ZMW, {args.steps} x {args.zmws_per_step} ZMWs in one pbccs_ccs_batch",
                       "slots": slots, "chunk": args.ccs_chunk or "planned", "parallelism": f"zmw-shard x{world}"},
            "zmw_status": statuses, "poa_wall_ms": round(st["total_ms"], 1),
-           "poa_device_ms": round(st["device_ms"], 1), "poa_thread_ms": round(st["thread_ms"], 1)}
+           "poa_device_ms": round(st["device_ms"], 1), "poa_thread_ms": round(st["thread_ms"], 1),
+           "host": hostu}
+    if any(v["launches"] for v in kstats.values()):   # the polish half's dominant kernel (the POA's: --stage poa)
+        out["roofline"] = make_roofline(kstats, local_time, None)
+        out["roofline"]["scope"] = "the polish kernels of the ccs run (the POA kernels' roofline is the --stage poa line)"
+        out["kernels"] = {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
+                              "gcells": round(v["cells"] / 1e9, 4), "gbytes": round(v["bytes"] / 1e9, 4)}
+                          for k, v in kstats.items() if v["launches"]}
+    parity_ok = True
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        out["cpu_baseline"] = ccs_cpu_baseline(args, min(args.cpu_sample, 160))
-        out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
+        cb, parity = ccs_cpu_baseline(args, settings, work, res, min(args.cpu_sample, 160))
+        out["cpu_baseline"], out["parity_sample"] = cb, parity
+        out["vs_cpu"] = round(out["value"] / cb["value"], 2)
+        out["vs_cpu_full_host"] = round(out["value"] / cb["full_host_value"], 3)
+        out["vs_cpu_note"] = cpu_share_note()
+        parity_ok = parity["ok"]
     if rank == 0:
         emit(out)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    if not parity_ok:
+        log(rank, f"[bench] PARITY FAILURE on the timed ccs run's sample: {out['parity_sample']}")
+        sys.exit(3)
 
 
 def make_roofline(stats, local_time, workload):
@@ -767,8 +1083,10 @@ def make_roofline(stats, local_time, workload):
             "source_digest": digest}
 
 
-def report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total_zmws, qstats=None):
+def report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total_zmws, qstats=None,
+           extra=None, settings=None):
     import torch.distributed as dist
+    extra = extra or {}
     stats = eng.kernel_stats(reset=True)
     counters = eng.counters(reset=True)
     statuses = {}
@@ -831,7 +1149,7 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
         "roofline": roofline,
         "kernels": {k: {"launches": v["launches"], "device_ms": round(v["device_ms"], 3),
                         "gcells": round(v["cells"] / 1e9, 4), "gbytes": round(v["bytes"] / 1e9, 4)}
-                    for k, v in stats.items()},
+                    for k, v in stats.items() if v["launches"]},
         "score_tasks": counters["score_tasks"],
         "mutations_scored": counters["mutations"],
         "band_memory_gb": {k: round(counters[k] / 2**30, 3) for k in
@@ -840,13 +1158,34 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
     }
     if qstats:   # configs[4]: records stream to rank 0 per chunk; tail_ms = rank 0's wait after its last chunk
         out["queue"] = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in qstats.items()}
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline(args)
-        out["vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
+    if "host" in extra:
+        out["host"] = extra["host"]
+    if "prepare" in extra:
+        out["prepare"] = extra["prepare"]
+    parity_ok = True
+    # the CPU leg on rank 0 (one rank: its records are the run's; several ranks: rank 0 holds the whole cell's
+    # records for the strong-scaling cell, its own for the weak-scaling lines)
+    if rank == 0 and args.cpu_sample > 0 and res and extra.get("zs") is not None and settings is not None:
+        zs, costs = extra["zs"], extra.get("costs")
+        if world == 1 or scaling == "strong":
+            idx = sample_indices(args, len(res), costs)
+            log(rank, f"[bench] CPU leg: {len(idx)} of the timed ZMWs on the restatement")
+            cb, parity = sampled_cpu_baseline(args, settings, zs, res, idx, costs)
+            if costs is not None:
+                cb["coverage"] = coverage(costs)
+            out["cpu_baseline"] = cb
+            out["parity_sample"] = parity
+            out["vs_cpu"] = round(value / cb["value"], 2)
+            out["vs_cpu_full_host"] = round(value / cb["full_host_value"], 3)
+            out["vs_cpu_note"] = cpu_share_note()
+            parity_ok = parity["ok"]
     if rank == 0:
         emit(out)
     if world > 1:
         dist.destroy_process_group()
+    if not parity_ok:
+        log(rank, f"[bench] PARITY FAILURE on the timed run's sample: {out['parity_sample']}")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -225,6 +225,9 @@ typedef struct {
     long long band_used_bytes;   /* max over batches: band cells the reads' last fills stored */
     long long pool_mapped_bytes; /* device memory the workspace slots' band pools hold mapped now */
     long long oom_retries;       /* device batches rerun after running the device out of memory */
+    long long create_host_ns;    /* pbccs_batch_create: per-ZMW host setup (Consensus.h:437-453: transition
+                                    tables, expectations, reverse complement, descriptors) */
+    long long create_upload_ns;  /* pbccs_batch_create: device reservations + the one-copy input upload */
 } pbccs_counters;
 int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset);
 

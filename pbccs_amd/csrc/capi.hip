@@ -49,6 +49,7 @@ struct pbccs_engine {
     int nextSlot = 0;
     std::mutex statsMu;        // counters / stats are merged from the slots' worker threads
     long long oomRetries = 0;   // device batches rerun after PBCCS_EOOM
+    long long createHostNs = 0, createUploadNs = 0;   // pbccs_batch_create: host setup / reservations + upload
     std::vector<std::unique_ptr<Workspace>> slots;
     // the POA draft step's device state (made on first use): kPoaSlices runners, one per concurrent slice
     // PBCCS_POA_SLICES overrides the slice count (A/B): more slices overlap one slice's host graph work with
@@ -267,9 +268,12 @@ int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset)
     for (const auto& s : eng->slots) mapped += (long long)s->val.mapped_bytes();
     out->pool_mapped_bytes = mapped;
     out->oom_retries = eng->oomRetries;
+    out->create_host_ns = eng->createHostNs;
+    out->create_upload_ns = eng->createUploadNs;
     if (reset) {
         eng->counters = Counters();
         eng->oomRetries = 0;
+        eng->createHostNs = eng->createUploadNs = 0;
     }
     return PBCCS_OK;
 }
@@ -518,6 +522,7 @@ static int create_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, con
     if (!eng || n < 0 || (n > 0 && !in) || !out) return fail(PBCCS_EINVAL, "bad argument");
     return guarded([&] {
         if (hipSetDevice(eng->device) != hipSuccess) return fail(PBCCS_EDEVICE, "hipSetDevice failed");
+        const auto t0 = std::chrono::steady_clock::now();
         std::unique_ptr<pbccs_batch> b(new pbccs_batch());
         b->eng = eng;
         pbccs_polish_options_default(&b->o);
@@ -553,7 +558,14 @@ static int create_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, con
                 if (r >= 0) b->allReads.push_back(r);
             }
         }
+        const auto t1 = std::chrono::steady_clock::now();
         b->B->Prepare();
+        const auto t2 = std::chrono::steady_clock::now();
+        {
+            std::lock_guard<std::mutex> lk(eng->statsMu);
+            eng->createHostNs += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+            eng->createUploadNs += std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+        }
         *out = b.release();
         return PBCCS_OK;
     });
@@ -1346,6 +1358,7 @@ int pbccs_quiver_polish_batch(pbccs_engine* eng, const pbccs_quiver_config* conf
         }
         quiver::QuiverBatch& qb = *eng->quiverBatch;
         qb.Reset();
+        qb.SetProfiling(eng->profiling);
         // the QuiverConfigTable, as pbccs_quiver_scorer_create builds it
         std::vector<std::pair<std::string, int>> table;
         std::vector<const pbccs_quiver_config*> cfgs;
@@ -1439,6 +1452,10 @@ int pbccs_quiver_polish_batch(pbccs_engine* eng, const pbccs_quiver_config* conf
         for (size_t k = 0; k < wantQv.size(); ++k) {
             pbccs_quiver_result& o = out[wantQv[k]];
             if (o.consensus_cap >= (int)qv[k].size()) std::copy(qv[k].begin(), qv[k].end(), o.qvs);
+        }
+        {
+            std::lock_guard<std::mutex> lk(eng->statsMu);
+            qb.CollectProfile(eng->stats);
         }
         return PBCCS_OK;
     });

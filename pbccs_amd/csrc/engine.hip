@@ -22,8 +22,10 @@ namespace pbccs {
         if (e_ != hipSuccess) throw DeviceError(hipGetErrorString(e_));      \
     } while (0)
 
-const char* const kKernelNames[kKernelKinds] = {"k_fill", "k_suffix", "k_enumerate", "k_score",  "k_reduce",
-                                                 "k_qv",   "k_best_subset", "k_compact", "k_fill_tall"};
+const char* const kKernelNames[kKernelKinds] = {"k_fill",       "k_suffix",      "k_enumerate", "k_score",
+                                                 "k_reduce",     "k_qv",          "k_best_subset", "k_compact",
+                                                 "k_fill_tall",  "k_qfill_grp",   "k_qfill_coop", "k_qfill",
+                                                 "k_qscore_mid"};
 
 namespace {
 

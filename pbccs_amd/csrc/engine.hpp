@@ -168,8 +168,11 @@ void ckpt_policy(int* K, int* minLen);
 // kKFill: the 16-lane (and opt-in lane) fills of typical bands; kKFillTall: the 64-lane and lane-serial fills of
 // tall bands (launched on their own streams), reported apart so each kind's launches never overlap each other
 // within one workspace slot
+// The Quiver family's kinds (kKQ*) are the QuiverBatch fills (four reads per wavefront, a wave per read on the side
+// stream, the lane-serial fill) and its batched middle-case scoring.
 enum KernelKind {
-    kKFill = 0, kKSuffix, kKEnumerate, kKScore, kKReduce, kKQv, kKSelect, kKCompact, kKFillTall, kKernelKinds
+    kKFill = 0, kKSuffix, kKEnumerate, kKScore, kKReduce, kKQv, kKSelect, kKCompact, kKFillTall,
+    kKQFillGrp, kKQFillCoop, kKQFillLane, kKQScoreMid, kKernelKinds
 };
 extern const char* const kKernelNames[kKernelKinds];
 

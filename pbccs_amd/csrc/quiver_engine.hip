@@ -124,6 +124,78 @@ QuiverBatch::~QuiverBatch()
     }
     if (evFork_) (void)hipEventDestroy(evFork_);
     if (evJoin_) (void)hipEventDestroy(evJoin_);
+    for (const Pending& p : pending_) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (hipEvent_t e : eventPool_) (void)hipEventDestroy(e);
+}
+
+void QuiverBatch::SetProfiling(bool on)
+{
+    profiling_ = on;
+    if (on && !dStats_.ptr) {
+        dStats_.reserve(8, false);
+        QHIP(hipMemsetAsync(dStats_.ptr, 0, 8 * sizeof(unsigned long long), stream_));
+    }
+}
+
+template <class F>
+void QuiverBatch::Timed(KernelKind k, F&& launch, hipStream_t st)
+{
+    if (!profiling_) {
+        launch();
+        return;
+    }
+    hipEvent_t ev[2];
+    for (int i = 0; i < 2; ++i) {
+        if (!eventPool_.empty()) {
+            ev[i] = eventPool_.back();
+            eventPool_.pop_back();
+        } else {
+            QHIP(hipEventCreate(&ev[i]));
+        }
+    }
+    QHIP(hipEventRecord(ev[0], st));
+    launch();
+    QHIP(hipEventRecord(ev[1], st));
+    pending_.push_back({(int)k, ev[0], ev[1]});
+    stats_[k].launches += 1;
+}
+
+void QuiverBatch::CollectProfile(KernelStat out[kKernelKinds])
+{
+    if (!pending_.empty()) {
+        QHIP(hipStreamSynchronize(stream_));
+        QHIP(hipStreamSynchronize(side_));
+        for (const Pending& p : pending_) {
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) stats_[p.kind].ms += ms;
+            else (void)hipGetLastError();
+            eventPool_.push_back(p.a);
+            eventPool_.push_back(p.b);
+        }
+        pending_.clear();
+    }
+    if (profiling_ && dStats_.ptr) {
+        unsigned long long h[8];
+        QHIP(hipMemcpyAsync(h, dStats_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
+        QHIP(hipStreamSynchronize(stream_));
+        const KernelKind kinds[3] = {kKQFillGrp, kKQFillCoop, kKQFillLane};
+        for (int k = 0; k < 3; ++k) {
+            stats_[kinds[k]].cells += (double)h[2 * k];
+            stats_[kinds[k]].bytes += (double)h[2 * k + 1];
+        }
+        QHIP(hipMemsetAsync(dStats_.ptr, 0, sizeof(h), stream_));
+        QHIP(hipStreamSynchronize(stream_));
+    }
+    for (int k = 0; k < kKernelKinds; ++k) {
+        out[k].launches += stats_[k].launches;
+        out[k].ms += stats_[k].ms;
+        out[k].cells += stats_[k].cells;
+        out[k].bytes += stats_[k].bytes;
+        stats_[k] = KernelStat();
+    }
 }
 
 void QuiverBatch::grow_scratch(unsigned long long requested)
@@ -425,6 +497,7 @@ QBatch QuiverBatch::View()
     b.rStatus = dRStatus_.ptr;
     b.rUsed = dRUsed_.ptr;
     b.rAlloc = dRAlloc_.ptr;
+    b.stats = profiling_ ? dStats_.ptr : nullptr;
     return b;
 }
 
@@ -491,13 +564,20 @@ void QuiverBatch::Fill(const std::vector<int>& readsIn)
         if (sideRun) {
             QHIP(hipEventRecord(evFork_, stream_));   // after the uploads above
             QHIP(hipStreamWaitEvent(side_, evFork_, 0));
-            launch_qfill_coop(B, dList_.ptr + g0, (int)coop.size(), ringRows, maxCols, side_);
-            launch_qfill_coop(B, dList_.ptr + g0 + coop.size(), (int)full.size(), maxRowsFull, maxColsFull, side_);
+            if (!coop.empty())
+                Timed(kKQFillCoop, [&] { launch_qfill_coop(B, dList_.ptr + g0, (int)coop.size(), ringRows, maxCols, side_); },
+                      side_);
+            if (!full.empty())
+                Timed(kKQFillCoop, [&] {
+                    launch_qfill_coop(B, dList_.ptr + g0 + coop.size(), (int)full.size(), maxRowsFull, maxColsFull, side_);
+                }, side_);
             QHIP(hipGetLastError());
             QHIP(hipEventRecord(evJoin_, side_));
         }
-        launch_qfill_grp(B, dList_.ptr, (int)grpList.size(), stream_);
-        launch_qfill(B, dList_.ptr + g0 + coop.size() + full.size(), (int)lane.size(), stream_);
+        if (!grpList.empty()) Timed(kKQFillGrp, [&] { launch_qfill_grp(B, dList_.ptr, (int)grpList.size(), stream_); }, stream_);
+        if (!lane.empty())
+            Timed(kKQFillLane, [&] { launch_qfill(B, dList_.ptr + g0 + coop.size() + full.size(), (int)lane.size(), stream_); },
+                  stream_);
         if (sideRun) QHIP(hipStreamWaitEvent(stream_, evJoin_, 0));
         QHIP(hipGetLastError());
         const size_t R = reads_.size();
@@ -845,7 +925,7 @@ void QuiverBatch::ScoreDeltas(const std::vector<int>& zs, const std::vector<std:
         MW.edgeList = dEdge_.ptr;
         MW.edgeCount = dEdgeCount_.ptr;
         MW.edgeCap = edgeCap;
-        launch_qscore_mid(View(), MW, waveStart[n], stream_);
+        Timed(kKQScoreMid, [&] { launch_qscore_mid(View(), MW, waveStart[n], stream_); }, stream_);
         QHIP(hipGetLastError());
         QHIP(hipMemcpyAsync(&nEdge, dEdgeCount_.ptr, sizeof(nEdge), hipMemcpyDeviceToHost, stream_));
         QHIP(hipStreamSynchronize(stream_));

@@ -138,6 +138,10 @@ public:
     float ReadScore(int r) const { return reads_[r].score; }
     long long Allocated(int r, int which) const { return reads_[r].alloc[which]; }
     float BaselineScore(int z) const;
+    // profiling: HIP events around the fill and middle-case scoring launches on their own streams, plus the fills'
+    // in-kernel stored-cell counters (QBatch::stats); CollectProfile adds them to `out` and clears
+    void SetProfiling(bool on);
+    void CollectProfile(KernelStat out[kKernelKinds]);
 
 private:
     struct HZmw {
@@ -181,7 +185,19 @@ private:
     // (the kernel's bump counter keeps counting past the cap) plus an eighth, so the rerun fits
     void grow_scratch(unsigned long long requested);
 
+    template <class F>
+    void Timed(KernelKind k, F&& launch, hipStream_t st);
+
     int device_ = 0;
+    bool profiling_ = false;
+    struct Pending {
+        int kind;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending_;
+    std::vector<hipEvent_t> eventPool_;
+    KernelStat stats_[kKernelKinds];
+    DevVec<unsigned long long> dStats_;
     hipStream_t stream_ = nullptr;
     // the fill's tall reads (k_qfill_coop's lists) run on a side stream beside k_qfill_grp: their long serial
     // chains overlap the grouped launch instead of following it

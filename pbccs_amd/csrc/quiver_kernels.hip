@@ -1354,6 +1354,14 @@ __device__ long long grp_fill(const QEvalG& ew, const GRead& R, const char* tbas
 }  // namespace
 
 // ---- k_qfill_coop: FillAlphaBeta with one wavefront per read (SparseSse recursors, reads < kQCoopMaxRows) --
+// Profiling: the stored cells and algorithmic bytes of a completed fill (every pass's band and column metadata).
+__device__ inline void qstat_add(unsigned long long* s, int kind, long long cells, long long cols)
+{
+    if (!s) return;
+    atomicAdd(s + 2 * kind, (unsigned long long)cells);
+    atomicAdd(s + 2 * kind + 1, (unsigned long long)(4 * cells + 12 * cols));
+}
+
 __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restrict__ reads, int n, int ldsRows,
                                                     int ldsCols)
 {
@@ -1382,7 +1390,7 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     bool ovf = false, tall = false;
-    long long needA = 0, needB = 0;
+    long long needA = 0, needB = 0, stCells = 0, stCols = 0;
     int curA = 0, curB = 2;
     bool aPassed = false, bPassed = false;
     auto passA = [&](bool guided) {
@@ -1391,6 +1399,7 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
         const long long u = coop_fill<false>(e, g, guided, self, aPassed, out, v.allocA, aPassed, ovf, qlds, ldsRows,
                                              v.hint, lane, win);
         tall = tall || u < 0;
+        if (!ovf && u >= 0) { stCells += u; stCols += J + 1; }
         needA = max(needA, u);
         curA = nxt;
         aPassed = true;
@@ -1402,6 +1411,7 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
         const long long u = coop_fill<true>(e, g, true, self, bPassed, out, v.allocB, bPassed, ovf, qlds, ldsRows,
                                             v.hint, lane, win);
         tall = tall || u < 0;
+        if (!ovf && u >= 0) { stCells += u; stCols += J + 1; }
         needB = max(needB, u);
         curB = nxt;
         bPassed = true;
@@ -1463,6 +1473,7 @@ __global__ void __launch_bounds__(64) k_qfill_coop(QBatch B, const int* __restri
         }
     }
     if (lane != 0) return;
+    if (!tall && !ovf) qstat_add(B.stats, kQStatCoop, stCells, stCols);
     if (tall) {
         B.rStatus[r] = kQTall;
         return;
@@ -1529,7 +1540,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     bool ovf = false, tall = false;
-    long long needA = 0, needB = 0;
+    long long needA = 0, needB = 0, stCells = 0, stCols = 0;
     int curA = 0, curB = 2;
     bool aPassed = false, bPassed = false;
     auto passA = [&](bool guided) {
@@ -1538,6 +1549,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
         const long long u = grp_fill<false>(ew, R, tbase, gb, guided, self, aPassed, out, allocA, aPassed, ovf, my,
                                             hint, g, gl, win);
         tall = tall || u < 0;
+        if (!ovf && u >= 0) { stCells += u; stCols += J + 1; }
         needA = max(needA, u);
         curA = nxt;
         aPassed = true;
@@ -1549,6 +1561,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
         const long long u = grp_fill<true>(ew, R, tbase, gb, true, self, bPassed, out, allocB, bPassed, ovf, my,
                                            hint, g, gl, win);
         tall = tall || u < 0;
+        if (!ovf && u >= 0) { stCells += u; stCols += J + 1; }
         needB = max(needB, u);
         curB = nxt;
         bPassed = true;
@@ -1605,6 +1618,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) k_
         }
     }
     if (gl != 0) return;
+    if (!tall && !ovf) qstat_add(B.stats, kQStatGrp, stCells, stCols);
     if (tall) {
         B.rStatus[r] = kQTall;
         return;
@@ -1641,13 +1655,14 @@ __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ 
         for (int j = 0; j <= J; ++j) m.range[j] = make_int2(0, 0);
     }
     bool ovf = false;
-    long long needA = 0, needB = 0;
+    long long needA = 0, needB = 0, stCells = 0, stCols = 0;
     int curA = 0, curB = 2;   // arena index of the latest alpha / beta pass
     bool aPassed = false, bPassed = false;
     auto passA = [&](bool guided) {
         const int nxt = aPassed ? (curA ^ 1) : 0;
         const QBand g = arena(v, curB), self = arena(v, curA), out = arena(v, nxt);
         const long long u = fill_alpha(e, guided ? &g : nullptr, aPassed ? &self : nullptr, out, v.allocA, aPassed, ovf);
+        if (!ovf) { stCells += u; stCols += J + 1; }
         needA = max(needA, u);
         curA = nxt;
         aPassed = true;
@@ -1657,6 +1672,7 @@ __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ 
         const int nxt = bPassed ? (curB ^ 1) : 2;
         const QBand g = arena(v, curA), self = arena(v, curB), out = arena(v, nxt);
         const long long u = fill_beta(e, &g, bPassed ? &self : nullptr, out, v.colbuf, v.allocB, bPassed, ovf);
+        if (!ovf) { stCells += u; stCols += J + 1; }
         needB = max(needB, u);
         curB = nxt;
         bPassed = true;
@@ -1687,6 +1703,7 @@ __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ 
         B.rStatus[r] = kQOverflow;
         return;
     }
+    qstat_add(B.stats, kQStatLane, stCells, stCols);
     B.rCurA[r] = curA;
     B.rCurB[r] = curB - 2;
     B.rFlips[r] = flips;

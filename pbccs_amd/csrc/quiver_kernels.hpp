@@ -44,7 +44,12 @@ struct QBatch {
     int* rStatus;
     long long* rUsed;          // [2 r] alpha / [2 r + 1] beta values needed (overflow sizing)
     long long* rAlloc;         // [2 r] alpha / [2 r + 1] beta AllocatedEntries
+    // profiling (nullable): per fill kind (kQStatGrp / kQStatCoop / kQStatLane) the band cells the completed fills
+    // stored over all their passes, and their algorithmic bytes (4 B per cell + 12 B per column per pass: range
+    // int2 + offset)
+    unsigned long long* stats;
 };
+enum QStatKind : int { kQStatGrp = 0, kQStatCoop = 1, kQStatLane = 2 };   // stats[2 k] cells, stats[2 k + 1] bytes
 
 __host__ __device__ inline int qcols(int J) { return J + 1; }
 

@@ -3,7 +3,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# PBCCS_LIB: load another in-tree build of the same library (A/B experiments, tools/gpu_ab.sh)
+# PBCCS_LIB: load another in-tree build of the same library (A/B experiments: tools/build_ab.sh, then the ab_lib
+# step of tools/gpu_steps.sh)
 LIB_PATH = os.environ.get("PBCCS_LIB") or os.path.join(HERE, "_lib", "libpbccs_amd.so")
 
 PBCCS_OK = 0
@@ -65,7 +66,8 @@ class CCounters(ctypes.Structure):
                 ("score_tasks", ctypes.c_longlong), ("mutations", ctypes.c_longlong),
                 ("band_top_bytes", ctypes.c_longlong), ("band_region_bytes", ctypes.c_longlong),
                 ("band_used_bytes", ctypes.c_longlong), ("pool_mapped_bytes", ctypes.c_longlong),
-                ("oom_retries", ctypes.c_longlong)]
+                ("oom_retries", ctypes.c_longlong), ("create_host_ns", ctypes.c_longlong),
+                ("create_upload_ns", ctypes.c_longlong)]
 
 
 class CQvModelParams(ctypes.Structure):

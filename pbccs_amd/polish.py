@@ -109,15 +109,20 @@ class PreparedBatch(_Marshalled):
 
     def __init__(self, zmws, settings=None, engine=None):
         from . import default_engine
+        import time
         self._lib = L.load()
         self.engine = engine or default_engine()
         self.settings = settings or ConsensusSettings()
+        t0 = time.perf_counter()
         super().__init__(zmws)
+        t1 = time.perf_counter()
         n = len(zmws)
         self._opts = self.settings._c()
         h = ctypes.c_void_p()
         L.check(L.load().pbccs_batch_create(self.engine._h, self._ins, n, ctypes.byref(self._opts), ctypes.byref(h)))
         self._h = h
+        self.marshal_s = t1 - t0                     # Python dicts -> the boundary's C structs
+        self.create_s = time.perf_counter() - t1     # pbccs_batch_create (per-ZMW setup + upload)
 
     def polish(self):
         L.check(L.load().pbccs_batch_polish(self._h, self._outs))

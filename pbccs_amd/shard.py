@@ -66,8 +66,15 @@ def dynamic_chunks(zmws, chunk):
 STORE_PART = 4 << 20   # bytes per value put on the rank-0 key-value store (whose values are capped at 8 MB)
 
 
+def _store_timeout_s(store, default=1800.0):
+    try:
+        return float(store.timeout.total_seconds())
+    except Exception:
+        return default
+
+
 def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chunk=256, polish_fn=None, store=None,
-                   group=None, stats=None):
+                   group=None, stats=None, collect_timeout=None):
     """Polish `zmws` across ranks through a dynamic pull queue: every rank takes the next
     chunk index from one shared counter -- an atomic fetch-add on the rank-0 key-value store, host-side, not a
     device collective -- until the queue is empty, so a rank that drew slow ZMWs (tall bands, long templates)
@@ -82,9 +89,15 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
     `zmws` may be a list or a lazily generated cell (synth.SmrtCell): a rank then materialises only the chunks
     it pulls, the next one on a helper thread while the current one polishes.
 
-    Rank 0 returns every ZMW's result in input order; the other ranks return None.  `stats` (a dict, optional)
-    receives the queue's counters on rank 0: chunks per rank, `tail_ms` (the time from rank 0's last chunk to
-    the last record) and `gen_ms` (this rank's time waiting for chunk generation)."""
+    A rank claims the next chunk before polishing the current one (so its generation overlaps the polish) only
+    while at least `world` chunks are left: near the end a pre-claimed chunk would sit idle on one rank while the
+    others have nothing to pull.
+
+    Rank 0 returns every ZMW's result in input order; the other ranks return None.  If no record arrives for
+    `collect_timeout` seconds (default: the store's timeout) while chunks other ranks took are outstanding, rank 0
+    raises instead of waiting forever on a rank that died.  `stats` (a dict, optional) receives the queue's
+    counters: on every rank `zmws_local` (ZMWs this rank polished) and `gen_ms` (its time waiting for chunk
+    generation); on rank 0 chunks per rank and `tail_ms` (the time from rank 0's last chunk to the last record)."""
     import pickle
     import threading
     import time
@@ -132,8 +145,12 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
             out[i] = rec
         return True
 
+    deadline_s = collect_timeout if collect_timeout is not None else _store_timeout_s(store)
+
     def collector():
         try:
+            last = time.perf_counter()   # the last record collected, or `final` being set
+            seen_final = False
             while True:
                 with lock:
                     todo = sorted(pending)
@@ -141,9 +158,16 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
                 with lock:
                     pending.difference_update(got)
                     empty = not pending
+                if final.is_set() and not seen_final:
+                    seen_final, last = True, time.perf_counter()
                 if final.is_set() and empty:
                     return
-                if not got:
+                if got:
+                    last = time.perf_counter()
+                elif todo and time.perf_counter() - last > deadline_s:
+                    raise RuntimeError(f"no record from the other ranks for {deadline_s:.0f} s; chunks still "
+                                       f"outstanding: {todo[:8]} (a rank died?)")
+                else:
                     time.sleep(0.005)
         except Exception as e:   # surfaced by the main thread
             collector_err.append(e)
@@ -174,6 +198,7 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
 
     gen = ThreadPoolExecutor(max_workers=1) if lazy else None
     gen_ms = 0.0
+    n_local = 0
     try:
         c = pull()
         fut = gen.submit(materialise, c) if gen else None
@@ -182,10 +207,13 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
             zs = fut.result() if gen else materialise(c)
             gen_ms += (time.perf_counter() - t0) * 1e3
             nxt = None
-            if gen:   # reserve and generate the next chunk while this one polishes
+            # claim and generate the next chunk while this one polishes, but only while at least `world` chunks
+            # are left: a chunk claimed early near the end would wait on this rank while the others run dry
+            if gen and len(chunks) - (c + 1) >= world:
                 nxt = pull()
                 fut = gen.submit(materialise, nxt)
             recs = polish_fn(zs)
+            n_local += len(zs)
             mine.add(c)
             if rank == 0:
                 taken[0] += 1
@@ -200,12 +228,18 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
                     for q in range(nparts):
                         store.set(f"{key}/done/{c}/p{q}", blob[q * STORE_PART:(q + 1) * STORE_PART])
                     store.set(f"{key}/done/{c}", str(nparts))
-            c = nxt if gen else pull()
+            if nxt is not None:
+                c = nxt
+            else:
+                c = pull()
+                if gen:
+                    fut = gen.submit(materialise, c)
     finally:
         if gen:
             gen.shutdown(wait=True)
     if stats is not None:
         stats["gen_ms"] = gen_ms
+        stats["zmws_local"] = n_local
     if rank != 0:
         return None
     t0 = time.perf_counter()

@@ -55,3 +55,54 @@ def test_roofline_marks_time_shared_launches_and_single_slot_figure(tmp_path, mo
     (prof / bench.SINGLE_SLOT_PROFILE).write_text(json.dumps(single))
     r = bench.make_roofline(stats, 1.5, "w")
     assert "stale" in r["single_slot"]["source"] and "frac" not in r["single_slot"]
+
+
+def _args(**kw):
+    import argparse
+    d = dict(cpu_sample=4, cpu_threads=2, seed=1, workload="2kb")
+    d.update(kw)
+    return argparse.Namespace(**d)
+
+
+def test_sample_indices_stride_and_capped_random_sample():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.sample_indices(_args(cpu_sample=4), 40) == [0, 10, 20, 30]
+    assert bench.sample_indices(_args(cpu_sample=64), 10) == list(range(10))
+    costs = [1e8] * 10 + [5e9] * 10   # the second half is costlier than a 10 kb / 8-pass ZMW
+    idx = bench.sample_indices(_args(cpu_sample=6), 20, costs)
+    assert len(idx) == 6 and idx == sorted(idx) and all(i < 10 for i in idx)
+    assert idx == bench.sample_indices(_args(cpu_sample=6), 20, costs)   # seeded
+    cov = bench.coverage(costs)
+    assert cov["eligible_zmws_frac"] == 0.5 and abs(cov["eligible_cost_frac"] - 1e9 / 51e9) < 1e-4
+
+
+def test_cpu_leg_checks_the_timed_records_and_fails_on_a_mismatch():
+    """The CPU leg polishes the sampled ZMWs on the restatement and compares them with the run's records: equal
+    records pass; one consensus edited, one nTested changed and one QV moved by 2 each fail that ZMW.  With a
+    cost model the rate is the ratio estimator's (the sample's CPU seconds per unit of cost x the mean cost)."""
+    sys.path.insert(0, ROOT)
+    import copy
+    import bench
+    import pbccs_amd
+    from pbccs_amd import synth
+    settings = pbccs_amd.ConsensusSettings()
+    zs = synth.make_zmws(6, 200, 5, seed=5)
+    recs = [bench.oracle_record(z, settings) for z in zs]
+    assert all(r["status"] in ("Success", "PoorQuality", "NonConvergent", "TooFewPasses", "TooManyUnusable")
+               for r in recs)
+    idx = [0, 2, 4]
+    cb, par = bench.sampled_cpu_baseline(_args(cpu_sample=3), settings, zs, recs, idx)
+    assert par["ok"] and par["n"] == 3 and par["consensus_equal"] == 3 and par["max_qv_diff"] == 0
+    assert cb["value"] > 0 and cb["cores"] == 2 and cb["full_host_value"] >= cb["value"]
+    bad = copy.deepcopy(recs)
+    ok = [i for i in idx if recs[i]["status"] == "Success"]
+    assert ok, [r["status"] for r in recs]
+    bad[ok[0]]["consensus"] = bad[ok[0]]["consensus"][:-1]
+    bad[ok[-1]]["qvs"] = [q + 2 for q in bad[ok[-1]]["qvs"]]
+    _, par = bench.sampled_cpu_baseline(_args(cpu_sample=3), settings, zs, bad, idx)
+    assert not par["ok"] and ok[0] in par["mismatched_zmws"] and ok[-1] in par["mismatched_zmws"]
+    costs = [bench.zmw_cost(z) for z in zs]
+    cb, par = bench.sampled_cpu_baseline(_args(cpu_sample=3), settings, zs, recs, idx, costs)
+    ex = cb["extrapolated"]
+    assert par["ok"] and abs(cb["value"] - 2 / ex["core_s_per_zmw"]) < 0.02 * cb["value"]

@@ -92,9 +92,10 @@ def _zmw(seed, length, passes):
 
 def _qvs_exact(got, exp):
     """ConsensusQVs against the restatement, exactly (tighter than the north_star's +-1): the scores are
-    bit-exact floats, k_qqv sums exp(score) per position with the device libm, and every position whose rounding
-    could depend on the libm (-10 log10(prob) within 1e-6 of a .5 boundary, or prob < 1e-12) is recomputed on the
-    host with the host libm (QuiverBatch::QVsMany)."""
+    bit-exact floats and k_qqv sums exp(score) per position with the device libm.  An ulp of exp / log10 moves
+    prob = 1 - 1/(1 + sum) by at most err = 4 eps + 16 eps sum, so k_qqv leaves to the host (QuiverBatch::QVsMany,
+    the host libm on the same float scores) every position whose -10 log10(prob) lies within 4.35 err / prob + 1e-6
+    of a .5 rounding boundary, and every position where 1 + sum rounded to 1.0 although sum > 0.4 eps."""
     return list(got) == list(exp)
 
 

@@ -29,15 +29,40 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _stand_in(rank, slow_rank=None, pad=0):
-    import time
+def _stand_in(rank, pad=0):
+    def polish(zs):
+        return [{"rank": rank, "draft": z["draft"][::-1], "pad": "A" * pad} for z in zs]
+    return polish
+
+
+def _stand_in_held(rank, world, fast_chunks=4):
+    """A stand-in whose schedule is fixed by store keys, not by timing: every rank's first chunk waits until every
+    rank holds a chunk (so each rank takes at least one); rank 1's first chunk then also waits until rank 0 has
+    finished `fast_chunks` chunks of its own (so rank 0, the fast rank, takes at least that many)."""
+    import torch.distributed as dist
+    store = dist.distributed_c10d._get_default_store()
+    state = {"calls": 0}
 
     def polish(zs):
-        if rank == slow_rank:
-            time.sleep(0.05 * len(zs))
-        elif slow_rank is not None:   # the fast rank takes a little time too, so the slow one's first pull is not
-            time.sleep(0.01 * len(zs))  # raced by the whole queue draining during its start-up
-        return [{"rank": rank, "draft": z["draft"][::-1], "pad": "A" * pad} for z in zs]
+        state["calls"] += 1
+        if state["calls"] == 1:
+            if store.add("test/started", 1) == world:
+                store.set("test/all_started", "1")
+            store.wait(["test/all_started"])
+            if rank == 1 and world > 1:
+                store.wait(["test/fast_done"])
+        out = [{"rank": rank, "draft": z["draft"][::-1], "pad": ""} for z in zs]
+        if rank == 0 and state["calls"] == fast_chunks:
+            store.set("test/fast_done", "1")
+        return out
+    return polish
+
+
+def _stand_in_dies(rank):
+    def polish(zs):
+        if rank == 1:
+            raise RuntimeError("rank 1 fails mid-chunk")
+        return [{"rank": rank, "draft": z["draft"][::-1], "pad": ""} for z in zs]
     return polish
 
 
@@ -47,11 +72,17 @@ def _worker(rank, world, port, zmws, out_q, use_gpu, mode="static", chunk=2):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        if mode in ("dynamic", "dynamic_big"):
+        if mode == "dead_peer":
+            try:
+                shard.polish_dynamic(zmws, chunk=chunk, polish_fn=_stand_in_dies(rank), collect_timeout=3.0)
+                res = "no error"
+            except RuntimeError as e:
+                res = f"raised: {e}"
+        elif mode in ("dynamic", "dynamic_big"):
             st = {}
             pad = (3 << 20) if mode == "dynamic_big" else 0   # 3 MB per record: chunks beyond the store's 8 MB values
-            res = shard.polish_dynamic(zmws, chunk=chunk,
-                                       polish_fn=None if use_gpu else _stand_in(rank, slow_rank=1, pad=pad), stats=st)
+            fn = None if use_gpu else (_stand_in(rank, pad=pad) if pad else _stand_in_held(rank, world))
+            res = shard.polish_dynamic(zmws, chunk=chunk, polish_fn=fn, stats=st)
             if rank == 0:
                 res = (res, st)
         elif use_gpu:
@@ -64,7 +95,7 @@ def _worker(rank, world, port, zmws, out_q, use_gpu, mode="static", chunk=2):
         dist.destroy_process_group()
 
 
-def _run(world, zmws, use_gpu=False, mode="static", chunk=2):
+def _run(world, zmws, use_gpu=False, mode="static", chunk=2, ok_exit=(0,)):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -74,7 +105,7 @@ def _run(world, zmws, use_gpu=False, mode="static", chunk=2):
     res = q.get(timeout=600)
     for p in procs:
         p.join(timeout=60)
-        assert p.exitcode == 0
+        assert p.exitcode in ok_exit
     return res
 
 
@@ -106,15 +137,34 @@ def test_dynamic_chunks_are_a_cost_ordered_partition():
 
 
 def test_gloo_world2_dynamic_queue_balances_and_keeps_order():
-    """Rank 1 is slow (its stand-in sleeps per ZMW): through the pull queue rank 0 takes more chunks, and
-    the gathered records still come back in input order."""
+    """Rank 1 is slow -- its first chunk is held until rank 0 has finished four chunks (store keys, no timing) --
+    so through the pull queue rank 0 takes more chunks, and the gathered records still come back in input order."""
     zmws = _toy_zmws(24)
     res, st = _run(2, zmws, mode="dynamic")
     assert [r["draft"] for r in res] == [z["draft"][::-1] for z in zmws]
     by_rank = [sum(1 for r in res if r["rank"] == k) for k in (0, 1)]
-    assert by_rank[1] >= 2 and by_rank[0] > by_rank[1], by_rank
+    assert by_rank[1] >= 2 and by_rank[0] >= 8, by_rank
     # records streamed per chunk: rank 0 saw every chunk, the other rank's through the store
     assert st["chunks"] == 12 and sum(st["chunks_by_rank"]) == 12 and st["chunks_by_rank"][1] >= 1
+    assert st["chunks_by_rank"][0] >= 4 and st["zmws_local"] == by_rank[0]
+
+
+def test_gloo_world8_dynamic_queue_every_rank_pulls_and_order_holds():
+    """Eight ranks (the node's eight GPUs) on one queue: every rank holds a chunk before any finishes (store keys),
+    so all eight take work; the 64 chunks come back complete and in input order."""
+    zmws = _toy_zmws(128)
+    res, st = _run(8, zmws, mode="dynamic")
+    assert [r["draft"] for r in res] == [z["draft"][::-1] for z in zmws]
+    assert st["chunks"] == 64 and sum(st["chunks_by_rank"]) == 64 and min(st["chunks_by_rank"]) >= 1
+    assert {r["rank"] for r in res} == set(range(8))
+
+
+def test_gloo_world2_dynamic_queue_raises_when_a_peer_dies():
+    """A rank that fails mid-chunk never stores its records: rank 0 must raise once no record has arrived for the
+    collect timeout, instead of waiting forever (bench.py's launcher is not the only caller)."""
+    zmws = _toy_zmws(12)
+    res = _run(2, zmws, mode="dead_peer", ok_exit=(0, 1))
+    assert res.startswith("raised:") and "no record" in res, res
 
 
 def test_gloo_world2_dynamic_queue_records_larger_than_a_store_value():
