@@ -604,10 +604,11 @@ def main():
     for b in batches:
         b.close()
     prep["create_frac_of_timed"] = round(prep["create_s"] / local_time, 4)
-    prep["note"] = ("outside the timed region (inputs resident in HBM when it starts): synth_s the synthetic "
-                    "subreads, marshal_s the C structs, create_s pbccs_batch_create (create_host_s of it the per-ZMW "
-                    "setup of Consensus.h:437-453 -- transition tables, expectations, reverse complement -- and "
-                    "create_upload_s the descriptor arena and read uploads)")
+    prep["note"] = ("outside the timed region (the reads resident in HBM when it starts): synth_s the synthetic "
+                    "subreads, marshal_s the C structs, create_s pbccs_batch_create (create_host_s of it the batch's "
+                    "copy of its inputs and the read pool, create_upload_s the reservations and the read upload).  "
+                    "Inside it: the per-ZMW setup of Consensus.h:437-453 (transition tables, expectations, "
+                    "reverse-complement template, descriptor arena), derive_thread_s_in_timed of slot-thread time")
     workload = (f"configs[1]: synthetic {args.length} bp insert, {args.passes} full passes, "
                 f"{args.zmws_per_step} ZMWs per step")
     report(args, rank, world, eng, slots, job_time, local_time, res, workload, "weak", len(res) * world,
@@ -1162,6 +1163,7 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
         out["host"] = extra["host"]
     if "prepare" in extra:
         out["prepare"] = extra["prepare"]
+        out["prepare"]["derive_thread_s_in_timed"] = round(counters.get("derive_ns", 0) / 1e9, 3)
     parity_ok = True
     # the CPU leg on rank 0 (one rank: its records are the run's; several ranks: rank 0 holds the whole cell's
     # records for the strong-scaling cell, its own for the weak-scaling lines)

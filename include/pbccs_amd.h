@@ -225,9 +225,10 @@ typedef struct {
     long long band_used_bytes;   /* max over batches: band cells the reads' last fills stored */
     long long pool_mapped_bytes; /* device memory the workspace slots' band pools hold mapped now */
     long long oom_retries;       /* device batches rerun after running the device out of memory */
-    long long create_host_ns;    /* pbccs_batch_create: per-ZMW host setup (Consensus.h:437-453: transition
-                                    tables, expectations, reverse complement, descriptors) */
-    long long create_upload_ns;  /* pbccs_batch_create: device reservations + the one-copy input upload */
+    long long create_host_ns;    /* pbccs_batch_create: the batch's own copy of its inputs and the read pool */
+    long long create_upload_ns;  /* pbccs_batch_create: device reservations + the read upload */
+    long long derive_ns;         /* the per-ZMW setup of Consensus.h:437-453 (transition tables, expectations,
+                                    reverse-complement template), run by the polish at its first device step */
 } pbccs_counters;
 int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset);
 
@@ -315,6 +316,26 @@ int pbccs_quiver_scorer_alignment(pbccs_quiver_scorer* s, int i, char* target, c
 int pbccs_quiver_refine_consensus(pbccs_quiver_scorer* s, const pbccs_refine_options* opts, long long* n_tested,
                                   long long* n_applied, int* converged);
 int pbccs_quiver_consensus_qvs(pbccs_quiver_scorer* s, int* qvs, int cap, int* n);
+
+/* QvEvaluator (Quiver/QvEvaluator.hpp:90-317): the four move scores of one read (QvSequenceFeatures,
+ * Features.hpp:69-100) against a template under QvModelParams, at n cells (i[k], j[k]), evaluated on the device
+ * with the recursions' own evaluator.  Inc(i, j) (:160-167), Del(i, j) with the pinStart / pinEnd rule (:169-184),
+ * Extra(i, j) (:186-193), Merge(i, j) (:195-207).  A cell outside a move's domain -- the reference's asserts:
+ * Inc 0 <= i < I, 0 <= j < J; Del 0 <= i <= I, 0 <= j < J; Extra 0 <= i < I, 0 <= j <= J; Merge 0 <= i < I,
+ * 0 <= j < J - 1 -- gives NaN.  Feature tracks of len floats (NULL = zeros; del_tag as float(char)); any output
+ * array may be NULL. */
+typedef struct {
+    const char* seq;
+    int len;
+    const float* ins_qv;
+    const float* subs_qv;
+    const float* del_qv;
+    const float* del_tag;
+    const float* merge_qv;
+} pbccs_qv_features;
+int pbccs_qv_evaluator_moves(pbccs_engine* eng, const pbccs_qv_features* read, const char* tpl, int tpl_len,
+                             const pbccs_qv_model_params* params, int pin_start, int pin_end, const int* i,
+                             const int* j, int n, float* inc, float* del, float* extra, float* merge);
 
 /* Batched Quiver polish: for every ZMW, what a caller of the scorer API above does with one scorer --
  * create over (configs, chemistries), AddRead each read (threshold NaN = its config's add_threshold),

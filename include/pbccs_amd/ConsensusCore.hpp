@@ -9,6 +9,7 @@
 //   Mutation, MutationType                    Mutation.hpp:50-129
 //   Arrow::AddReadResult, ArrowMultiReadMutationScorer   Arrow/MultiReadMutationScorer.hpp:60-284
 //   RefineOptions, RefineConsensus, ConsensusQVs          Consensus.hpp:48-79
+// The Quiver family's classes are in pbccs_amd/Quiver.hpp (as ConsensusCore keeps them under Quiver/).
 // Errors surface as ConsensusCore-style exceptions on the C++ side (the ABI itself never throws).
 #pragma once
 

@@ -409,6 +409,30 @@ class QuiverScorer:
         return list(out[:n])
 
 
+def qv_eval_moves(seq, tpl, params, cells, features=None, pin_start=True, pin_end=True):
+    """QvEvaluator's Inc / Del / Extra / Merge (QvEvaluator.hpp:153-207) at the (i, j) cells: four lists, NaN outside
+    a move's domain.  features: dict of ins/subs/del/del_tag/merge lists (del_tag as characters)."""
+    L = _qlib()
+    f = L.qorc_eval_moves
+    F = ctypes.POINTER(ctypes.c_float)
+    f.argtypes = [ctypes.c_char_p] + [F] * 5 + [ctypes.c_char_p, F, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                                 ctypes.c_int, F]
+    feats = features or {}
+    arrs = []
+    for k in ("ins", "subs", "del", "del_tag", "merge"):
+        v = feats.get(k)
+        if v is None:
+            arrs.append(None)
+        else:
+            arrs.append(_farr([float(ord(c)) if isinstance(c, str) else float(c) for c in v]))
+    n = len(cells)
+    out = (ctypes.c_float * max(1, 4 * n))()
+    f(seq.encode(), *arrs, tpl.encode(), _farr(qv_params(params)), 1 if pin_start else 0, 1 if pin_end else 0,
+      _iarr([c[0] for c in cells] or [0]), _iarr([c[1] for c in cells] or [0]), n, out)
+    return [list(out[k * n:(k + 1) * n]) for k in range(4)]
+
+
 def quiver_log_add(a, b):
     return _qlib().qorc_log_add(a, b)
 

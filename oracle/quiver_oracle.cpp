@@ -1229,4 +1229,44 @@ int qorc_scorer_alignment(void* h, int r, char* target, char* query, int cap)
     return (int)t.size();
 }
 
+// QvEvaluator's four moves at listed cells (QvEvaluator.hpp:153-207), NaN outside each move's domain (the
+// reference's asserts); out: 4 x n floats, move-major (Inc, Del, Extra, Merge).  Tracks NULL = zeros.
+void qorc_eval_moves(const char* seq, const float* ins, const float* subs, const float* del, const float* delTag,
+                     const float* merge, const char* tpl, const float* params, int pinStart, int pinEnd,
+                     const int* ci, const int* cj, int n, float* out)
+{
+    Evaluator e;
+    e.rd.seq = seq;
+    const size_t I = e.rd.seq.size();
+    auto fill = [&](std::vector<float>& v, const float* src) {
+        v.assign(I, 0.0f);
+        if (src)
+            for (size_t i = 0; i < I; ++i) v[i] = src[i];
+    };
+    fill(e.rd.ins, ins);
+    fill(e.rd.subs, subs);
+    fill(e.rd.del, del);
+    fill(e.rd.delTag, delTag);
+    fill(e.rd.merge, merge);
+    float* f[10] = {&e.pm.Match, &e.pm.Mismatch, &e.pm.MismatchS, &e.pm.Branch, &e.pm.BranchS, &e.pm.DeletionN,
+                    &e.pm.DeletionWithTag, &e.pm.DeletionWithTagS, &e.pm.Nce, &e.pm.NceS};
+    for (int k = 0; k < 10; ++k) *f[k] = params[k];
+    for (int k = 0; k < 4; ++k) {
+        e.pm.Merge[k] = params[10 + k];
+        e.pm.MergeS[k] = params[14 + k];
+    }
+    e.tpl = tpl;
+    e.pinStart = pinStart != 0;
+    e.pinEnd = pinEnd != 0;
+    const int Ii = e.I(), J = e.J();
+    const float nan = std::numeric_limits<float>::quiet_NaN();
+    for (int k = 0; k < n; ++k) {
+        const int i = ci[k], j = cj[k];
+        out[k] = (i >= 0 && i < Ii && j >= 0 && j < J) ? e.Inc(i, j) : nan;
+        out[n + k] = (i >= 0 && i <= Ii && j >= 0 && j < J) ? e.Del(i, j) : nan;
+        out[2 * n + k] = (i >= 0 && i < Ii && j >= 0 && j <= J) ? e.Extra(i, j) : nan;
+        out[3 * n + k] = (i >= 0 && i < Ii && j >= 0 && j < J - 1) ? e.Merge(i, j) : nan;
+    }
+}
+
 }  // extern "C"

@@ -254,7 +254,7 @@ from .polish import (ConsensusSettings, PreparedBatch, plan_batches, polish_many
                      polish_zmws)  # batched ccs driver
 from . import quiver as _quiver  # noqa: E402
 from .quiver import (QvModelParams, QuiverConfig, QuiverConfigTable,  # noqa: E402,F401
-                     QuiverMultiReadMutationScorer, ALL_MOVES, BASIC_MOVES)
+                     QuiverMultiReadMutationScorer, QvEvaluator, QvSequenceFeatures, ALL_MOVES, BASIC_MOVES)
 
 __all__ = [
     "ArrowConfig", "ArrowMultiReadMutationScorer", "ConsensusQVs", "ConsensusSettings", "Engine", "Mutation",

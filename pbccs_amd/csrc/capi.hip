@@ -270,6 +270,7 @@ int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset)
     out->oom_retries = eng->oomRetries;
     out->create_host_ns = eng->createHostNs;
     out->create_upload_ns = eng->createUploadNs;
+    out->derive_ns = eng->counters.deriveNs;
     if (reset) {
         eng->counters = Counters();
         eng->oomRetries = 0;
@@ -505,6 +506,7 @@ static void merge_engine_stats(pbccs_engine* eng, ArrowBatch& B)
         eng->counters.scoreLaunches += c.scoreLaunches;
         eng->counters.scoreTasks += c.scoreTasks;
         eng->counters.mutations += c.mutations;
+        eng->counters.deriveNs += c.deriveNs;
         eng->counters.bandTopBytes = std::max(eng->counters.bandTopBytes, c.bandTopBytes);
         eng->counters.bandRegionBytes = std::max(eng->counters.bandRegionBytes, c.bandRegionBytes);
         eng->counters.bandUsedBytes = std::max(eng->counters.bandUsedBytes, c.bandUsedBytes);
@@ -1329,6 +1331,65 @@ int pbccs_quiver_consensus_qvs(pbccs_quiver_scorer* s, int* qvs, int cap, int* n
         *n = (int)q.size();
         if ((int)q.size() > cap || !qvs) return fail(PBCCS_ERANGE, "buffer too small");
         std::copy(q.begin(), q.end(), qvs);
+        return PBCCS_OK;
+    });
+}
+
+int pbccs_qv_evaluator_moves(pbccs_engine* eng, const pbccs_qv_features* read, const char* tpl, int tpl_len,
+                             const pbccs_qv_model_params* params, int pin_start, int pin_end, const int* i,
+                             const int* j, int n, float* inc, float* del, float* extra, float* merge)
+{
+    if (!eng || !read || !read->seq || read->len < 0 || !tpl || tpl_len < 0 || !params || n < 0 ||
+        (n > 0 && (!i || !j)))
+        return fail(PBCCS_EINVAL, "bad argument");
+    if (n == 0) return PBCCS_OK;
+    return guarded([&] {
+        if (hipSetDevice(eng->device) != hipSuccess) return fail(PBCCS_EDEVICE, "hipSetDevice failed");
+        const int I = read->len;
+        // one device block: QParams | 5 feature tracks | cells i, j | outputs | read bases | template
+        pbccs_quiver_config c{};
+        c.params = *params;
+        c.moves_available = 15;
+        const quiver::QParams qp = qparams(c);
+        std::vector<float> feat((size_t)5 * std::max(I, 1), 0.0f);
+        const float* tr[5] = {read->ins_qv, read->subs_qv, read->del_qv, read->del_tag, read->merge_qv};
+        for (int k = 0; k < 5; ++k)
+            if (tr[k]) std::copy(tr[k], tr[k] + I, feat.begin() + (size_t)k * std::max(I, 1));
+        auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const size_t oP = 0, oF = up(sizeof(qp)), oI = oF + up(feat.size() * 4), oJ = oI + up((size_t)n * 4),
+                     oO = oJ + up((size_t)n * 4), oS = oO + up((size_t)16 * n), oT = oS + up((size_t)I + 1),
+                     top = oT + up((size_t)tpl_len + 1);
+        std::vector<char> h(top, 0);
+        std::memcpy(h.data() + oP, &qp, sizeof(qp));
+        std::memcpy(h.data() + oF, feat.data(), feat.size() * 4);
+        std::memcpy(h.data() + oI, i, (size_t)n * 4);
+        std::memcpy(h.data() + oJ, j, (size_t)n * 4);
+        std::memcpy(h.data() + oS, read->seq, I);
+        std::memcpy(h.data() + oT, tpl, tpl_len);
+        DevVec<char> d;
+        d.reserve(top, false);
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return fail(PBCCS_EDEVICE, "stream");
+        struct StreamGuard {
+            hipStream_t s;
+            ~StreamGuard() { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); }
+        } guard{st};
+        if (hipMemcpyAsync(d.ptr, h.data(), top, hipMemcpyHostToDevice, st) != hipSuccess)
+            return fail(PBCCS_EDEVICE, "upload failed");
+        const float* df = reinterpret_cast<const float*>(d.ptr + oF);
+        const size_t F = std::max(I, 1);
+        quiver::QRead r{d.ptr + oS, df, df + F, df + 2 * F, df + 3 * F, df + 4 * F, I};
+        quiver::launch_qv_moves(r, reinterpret_cast<const quiver::QParams*>(d.ptr + oP), d.ptr + oT, tpl_len,
+                                pin_start ? 1 : 0, pin_end ? 1 : 0, reinterpret_cast<const int*>(d.ptr + oI),
+                                reinterpret_cast<const int*>(d.ptr + oJ), n, reinterpret_cast<float*>(d.ptr + oO), st);
+        if (hipGetLastError() != hipSuccess) return fail(PBCCS_EDEVICE, "k_qv_moves launch failed");
+        std::vector<float> out((size_t)4 * n);
+        if (hipMemcpyAsync(out.data(), d.ptr + oO, out.size() * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return fail(PBCCS_EDEVICE, "download failed");
+        float* dst[4] = {inc, del, extra, merge};
+        for (int k = 0; k < 4; ++k)
+            if (dst[k]) std::copy(out.begin() + (size_t)k * n, out.begin() + (size_t)(k + 1) * n, dst[k]);
         return PBCCS_OK;
     });
 }

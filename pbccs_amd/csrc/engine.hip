@@ -353,7 +353,7 @@ void ArrowBatch::Prepare()
     dAPre_.reserve(cols, false);
     dBSuf_.reserve(cols, false);
     dVal_.reserve(std::max<long long>(valTop_, 1), false);
-    UploadDescriptors();
+    UploadReads();
     long long mut = 0, delta = 0, pos = 0;
     for (const HZmw& z : zmws_) {
         const long long M = unique_mutation_count(z.tpl) + 64;
@@ -395,13 +395,7 @@ int ArrowBatch::AddZmw(const std::string& tpl, const double snr[4], const ArrowO
     if (!(opt.scoreDiff >= 0.0)) throw std::invalid_argument("ScoreDiff must be positive!");   // ArrowConfig.hpp:72-77
     HZmw z;
     z.tpl = tpl;
-    transition_table(snr, z.trans);
-    device_context_table(z.trans, z.ctx);
-    for (int k = 0; k < 9; ++k) {
-        const std::pair<double, double> mv = expected_context_ll(k < 8 ? z.trans[k] : TransParams(), kMismatchProbability);
-        z.ctxMeanVar[k][0] = mv.first;
-        z.ctxMeanVar[k][1] = mv.second;
-    }
+    for (int k = 0; k < 4; ++k) z.snr[k] = snr[k];
     z.opt = opt;
     z.readBegin = (int)reads_.size();
     z.nReads = 0;
@@ -410,9 +404,33 @@ int ArrowBatch::AddZmw(const std::string& tpl, const double snr[4], const ArrowO
     z.tplOff = tplTop_;
     tplTop_ += 2LL * z.tplCap;
     zmws_.push_back(z);
-    UploadTemplate((int)zmws_.size() - 1);
     descDirty_ = true;
     return (int)zmws_.size() - 1;
+}
+
+// Consensus.h:437-453 per ZMW: ArrowConfig(ContextParameters(snr)) -- the transition table of every context, its
+// device form and the context expectations of the z-score gate -- and the scorer's forward / reverse-complement
+// template pair.  Runs once per ZMW, at the first device operation after AddZmw.
+void ArrowBatch::DeriveZmws()
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    bool any = false;
+    for (size_t zi = 0; zi < zmws_.size(); ++zi) {
+        HZmw& z = zmws_[zi];
+        if (z.derived) continue;
+        transition_table(z.snr, z.trans);
+        device_context_table(z.trans, z.ctx);
+        for (int k = 0; k < 9; ++k) {
+            const std::pair<double, double> mv = expected_context_ll(k < 8 ? z.trans[k] : TransParams(), kMismatchProbability);
+            z.ctxMeanVar[k][0] = mv.first;
+            z.ctxMeanVar[k][1] = mv.second;
+        }
+        z.derived = true;
+        UploadTemplate((int)zi);
+        any = true;
+    }
+    if (any)
+        counters_.deriveNs += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
 }
 
 int ArrowBatch::AppendRead(int z, const std::string& seq, int strand, int ts, int te)
@@ -536,8 +554,21 @@ bool ArrowBatch::Relayout(const std::vector<int>& list)
     return true;
 }
 
+void ArrowBatch::UploadReads()
+{
+    // 32 bytes of slack at the end: the lane fill loads read bases 8 at a time (two aligned words), and
+    // its prefetch of the rows past a band may reach 24 bytes beyond a read
+    dSeq_.reserve(hSeq_.size() + 32, true);
+    if (hSeq_.size() > seqUploaded_) {
+        PBCCS_HIP(hipMemcpyAsync(dSeq_.ptr + seqUploaded_, hSeq_.data() + seqUploaded_, hSeq_.size() - seqUploaded_,
+                                 hipMemcpyHostToDevice, stream_));
+        seqUploaded_ = hSeq_.size();
+    }
+}
+
 void ArrowBatch::UploadDescriptors()
 {
+    DeriveZmws();
     if (!descDirty_) return;
     const int Z = (int)zmws_.size(), R = (int)reads_.size();
     std::vector<int> zf(Z), zr(Z), zl(Z), zb(Z), zn(Z);
@@ -629,14 +660,7 @@ void ArrowBatch::UploadDescriptors()
     pRZmw_ = reinterpret_cast<int*>(base + oRz);
     pRCkpt_ = reinterpret_cast<int*>(base + oRck);
     pTpl_ = base + oTpl;
-    // 32 bytes of slack at the end: the lane fill loads read bases 8 at a time (two aligned words), and
-    // its prefetch of the rows past a band may reach 24 bytes beyond a read
-    dSeq_.reserve(hSeq_.size() + 32, true);
-    if (hSeq_.size() > seqUploaded_) {
-        PBCCS_HIP(hipMemcpyAsync(dSeq_.ptr + seqUploaded_, hSeq_.data() + seqUploaded_, hSeq_.size() - seqUploaded_,
-                                 hipMemcpyHostToDevice, stream_));
-        seqUploaded_ = hSeq_.size();
-    }
+    UploadReads();
     const size_t cols = std::max<long long>(colTop_, 1);
     dARange_.reserve(cols, true);
     dBRange_.reserve(cols, true);

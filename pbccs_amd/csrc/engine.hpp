@@ -159,6 +159,7 @@ struct Counters {   // work counters for the roofline report (bench.py)
     // band value pool of the batch, bytes (maxima over the batches merged into an engine's counters):
     // bump top (everything ever handed out), current regions (2 x capacity per read), cells in use
     long long bandTopBytes = 0, bandRegionBytes = 0, bandUsedBytes = 0;
+    long long deriveNs = 0;      // DeriveZmws: the per-ZMW setup of Consensus.h:437-453 (host)
 };
 
 // Checkpointed-band policy: interval K (0 = off) and the shortest window it applies to;
@@ -271,7 +272,10 @@ public:
     const Counters& counters();
     void ResetCounters() { counters_ = Counters(); }
     hipStream_t stream() const { return stream_; }
-    // Upload everything and reserve the largest round's buffers (so a timed polish does no H2D of inputs).
+    // Upload the reads and reserve the largest round's buffers (so a timed polish does no H2D of read bases).
+    // The per-ZMW setup of Consensus.h:437-453 -- the ArrowConfig's transition tables and expectations, the
+    // reverse-complement template, the descriptor arena -- runs at the first device operation (DeriveZmws, from
+    // UploadDescriptors), i.e. inside the polish.
     void Prepare();
     void SetProfiling(bool on);
     // Resolve pending events and in-kernel counters into `out` (added), then clear.
@@ -280,6 +284,8 @@ public:
 private:
     struct HZmw {
         std::string tpl;
+        double snr[4];
+        bool derived = false;   // trans / ctx / ctxMeanVar / the template pool's copies computed (DeriveZmws)
         double ctx[45];
         TransParams trans[8];
         double ctxMeanVar[9][2];
@@ -309,6 +315,8 @@ private:
     };
 
     void EnsureZmwUploaded();
+    void DeriveZmws();
+    void UploadReads();
     void UploadDescriptors();
     void UploadTemplate(int z);
     void EnsureCapacity(int r);

@@ -2297,6 +2297,38 @@ __global__ void __launch_bounds__(64) k_qalign(QBatch B, const int* __restrict__
     nMoves[t] = k;
 }
 
+// ---- k_qv_moves: QvEvaluator's move scores (Quiver/QvEvaluator.hpp:153-207) at listed cells ----------------
+// One lane per (i, j): Inc, Del (with QvEvaluator's pinStart / pinEnd rule, :169-184), Extra and Merge, each NaN
+// where the cell is outside the move's domain (the reference's asserts).  out: 4 x n floats (move-major).
+__global__ void __launch_bounds__(256) k_qv_moves(QEval e, int pinStart, int pinEnd, const int* __restrict__ ci,
+                                                  const int* __restrict__ cj, int n, float* __restrict__ out)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int i = ci[t], j = cj[t], I = e.I(), J = e.J();
+    const float nan = __builtin_nanf("");
+    float inc = nan, del = nan, extra = nan, merge = nan;
+    if (i >= 0 && i < I && j >= 0 && j < J) inc = e.Inc(i, j);
+    if (i >= 0 && i <= I && j >= 0 && j < J) del = ((!pinStart && i == 0) || (!pinEnd && i == I)) ? 0.0f : e.Del(i, j);
+    if (i >= 0 && i < I && j >= 0 && j <= J) extra = e.Extra(i, j);
+    if (i >= 0 && i < I && j >= 0 && j < J - 1) merge = e.Merge(i, j);
+    out[t] = inc;
+    out[n + t] = del;
+    out[2 * n + t] = extra;
+    out[3 * n + t] = merge;
+}
+
+void launch_qv_moves(const QRead& r, const QParams* p, const char* tpl, int tplLen, int pinStart, int pinEnd,
+                     const int* ci, const int* cj, int n, float* out, hipStream_t s)
+{
+    if (n <= 0) return;
+    QEval e;
+    e.r = r;
+    e.p = p;
+    e.t = QTpl{tpl, tplLen};
+    hipLaunchKernelGGL(k_qv_moves, dim3((n + 255) / 256), dim3(256), 0, s, e, pinStart, pinEnd, ci, cj, n, out);
+}
+
 void launch_qalign(const QBatch& B, const int* reads, int n, const long long* moveOff, unsigned char* moves,
                    int* nMoves, hipStream_t s)
 {

@@ -152,6 +152,11 @@ void launch_qfill_grp(const QBatch& B, const int* reads, int n, hipStream_t s);
 void launch_qscore(const QBatch& B, const QScoreWork& W, hipStream_t s);
 void launch_qscore_mid(const QBatch& B, const QMidWork& W, long long nWaves, hipStream_t s);
 void launch_qreduce(const QReduceWork& W, hipStream_t s);
+// QvEvaluator (Quiver/QvEvaluator.hpp:90-317) on one read's features against `tpl`: Inc, Del, Extra and Merge at the
+// n cells (ci[k], cj[k]) into out[0 .. 4n) (move-major; NaN outside a move's domain).  r, p, tpl, ci, cj, out are
+// device pointers.
+void launch_qv_moves(const QRead& r, const QParams* p, const char* tpl, int tplLen, int pinStart, int pinEnd,
+                     const int* ci, const int* cj, int n, float* out, hipStream_t s);
 // RecursorBase::Alignment per listed read: moves (from the end) at moveOff[t], nMoves[t] of them
 void launch_qalign(const QBatch& B, const int* reads, int n, const long long* moveOff, unsigned char* moves,
                    int* nMoves, hipStream_t s);

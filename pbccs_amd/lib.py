@@ -67,7 +67,7 @@ class CCounters(ctypes.Structure):
                 ("band_top_bytes", ctypes.c_longlong), ("band_region_bytes", ctypes.c_longlong),
                 ("band_used_bytes", ctypes.c_longlong), ("pool_mapped_bytes", ctypes.c_longlong),
                 ("oom_retries", ctypes.c_longlong), ("create_host_ns", ctypes.c_longlong),
-                ("create_upload_ns", ctypes.c_longlong)]
+                ("create_upload_ns", ctypes.c_longlong), ("derive_ns", ctypes.c_longlong)]
 
 
 class CQvModelParams(ctypes.Structure):
@@ -88,6 +88,12 @@ class CQuiverRead(ctypes.Structure):
                 ("del_tag", ctypes.POINTER(ctypes.c_float)), ("merge_qv", ctypes.POINTER(ctypes.c_float)),
                 ("chemistry", ctypes.c_char_p), ("strand", ctypes.c_int), ("tstart", ctypes.c_int),
                 ("tend", ctypes.c_int), ("threshold", ctypes.c_float)]
+
+
+class CQvFeatures(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_char_p), ("len", ctypes.c_int), ("ins_qv", ctypes.POINTER(ctypes.c_float)),
+                ("subs_qv", ctypes.POINTER(ctypes.c_float)), ("del_qv", ctypes.POINTER(ctypes.c_float)),
+                ("del_tag", ctypes.POINTER(ctypes.c_float)), ("merge_qv", ctypes.POINTER(ctypes.c_float))]
 
 
 class CQuiverZmw(ctypes.Structure):
@@ -196,6 +202,8 @@ SIGNATURES = {
     "pbccs_quiver_scorer_alignment": (I, [P, I, ctypes.c_char_p, ctypes.c_char_p, I, PI]),
     "pbccs_quiver_refine_consensus": (I, [P, ctypes.POINTER(CRefineOptions), PLL, PLL, PI]),
     "pbccs_quiver_consensus_qvs": (I, [P, PI, I, PI]),
+    "pbccs_qv_evaluator_moves": (I, [P, ctypes.POINTER(CQvFeatures), ctypes.c_char_p, I, ctypes.POINTER(CQvModelParams),
+                                     I, I, PI, PI, I, PF, PF, PF, PF]),
     "pbccs_quiver_polish_batch": (I, [P, ctypes.POINTER(CQuiverConfig), ctypes.POINTER(ctypes.c_char_p), I,
                                       ctypes.POINTER(CQuiverZmw), I, ctypes.POINTER(CRefineOptions),
                                       ctypes.POINTER(CQuiverResult)]),

@@ -88,6 +88,110 @@ class QuiverConfigTable:
         return True
 
 
+class QvSequenceFeatures:
+    """QvSequenceFeatures (Features.hpp:69-100): the bases and the five QV tracks (InsQv, SubsQv, DelQv, DelTag,
+    MergeQv); a missing track reads as zeros; DelTag may hold characters or their float codes."""
+
+    def __init__(self, seq, ins_qv=None, subs_qv=None, del_qv=None, del_tag=None, merge_qv=None):
+        n = len(seq)
+        self.Sequence = seq
+        self.SequenceAsFloat = [float(ord(c)) for c in seq]
+
+        def track(v, tag=False):
+            if v is None:
+                return [0.0] * n
+            if len(v) != n:
+                raise ValueError("feature track length differs from the sequence")
+            return [float(ord(x)) if tag and isinstance(x, str) else float(x) for x in v]
+        self.InsQv, self.SubsQv, self.DelQv = track(ins_qv), track(subs_qv), track(del_qv)
+        self.DelTag, self.MergeQv = track(del_tag, True), track(merge_qv)
+
+    def Length(self):
+        return len(self.Sequence)
+
+    def __getitem__(self, i):
+        return self.Sequence[i]
+
+    def _c(self):
+        f = _lib_mod.CQvFeatures()
+        f.seq = self.Sequence.encode()
+        f.len = len(self.Sequence)
+        self._keep = []
+        for name, v in (("ins_qv", self.InsQv), ("subs_qv", self.SubsQv), ("del_qv", self.DelQv),
+                        ("del_tag", self.DelTag), ("merge_qv", self.MergeQv)):
+            a = (ctypes.c_float * max(1, len(v)))(*v)
+            self._keep.append(a)
+            setattr(f, name, ctypes.cast(a, ctypes.POINTER(ctypes.c_float)))
+        return f
+
+
+class QvEvaluator:
+    """QvEvaluator (Quiver/QvEvaluator.hpp:90-317): the move scores of one read against a template, evaluated on
+    the device by the recursions' own evaluator (pbccs_qv_evaluator_moves).  Inc / Del / Extra / Merge take one
+    cell; Moves takes many (one launch).  A cell outside a move's domain (the reference asserts) gives NaN."""
+
+    def __init__(self, features, tpl, params, pin_start=True, pin_end=True, read_name="", engine=None):
+        from . import default_engine
+        self._f = features if isinstance(features, QvSequenceFeatures) else QvSequenceFeatures(features)
+        self._tpl, self._p = tpl, params
+        self._pins = (bool(pin_start), bool(pin_end))
+        self._name = read_name
+        self._eng = engine or default_engine()
+
+    def ReadName(self):
+        return self._name
+
+    def Basecalls(self):
+        return self._f.Sequence
+
+    def Template(self, tpl=None):
+        if tpl is None:
+            return self._tpl
+        self._tpl = tpl
+
+    def ReadLength(self):
+        return self._f.Length()
+
+    def TemplateLength(self):
+        return len(self._tpl)
+
+    def PinStart(self):
+        return self._pins[0]
+
+    def PinEnd(self):
+        return self._pins[1]
+
+    def IsMatch(self, i, j):
+        return self._f.Sequence[i] == self._tpl[j]
+
+    def Moves(self, cells):
+        """(Inc, Del, Extra, Merge) lists at the (i, j) cells."""
+        n = len(cells)
+        if n == 0:
+            return [], [], [], []
+        ci = (ctypes.c_int * n)(*[c[0] for c in cells])
+        cj = (ctypes.c_int * n)(*[c[1] for c in cells])
+        outs = [(ctypes.c_float * n)() for _ in range(4)]
+        f = self._f._c()
+        p = self._p._c()
+        _lib_mod.check(load().pbccs_qv_evaluator_moves(self._eng._h, ctypes.byref(f), self._tpl.encode(),
+                                                        len(self._tpl), ctypes.byref(p), int(self._pins[0]),
+                                                        int(self._pins[1]), ci, cj, n, *outs))
+        return tuple(list(o) for o in outs)
+
+    def Inc(self, i, j):
+        return self.Moves([(i, j)])[0][0]
+
+    def Del(self, i, j):
+        return self.Moves([(i, j)])[1][0]
+
+    def Extra(self, i, j):
+        return self.Moves([(i, j)])[2][0]
+
+    def Merge(self, i, j):
+        return self.Moves([(i, j)])[3][0]
+
+
 class QuiverMultiReadMutationScorer:
     """MultiReadMutationScorer<SparseSse{Qv,QvSumProduct}Recursor> (Quiver/MultiReadMutationScorer.cpp)."""
 

@@ -311,3 +311,24 @@ def test_quiver_tall_band_fill_paths_match_oracle(score_diff, sum_product):
     vals = g.s.ScoreMany([g.P.Mutation(t, s, b) for (t, s, b) in muts])
     for (t, s, b), v in zip(muts, vals):
         assert v == o.score(t, s, b), (t, s, b)
+
+
+@pytest.mark.parametrize("pins", [(True, True), (False, False)])
+def test_qv_evaluator_python_mirror_matches_oracle(pins):
+    """pbccs_amd.QvEvaluator (the Python mirror of QvEvaluator.hpp:90-317 over pbccs_qv_evaluator_moves): every
+    cell's Inc / Del / Extra / Merge equals the oracle's evaluator, NaN outside each move's domain."""
+    import math
+    import pbccs_amd as P
+    rng = np.random.default_rng(5)
+    tpl = "".join(rng.choice(list("ACGT"), size=30)) + "CCCAAA"
+    seq = tpl[2:20] + "AAA" + tpl[21:34]
+    f = _features(rng, seq)
+    feats = P.QvSequenceFeatures(seq, f["ins"], f["subs"], f["del"], f["del_tag"], f["merge"])
+    ev = P.QvEvaluator(feats, tpl, P.QvModelParams(**PARAMS2), pin_start=pins[0], pin_end=pins[1])
+    cells = [(i, j) for i in range(-1, len(seq) + 2) for j in range(-1, len(tpl) + 2)]
+    got = ev.Moves(cells)
+    exp = O.qv_eval_moves(seq, tpl, PARAMS2, cells, f, pin_start=pins[0], pin_end=pins[1])
+    for k in range(4):
+        for a, b in zip(got[k], exp[k]):
+            assert (math.isnan(a) and math.isnan(b)) or a == b
+    assert ev.Inc(0, 0) == exp[0][cells.index((0, 0))] and ev.ReadLength() == len(seq)
