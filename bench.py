@@ -1084,6 +1084,26 @@ def make_roofline(stats, local_time, workload):
             "source_digest": digest}
 
 
+FILL_WORK_SLOTS = ("counted_cells", "tall_abort_cells", "regrow_cells", "overflow_cells", "group_chunk_steps",
+                   "wave_chunk_issues", "reads", "passes")
+
+
+def fill_work_report(w):
+    """PBCCS_FILL_WORK=1 (CoopFill::work): where each fill kind's computed cells went, and how busy its wavefronts'
+    groups were.  computed = counted + thrown away by a tall abort + count-only regrow passes + count-only overflow
+    fills; lockstep = the groups' chunk steps / (groups per wave x the wave's chunk issues)."""
+    out = {}
+    for k, (name, groups) in enumerate((("k_fill", 4), ("k_fill_tall", 1))):
+        d = dict(zip(FILL_WORK_SLOTS, w[8 * k:8 * k + 8]))
+        comp = d["counted_cells"] + d["tall_abort_cells"] + d["regrow_cells"] + d["overflow_cells"]
+        d["computed_cells"] = comp
+        d["counted_frac"] = round(d["counted_cells"] / comp, 4) if comp else None
+        d["lockstep_eff"] = round(d["group_chunk_steps"] / (groups * d["wave_chunk_issues"]), 4) \
+            if d["wave_chunk_issues"] else None
+        out[name] = d
+    return out
+
+
 def report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total_zmws, qstats=None,
            extra=None, settings=None):
     import torch.distributed as dist
@@ -1159,6 +1179,8 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
     }
     if qstats:   # configs[4]: records stream to rank 0 per chunk; tail_ms = rank 0's wait after its last chunk
         out["queue"] = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in qstats.items()}
+    if any(counters.get("fill_work") or []):
+        out["fill_work"] = fill_work_report(counters["fill_work"])
     if "host" in extra:
         out["host"] = extra["host"]
     if "prepare" in extra:

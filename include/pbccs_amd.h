@@ -229,6 +229,10 @@ typedef struct {
     long long create_upload_ns;  /* pbccs_batch_create: device reservations + the read upload */
     long long derive_ns;         /* the per-ZMW setup of Consensus.h:437-453 (transition tables, expectations,
                                     reverse-complement template), run by the polish at its first device step */
+    long long fill_work[16];     /* PBCCS_FILL_WORK=1 diagnostics, per fill kind k (0: 16-lane, 1: 64-lane) at
+                                    [8 k + ...]: counted cells, cells thrown away by a tall abort, count-only
+                                    regrow cells, count-only overflow cells, group chunk steps, wave chunk issues,
+                                    reads, counted passes */
 } pbccs_counters;
 int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset);
 

@@ -107,6 +107,19 @@ struct CoopFill {
     // diagnostics (PBCCS_FILL_PATHS=2): per listed read [6]: wall-clock start / end (100 MHz), shader cycles,
     // cells, passes, columns
     long long* trace = nullptr;
+    // diagnostics (PBCCS_FILL_WORK=1): where the fill's computed cells go, per kind (k = 0: the 16-lane fill,
+    // 1: the 64-lane fills) at work[kFillWorkSlots * k + ...] (kFillWork*)
+    unsigned long long* work = nullptr;
+};
+// work[] slots per fill kind: cells of the passes that count (the bench's GCUPS); cells computed and thrown away
+// because the read aborted as too tall (its passes restart on the 64-lane path); cells of count-only passes that
+// re-run after a regrow; cells of fills that ended in count-only overflow (re-run by the host); the groups' chunk
+// steps (a G x R-row chunk of a column's chain); the wavefront's chunk issues (the chunk body executed for some
+// subset of the wave's groups: 4 x issues - steps are group-steps spent idle or serialised in lock-step); reads;
+// counted passes
+enum FillWork : int {
+    kFillWorkCells = 0, kFillWorkTallAbort, kFillWorkRegrow, kFillWorkOverflow, kFillWorkSteps, kFillWorkIssues,
+    kFillWorkReads, kFillWorkPasses, kFillWorkSlots
 };
 size_t coop_group_bytes(int hcap, int readWords, int tplWords);
 constexpr int kNarrowGroupLanes = 16;   // typical bands: lanes per read (four reads per wavefront)

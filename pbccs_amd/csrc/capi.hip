@@ -271,6 +271,7 @@ int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset)
     out->create_host_ns = eng->createHostNs;
     out->create_upload_ns = eng->createUploadNs;
     out->derive_ns = eng->counters.deriveNs;
+    for (int k = 0; k < 16; ++k) out->fill_work[k] = eng->counters.fillWork[k];
     if (reset) {
         eng->counters = Counters();
         eng->oomRetries = 0;
@@ -507,6 +508,7 @@ static void merge_engine_stats(pbccs_engine* eng, ArrowBatch& B)
         eng->counters.scoreTasks += c.scoreTasks;
         eng->counters.mutations += c.mutations;
         eng->counters.deriveNs += c.deriveNs;
+        for (int k = 0; k < 16; ++k) eng->counters.fillWork[k] += c.fillWork[k];
         eng->counters.bandTopBytes = std::max(eng->counters.bandTopBytes, c.bandTopBytes);
         eng->counters.bandRegionBytes = std::max(eng->counters.bandRegionBytes, c.bandRegionBytes);
         eng->counters.bandUsedBytes = std::max(eng->counters.bandUsedBytes, c.bandUsedBytes);

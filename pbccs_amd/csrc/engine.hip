@@ -303,6 +303,13 @@ void ArrowBatch::ResolveEvents()
 
 const Counters& ArrowBatch::counters()
 {
+    if (dFillWork_.ptr) {   // PBCCS_FILL_WORK diagnostics: fold the device counters in and clear them
+        unsigned long long h[16];
+        PBCCS_HIP(hipMemcpyAsync(h, dFillWork_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
+        PBCCS_HIP(hipMemsetAsync(dFillWork_.ptr, 0, sizeof(h), stream_));
+        PBCCS_HIP(hipStreamSynchronize(stream_));
+        for (int k = 0; k < 16; ++k) counters_.fillWork[k] += (long long)h[k];
+    }
     long long region = 0, used = 0;
     for (const HRead& r : reads_) {
         region += 2 * r.valCap;
@@ -808,6 +815,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     static const bool pathTrace = std::getenv("PBCCS_FILL_PATHS") != nullptr;
     // PBCCS_FILL_PATHS=2: also per launch the slowest read (its wall ms, cycles per cell, cells, passes)
     static const bool pathTrace2 = pathTrace && std::getenv("PBCCS_FILL_PATHS")[0] == '2';
+    // PBCCS_FILL_WORK=1: where the fills' computed cells go (CoopFill::work; counters().fillWork)
+    static const bool fillWork = std::getenv("PBCCS_FILL_WORK") != nullptr;
     for (int attempt = 0;; ++attempt) {
         // route reads whose buffers do not fit this path's LDS budget to the next path
         for (int p = 0; p < kPaths; ++p) {
@@ -948,6 +957,13 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             }
             const int* lp = dList_.ptr + off;
             const hipStream_t st = p <= 1 ? stream_ : stream2_;
+            if (fillWork) {
+                if (!dFillWork_.ptr) {
+                    dFillWork_.reserve(16, false);
+                    PBCCS_HIP(hipMemsetAsync(dFillWork_.ptr, 0, 16 * sizeof(unsigned long long), stream_));
+                }
+                F.work = dFillWork_.ptr;
+            }
             if (pathTrace2) {   // on the launch's own stream (the tall ones run beside stream_)
                 dCoopTrace_[p].reserve((size_t)6 * n, false);
                 PBCCS_HIP(hipMemsetAsync(dCoopTrace_[p].ptr, 0, sizeof(long long) * 6 * n, st));

@@ -160,6 +160,7 @@ struct Counters {   // work counters for the roofline report (bench.py)
     // bump top (everything ever handed out), current regions (2 x capacity per read), cells in use
     long long bandTopBytes = 0, bandRegionBytes = 0, bandUsedBytes = 0;
     long long deriveNs = 0;      // DeriveZmws: the per-ZMW setup of Consensus.h:437-453 (host)
+    long long fillWork[16] = {}; // PBCCS_FILL_WORK=1: CoopFill::work summed (2 kinds x kFillWorkSlots)
 };
 
 // Checkpointed-band policy: interval K (0 = off) and the shortest window it applies to;
@@ -339,6 +340,7 @@ private:
     DevVec<int> dNSel_;
     DevVec<double> dColScratch_;          // the hybrid fill path's column rows past its LDS buffers
     DevVec<long long> dCoopTrace_[4];     // PBCCS_FILL_PATHS=2 diagnostics: per-read fill timing, per path
+    DevVec<unsigned long long> dFillWork_;   // PBCCS_FILL_WORK=1 diagnostics: CoopFill::work
     DevVec<unsigned long long> dBump_;   // in-kernel band growth: the value pool's free top
     std::unique_ptr<Workspace> ownWs_;
     Workspace* ws_;

@@ -100,6 +100,21 @@ struct PassOut {
     int maxH;         // the pass's tallest column (rows)
 };
 
+// PBCCS_FILL_WORK diagnostics (CoopFill::work): the group's chunk steps and, per lane, the chunk bodies this lane
+// issued as the wave's first active lane (so the lanes' sum is the wave's chunk issues)
+struct Work {
+    bool on;
+    long long steps;
+    long long issues;
+};
+__device__ __forceinline__ void count_issue(Work& W)
+{
+    if (W.on) {
+        const unsigned long long act = __ballot(1);
+        if ((int)(threadIdx.x & 63) == __ffsll((long long)act) - 1) W.issues += 1;
+    }
+}
+
 // Column rows in global memory (the hybrid path's rows past the LDS buffer): a column's rows are written by
 // one lane and read by its neighbours in the next column, so the group's stores must have completed before
 // the next column's loads.  One workgroup-scope fence after each column that reached global rows (the group
@@ -202,7 +217,8 @@ __device__ double finish_log_scales(const Task<G>& T, const Band& m, int J)
 // A column's rows run in chunks of CH = G x R rows, R consecutive rows per lane (lane l: rows i0 + l R ..
 // i0 + l R + R - 1); R > 1 hands the chain on once per R rows (insertion_chain_rows).
 template <int G, int R>
-__device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO)
+__device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO,
+                              Work& W)
 {
     constexpr int CH = G * R;
     const Band* guide = guided ? &o : nullptr;
@@ -277,7 +293,13 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         if (b < I) {
             double carry = 0.0;
             for (int i0 = b;; i0 += CH) {
-                if ((nc + 1) * CH > T.rowsCap) { out.tall = true; return out; }
+                if ((nc + 1) * CH > T.rowsCap) {
+                    out.tall = true;
+                    out.used = used;
+                    W.steps += nc;
+                    return out;
+                }
+                count_issue(W);
                 const int ib = i0 + lane * R;   // the lane's first row of the chunk
                 double m[R], k[R], d[R], x[R];
                 {
@@ -443,6 +465,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         if ((jb == G - 1 || j == J - 1) && !counting && lane <= jb) a.L(j - jb + lane) = (myF != 1.0) ? log(myF) : 0.0;
         used += e - b;
         stored += add;
+        W.steps += nc;
         col_fence(T.gcol && nc * CH > T.hcap);   // the next column's lanes read rows this column's lanes wrote
         prev ^= 1;
         cur ^= 1;
@@ -482,7 +505,8 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
 
 // ---- FillBeta (SimpleRecursor.cpp:183-296); rows run bottom-up, stored bottom-up --------------------
 template <int G, int R>
-__device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO)
+__device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO,
+                             Work& W)
 {
     constexpr int CH = G * R;
     const Band* guide = guided ? &o : nullptr;
@@ -550,7 +574,13 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         if (e - 1 > 0) {
             double carry = 0.0;
             for (int c = 0;; ++c) {
-                if ((c + 1) * CH > T.rowsCap) { out.tall = true; return out; }
+                if ((c + 1) * CH > T.rowsCap) {
+                    out.tall = true;
+                    out.used = used;
+                    W.steps += nc;
+                    return out;
+                }
+                count_issue(W);
                 const int ob = c * CH + lane * R;   // the lane's first offset (row e - 1 - ob)
                 double m[R], k[R], d[R], x[R];
                 {
@@ -710,6 +740,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         if ((jb == G - 1 || j == 1) && !counting && lane <= jb) bm.L(j + jb - lane) = (myF != 1.0) ? log(myF) : 0.0;
         used += e - b;
         stored += add;
+        W.steps += nc;
         col_fence(T.gcol && nc * CH > T.hcap);
         nxt ^= 1;
         cur ^= 1;
@@ -866,9 +897,9 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     long long needA = 0, needB = 0;
     unsigned long long cells = 0, passes = 0;
     int flips = 0;
-    auto fail_tall = [&]() {
-        if (lane == 0) B.rStatus[r] = kFillTall;
-    };
+    Work W{F.work != nullptr, 0, 0};
+    unsigned long long regrowCells = 0, abortCells = 0;
+    bool tallAbort = false;
     // MutationScorer ctor -> FillAlphaBeta (SimpleRecursor.cpp:642-691), as a pass sequencer with one
     // call site per matrix (every inlined pass costs registers and instruction cache):
     //   step 0: alpha(Null guide); step 1: beta(alpha guide); if either used >= 4% of the matrix, the
@@ -904,10 +935,15 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
         }
         const bool guided = step > 0, self = step > 1;
         PassOut o;
-        if (doAlpha) o = coop_alpha<G, R>(T, a, bm, guided, self, ovf, ub);
-        else o = coop_beta<G, R>(T, bm, a, guided, self, ovf, ua);
-        if (o.tall) return fail_tall();
+        if (doAlpha) o = coop_alpha<G, R>(T, a, bm, guided, self, ovf, ub, W);
+        else o = coop_beta<G, R>(T, bm, a, guided, self, ovf, ua, W);
+        if (o.tall) {   // every cell so far is thrown away: the read restarts on the 64-lane path
+            tallAbort = true;
+            abortCells = cells + (unsigned long long)o.used;
+            break;
+        }
         if (o.regrow) {   // exact region for this pass, then run it again (count-only if the pool is full)
+            regrowCells += (unsigned long long)o.used;
             // (two calls, not a selected reference: the bands then stay in registers)
             const bool moved = ++regrows <= 8 && (doAlpha ? regrow_bands<G>(T, a, bm, true, o.stored, sb)
                                                           : regrow_bands<G>(T, bm, a, false, o.stored, sa));
@@ -938,6 +974,24 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
                 break;
             }
         }
+    }
+    if (W.on) {   // PBCCS_FILL_WORK: where this read's computed cells went (every lane: its issue count)
+        unsigned long long* w = F.work + (G == 64 ? kFillWorkSlots : 0);
+        if (W.issues) atomicAdd(&w[kFillWorkIssues], (unsigned long long)W.issues);
+        if (lane == 0) {
+            atomicAdd(&w[kFillWorkSteps], (unsigned long long)W.steps);
+            atomicAdd(&w[kFillWorkReads], 1ull);
+            atomicAdd(&w[kFillWorkRegrow], regrowCells);
+            if (tallAbort) atomicAdd(&w[kFillWorkTallAbort], abortCells);
+            else {
+                atomicAdd(&w[ovf ? kFillWorkOverflow : kFillWorkCells], cells);
+                if (!ovf) atomicAdd(&w[kFillWorkPasses], passes);
+            }
+        }
+    }
+    if (tallAbort) {
+        if (lane == 0) B.rStatus[r] = kFillTall;
+        return;
     }
     const double av = log(pa.last) + pa.sumL;
     const double bv = log(pb.last) + pb.sumL;

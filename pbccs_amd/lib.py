@@ -67,7 +67,8 @@ class CCounters(ctypes.Structure):
                 ("band_top_bytes", ctypes.c_longlong), ("band_region_bytes", ctypes.c_longlong),
                 ("band_used_bytes", ctypes.c_longlong), ("pool_mapped_bytes", ctypes.c_longlong),
                 ("oom_retries", ctypes.c_longlong), ("create_host_ns", ctypes.c_longlong),
-                ("create_upload_ns", ctypes.c_longlong), ("derive_ns", ctypes.c_longlong)]
+                ("create_upload_ns", ctypes.c_longlong), ("derive_ns", ctypes.c_longlong),
+                ("fill_work", ctypes.c_longlong * 16)]
 
 
 class CQvModelParams(ctypes.Structure):

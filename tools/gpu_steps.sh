@@ -100,6 +100,15 @@ step() {
       done
       python3 tools/pmc_summary.py $(find $OUT/pmc1 $OUT/pmc2 -name '*counter_collection.csv') > $OUT/pmc_summary.txt && \
         head -60 $OUT/pmc_summary.txt ;;
+    valu)     # VALU instructions per counted cell and LDS bank conflicts per kernel: one SQ pass with profiling on
+      timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES \
+        -f csv -d $OUT/valu -o pmc -- $BENCH --cpu-sample 0 --steps 5 --warmup 1 > $OUT/valu.json 2> $OUT/valu.err \
+        || { echo "valu pass failed"; return 1; }
+      python3 tools/valu_per_cell.py "$(find $OUT/valu -name '*counter_collection.csv' | head -1)" $OUT/valu.json \
+        $OUT/valu_per_cell.json "$(python3 -c 'import bench; print(bench.kernel_source_digest())')" ;;
+    work)     # where the fills' computed cells go (PBCCS_FILL_WORK=1 in-kernel counters), the driver's shape, 5 steps
+      PBCCS_FILL_WORK=1 timeout -k 10 300 $BENCH --steps 5 --warmup 1 --cpu-sample 0 > $OUT/work.json 2> $OUT/work.err && \
+        python3 -c "import json; d=json.load(open('$OUT/work.json')); print(d['value'], json.dumps(d.get('fill_work')))" ;;
     traffic)  # HBM bytes of the fills and k_score: FETCH_SIZE and WRITE_SIZE passes (they do not fit one pass)
       timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o pmc -- $BENCH --cpu-sample 0 --steps 5 \
         --warmup 1 > $OUT/fetch.json 2> $OUT/fetch.err || { echo "fetch pass failed"; return 1; }
