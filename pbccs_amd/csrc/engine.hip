@@ -203,15 +203,42 @@ void ckpt_policy(int* K, int* minLen)   // read per batch: tests switch it at ru
     *minLen = std::max(0, env_int("PBCCS_CKPT_MIN_LEN", kCkptDefaultMinLen));
 }
 
+Workspace::~Workspace()
+{
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (stream2) (void)hipStreamSynchronize(stream2);
+    for (hipEvent_t e : eventPool) (void)hipEventDestroy(e);
+    if (evFork) (void)hipEventDestroy(evFork);
+    if (evJoin) (void)hipEventDestroy(evJoin);
+    if (stream2) (void)hipStreamDestroy(stream2);
+    if (stream) (void)hipStreamDestroy(stream);
+}
+
+void Workspace::EnsureStreams()
+{
+    if (stream) return;
+    PBCCS_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    PBCCS_HIP(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+    PBCCS_HIP(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
+    PBCCS_HIP(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
+}
+
 ArrowBatch::ArrowBatch(int device, Workspace* shared)
     : device_(device),
       ownWs_(shared ? nullptr : new Workspace()),
       ws_(shared ? shared : ownWs_.get()),
+      dSelBase_(ws_->selBase), dNSel_(ws_->nSel), dColScratch_(ws_->colScratch), dBump_(ws_->bump),
+      hDesc_(ws_->hDesc), dCkPairs_(ws_->ckPairs), dCkStart_(ws_->ckStart), dRBaseline_(ws_->rBaseline),
+      dRFlips_(ws_->rFlips), dRStatus_(ws_->rStatus), dUsedA_(ws_->usedA), dUsedB_(ws_->usedB), dMaxH_(ws_->maxH),
+      dWZmw_(ws_->wZmw), dWNMut_(ws_->wNMut), dWMutBase_(ws_->wMutBase), dWDeltaBase_(ws_->wDeltaBase),
+      dWWaveStart_(ws_->wWaveStart), dWMutStart_(ws_->wMutStart), dWPosStart_(ws_->wPosStart),
+      dWPosBase_(ws_->wPosBase), dWQvBase_(ws_->wQvBase),
       dARange_(ws_->aRange), dBRange_(ws_->bRange), dAOff_(ws_->aOff), dBOff_(ws_->bOff), dALs_(ws_->aLs),
       dBLs_(ws_->bLs), dAPre_(ws_->aPre), dBSuf_(ws_->bSuf), dVal_(ws_->val), dCodes_(ws_->codes),
       dPosOff_(ws_->posOff), dQv_(ws_->qv), dList_(ws_->list), dEdge_(ws_->edge), dEdgeCount_(ws_->edgeCount),
       dDelta_(ws_->delta), dScore_(ws_->score), dFav_(ws_->fav), dScratch_(ws_->scratch),
-      dScratchTop_(ws_->scratchTop), dScratchOverflow_(ws_->scratchOverflow)
+      dScratchTop_(ws_->scratchTop), dScratchOverflow_(ws_->scratchOverflow), dStats_(ws_->stats),
+      eventPool_(ws_->eventPool)
 {
     PBCCS_HIP(hipSetDevice(device_));
     // first value-region estimate per read (PBCCS_INITIAL_BAND_HEIGHT overrides it: tests use a tiny one
@@ -219,10 +246,11 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared)
     if (const char* e = std::getenv("PBCCS_INITIAL_BAND_HEIGHT")) initialBandHeight_ = std::max(1, std::atoi(e));
     ckpt_policy(&ckptK_, &ckptMinLen_);
     ckptAll_ = std::min(kCkptMaxK, std::max(0, env_int("PBCCS_CKPT_ALL", 0)));
-    PBCCS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    PBCCS_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
-    PBCCS_HIP(hipEventCreateWithFlags(&evFork_, hipEventDisableTiming));
-    PBCCS_HIP(hipEventCreateWithFlags(&evJoin_, hipEventDisableTiming));
+    ws_->EnsureStreams();
+    stream_ = ws_->stream;
+    stream2_ = ws_->stream2;
+    evFork_ = ws_->evFork;
+    evJoin_ = ws_->evJoin;
     dScratch_.reserve(kInitialScratch, false);
     dScratchTop_.reserve(1, false);
     // the read pool starts with 16 bytes of padding (see UploadDescriptors: word loads of read bases)
@@ -233,18 +261,14 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared)
 
 ArrowBatch::~ArrowBatch()
 {
+    // the streams and events belong to the workspace (the slot's next batch reuses them): wait, do not destroy
     if (stream_) {
         (void)hipStreamSynchronize(stream_);
-        for (const Pending& p : pending_) {
-            (void)hipEventDestroy(p.a);
-            (void)hipEventDestroy(p.b);
-        }
-        for (hipEvent_t e : eventPool_) (void)hipEventDestroy(e);
         (void)hipStreamSynchronize(stream2_);
-        (void)hipEventDestroy(evFork_);
-        (void)hipEventDestroy(evJoin_);
-        (void)hipStreamDestroy(stream2_);
-        (void)hipStreamDestroy(stream_);
+        for (const Pending& p : pending_) {
+            eventPool_.push_back(p.a);
+            eventPool_.push_back(p.b);
+        }
     }
 }
 

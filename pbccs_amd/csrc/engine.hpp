@@ -186,9 +186,32 @@ struct KernelStat {
 };
 
 // Large device pools.  A batch either owns one (fine-grained scorers) or borrows its engine's (batch
-// polish): batches polish one after another, so they stream through one resident workspace.
+// polish): batches polish one after another, so they stream through one resident workspace.  The workspace also
+// keeps the batches' HIP streams, events and per-round scratch, so a slot that polishes one batch after another
+// (the work queue, ccs chunks) allocates, frees and creates nothing in steady state: a hipFree or a stream
+// destroy between batches synchronises with every other slot's work.
 struct Workspace {
     explicit Workspace(bool vmm = false) { val.allowVmm = vmm; }
+    ~Workspace();
+    Workspace(const Workspace&) = delete;
+    Workspace& operator=(const Workspace&) = delete;
+    void EnsureStreams();   // creates the streams and fork/join events once
+    hipStream_t stream = nullptr, stream2 = nullptr;   // a batch's main stream; the tall fills' stream
+    hipEvent_t evFork = nullptr, evJoin = nullptr;
+    std::vector<hipEvent_t> eventPool;                 // timing events (profiling)
+    // per-round scratch of the batch polishing on this slot
+    DevVec<long long> selBase;
+    DevVec<int> nSel;
+    DevVec<double> colScratch;
+    DevVec<unsigned long long> bump;
+    PinnedBuf hDesc;
+    DevVec<int2> ckPairs;
+    DevVec<long long> ckStart;
+    DevVec<double> rBaseline;
+    DevVec<int> rFlips, rStatus, usedA, usedB, maxH;
+    DevVec<int> wZmw, wNMut;
+    DevVec<long long> wMutBase, wDeltaBase, wWaveStart, wMutStart, wPosStart, wPosBase, wQvBase;
+    DevVec<unsigned long long> stats;
     // per-read compact bands (what scoring reads)
     DevVec<int2> aRange, bRange;
     DevVec<int> aOff, bOff;
@@ -333,17 +356,17 @@ private:
                   bool needPositions, bool phased = false);
 
     int device_ = 0;
-    hipStream_t stream_ = nullptr;
-    hipStream_t stream2_ = nullptr;      // second stream for the tall-band fill path
-    hipEvent_t evFork_ = nullptr, evJoin_ = nullptr;
-    DevVec<long long> dSelBase_;          // phased scoring: per-item ranges of the surviving mutations
-    DevVec<int> dNSel_;
-    DevVec<double> dColScratch_;          // the hybrid fill path's column rows past its LDS buffers
-    DevVec<long long> dCoopTrace_[4];     // PBCCS_FILL_PATHS=2 diagnostics: per-read fill timing, per path
-    DevVec<unsigned long long> dFillWork_;   // PBCCS_FILL_WORK=1 diagnostics: CoopFill::work
-    DevVec<unsigned long long> dBump_;   // in-kernel band growth: the value pool's free top
     std::unique_ptr<Workspace> ownWs_;
     Workspace* ws_;
+    hipStream_t stream_ = nullptr;       // the workspace's streams (ws_->stream / stream2)
+    hipStream_t stream2_ = nullptr;      // second stream for the tall-band fill path
+    hipEvent_t evFork_ = nullptr, evJoin_ = nullptr;
+    DevVec<long long>& dSelBase_;         // phased scoring: per-item ranges of the surviving mutations
+    DevVec<int>& dNSel_;
+    DevVec<double>& dColScratch_;         // the hybrid fill path's column rows past its LDS buffers
+    DevVec<long long> dCoopTrace_[4];     // PBCCS_FILL_PATHS=2 diagnostics: per-read fill timing, per path
+    DevVec<unsigned long long> dFillWork_;   // PBCCS_FILL_WORK=1 diagnostics: CoopFill::work
+    DevVec<unsigned long long>& dBump_;  // in-kernel band growth: the value pool's free top
     std::vector<HZmw> zmws_;
     std::vector<HRead> reads_;
     long long tplTop_ = 0, seqTop_ = 0, colTop_ = 0, valTop_ = 0;
@@ -358,23 +381,24 @@ private:
     // template pool live in one device arena, filled by one copy from a page-locked staging buffer per
     // UploadDescriptors (UploadDescriptors sets the typed views below).
     DevVec<char> dDesc_, dSeq_;
-    PinnedBuf hDesc_;
+    PinnedBuf& hDesc_;
     int *pZFwd_ = nullptr, *pZRev_ = nullptr, *pZLen_ = nullptr, *pZReadBegin_ = nullptr, *pZNReads_ = nullptr;
     double* pZCtx_ = nullptr;
     char* pTpl_ = nullptr;
     long long *pRSeqOff_ = nullptr, *pRColBase_ = nullptr, *pRValA_ = nullptr, *pRValB_ = nullptr, *pRValCap_ = nullptr;
     int *pRLen_ = nullptr, *pRStrand_ = nullptr, *pRTs_ = nullptr, *pRTe_ = nullptr, *pRActive_ = nullptr,
         *pRZmw_ = nullptr, *pRCkpt_ = nullptr;
-    DevVec<int2> dCkPairs_;        // k_score_ckpt task list of a scoring phase
-    DevVec<long long> dCkStart_;
+    DevVec<int2>& dCkPairs_;       // k_score_ckpt task list of a scoring phase
+    DevVec<long long>& dCkStart_;
     // checkpointed bands: interval K for tall-path reads of windows >= ckptMinLen_; ckptAll_ (test hook
     // PBCCS_CKPT_ALL) puts every cooperative fill on checkpoints
     int ckptK_ = 0, ckptMinLen_ = 0, ckptAll_ = 0;
     long long ckSlotCap_ = 0;
-    DevVec<double> dRBaseline_;
-    DevVec<int> dRFlips_, dRStatus_, dUsedA_, dUsedB_, dMaxH_;
-    DevVec<int> dWZmw_, dWNMut_;
-    DevVec<long long> dWMutBase_, dWDeltaBase_, dWWaveStart_, dWMutStart_, dWPosStart_, dWPosBase_, dWQvBase_;
+    DevVec<double>& dRBaseline_;
+    DevVec<int>& dRFlips_, &dRStatus_, &dUsedA_, &dUsedB_, &dMaxH_;
+    DevVec<int>& dWZmw_, &dWNMut_;
+    DevVec<long long>& dWMutBase_, &dWDeltaBase_, &dWWaveStart_, &dWMutStart_, &dWPosStart_, &dWPosBase_,
+        &dWQvBase_;
     // workspace pools (aliases into *ws_)
     DevVec<int2>& dARange_;
     DevVec<int2>& dBRange_;
@@ -404,14 +428,14 @@ private:
     Counters counters_;
     // profiling
     bool profiling_ = false;
-    DevVec<unsigned long long> dStats_;
+    DevVec<unsigned long long>& dStats_;
     DevVec<long long> dTrace_;   // PBCCS_FILL_TRACE diagnostics
     struct Pending {
         int kind;
         hipEvent_t a, b;
     };
     std::vector<Pending> pending_;
-    std::vector<hipEvent_t> eventPool_;
+    std::vector<hipEvent_t>& eventPool_;
     KernelStat stats_[kKernelKinds];
 };
 

@@ -806,11 +806,13 @@ bool QuiverBatch::Alignment(int r, std::string* target, std::string* query)
     put(dList_, std::vector<int>{r}, stream_);
     put(dMoveOff_, std::vector<long long>{0}, stream_);
     dMoves_.reserve((size_t)I + J + 1, false);
-    dOff_.reserve(1, false);
-    launch_qalign(View(), dList_.ptr, 1, dMoveOff_.ptr, dMoves_.ptr, dOff_.ptr, stream_);
+    // the move count has its own buffer: dOff_ is the bands' column offsets (QBatch::off), which the count once
+    // overwrote (column 0 of the first arena), so a second Alignment of the read walked a damaged band
+    dNMoves_.reserve(1, false);
+    launch_qalign(View(), dList_.ptr, 1, dMoveOff_.ptr, dMoves_.ptr, dNMoves_.ptr, stream_);
     QHIP(hipGetLastError());
     int n = 0;
-    QHIP(hipMemcpyAsync(&n, dOff_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    QHIP(hipMemcpyAsync(&n, dNMoves_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
     QHIP(hipStreamSynchronize(stream_));
     if (n < 0) throw DeviceError("quiver alignment: no valid move (alpha not filled?)");
     std::vector<unsigned char> mv(n);

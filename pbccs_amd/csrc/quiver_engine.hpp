@@ -226,6 +226,7 @@ private:
     DevVec<unsigned long long> dScratchTop_;
     DevVec<long long> dMoveOff_;
     DevVec<unsigned char> dMoves_;
+    DevVec<int> dNMoves_;   // k_qalign's move count per listed read
     // batched rounds
     DevVec<long long> dWTaskStart_, dWMutBase_, dSel_, dSelCount_, dSelBase_;
     DevVec<long long> dWaveStart_, dWMutCount_, dEdge_;   // k_qscore_mid work + its edge-case task list

@@ -332,3 +332,23 @@ def test_qv_evaluator_python_mirror_matches_oracle(pins):
         for a, b in zip(got[k], exp[k]):
             assert (math.isnan(a) and math.isnan(b)) or a == b
     assert ev.Inc(0, 0) == exp[0][cells.index((0, 0))] and ev.ReadLength() == len(seq)
+
+
+def test_quiver_alignment_leaves_the_bands_intact():
+    """RecursorBase::Alignment is a read-only walk of the alpha band: asking twice gives the same alignment, and
+    the scores after it are unchanged (the move count once landed in the bands' column-offset array)."""
+    k = KATS["kats"][0]
+    g = GpuQuiver(k["tpl"], KATS["params"], moves=k["moves"], score_diff=k["score_diff"],
+                  fast_threshold=k["fast_threshold"])
+    g.add_read(k["reads"][0]["seq"], 0, 0, len(k["tpl"]))
+    first = g.alignment(0)
+    assert first == ("GATG", "GATG")
+    assert g.alignment(0) == first and g.alignment(0) == first
+    tpl, reads = _zmw(131, 120, 4)
+    g, o = _pair(tpl, reads, False)
+    muts = O.unique_mutations(tpl)[:200]
+    before = g.s.ScoreMany([g.P.Mutation(t, s, b) for (t, s, b) in muts])
+    for r in range(g.s.NumReads()):
+        if g.s.ReadInfo(r)["active"]:
+            assert g.alignment(r) == g.alignment(r) == o.alignment(r)
+    assert g.s.ScoreMany([g.P.Mutation(t, s, b) for (t, s, b) in muts]) == before
