@@ -841,6 +841,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     static const bool pathTrace2 = pathTrace && std::getenv("PBCCS_FILL_PATHS")[0] == '2';
     // PBCCS_FILL_WORK=1: where the fills' computed cells go (CoopFill::work; counters().fillWork)
     static const bool fillWork = std::getenv("PBCCS_FILL_WORK") != nullptr;
+    // PBCCS_FILL_QUEUE=0: the 16-lane fill's groups keep their static reads (A/B)
+    static const bool fillQueue = env_int("PBCCS_FILL_QUEUE", 1) != 0;
     for (int attempt = 0;; ++attempt) {
         // route reads whose buffers do not fit this path's LDS budget to the next path
         for (int p = 0; p < kPaths; ++p) {
@@ -981,6 +983,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             }
             const int* lp = dList_.ptr + off;
             const hipStream_t st = p <= 1 ? stream_ : stream2_;
+            if (p == 1 && fillQueue) {   // the 16-lane groups take their reads from a counter (k_fill_coop)
+                ws_->fillQueue.reserve(1, false);
+                PBCCS_HIP(hipMemsetAsync(ws_->fillQueue.ptr, 0, sizeof(unsigned), st));
+                F.queue = ws_->fillQueue.ptr;
+            }
             if (fillWork) {
                 if (!dFillWork_.ptr) {
                     dFillWork_.reserve(16, false);

@@ -212,6 +212,7 @@ struct Workspace {
     DevVec<int> wZmw, wNMut;
     DevVec<long long> wMutBase, wDeltaBase, wWaveStart, wMutStart, wPosStart, wPosBase, wQvBase;
     DevVec<unsigned long long> stats;
+    DevVec<unsigned> fillQueue;   // the 16-lane fill's dynamic task counter (CoopFill::queue)
     // per-read compact bands (what scoring reads)
     DevVec<int2> aRange, bRange;
     DevVec<int> aOff, bOff;

@@ -782,17 +782,12 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 // LDS per group: 2 column buffers (hcap doubles each), the ZMW's transition table, nibble-packed read
 // and template window.
 // ------------------------------------------------------------------------------------------------
-template <int G, int MINW, bool GC, int R>
-__global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
+// One listed read's FillAlphaBeta by the G-lane group whose LDS slot starts at gbase (task t of the launch).
+template <int G, bool GC, int R>
+__device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, const int* __restrict__ reads, int n,
+                                          int t, unsigned char* gbase)
 {
-    extern __shared__ __align__(16) unsigned char smem[];
-    // tall reads are the latency-critical path of every refine round: issue ahead of the 16-lane fills
-    // and score waves that share the SIMD (F.prio = 0 leaves the default priority)
-    if (F.prio) __builtin_amdgcn_s_setprio(3);
-    const int grp = threadIdx.x / G;
-    const int t = blockIdx.x * (64 / G) + grp;
     const int lane = threadIdx.x & (G - 1);
-    unsigned char* gbase = smem + (size_t)grp * F.groupBytes;
     // LDS: two column buffers of hcap rows, ctx, read, template.  GC (hybrid): rows past hcap go to this
     // slot's part of F.colScratch (2 x gRows doubles)
     double* col = reinterpret_cast<double*>(gbase);
@@ -840,7 +835,10 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
             }
         }
     }
-    __syncthreads();
+    // the group's own LDS slot: its lanes' stores above complete before their loads below (one wavefront; the
+    // fence keeps the compiler from moving loads above them).  No block barrier: with the dynamic queue the other
+    // groups of the wavefront are at other points of their own reads
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     if (!valid) return;
     if (bad) {
         if (lane == 0) B.rStatus[r] = (I < 1 || J < 1) ? kFillBadInput : kFillOverflow;
@@ -849,7 +847,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
 
     Task<G> T;
     T.g.lane = lane;
-    T.g.base = threadIdx.x & ~(G - 1);
+    T.g.base = (int)threadIdx.x & ~(G - 1);
     T.I = I;
     T.J = J;
     T.L = tv.L;
@@ -1024,6 +1022,40 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
             }
         }
     }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// k_fill_coop: one G-lane group per read; 64 / G groups per 64-thread block (one wavefront).
+// LDS per group: 2 column buffers (hcap doubles each), the ZMW's transition table, nibble-packed read
+// and template window.
+// Static assignment: group g of block b fills task 4b + g (G = 16) / task b (G = 64).  Dynamic (F.queue, the
+// 16-lane path): a group that finishes its read takes the launch's next task from a counter, so the four groups
+// of a wavefront stay busy until the list runs out instead of idling in lock-step behind their slowest read (the
+// wavefront's chunk issues were 36% idle group slots, profiles/r5c_fill_work_bench.json).
+// ------------------------------------------------------------------------------------------------
+template <int G, int MINW, bool GC, int R>
+__global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    // tall reads are the latency-critical path of every refine round: issue ahead of the 16-lane fills
+    // and score waves that share the SIMD (F.prio = 0 leaves the default priority)
+    if (F.prio) __builtin_amdgcn_s_setprio(3);
+    const int grp = threadIdx.x / G;
+    unsigned char* gbase = smem + (size_t)grp * F.groupBytes;
+    if (G < 64 && F.queue) {
+        const int lane = threadIdx.x & (G - 1);
+        const int base = (int)threadIdx.x & ~(G - 1);
+        for (;;) {
+            int t = 0;
+            if (lane == 0) t = (int)atomicAdd(F.queue, 1u);
+            t = __shfl(t, base, 64);
+            if (t >= n) break;
+            fill_read<G, GC, R>(B, F, reads, n, t, gbase);
+        }
+        return;
+    }
+    fill_read<G, GC, R>(B, F, reads, n, blockIdx.x * (64 / G) + grp, gbase);
 }
 
 size_t coop_group_bytes(int hcap, int readWords, int tplWords)

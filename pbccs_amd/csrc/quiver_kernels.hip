@@ -67,7 +67,7 @@ __device__ __forceinline__ long long col_base(const QEval& e, int j, int beginRo
 {
     return e.p->dense ? (long long)j * (e.I() + 1) + beginRow : used;
 }
-// values an arena must hold for one pass
+// values an arena must hold for one pass of `used` entries
 __device__ __forceinline__ long long values_needed(const QEval& e, long long used)
 {
     return e.p->dense ? (long long)(e.J() + 1) * (e.I() + 1) : used;
@@ -153,7 +153,7 @@ __device__ __forceinline__ long long fill_alpha(const QEval& e, const QBand* gui
         for (i = beginRow; i < endRow && out.Get(i, j) < thr; ++i) {}
         hb = i;
     }
-    return values_needed(e, used);
+    return used;   // UsedEntries (the reband test); the arena needs values_needed(e, used)
 }
 
 // ---- SseRecursor::FillBeta (SseRecursor.cpp:216-353) -----------------------------------------------------
@@ -243,7 +243,7 @@ __device__ __forceinline__ long long fill_beta(const QEval& e, const QBand* guid
         for (i = endRow; i > beginRow && out.Get(i - 1, j) < thr; i--) {}
         he = i;
     }
-    return values_needed(e, used);
+    return used;   // UsedEntries; the arena needs values_needed(e, used)
 }
 
 // ---- SseRecursor::ExtendAlpha (SseRecursor.cpp:433-551) --------------------------------------------------
@@ -1661,9 +1661,10 @@ __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ 
     auto passA = [&](bool guided) {
         const int nxt = aPassed ? (curA ^ 1) : 0;
         const QBand g = arena(v, curB), self = arena(v, curA), out = arena(v, nxt);
+        // u: UsedEntries (RecursorBase's reband test); a dense arena holds every cell (values_needed)
         const long long u = fill_alpha(e, guided ? &g : nullptr, aPassed ? &self : nullptr, out, v.allocA, aPassed, ovf);
         if (!ovf) { stCells += u; stCols += J + 1; }
-        needA = max(needA, u);
+        needA = max(needA, values_needed(e, u));
         curA = nxt;
         aPassed = true;
         return u;
@@ -1673,7 +1674,7 @@ __global__ void __launch_bounds__(64) k_qfill(QBatch B, const int* __restrict__ 
         const QBand g = arena(v, curA), self = arena(v, curB), out = arena(v, nxt);
         const long long u = fill_beta(e, &g, bPassed ? &self : nullptr, out, v.colbuf, v.allocB, bPassed, ovf);
         if (!ovf) { stCells += u; stCols += J + 1; }
-        needB = max(needB, u);
+        needB = max(needB, values_needed(e, u));
         curB = nxt;
         bPassed = true;
         return u;
