@@ -823,12 +823,13 @@ int pbccs_engine_reserve_pool(pbccs_engine* eng, size_t bytes_per_slot)
 }
 
 // ---- ZMW work queue ------------------------------------------------------------------------------
-// Estimated FP64 band footprint of one ZMW at its high-water mark.  Per read: two band regions of ~32 rows
-// x window plus column metadata and score deltas (the typical band), plus the expected share of reads
-// whose first band explodes (the tall-band paths hold ~1-22% of the (I+1)(J+1) matrix).  Fitted to the
-// measured pools with exact band regrow (fill_coop.hip regrow_bands): 13.4 MB per 2 kb / 10-pass ZMW
-// (estimate 14.8 MB, profiles/r2h6_regrow_slots), ~0.75 GB per 10 kb / 8-pass ZMW (estimate 0.73 GB,
-// profiles/r2h7_regrow_ab).
+// Estimated FP64 band footprint of one ZMW at its high-water mark (zmw_est_bytes below).  Per read: two band
+// regions of ~32 rows x window plus column metadata (the typical band), plus the expected share of bands that
+// explode on the reband, whose fraction of the (I+1)(J+1) matrix grows with the window (oracle band statistics,
+// DESIGN.md §6).  Checks: 2 kb / 10 passes ~19 MB (measured 13.5 MB, profiles/r2h6_regrow_slots), 10 kb / 8 passes
+// ~150 MB with checkpointed bands (measured 142 MB: 68 GB for 480 ZMWs, profiles/r3b_bench_10kb_ckpt8.json),
+// 20 kb ~120 MB per read (the round-4 estimate, 63 MB, let 8 slots run the device out of memory 27 times on the
+// configs[3] mix).
 // Band-pool bytes the workspace slots hold mapped.
 static size_t slot_pool_bytes(pbccs_engine* eng)
 {
@@ -845,10 +846,19 @@ static double zmw_est_bytes(const pbccs_zmw_input& z)
     for (int k = 0; k < z.n_reads; ++k) {
         const double J = std::max(1, z.tends ? z.tends[k] - (z.tstarts ? z.tstarts[k] : 0) : z.draft_len);
         const double I = z.lens ? std::max(0, z.lens[k]) : J;
+        const double cells = (I + 1) * (J + 1);
+        // the typical band: the first regions ((J + 66) x 16 values per matrix) and the column metadata
         const double typical = J * 0.5 * (2 * 32 * 8 * 1.25 + 80 + 8 * 8);
-        double tall = std::min(0.15 * 8.0 * (I + 1) * (J + 1), 8.7e7 * std::pow(J / 1e4, 3.0));
+        // bands that explode on the 4%-of-matrix reband: the oracle's AddRead stores, per matrix, a mean fraction
+        // of the (I+1)(J+1) matrix over all reads that grows with the window -- 0.023 / 0.044 / 0.074 / 0.098 at
+        // 5 / 10 / 15 / 20 kb (6 reads each; 1 / 2 / 4 / 4 of them exploded to 0.05-0.21) -- held in exact regions
+        // (+1/16 slack, regrow_bands), plus the tall reads' abandoned first regions (4% of the matrix, pt of the
+        // reads: ~1 in 10 at 2 kb, 2 in 3 at 15-20 kb)
+        const double frac = std::min(0.12, 0.005 * J / 1000.0);
+        const double pt = std::min(0.7, 0.08 + J / 30000.0);
+        double tall = 2.0 * 8.0 * frac * cells * (1.0 + 1.0 / 16) + pt * 2.0 * 8.0 * cells / 25.0;
         // checkpointed tall bands: every K-th column plus the kept tails of both matrices
-        if (K > 0 && J >= minLen) tall = tall / K + 2.0 * 8.0 * (kCkptTail + 1) * (I + 1);
+        if (K > 0 && J >= minLen) tall = tall / K + pt * 2.0 * 8.0 * (kCkptTail + 1) * (I + 1);
         b += typical + tall;
     }
     return std::max(b, 4096.0);

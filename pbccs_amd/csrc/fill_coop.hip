@@ -1044,14 +1044,25 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     const int grp = threadIdx.x / G;
     unsigned char* gbase = smem + (size_t)grp * F.groupBytes;
     if (G < 64 && F.queue) {
+        // a wave-uniform loop (it runs while some group of the wavefront holds a task); a group whose read is done
+        // takes the next one.  (The first form -- a per-group loop with the exit inside -- was miscompiled into an
+        // inner loop that re-ran task 0 without taking the next: it hung.)
         const int lane = threadIdx.x & (G - 1);
         const int base = (int)threadIdx.x & ~(G - 1);
+        bool need = true;
+        int t = n;
         for (;;) {
-            int t = 0;
-            if (lane == 0) t = (int)atomicAdd(F.queue, 1u);
-            t = __shfl(t, base, 64);
-            if (t >= n) break;
-            fill_read<G, GC, R>(B, F, reads, n, t, gbase);
+            if (need) {
+                int v = 0;
+                if (lane == 0) v = (int)atomicAdd(F.queue, 1u);
+                t = __shfl(v, base, 64);
+                need = false;
+            }
+            if (__ballot(t < n) == 0) break;
+            if (t < n) {
+                fill_read<G, GC, R>(B, F, reads, n, t, gbase);
+                need = true;
+            }
         }
         return;
     }

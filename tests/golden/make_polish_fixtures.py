@@ -7,8 +7,11 @@ holds only the input digest and the oracle's outputs:
   oracle/arrow_oracle.cpp (AddRead, RefineConsensus, ConsensusQVs).
   tests/golden/polish_mixed_long.json -- mixed_long_zmws() (configs[3] shape: a 15.2 kb insert with 21
   passes beside a 0.7 kb / 3-pass and a 4.8 kb / 14-pass ZMW at random SNRs), the same records.
+  tests/golden/polish_20kb.json -- long20_zmws(): configs[3]'s top length, a 20 kb insert with 24 passes (the
+  widest bands of the mix, SimpleRecursor.cpp:642-691's reband at its largest), the same records.
 
-Usage: make_polish_fixtures.py [10kb|mixed_long]  (default: both; the 15 kb ZMW takes ~10 CPU-minutes)
+Usage: make_polish_fixtures.py [10kb|mixed_long|20kb]  (default: all; the 15 kb ZMW takes ~10 CPU-minutes, the
+20 kb one ~30)
 
 The oracle is test infrastructure (CPU restatement of the reference path, oracle/ header); the GPU test
 compares the engine's batch polish against these records.
@@ -46,6 +49,12 @@ def mixed_long_zmws():
             synth.make_zmw(rng, 4800, 14, tuple(float(x) for x in rng.uniform(6.0, 14.0, size=4)))]
 
 
+def long20_zmws():
+    """configs[3]'s upper end: one 20 kb ZMW with 24 passes at configs[1]'s SNR."""
+    rng = np.random.Generator(np.random.PCG64(2020))
+    return [synth.make_zmw(rng, 20000, 24)]
+
+
 def record(z):
     e = O.polish_zmw(z["draft"], z["reads"], z["snr"])
     return {
@@ -69,11 +78,13 @@ def write(name, inputs, zs):
 
 
 def main():
-    which = sys.argv[1:] or ["10kb", "mixed_long"]
+    which = sys.argv[1:] or ["10kb", "mixed_long", "20kb"]
     if "10kb" in which:
         write("polish_10kb.json", "synth.make_zmws(2, 10000, 8, seed=82)", synth.make_zmws(2, 10000, 8, seed=82))
     if "mixed_long" in which:
         write("polish_mixed_long.json", "make_polish_fixtures.mixed_long_zmws()", mixed_long_zmws())
+    if "20kb" in which:
+        write("polish_20kb.json", "make_polish_fixtures.long20_zmws()", long20_zmws())
 
 
 if __name__ == "__main__":

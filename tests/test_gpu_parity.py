@@ -426,3 +426,27 @@ def test_polish_mixed_long_matches_fixture(P):
             got = [min(max(q, 0), 93) for q in r["qvs"]]
             exp = [ord(c) - 33 for c in e["qvs"]]
             assert len(got) == len(exp) and max(abs(a - b) for a, b in zip(got, exp)) <= 1
+
+
+def test_polish_20kb_matches_fixture(P):
+    """configs[3]'s top length: a 20 kb insert with 24 passes -- the widest bands of the mixed workload, where
+    the 4%-of-matrix reband (SimpleRecursor.cpp:642-691) explodes furthest and the bands are checkpointed --
+    through the work queue against the oracle's committed record (tests/golden/make_polish_fixtures.py 20kb,
+    ~30 CPU-minutes); the input is regenerated and checked by digest."""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_polish_fixtures import digest, long20_zmws
+    fx = json.load(open(os.path.join(GOLD, "polish_20kb.json")))
+    zs = long20_zmws()
+    assert len(zs[0]["draft"]) >= 19000 and len(zs[0]["reads"]) >= 24
+    res = P.polish_stream(zs)
+    for z, r, e in zip(zs, res, fx["zmws"]):
+        assert digest(z) == e["digest"]
+        assert r["add_read_results"] == e["add_read_results"]
+        assert sum(1 for s in e["add_read_results"] if s == 0) >= 3   # a polished ZMW, not a gated one
+        assert (r["n_tested"], r["n_applied"]) == (e["n_tested"], e["n_applied"])
+        assert e["converged"] and r["status"] in ("Success", "PoorQuality")
+        assert r["consensus"] == e["consensus"]
+        got = [min(max(q, 0), 93) for q in r["qvs"]]
+        exp = [ord(c) - 33 for c in e["qvs"]]
+        assert len(got) == len(exp) and max(abs(a - b) for a, b in zip(got, exp)) <= 1

@@ -25,8 +25,8 @@ step() {
   case $s in
     ubench)   # chain-step variants (tools/ubench/chain_step.hip, built in-tree beforehand)
       timeout -k 10 120 tools/ubench/chain_step > $OUT/ubench.txt 2>&1 && cat $OUT/ubench.txt ;;
-    tests)
-      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    tests)    # -v -u: each test's name reaches the log as it starts, so a hang names its test
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread \
         > $OUT/pytest_gpu.log 2>&1; local rc=$?; tail -3 $OUT/pytest_gpu.log; return $rc ;;
     smoke)
       timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && tail -1 $OUT/smoke.log ;;
@@ -85,7 +85,7 @@ step() {
         echo "tall=$v $(summ $OUT/ab_tall_$k.json)"
       done ;;
     tests_sel)    # the GPU tests of the files in TESTS only
-      timeout -k 10 600 python3 -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread \
+      timeout -k 10 600 python3 -u -m pytest $TESTS -m gpu -x -v --timeout 150 --timeout-method thread \
         > $OUT/pytest_sel.log 2>&1; local rc=$?; tail -3 $OUT/pytest_sel.log; return $rc ;;
     tests_fill)   # the fill / checkpoint parity tests only
       timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_ckpt_gpu.py -m gpu -x -q --timeout 300 \
