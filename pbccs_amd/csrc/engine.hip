@@ -251,6 +251,7 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared)
     stream2_ = ws_->stream2;
     evFork_ = ws_->evFork;
     evJoin_ = ws_->evJoin;
+    const StreamScope bound(stream_);   // stream-ordered DevVec growth for this batch's calls (engine.hpp)
     dScratch_.reserve(kInitialScratch, false);
     dScratchTop_.reserve(1, false);
     // the read pool starts with 16 bytes of padding (see UploadDescriptors: word loads of read bases)
@@ -277,6 +278,7 @@ ArrowBatch::~ArrowBatch()
 // ------------------------------------------------------------------------------------------------
 void ArrowBatch::SetProfiling(bool on)
 {
+    const StreamScope bound(stream_);
     profiling_ = on;
     if (on) {
         dStats_.reserve(16, false);
@@ -327,6 +329,7 @@ void ArrowBatch::ResolveEvents()
 
 const Counters& ArrowBatch::counters()
 {
+    const StreamScope bound(stream_);
     if (dFillWork_.ptr) {   // PBCCS_FILL_WORK diagnostics: fold the device counters in and clear them
         unsigned long long h[16];
         PBCCS_HIP(hipMemcpyAsync(h, dFillWork_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
@@ -347,6 +350,7 @@ const Counters& ArrowBatch::counters()
 
 void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
 {
+    const StreamScope bound(stream_);
     ResolveEvents();
     if (profiling_) {
         unsigned long long h[16];
@@ -373,6 +377,7 @@ void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
 
 void ArrowBatch::Prepare()
 {
+    const StreamScope bound(stream_);
     // the workspace may hold another (finished) batch's bands: size it without preserving them
     const size_t cols = std::max<long long>(colTop_, 1);
     dARange_.reserve(cols, false);
@@ -599,6 +604,7 @@ void ArrowBatch::UploadReads()
 
 void ArrowBatch::UploadDescriptors()
 {
+    const StreamScope bound(stream_);
     DeriveZmws();
     if (!descDirty_) return;
     const int Z = (int)zmws_.size(), R = (int)reads_.size();
@@ -760,6 +766,7 @@ DevBatch ArrowBatch::View() const
 // the kernel reported.  Bands land directly in the compact layout; k_suffix adds the log-scale sums.
 void ArrowBatch::FillReads(const std::vector<int>& readsIn)
 {
+    const StreamScope bound(stream_);
     // Cooperative paths (fill_coop.hip): 1: 16 lanes / 64 rows; 2: 64 lanes / 1024 rows, LDS only; 3: 64 lanes,
     // as many rows as LDS holds and the rest of a column in global memory (the hybrid path: never too tall, so a
     // fill re-routes a read at most twice).  Reads whose bases do not fit LDS beside 64 rows go to the
@@ -841,8 +848,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     static const bool pathTrace2 = pathTrace && std::getenv("PBCCS_FILL_PATHS")[0] == '2';
     // PBCCS_FILL_WORK=1: where the fills' computed cells go (CoopFill::work; counters().fillWork)
     static const bool fillWork = std::getenv("PBCCS_FILL_WORK") != nullptr;
-    // PBCCS_FILL_QUEUE=0: the 16-lane fill's groups keep their static reads (A/B)
-    static const bool fillQueue = env_int("PBCCS_FILL_QUEUE", 1) != 0;
+    // PBCCS_FILL_QUEUE=1: the 16-lane fill's groups take reads from a per-launch counter (measured no faster: opt-in)
+    static const bool fillQueue = env_int("PBCCS_FILL_QUEUE", 0) != 0;
     for (int attempt = 0;; ++attempt) {
         // route reads whose buffers do not fit this path's LDS budget to the next path
         for (int p = 0; p < kPaths; ++p) {
@@ -1119,6 +1126,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
 
 void ArrowBatch::FillReadsSerial(const std::vector<int>& readsIn)
 {
+    const StreamScope bound(stream_);
     std::vector<int> todo(readsIn);
     for (int r : todo)   // the lane-serial fill keeps full bands
         if (reads_[r].ckpt != 0) {
@@ -1321,6 +1329,7 @@ void ArrowBatch::ZScores(int zi, double* zg, double* za, std::vector<double>* zs
 void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vector<int>>* codes, double fastThr,
                           bool needPositions, bool phased)
 {
+    const StreamScope bound(stream_);
     UploadDescriptors();
     const int n = (int)zl.size();
     rNMut_.assign(n, 0);
@@ -1571,6 +1580,7 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
 void ArrowBatch::ScoreLists(const std::vector<int>& zl, const std::vector<std::vector<int>>& codes, double fastThr,
                             std::vector<std::vector<double>>* scores, std::vector<std::vector<double>>* perRead)
 {
+    const StreamScope bound(stream_);
     RunRound(zl, &codes, fastThr, false);
     std::vector<double> s, d;
     download(s, dScore_, rTotalMut_, stream_);
@@ -1601,6 +1611,7 @@ static bool apply_host(std::string* tpl, const std::vector<Mutation>& muts, std:
 
 bool ArrowBatch::ApplyMutations(int zi, const std::vector<Mutation>& muts)
 {
+    const StreamScope bound(stream_);
     HZmw& z = zmws_[zi];
     std::vector<int> mtp;
     if (!apply_host(&z.tpl, muts, &mtp)) return false;
@@ -1656,6 +1667,7 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
                         std::vector<long long>* nTested, std::vector<long long>* nApplied, bool needFinalState,
                         std::vector<std::vector<int>>* qvsOnConverge)
 {
+    const StreamScope bound(stream_);
     const int n = (int)zl.size();
     converged->assign(n, 0);
     if (qvsOnConverge) qvsOnConverge->assign(n, {});
@@ -1994,6 +2006,7 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
 // ------------------------------------------------------------------------------------------------
 void ArrowBatch::QVs(const std::vector<int>& zl, std::vector<std::vector<int>>* qvs)
 {
+    const StreamScope bound(stream_);
     RunRound(zl, nullptr, -std::numeric_limits<double>::max(), true);
     std::vector<long long> qvBase(zl.size());
     for (size_t k = 0; k < zl.size(); ++k) qvBase[k] = rPosStart_[k];

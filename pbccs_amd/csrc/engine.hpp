@@ -52,7 +52,27 @@ public:
     explicit DeviceOom(std::string what) : DeviceError(std::move(what)) {}
 };
 
-// Device buffer with geometric growth (contents optionally preserved).
+// The stream a growing DevVec orders its copy after: the batch doing device work on this thread sets it
+// (ArrowBatch::Bind).  With none set, growth synchronises the whole device (the old, conservative behaviour).
+inline hipStream_t& devvec_stream()
+{
+    static thread_local hipStream_t s = nullptr;
+    return s;
+}
+// Binds a stream for the scope (restoring the previous binding on exit, so nested calls and other engines'
+// buffers on the same thread keep their own ordering).
+struct StreamScope {
+    hipStream_t prev;
+    explicit StreamScope(hipStream_t s) : prev(devvec_stream()) { devvec_stream() = s; }
+    ~StreamScope() { devvec_stream() = prev; }
+    StreamScope(const StreamScope&) = delete;
+    StreamScope& operator=(const StreamScope&) = delete;
+};
+
+// Device buffer with geometric growth (contents optionally preserved).  With a stream bound (devvec_stream) the
+// growth is stream-ordered: the copy of the old contents is queued on that stream, and the old buffer -- which
+// work still queued may read -- is kept until release() instead of freed at once.  Nothing synchronises the
+// device: a hipDeviceSynchronize + hipFree per growth stalled every other workspace slot's work.
 template <class T>
 struct DevVec {
     T* ptr = nullptr;
@@ -69,14 +89,22 @@ struct DevVec {
             throw DeviceOom("hipMalloc failed (device memory): " + std::to_string(nc * sizeof(T) >> 20) +
                               " MB requested, " + std::to_string(fr >> 20) + " MB free");
         }
-        if (keep && ptr && cap) {
-            if (hipDeviceSynchronize() != hipSuccess ||
-                hipMemcpy(p, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice) != hipSuccess)
+        const hipStream_t st = devvec_stream();
+        if (st) {
+            if (keep && ptr && cap &&
+                hipMemcpyAsync(p, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice, st) != hipSuccess)
                 throw DeviceError("device copy failed");
-        }
-        if (ptr) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(ptr);
+            if (ptr) retired_.push_back(ptr);
+        } else {
+            if (keep && ptr && cap) {
+                if (hipDeviceSynchronize() != hipSuccess ||
+                    hipMemcpy(p, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice) != hipSuccess)
+                    throw DeviceError("device copy failed");
+            }
+            if (ptr) {
+                (void)hipDeviceSynchronize();
+                (void)hipFree(ptr);
+            }
         }
         ptr = p;
         cap = nc;
@@ -84,6 +112,8 @@ struct DevVec {
     void release()
     {
         if (ptr) (void)hipFree(ptr);
+        for (T* q : retired_) (void)hipFree(q);
+        retired_.clear();
         ptr = nullptr;
         cap = 0;
     }
@@ -91,6 +121,9 @@ struct DevVec {
     DevVec(const DevVec&) = delete;
     DevVec& operator=(const DevVec&) = delete;
     ~DevVec() { release(); }
+
+private:
+    std::vector<T*> retired_;   // outgrown buffers of stream-ordered growth (freed by release)
 };
 
 // Page-locked host staging (grow-only): copies from it go to the DMA engines asynchronously, where a copy from
