@@ -6,7 +6,10 @@ fails (HSA_STATUS_ERROR_OUT_OF_RESOURCES aborted a 12-slot run in round 1, profi
 Reads the `-Rpass-analysis=kernel-resource-usage` remarks hipcc wrote for each object (*.res) and exits 1
 naming every offending kernel.
 Usage: check_resources.py FILE.res...
+A/B builds only (tools/build_ab.sh): PBCCS_ALLOW_SCRATCH=<substring> exempts the kernels whose mangled name
+contains it (reported, not failed), so a spilling variant can be measured before the rule is revisited.
 """
+import os
 import re
 import sys
 
@@ -14,6 +17,7 @@ import sys
 def main(paths):
     bad = []
     kernels = 0
+    allow = os.environ.get("PBCCS_ALLOW_SCRATCH", "")
     for p in paths:
         name = None
         for line in open(p, errors="replace"):
@@ -28,6 +32,11 @@ def main(paths):
             m = re.search(r"VGPRs Spill: (\d+)", line)
             if m and int(m.group(1)) > 0:
                 bad.append(f"{p}: {name}: {m.group(1)} VGPRs spilled")
+    if allow:
+        exempt = [b for b in bad if allow in b]
+        for b in exempt:
+            print(f"kernel resource check: exempted (PBCCS_ALLOW_SCRATCH) {b}")
+        bad = [b for b in bad if allow not in b]
     if bad:
         print("kernel resource check failed:\n  " + "\n  ".join(bad), file=sys.stderr)
         return 1

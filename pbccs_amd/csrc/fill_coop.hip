@@ -66,10 +66,16 @@ struct Task {
     // buffer b (0 / 1), row k (no runtime-indexed pointer arrays: they would live in scratch).  The hybrid
     // path selects an LDS or global address per lane and accesses it through one generic (flat) pointer.
     // (buffer 1 follows buffer 0 in both places: offsets, not a selected pointer member, keep T in registers)
+    // R = 2 (split): the LDS rows of a buffer are two planes, even rows then odd rows (row k at (k & 1) hcap / 2 +
+    // k / 2).  A lane's rows are k0 + 2 lane + r with k0 + r of one parity across the group, so every LDS access
+    // of the group lands in one plane at consecutive doubles -- no bank conflicts (a 16-byte lane stride into one
+    // linear buffer put two lanes on each bank: 27% of the tall fill's LDS cycles, profiles/r4h2_pmc_summary.txt).
+    bool split;
+    __device__ __forceinline__ int lrow(int k) const { return split ? (k & 1) * (hcap >> 1) + (k >> 1) : k; }
     __device__ __forceinline__ double* cptr(int b, int k) const
     {
-        if (!gcol) return lds0 + (b ? hcap : 0) + k;
-        return k < hcap ? lds0 + (b ? hcap : 0) + k : glob0 + (b ? glob1 - glob0 : 0) + (k - hcap);
+        if (!gcol) return lds0 + (b ? hcap : 0) + lrow(k);
+        return k < hcap ? lds0 + (b ? hcap : 0) + lrow(k) : glob0 + (b ? glob1 - glob0 : 0) + (k - hcap);
     }
     __device__ __forceinline__ double cget(int b, int k) const { return *cptr(b, k); }
     __device__ __forceinline__ void cset(int b, int k, double v) const { *cptr(b, k) = v; }
@@ -860,6 +866,7 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
     T.glob0 = GC ? F.colScratch + (size_t)t * 2 * F.gRows : nullptr;
     T.glob1 = GC ? T.glob0 + F.gRows : nullptr;
     T.hcap = F.hcap;
+    T.split = R == 2;   // launch_fill_coop checks that hcap holds whole chunks (even)
     T.rowsCap = GC ? F.hcap + F.gRows : F.hcap;
     T.gcol = GC;
     T.chainExit = F.chainExit;
@@ -1111,8 +1118,8 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     for (Entry& x : ks)
         if (x.g == G && x.r == R && x.gc == gc) e = &x;
     if (!e) throw std::runtime_error("no fill kernel for this group size / rows per lane / column buffer");
-    if (R > 1 && (gc ? (F.hcap + F.gRows) : F.hcap) % (G * R) != 0)
-        throw std::runtime_error("fill column buffers must hold whole chunks of G x rows rows");
+    if (R > 1 && ((gc ? (F.hcap + F.gRows) : F.hcap) % (G * R) != 0 || F.hcap % 2 != 0))
+        throw std::runtime_error("fill column buffers must hold whole chunks of G x rows rows (and even LDS rows)");
     if (!e->attr) {   // dynamic LDS beyond 64 KB must be enabled per kernel
         (void)hipFuncSetAttribute((const void*)e->k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         e->attr = true;
