@@ -91,6 +91,10 @@ void VmPool::reserve(size_t n, bool keep)
         vmm_ = hipMemAddressReserve(&va, kVaBytes, 0, nullptr, 0) == hipSuccess && va != nullptr;
         if (vmm_) ptr = static_cast<double*>(va);
         else (void)hipGetLastError();
+        if (oldVa_) {   // the reservation unmap_all left: the new one is taken, so it cannot come back as this one
+            (void)hipMemAddressFree(oldVa_, kVaBytes);
+            oldVa_ = nullptr;
+        }
     }
     if (!vmm_) {
         fallback_.reserve(n, keep);
@@ -182,10 +186,19 @@ void VmPool::unmap_all()
     sizes_.clear();
     mappedBytes_ = 0;
     cap = 0;
+    // The next mapping takes a fresh address range: mapping new granules at the addresses just unmapped gave
+    // wrong POA drafts (a POA pool released and mapped again between calls, every kernel serialised -- not a
+    // race; a fresh range fixed it, tools/ccs_draft_dbg.py).  This range is freed once the next
+    // one is reserved, so the two differ.
+    oldVa_ = ptr;
+    ptr = nullptr;
+    tried_ = false;
+    vmm_ = false;
 }
 
 VmPool::~VmPool()
 {
+    if (oldVa_) (void)hipMemAddressFree(oldVa_, kVaBytes);
     if (!vmm_) return;
     (void)hipDeviceSynchronize();
     size_t off = 0;

@@ -165,7 +165,8 @@ struct VmPool {
     // Best effort: map granules towards n doubles until the device runs out of memory (no throw).
     // Only meaningful on the VMM path (the hipMalloc fallback would have to copy): there it is a no-op.
     void try_reserve(size_t n);
-    // Unmap every granule (the address reservation stays); the next reserve maps afresh.  Synchronises.
+    // Unmap every granule; the next reserve maps afresh at a new address range (never at the addresses just
+    // unmapped, see unmap_all).  Synchronises.
     void unmap_all();
     size_t mapped_bytes() const { return vmm_ ? mappedBytes_ : cap * sizeof(double); }
     ~VmPool();
@@ -177,6 +178,7 @@ private:
     static constexpr size_t kVaBytes = 1ull << 39;      // 512 GB of address space
     static constexpr size_t kChunkBytes = 1ull << 30;   // mapping granule
     bool tried_ = false, vmm_ = false;
+    void* oldVa_ = nullptr;   // an unmapped reservation, freed once the next one is taken (unmap_all)
     size_t mappedBytes_ = 0;
     std::vector<hipMemGenericAllocationHandle_t> handles_;
     std::vector<size_t> sizes_;

@@ -156,28 +156,30 @@ def test_poa_wide_scores_long_reads(P):
             O.poa_consensus(reads, mode, 2, graphviz_flags=3)
 
 
+class _OraclePoa:
+    """The oracle's SparsePoa behind driver.zmw_input's POA interface (reads added one at a time)."""
+    def __init__(self):
+        self.reads = []
+
+    def orient_and_add_read(self, seq):
+        self.reads.append(seq)
+        return O.sparse_poa(self.reads)["keys"][-1]
+
+    def find_consensus(self, min_cov):
+        r = O.sparse_poa(self.reads, min_cov)
+        return r["consensus"], dict(enumerate(r["summaries"]))
+
+
 def test_driver_zmw_input_with_gpu_poa(P):
     """driver.zmw_input (FilterReads -> POA -> ExtractMappedRead) with the GPU SparsePoa equals the same
     driver with the oracle's POA."""
     poa, eng = P
     from pbccs_amd import driver
 
-    class OraclePoa:
-        def __init__(self):
-            self.reads = []
-
-        def orient_and_add_read(self, seq):
-            self.reads.append(seq)
-            return O.sparse_poa(self.reads)["keys"][-1]
-
-        def find_consensus(self, min_cov):
-            r = O.sparse_poa(self.reads, min_cov)
-            return r["consensus"], dict(enumerate(r["summaries"]))
-
     for reads in _synthetic_subreads(3, (400, 900), (5, 9), seed=33):
         chunk = {"snr": [10.0, 7.0, 5.0, 11.0], "reads": [{"seq": s} for s in reads]}
         st_g, z_g = driver.zmw_input(chunk, poa.SparsePoa(eng))
-        st_o, z_o = driver.zmw_input(chunk, OraclePoa())
+        st_o, z_o = driver.zmw_input(chunk, _OraclePoa())
         assert st_g == st_o and z_g == z_o
 
 
@@ -187,35 +189,18 @@ def test_driver_batch_matches_per_zmw_driver(P):
     poa, eng = P
     from pbccs_amd import driver
 
-    class OraclePoa:
-        def __init__(self):
-            self.reads = []
-
-        def orient_and_add_read(self, seq):
-            self.reads.append(seq)
-            return O.sparse_poa(self.reads)["keys"][-1]
-
-        def find_consensus(self, min_cov):
-            r = O.sparse_poa(self.reads, min_cov)
-            return r["consensus"], dict(enumerate(r["summaries"]))
-
     chunks = [{"snr": [10.0, 7.0, 5.0, 11.0], "reads": [{"seq": s} for s in reads]}
               for reads in _synthetic_subreads(5, (300, 700), (3, 8), seed=44)]
     chunks.append({"snr": [8.0, 8.0, 8.0, 8.0], "reads": [{"seq": "ACGT"}]})   # median below min_length
     for cov in (None, 3):
         got = driver.zmw_inputs_batch(chunks, max_poa_coverage=cov, engine=eng)
         for c, g in zip(chunks, got):
-            assert g == driver.zmw_input(c, OraclePoa(), max_poa_coverage=cov)
+            assert g == driver.zmw_input(c, _OraclePoa(), max_poa_coverage=cov)
     assert got[-1] == ("NoSubreads", None)
 
 
-def test_native_ccs_batch_matches_python_driver(P):
-    """pbccs_ccs_batch (FilterReads, POA, ExtractMappedRead, polish in one native call) equals the Python
-    driver (zmw_inputs_batch) followed by polish_zmws: statuses, drafts, consensus, QVs, per-key AddRead
-    results and counts.  Includes partial passes (flags) and a ZMW with no usable subread."""
-    poa, eng = P
-    import pbccs_amd
-    from pbccs_amd import driver
+def _ccs_chunks():
+    """Six synthetic ZMWs with partial passes (flags), zero-length subreads and a ZMW with no usable subread."""
     rng = np.random.default_rng(8)
     chunks = []
     for reads in _synthetic_subreads(6, (300, 900), (3, 9), seed=55):
@@ -225,8 +210,32 @@ def test_native_ccs_batch_matches_python_driver(P):
     # zero-length subreads, first and later in the input: they count in FilterReads but the POA never adds them
     chunks[0]["reads"].insert(0, {"seq": ""})
     chunks[1]["reads"].insert(2, {"seq": "", "flags": 3})
+    return chunks
+
+
+def test_native_ccs_batch_matches_python_driver(P):
+    """pbccs_ccs_batch (FilterReads, POA, ExtractMappedRead, polish in one native call) equals the Python
+    driver (zmw_inputs_batch) followed by polish_zmws: statuses, drafts, consensus, QVs, per-key AddRead
+    results and counts.  Includes partial passes (flags) and a ZMW with no usable subread."""
+    poa, eng = P
+    chunks = _ccs_chunks()
     for cov in (None, 3):
         _check_native_ccs(chunks, cov, eng)
+
+
+def test_poa_drafts_after_pool_release_match_oracle(P):
+    """pbccs_ccs_batch unmaps the POA score pools when it ends; the next POA maps them again.  Mapping new
+    memory at the addresses just unmapped gave wrong drafts in later POA calls (VmPool::unmap_all now moves
+    to a fresh address range).  Drafts from zmw_inputs_batch after each of several ccs calls equal the
+    oracle's SparsePoa."""
+    poa, eng = P
+    from pbccs_amd import driver
+    chunks = _ccs_chunks()
+    want = {cov: [driver.zmw_input(c, _OraclePoa(), max_poa_coverage=cov) for c in chunks] for cov in (None, 3)}
+    for _ in range(2):
+        for cov in (None, 3):
+            driver.ccs_batch(chunks, engine=eng, max_poa_coverage=cov)
+            assert driver.zmw_inputs_batch(chunks, max_poa_coverage=cov, engine=eng) == want[cov]
 
 
 def _check_native_ccs(chunks, cov, eng):
