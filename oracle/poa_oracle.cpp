@@ -500,7 +500,7 @@ int orc_poa_consensus(const char** reads, int n, int mode, int min_cov, char* se
 }
 
 // SparsePoa, as Consensus.h's PoaConsensus drives it (include/pacbio/ccs/Consensus.h:352-390): reads added
-// in order with OrientAndAddRead (nullptr reads -- given as NULL -- get key -1) until max_cov reads were
+// in order with OrientAndAddRead (nullptr and empty reads get key -1) until max_cov reads were
 // taken, then FindConsensus(min_cov; < 0 -> Consensus.h's (cov < 5) ? 1 : (cov + 1) / 2 - 1).
 // keys[r] per input read (-2: not reached); per POA key k: rc[k], extents[4k..4k+3] = read begin/end,
 // consensus begin/end.  Returns the consensus length; *n_keys = number of POA keys.
@@ -511,7 +511,10 @@ int orc_sparse_poa(const char** reads, int n, int min_cov, long max_cov, int* ke
     long cov = 0;
     for (int r = 0; r < n; ++r) keys[r] = -2;
     for (int r = 0; r < n; ++r) {
-        const int key = reads[r] ? sp.OrientAndAddRead(std::string(reads[r])) : -1;
+        // An empty read gets key -1, as in the engine (pbccs_poa_batch / pbccs_ccs_batch): the reference asserts a
+        // non-empty read in AddFirstRead and TryAddRead (PoaGraphImpl.cpp:375,391) and threads a null vertex for an
+        // empty first read in a release build, so it defines no behaviour to restate.
+        const int key = (reads[r] && reads[r][0]) ? sp.OrientAndAddRead(std::string(reads[r])) : -1;
         keys[r] = key;
         if (key >= 0 && (++cov) >= max_cov) break;
     }

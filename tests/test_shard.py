@@ -49,7 +49,7 @@ def _stand_in_held(rank, world, fast_chunks=4):
             if store.add("test/started", 1) == world:
                 store.set("test/all_started", "1")
             store.wait(["test/all_started"])
-            if rank == 1 and world > 1:
+            if rank == 1 and world == 2:   # (with more ranks the others may drain the queue before rank 0's fourth)
                 store.wait(["test/fast_done"])
         out = [{"rank": rank, "draft": z["draft"][::-1], "pad": ""} for z in zs]
         if rank == 0 and state["calls"] == fast_chunks:
@@ -58,8 +58,19 @@ def _stand_in_held(rank, world, fast_chunks=4):
     return polish
 
 
-def _stand_in_dies(rank):
+def _stand_in_dies(rank, world):
+    """Rank 1 fails in its first chunk; every rank's first chunk waits until each rank holds one (store keys), so
+    rank 1 always gets a chunk to fail in (rank 0 cannot drain the queue first)."""
+    import torch.distributed as dist
+    store = dist.distributed_c10d._get_default_store()
+    state = {"calls": 0}
+
     def polish(zs):
+        state["calls"] += 1
+        if state["calls"] == 1:
+            if store.add("test/started", 1) == world:
+                store.set("test/all_started", "1")
+            store.wait(["test/all_started"])
         if rank == 1:
             raise RuntimeError("rank 1 fails mid-chunk")
         return [{"rank": rank, "draft": z["draft"][::-1], "pad": ""} for z in zs]
@@ -74,7 +85,7 @@ def _worker(rank, world, port, zmws, out_q, use_gpu, mode="static", chunk=2):
     try:
         if mode == "dead_peer":
             try:
-                shard.polish_dynamic(zmws, chunk=chunk, polish_fn=_stand_in_dies(rank), collect_timeout=3.0)
+                shard.polish_dynamic(zmws, chunk=chunk, polish_fn=_stand_in_dies(rank, world), collect_timeout=3.0)
                 res = "no error"
             except RuntimeError as e:
                 res = f"raised: {e}"
