@@ -1084,6 +1084,63 @@ def make_roofline(stats, local_time, workload):
             "source_digest": digest}
 
 
+# MI355X_MICROARCH.md: 256 CUs x 4 SIMDs; per SIMD 8 wave slots and a 512-entry-per-lane VGPR file (allocation
+# granule 8); a wave64 VALU instruction issues over 4 cycles of the SIMD's 16 lanes; engine clock 2.4 GHz
+SIMDS, WAVE_SLOTS_PER_SIMD, VGPRS_PER_SIMD_LANE, VALU_CYCLES_PER_INST, ENGINE_HZ = 1024, 8, 512, 4, 2.4e9
+# the kernel families whose wavefronts stamp their resident time (arrow_device.hpp WaveSlot) and their kernels'
+# mangled-name stems in the build's resource table (pbccs_amd/_lib/kernel_resources.json, check_resources.py)
+WAVE_FAMILIES = {"k_fill": ("k_fill_coopILi16E",), "k_fill_tall": ("k_fill_coopILi64E",),
+                 "k_score": ("7k_scoreE", "12k_score_edgeE", "12k_score_ckptE"), "k_suffix": ("8k_suffixE",),
+                 "k_reduce": ("8k_reduceE",)}
+VALU_PROFILE = "r5_valu_per_cell.json"   # SQ_INSTS_VALU per kernel family (tools/gpu_steps.sh valu)
+
+
+def occupancy_report(stats, local_time):
+    """Which device resource the concurrent batches fill, from in-kernel wave stamps: each
+    wavefront of the fill / score / suffix / reduce kernels adds its start-to-end time (`wave_s`), so over the timed
+    region a family's wave_s / wall = its average resident wavefronts.  Against the device: wave slots (8 per SIMD),
+    the VGPR file (a family's allocation per wave from the build's resource table, x its resident waves, over
+    1024 SIMDs x 512), and VALU issue (SQ_INSTS_VALU per launch from the committed PMC pass of the same sources x
+    this run's launches x 4 cycles, over the SIMDs' cycles).  Wave time counts waiting waves too: the fraction of
+    the VGPR file held is the occupancy the batches reach, the VALU fraction what they issue with it."""
+    if local_time <= 0:
+        return None
+    rpath = os.path.join(ROOT, "pbccs_amd", "_lib", "kernel_resources.json")
+    res = json.load(open(rpath)) if os.path.exists(rpath) else {}
+    fams, waves_tot, vgpr_tot = {}, 0.0, 0.0
+    for fam, stems in WAVE_FAMILIES.items():
+        s = stats.get(fam)
+        if not s or not s.get("wave_s"):
+            continue
+        allocs = [((v.get("vgprs", 0) + v.get("agprs", 0) + 7) // 8) * 8 for k, v in res.items()
+                  if any(st in k for st in stems)]
+        alloc = max(allocs) if allocs else None
+        waves = s["wave_s"] / local_time
+        waves_tot += waves
+        if alloc:
+            vgpr_tot += waves * alloc
+        fams[fam] = {"resident_waves": round(waves, 1), "vgprs_per_lane": alloc,
+                     "waves_per_simd_limit": min(WAVE_SLOTS_PER_SIMD, VGPRS_PER_SIMD_LANE // alloc) if alloc else None}
+    out = {"families": fams, "resident_waves": round(waves_tot, 1),
+           "waves_per_simd": round(waves_tot / SIMDS, 3),
+           "wave_slot_frac": round(waves_tot / (SIMDS * WAVE_SLOTS_PER_SIMD), 4),
+           "vgpr_file_frac": round(vgpr_tot / (SIMDS * VGPRS_PER_SIMD_LANE), 4) if res else None,
+           "resource_table": "pbccs_amd/_lib/kernel_resources.json" if res else "missing (build the library)"}
+    vpath = os.path.join(ROOT, "profiles", VALU_PROFILE)
+    if os.path.exists(vpath):
+        v = json.load(open(vpath))
+        if v.get("source_digest") == kernel_source_digest():
+            cyc = 0.0
+            for fam, d in v.get("kernels", {}).items():
+                if fam in stats and d.get("valu_insts") and d.get("dispatches"):
+                    cyc += d["valu_insts"] / d["dispatches"] * stats[fam]["launches"] * VALU_CYCLES_PER_INST
+            out["valu_issue_frac"] = round(cyc / (local_time * ENGINE_HZ * SIMDS), 4)
+            out["valu_source"] = f"profiles/{VALU_PROFILE} (rocprofv3 --pmc SQ_INSTS_VALU, same sources)"
+        else:
+            out["valu_source"] = f"profiles/{VALU_PROFILE} is stale: sources {v.get('source_digest')}"
+    return out
+
+
 FILL_WORK_SLOTS = ("counted_cells", "tall_abort_cells", "regrow_cells", "overflow_cells", "group_chunk_steps",
                    "wave_chunk_issues", "reads", "passes")
 
@@ -1135,6 +1192,13 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
         gcups = float(t.item()) / job_time / 1e9
 
     roofline = make_roofline(stats, local_time, workload)
+    occ = occupancy_report(stats, local_time)
+    if occ:
+        roofline["occupancy"] = occ
+        roofline["binding_measured"] = (
+            f"over the timed region {occ['waves_per_simd']} waves resident per SIMD ({occ['wave_slot_frac']} of the "
+            f"wave slots), holding {occ['vgpr_file_frac']} of the VGPR file; VALU issue "
+            f"{occ.get('valu_issue_frac', 'n/a')} of the SIMDs' cycles (roofline.occupancy)")
     out = {
         "metric": "CCS ZMWs/sec (and GCUPS) at 1/2/4/8 MI355X vs host-CPU ccs",
         "stage": "polish: Consensus.h:436-552 from the POA draft on (AddRead gates, RefineConsensus, "

@@ -238,13 +238,16 @@ int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset);
 
 /* Per-kernel profile (enabled by pbccs_engine_set_profiling): launches, summed device time from HIP
  * events on the engine's stream, and algorithmic work counted in-kernel: `cells` DP cell-updates,
- * `bytes` algorithmic band bytes (8 B per stored/read band cell + 16 B per column). */
+ * `bytes` algorithmic band bytes (8 B per stored/read band cell + 16 B per column),
+ * `wave_s` wavefront-seconds resident on the device (each wavefront's start-to-end time, summed; over a
+ * timed region it gives the family's average resident waves; the fills, k_score family, k_suffix, k_reduce). */
 typedef struct {
     char name[32];
     long long launches;
     double device_ms;
     double cells;
     double bytes;
+    double wave_s;
 } pbccs_kernel_stat;
 int pbccs_engine_set_profiling(pbccs_engine* eng, int on);
 int pbccs_engine_kernel_stats(pbccs_engine* eng, pbccs_kernel_stat* out, int cap, int* n, int reset);

@@ -103,7 +103,8 @@ class Engine:
         n = ctypes.c_int()
         _lib_mod.check(load().pbccs_engine_kernel_stats(self._h, arr, 16, ctypes.byref(n), 1 if reset else 0))
         return {arr[i].name.decode(): {"launches": arr[i].launches, "device_ms": arr[i].device_ms,
-                                       "cells": arr[i].cells, "bytes": arr[i].bytes} for i in range(n.value)}
+                                       "cells": arr[i].cells, "bytes": arr[i].bytes, "wave_s": arr[i].wave_s}
+                for i in range(n.value)}
 
     def counters(self, reset=False):
         c = _lib_mod.CCounters()

@@ -294,7 +294,7 @@ __device__ __forceinline__ double add8(double s, const double* __restrict__ t)
     return s;
 }
 
-__global__ void __launch_bounds__(256) k_suffix(DevBatch B, const int* __restrict__ reads, int n, int withPrefix)
+__device__ __forceinline__ void k_suffix_body(DevBatch B, const int* __restrict__ reads, int n, int withPrefix)
 {
     __shared__ double tile[kSuffixTile];
     const int r = reads[blockIdx.x];
@@ -350,6 +350,12 @@ __global__ void __launch_bounds__(256) k_suffix(DevBatch B, const int* __restric
         run = run + als[k];
         pre[k + 1] = run;
     }
+}
+__global__ void __launch_bounds__(256) k_suffix(DevBatch B, const int* __restrict__ reads, int n, int withPrefix)
+{
+    const long long wt0 = wave_t0(B.stats);
+    k_suffix_body(B, reads, n, withPrefix);
+    wave_ticks(B.stats, kWaveSuffix, wt0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -985,6 +991,9 @@ struct WaveStage {
 #endif
 __global__ void __launch_bounds__(256) PBCCS_SCORE_OCC k_score(DevBatch B, ScoreWork W, ScoreScratch scratch)
 {
+    // the start stamp waits in LDS: k_score sits at its register budget
+    __shared__ long long wt0[kScoreWaves];
+    if ((threadIdx.x & 63) == 0) wt0[threadIdx.x >> 6] = wave_t0(B.stats);
     __shared__ WaveStage stage[kScoreWaves];
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: the item search and per-item loads go scalar
     const long long wave = (long long)blockIdx.x * kScoreWaves + wid;
@@ -1114,12 +1123,15 @@ __global__ void __launch_bounds__(256) PBCCS_SCORE_OCC k_score(DevBatch B, Score
             atomicAdd(&B.stats[2 * kStatScore], c);
             atomicAdd(&B.stats[2 * kStatScore + 1], b);
         }
+        if (lane == 0)
+            atomicAdd(&B.stats[kWaveScore], (unsigned long long)((long long)__builtin_amdgcn_s_memrealtime() - wt0[wid]));
     }
 }
 
+
 // Edge cases of ScoreMutation (ExtendAlpha to the end, ExtendBeta to the start, whole refill), listed
 // by k_score.  A separate kernel keeps their 4-column register state out of k_score's budget.
-__global__ void __launch_bounds__(64) k_score_edge(DevBatch B, ScoreWork W, ScoreScratch scratch)
+__device__ __forceinline__ void k_score_edge_body(DevBatch B, ScoreWork W, ScoreScratch scratch)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= *W.edgeCount || t >= W.edgeCap) return;
@@ -1137,6 +1149,12 @@ __global__ void __launch_bounds__(64) k_score_edge(DevBatch B, ScoreWork W, Scor
         atomicAdd(&B.stats[2 * kStatScore], st.cells);
         atomicAdd(&B.stats[2 * kStatScore + 1], st.bytes);
     }
+}
+__global__ void __launch_bounds__(64) k_score_edge(DevBatch B, ScoreWork W, ScoreScratch scratch)
+{
+    const long long wt0 = wave_t0(B.stats);
+    k_score_edge_body(B, W, scratch);
+    wave_ticks(B.stats, kWaveScore, wt0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1309,7 +1327,7 @@ __device__ void replay_beta(const ReplayRead& X, int j, const double* nxt, int p
             }
 }
 
-__global__ void __launch_bounds__(64) k_score_ckpt(DevBatch B, ScoreWork W, CkptWork C)
+__device__ __forceinline__ void k_score_ckpt_body(DevBatch B, ScoreWork W, CkptWork C)
 {
     __shared__ int sOff[kCkptCols];
     const int lane = threadIdx.x;
@@ -1476,9 +1494,15 @@ __global__ void __launch_bounds__(64) k_score_ckpt(DevBatch B, ScoreWork W, Ckpt
         }
     }
 }
+__global__ void __launch_bounds__(64) k_score_ckpt(DevBatch B, ScoreWork W, CkptWork C)
+{
+    const long long wt0 = wave_t0(B.stats);
+    k_score_ckpt_body(B, W, C);
+    wave_ticks(B.stats, kWaveScore, wt0);
+}
 
 // Ordered reduction over reads with the fast-score break (MultiReadMutationScorer.cpp:352-362).
-__global__ void __launch_bounds__(256) k_reduce(DevBatch B, ScoreWork W, double fastThr, double* __restrict__ score,
+__device__ __forceinline__ void k_reduce_body(DevBatch B, ScoreWork W, double fastThr, double* __restrict__ score,
                                                 unsigned char* __restrict__ fav)
 {
     const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1505,6 +1529,13 @@ __global__ void __launch_bounds__(256) k_reduce(DevBatch B, ScoreWork W, double 
     }
     score[W.mutBase[k] + m] = sum;
     fav[W.mutBase[k] + m] = (sum > 0.04) ? 1 : 0;   // MIN_FAVORABLE_SCOREDIFF, MultiReadMutationScorer.cpp:56
+}
+__global__ void __launch_bounds__(256) k_reduce(DevBatch B, ScoreWork W, double fastThr, double* __restrict__ score,
+                                                unsigned char* __restrict__ fav)
+{
+    const long long wt0 = wave_t0(B.stats);
+    k_reduce_body(B, W, fastThr, score, fav);
+    wave_ticks(B.stats, kWaveReduce, wt0);
 }
 
 // The reduction's ordered prefix over the first readHi reads only (same sums, same break).

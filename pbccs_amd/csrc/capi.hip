@@ -1038,6 +1038,7 @@ int pbccs_engine_kernel_stats(pbccs_engine* eng, pbccs_kernel_stat* out, int cap
         out[k].device_ms = eng->stats[k].ms;
         out[k].cells = eng->stats[k].cells;
         out[k].bytes = eng->stats[k].bytes;
+        out[k].wave_s = eng->stats[k].waveTicks / 1e8;   // s_memrealtime runs at 100 MHz
         if (reset) eng->stats[k] = KernelStat();
     }
     return PBCCS_OK;

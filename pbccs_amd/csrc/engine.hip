@@ -375,6 +375,11 @@ void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
         stats_[kKFillTall].bytes += (double)h[2 * kStatFillTall + 1];
         stats_[kKScore].cells += (double)h[2 * kStatScore];
         stats_[kKScore].bytes += (double)h[2 * kStatScore + 1];
+        stats_[kKFill].waveTicks += (double)h[kWaveFill];
+        stats_[kKFillTall].waveTicks += (double)h[kWaveFillTall];
+        stats_[kKScore].waveTicks += (double)h[kWaveScore];   // k_score, k_score_edge, k_score_ckpt
+        stats_[kKSuffix].waveTicks += (double)h[kWaveSuffix];
+        stats_[kKReduce].waveTicks += (double)h[kWaveReduce];
         static const bool trace = std::getenv("PBCCS_ROUND_TRACE") != nullptr;
         if (trace) std::fprintf(stderr, "[fillcells] g16=%llu g64=%llu\n", h[8], h[9]);
         PBCCS_HIP(hipMemsetAsync(dStats_.ptr, 0, sizeof(h), stream_));
@@ -384,6 +389,7 @@ void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
         out[k].ms += stats_[k].ms;
         out[k].cells += stats_[k].cells;
         out[k].bytes += stats_[k].bytes;
+        out[k].waveTicks += stats_[k].waveTicks;
         stats_[k] = KernelStat();
     }
 }

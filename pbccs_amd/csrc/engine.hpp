@@ -218,6 +218,7 @@ struct KernelStat {
     double ms = 0.0;      // summed HIP-event time on the engine stream
     double cells = 0.0;   // algorithmic DP cell-updates (in-kernel counters)
     double bytes = 0.0;   // algorithmic band bytes
+    double waveTicks = 0.0;   // resident wavefront time, s_memrealtime ticks (arrow_device.hpp WaveSlot)
 };
 
 // Large device pools.  A batch either owns one (fine-grained scorers) or borrows its engine's (batch

@@ -1045,6 +1045,7 @@ template <int G, int MINW, bool GC, int R>
 __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
 {
     extern __shared__ __align__(16) unsigned char smem[];
+    const long long wt0 = wave_t0(B.stats);
     // tall reads are the latency-critical path of every refine round: issue ahead of the 16-lane fills
     // and score waves that share the SIMD (F.prio = 0 leaves the default priority)
     if (F.prio) __builtin_amdgcn_s_setprio(3);
@@ -1071,9 +1072,10 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
                 need = true;
             }
         }
-        return;
+    } else {
+        fill_read<G, GC, R>(B, F, reads, n, blockIdx.x * (64 / G) + grp, gbase);
     }
-    fill_read<G, GC, R>(B, F, reads, n, blockIdx.x * (64 / G) + grp, gbase);
+    wave_ticks(B.stats, G == 64 ? kWaveFillTall : kWaveFill, wt0);
 }
 
 size_t coop_group_bytes(int hcap, int readWords, int tplWords)

@@ -58,7 +58,7 @@ class CZmwOutput(ctypes.Structure):
 
 class CKernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_longlong), ("device_ms", ctypes.c_double),
-                ("cells", ctypes.c_double), ("bytes", ctypes.c_double)]
+                ("cells", ctypes.c_double), ("bytes", ctypes.c_double), ("wave_s", ctypes.c_double)]
 
 
 class CCounters(ctypes.Structure):

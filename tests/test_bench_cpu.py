@@ -5,6 +5,7 @@ import json
 import os
 import subprocess
 import sys
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -106,3 +107,22 @@ def test_cpu_leg_checks_the_timed_records_and_fails_on_a_mismatch():
     cb, par = bench.sampled_cpu_baseline(_args(cpu_sample=3), settings, zs, recs, idx, costs)
     ex = cb["extrapolated"]
     assert par["ok"] and abs(cb["value"] - 2 / ex["core_s_per_zmw"]) < 0.02 * cb["value"]
+
+
+def test_occupancy_report_from_wave_stamps():
+    """roofline.occupancy: resident waves = wave-seconds / wall; the VGPR share uses the build's resource table
+    (allocation rounded up to 8 registers) over 1024 SIMDs x 512."""
+    import json
+    import os
+    import bench
+    table = os.path.join(bench.ROOT, "pbccs_amd", "_lib", "kernel_resources.json")
+    if not os.path.exists(table):
+        pytest.skip("library not built")
+    res = json.load(open(table))
+    fill = [v for k, v in res.items() if "k_fill_coopILi16E" in k][0]
+    alloc = (fill["vgprs"] + fill["agprs"] + 7) // 8 * 8
+    occ = bench.occupancy_report({"k_fill": {"wave_s": 2048.0, "launches": 4}}, 2.0)
+    assert occ["resident_waves"] == 1024.0 and occ["waves_per_simd"] == 1.0
+    assert occ["families"]["k_fill"]["vgprs_per_lane"] == alloc
+    assert abs(occ["vgpr_file_frac"] - round(1024 * alloc / (1024 * 512), 4)) < 1e-9
+    assert occ["wave_slot_frac"] == round(1 / 8, 4)

@@ -17,7 +17,7 @@ def kind(name):
         return "k_fill"
     if n.startswith("k_fill_coop<64"):
         return "k_fill_tall"
-    for k in ("k_score_ckpt", "k_score_edge", "k_score", "k_suffix", "k_qfill_grp", "k_qfill_coop", "k_qscore_mid"):
+    for k in ("k_score_ckpt", "k_score_edge", "k_score", "k_suffix", "k_reduce", "k_qfill_grp", "k_qfill_coop", "k_qscore_mid"):
         if n.startswith(k + "(") or n.startswith(k + "<") or n == k:
             return k
     return None
