@@ -89,7 +89,9 @@ struct DevVec {
             throw DeviceOom("hipMalloc failed (device memory): " + std::to_string(nc * sizeof(T) >> 20) +
                               " MB requested, " + std::to_string(fr >> 20) + " MB free");
         }
-        const hipStream_t st = devvec_stream();
+        // PBCCS_DEVVEC_SYNC=1 (A/B): the old device-wide synchronising growth
+        static const bool forceSync = std::getenv("PBCCS_DEVVEC_SYNC") && std::getenv("PBCCS_DEVVEC_SYNC")[0] == '1';
+        const hipStream_t st = forceSync ? nullptr : devvec_stream();
         if (st) {
             if (keep && ptr && cap &&
                 hipMemcpyAsync(p, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice, st) != hipSuccess)
