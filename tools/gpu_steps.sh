@@ -131,6 +131,16 @@ step() {
           echo "lib=$v $(summ $OUT/ab_lib_$k.json) $(python3 -c "import json; d=json.load(open('$OUT/ab_lib_$k.json')); print({n: round(v['device_ms']/max(1,v['launches']),2) for n,v in d['kernels'].items() if n in ('k_score','k_fill','k_fill_tall','k_suffix')})")"
         done
       done ;;
+    ab_tree)  # interleaved A/B of whole trees (git worktrees of older revisions under _ab/, built in-tree): TREES="a b"
+      local k=0
+      for rep in 1 2; do
+        for v in ${TREES:-. _ab/be29dbd}; do
+          k=$((k+1))
+          (cd $v && timeout -k 10 300 python3 -u bench.py --steps ${ABSTEPS:-10} --warmup 2 --cpu-sample 0 ${ABARGS:-}) \
+            > $OUT/ab_tree_$k.json 2> $OUT/ab_tree_$k.err || return 1
+          echo "tree=$v $(summ $OUT/ab_tree_$k.json)"
+        done
+      done ;;
     ab_env)   # interleaved A/B of environment settings: ENVS="A=1 A=0" (one KEY=VALUE per variant; "-" = none), 2 runs each
       local k=0
       for rep in 1 2; do
