@@ -1103,9 +1103,10 @@ def occupancy_report(stats, local_time):
     1024 SIMDs x 512), and VALU issue (SQ_INSTS_VALU per launch from the committed PMC pass of the same sources x
     this run's launches x 4 cycles, over the SIMDs' cycles).  Wave time counts waiting waves too: the fraction of
     the VGPR file held is the occupancy the batches reach, the VALU fraction what they issue with it."""
-    if local_time <= 0:
-        return None
-    rpath = os.path.join(ROOT, "pbccs_amd", "_lib", "kernel_resources.json")
+    if local_time <= 0 or not any(s.get("wave_s") for s in stats.values()):
+        return None   # the default build has the stamps compiled out (PBCCS_WAVE_STAMPS; they cost 5%)
+    from pbccs_amd import lib as _L
+    rpath = os.path.join(os.path.dirname(_L.LIB_PATH), "kernel_resources.json")   # the loaded build's table
     res = json.load(open(rpath)) if os.path.exists(rpath) else {}
     fams, waves_tot, vgpr_tot = {}, 0.0, 0.0
     for fam, stems in WAVE_FAMILIES.items():
@@ -1125,7 +1126,8 @@ def occupancy_report(stats, local_time):
            "waves_per_simd": round(waves_tot / SIMDS, 3),
            "wave_slot_frac": round(waves_tot / (SIMDS * WAVE_SLOTS_PER_SIMD), 4),
            "vgpr_file_frac": round(vgpr_tot / (SIMDS * VGPRS_PER_SIMD_LANE), 4) if res else None,
-           "resource_table": "pbccs_amd/_lib/kernel_resources.json" if res else "missing (build the library)"}
+           "resource_table": os.path.relpath(rpath, ROOT) if res else "missing (build the library)",
+           "build": "PBCCS_WAVE_STAMPS=1 (the occupancy build, tools/gpu_steps.sh occ)"}
     vpath = os.path.join(ROOT, "profiles", VALU_PROFILE)
     if os.path.exists(vpath):
         v = json.load(open(vpath))

@@ -110,14 +110,18 @@ enum StatKind : int { kStatFill = 0, kStatSuffix = 1, kStatScore = 2, kStatFillT
 // ticks from its first instruction to its end (wave_t0 / wave_ticks).  Over the timed region it gives the waves of
 // each family resident on the device on average -- what the concurrent batches hold of its wave slots and VGPR file.
 enum WaveSlot : int { kWaveFill = 10, kWaveFillTall = 11, kWaveScore = 12, kWaveSuffix = 13, kWaveReduce = 14 };
+#ifndef PBCCS_WAVE_STAMPS   // 1: the occupancy build (tools/gpu_steps.sh occ); off by default: the stamps cost 5% (A/B)
+#define PBCCS_WAVE_STAMPS 0
+#endif
 __device__ __forceinline__ long long wave_t0(const unsigned long long* stats)
 {
+    if (!PBCCS_WAVE_STAMPS) return 0;
     return stats ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
 }
 // at a point every lane of the wavefront that is still running reaches once (the end of the kernel)
 __device__ __forceinline__ void wave_ticks(unsigned long long* stats, int slot, long long t0)
 {
-    if (!stats) return;
+    if (!PBCCS_WAVE_STAMPS || !stats) return;
     const long long t1 = (long long)__builtin_amdgcn_s_memrealtime();
     const unsigned long long act = __ballot(1);
     if ((int)(threadIdx.x & 63) == __ffsll((long long)act) - 1) atomicAdd(&stats[slot], (unsigned long long)(t1 - t0));

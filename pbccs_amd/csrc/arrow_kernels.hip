@@ -993,7 +993,7 @@ __global__ void __launch_bounds__(256) PBCCS_SCORE_OCC k_score(DevBatch B, Score
 {
     // the start stamp waits in LDS: k_score sits at its register budget
     __shared__ long long wt0[kScoreWaves];
-    if ((threadIdx.x & 63) == 0) wt0[threadIdx.x >> 6] = wave_t0(B.stats);
+    if (PBCCS_WAVE_STAMPS && (threadIdx.x & 63) == 0) wt0[threadIdx.x >> 6] = wave_t0(B.stats);
     __shared__ WaveStage stage[kScoreWaves];
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: the item search and per-item loads go scalar
     const long long wave = (long long)blockIdx.x * kScoreWaves + wid;
@@ -1123,7 +1123,7 @@ __global__ void __launch_bounds__(256) PBCCS_SCORE_OCC k_score(DevBatch B, Score
             atomicAdd(&B.stats[2 * kStatScore], c);
             atomicAdd(&B.stats[2 * kStatScore + 1], b);
         }
-        if (lane == 0)
+        if (PBCCS_WAVE_STAMPS && lane == 0)
             atomicAdd(&B.stats[kWaveScore], (unsigned long long)((long long)__builtin_amdgcn_s_memrealtime() - wt0[wid]));
     }
 }

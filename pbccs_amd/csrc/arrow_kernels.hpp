@@ -110,8 +110,6 @@ struct CoopFill {
     // diagnostics (PBCCS_FILL_WORK=1): where the fill's computed cells go, per kind (k = 0: the 16-lane fill,
     // 1: the 64-lane fills) at work[kFillWorkSlots * k + ...] (kFillWork*)
     unsigned long long* work = nullptr;
-    // 16-lane path: the launch's task counter (zeroed before the launch); nullptr = static assignment
-    unsigned* queue = nullptr;
 };
 // work[] slots per fill kind: cells of the passes that count (the bench's GCUPS); cells computed and thrown away
 // because the read aborted as too tall (its passes restart on the 64-lane path); cells of count-only passes that

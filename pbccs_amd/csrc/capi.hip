@@ -534,7 +534,8 @@ static int create_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, con
         b->n = n;
         b->slot = slot >= 0 ? slot : eng->nextSlot++ % std::max(1, eng->concurrency);
         b->inputs.assign(in, n);
-        b->B.reset(new ArrowBatch(eng->device, eng->Slot(b->slot)));
+        // every batch gets its own streams (ArrowBatch's ownStreams)
+        b->B.reset(new ArrowBatch(eng->device, eng->Slot(b->slot), true));
         b->B->SetProfiling(eng->profiling);
         ArrowOptions ao;
         ao.scoreDiff = b->o.score_diff;

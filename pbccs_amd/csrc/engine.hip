@@ -236,7 +236,7 @@ void Workspace::EnsureStreams()
     PBCCS_HIP(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
 }
 
-ArrowBatch::ArrowBatch(int device, Workspace* shared)
+ArrowBatch::ArrowBatch(int device, Workspace* shared, bool ownStreams)
     : device_(device),
       ownWs_(shared ? nullptr : new Workspace()),
       ws_(shared ? shared : ownWs_.get()),
@@ -259,11 +259,19 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared)
     if (const char* e = std::getenv("PBCCS_INITIAL_BAND_HEIGHT")) initialBandHeight_ = std::max(1, std::atoi(e));
     ckpt_policy(&ckptK_, &ckptMinLen_);
     ckptAll_ = std::min(kCkptMaxK, std::max(0, env_int("PBCCS_CKPT_ALL", 0)));
-    ws_->EnsureStreams();
-    stream_ = ws_->stream;
-    stream2_ = ws_->stream2;
-    evFork_ = ws_->evFork;
-    evJoin_ = ws_->evJoin;
+    if (ownStreams) {
+        ownStreams_ = true;
+        PBCCS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+        PBCCS_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
+        PBCCS_HIP(hipEventCreateWithFlags(&evFork_, hipEventDisableTiming));
+        PBCCS_HIP(hipEventCreateWithFlags(&evJoin_, hipEventDisableTiming));
+    } else {
+        ws_->EnsureStreams();
+        stream_ = ws_->stream;
+        stream2_ = ws_->stream2;
+        evFork_ = ws_->evFork;
+        evJoin_ = ws_->evJoin;
+    }
     const StreamScope bound(stream_);   // stream-ordered DevVec growth for this batch's calls (engine.hpp)
     dScratch_.reserve(kInitialScratch, false);
     dScratchTop_.reserve(1, false);
@@ -282,6 +290,12 @@ ArrowBatch::~ArrowBatch()
         for (const Pending& p : pending_) {
             eventPool_.push_back(p.a);
             eventPool_.push_back(p.b);
+        }
+        if (ownStreams_) {
+            (void)hipEventDestroy(evFork_);
+            (void)hipEventDestroy(evJoin_);
+            (void)hipStreamDestroy(stream2_);
+            (void)hipStreamDestroy(stream_);
         }
     }
 }
@@ -867,8 +881,6 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
     static const bool pathTrace2 = pathTrace && std::getenv("PBCCS_FILL_PATHS")[0] == '2';
     // PBCCS_FILL_WORK=1: where the fills' computed cells go (CoopFill::work; counters().fillWork)
     static const bool fillWork = std::getenv("PBCCS_FILL_WORK") != nullptr;
-    // PBCCS_FILL_QUEUE=1: the 16-lane fill's groups take reads from a per-launch counter (measured no faster: opt-in)
-    static const bool fillQueue = env_int("PBCCS_FILL_QUEUE", 0) != 0;
     for (int attempt = 0;; ++attempt) {
         // route reads whose buffers do not fit this path's LDS budget to the next path
         for (int p = 0; p < kPaths; ++p) {
@@ -1009,11 +1021,6 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             }
             const int* lp = dList_.ptr + off;
             const hipStream_t st = p <= 1 ? stream_ : stream2_;
-            if (p == 1 && fillQueue) {   // the 16-lane groups take their reads from a counter (k_fill_coop)
-                ws_->fillQueue.reserve(1, false);
-                PBCCS_HIP(hipMemsetAsync(ws_->fillQueue.ptr, 0, sizeof(unsigned), st));
-                F.queue = ws_->fillQueue.ptr;
-            }
             if (fillWork) {
                 if (!dFillWork_.ptr) {
                     dFillWork_.reserve(16, false);

@@ -250,7 +250,6 @@ struct Workspace {
     DevVec<int> wZmw, wNMut;
     DevVec<long long> wMutBase, wDeltaBase, wWaveStart, wMutStart, wPosStart, wPosBase, wQvBase;
     DevVec<unsigned long long> stats;
-    DevVec<unsigned> fillQueue;   // the 16-lane fill's dynamic task counter (CoopFill::queue)
     // per-read compact bands (what scoring reads)
     DevVec<int2> aRange, bRange;
     DevVec<int> aOff, bOff;
@@ -278,7 +277,12 @@ struct Workspace {
 
 class ArrowBatch {
 public:
-    explicit ArrowBatch(int device, Workspace* shared = nullptr);
+    // ownStreams: the batch creates (and destroys) its own streams; otherwise it uses the workspace's.  The batch
+    // polish passes true: with the slot's streams shared by its batches, a batch rerun after another ran the device
+    // out of memory (pools unmapped and mapped again) scored wrong (tools/oom_dbg.py: 23 of 26 ZMWs; cause not
+    // found -- own streams, or own per-round buffers, each made it exact), and own streams measured +2.6% at the
+    // driver's command (interleaved A/B).  The fine-grained scorers keep the workspace's.
+    explicit ArrowBatch(int device, Workspace* shared = nullptr, bool ownStreams = false);
     ~ArrowBatch();
     ArrowBatch(const ArrowBatch&) = delete;
     ArrowBatch& operator=(const ArrowBatch&) = delete;
@@ -398,6 +402,7 @@ private:
     std::unique_ptr<Workspace> ownWs_;
     Workspace* ws_;
     hipStream_t stream_ = nullptr;       // the workspace's streams (ws_->stream / stream2)
+    bool ownStreams_ = false;            // this batch's own streams and events (the constructor's ownStreams)
     hipStream_t stream2_ = nullptr;      // second stream for the tall-band fill path
     hipEvent_t evFork_ = nullptr, evJoin_ = nullptr;
     DevVec<long long>& dSelBase_;         // phased scoring: per-item ranges of the surviving mutations

@@ -842,8 +842,7 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
         }
     }
     // the group's own LDS slot: its lanes' stores above complete before their loads below (one wavefront; the
-    // fence keeps the compiler from moving loads above them).  No block barrier: with the dynamic queue the other
-    // groups of the wavefront are at other points of their own reads
+    // fence keeps the compiler from moving loads above them)
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     if (!valid) return;
     if (bad) {
@@ -1036,10 +1035,10 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
 // k_fill_coop: one G-lane group per read; 64 / G groups per 64-thread block (one wavefront).
 // LDS per group: 2 column buffers (hcap doubles each), the ZMW's transition table, nibble-packed read
 // and template window.
-// Static assignment: group g of block b fills task 4b + g (G = 16) / task b (G = 64).  Dynamic (F.queue, the
-// 16-lane path): a group that finishes its read takes the launch's next task from a counter, so the four groups
-// of a wavefront stay busy until the list runs out instead of idling in lock-step behind their slowest read (the
-// wavefront's chunk issues were 36% idle group slots, profiles/r5c_fill_work_bench.json).
+// Group g of block b fills task 4b + g (G = 16) / task b (G = 64).  (A dynamic assignment -- a group that finished
+// its read taking the launch's next task from a counter, against the 36% idle group slots of lock-step waves,
+// profiles/r5c_fill_work_bench.json -- measured no faster, and its second inlined copy of the fill cost 5% of the
+// headline in instruction-cache footprint: removed)
 // ------------------------------------------------------------------------------------------------
 template <int G, int MINW, bool GC, int R>
 __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
@@ -1051,30 +1050,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     if (F.prio) __builtin_amdgcn_s_setprio(3);
     const int grp = threadIdx.x / G;
     unsigned char* gbase = smem + (size_t)grp * F.groupBytes;
-    if (G < 64 && F.queue) {
-        // a wave-uniform loop (it runs while some group of the wavefront holds a task); a group whose read is done
-        // takes the next one.  (The first form -- a per-group loop with the exit inside -- was miscompiled into an
-        // inner loop that re-ran task 0 without taking the next: it hung.)
-        const int lane = threadIdx.x & (G - 1);
-        const int base = (int)threadIdx.x & ~(G - 1);
-        bool need = true;
-        int t = n;
-        for (;;) {
-            if (need) {
-                int v = 0;
-                if (lane == 0) v = (int)atomicAdd(F.queue, 1u);
-                t = __shfl(v, base, 64);
-                need = false;
-            }
-            if (__ballot(t < n) == 0) break;
-            if (t < n) {
-                fill_read<G, GC, R>(B, F, reads, n, t, gbase);
-                need = true;
-            }
-        }
-    } else {
-        fill_read<G, GC, R>(B, F, reads, n, blockIdx.x * (64 / G) + grp, gbase);
-    }
+    fill_read<G, GC, R>(B, F, reads, n, blockIdx.x * (64 / G) + grp, gbase);
     wave_ticks(B.stats, G == 64 ? kWaveFillTall : kWaveFill, wt0);
 }
 

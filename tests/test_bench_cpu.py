@@ -122,6 +122,7 @@ def test_occupancy_report_from_wave_stamps():
     fill = [v for k, v in res.items() if "k_fill_coopILi16E" in k][0]
     alloc = (fill["vgprs"] + fill["agprs"] + 7) // 8 * 8
     occ = bench.occupancy_report({"k_fill": {"wave_s": 2048.0, "launches": 4}}, 2.0)
+    assert bench.occupancy_report({"k_fill": {"wave_s": 0.0, "launches": 4}}, 2.0) is None
     assert occ["resident_waves"] == 1024.0 and occ["waves_per_simd"] == 1.0
     assert occ["families"]["k_fill"]["vgprs_per_lane"] == alloc
     assert abs(occ["vgpr_file_frac"] - round(1024 * alloc / (1024 * 512), 4)) < 1e-9

@@ -131,6 +131,11 @@ step() {
           echo "lib=$v $(summ $OUT/ab_lib_$k.json) $(python3 -c "import json; d=json.load(open('$OUT/ab_lib_$k.json')); print({n: round(v['device_ms']/max(1,v['launches']),2) for n,v in d['kernels'].items() if n in ('k_score','k_fill','k_fill_tall','k_suffix')})")"
         done
       done ;;
+    occ)      # the driver's command on the occupancy build (wave stamps on: built by
+              # AB_FLAGS="-DPBCCS_WAVE_STAMPS=1" AB_OUT=pbccs_amd/_lib_occ tools/build_ab.sh HEAD): roofline.occupancy
+      PBCCS_LIB=pbccs_amd/_lib_occ/libpbccs_amd.so timeout -k 10 400 $BENCH --gpus 1 --steps 20 --warmup 5 \
+        --cpu-sample 0 > $OUT/bench_occ.json 2> $OUT/bench_occ.err && summ $OUT/bench_occ.json && \
+        python3 -c "import json; d=json.load(open('$OUT/bench_occ.json')); print(json.dumps(d['roofline'].get('occupancy')))" ;;
     ab_tree)  # interleaved A/B of whole trees (git worktrees of older revisions under _ab/, built in-tree): TREES="a b"
       local k=0
       for rep in 1 2; do
