@@ -1090,7 +1090,7 @@ SIMDS, WAVE_SLOTS_PER_SIMD, VGPRS_PER_SIMD_LANE, VALU_CYCLES_PER_INST, ENGINE_HZ
 # the kernel families whose wavefronts stamp their resident time (arrow_device.hpp WaveSlot) and their kernels'
 # mangled-name stems in the build's resource table (pbccs_amd/_lib/kernel_resources.json, check_resources.py)
 WAVE_FAMILIES = {"k_fill": ("k_fill_coopILi16E",), "k_fill_tall": ("k_fill_coopILi64E",),
-                 "k_score": ("7k_scoreE", "12k_score_edgeE", "12k_score_ckptE"), "k_suffix": ("8k_suffixE",),
+                 "k_score": ("7k_scoreE",), "k_suffix": ("8k_suffixE",),
                  "k_reduce": ("8k_reduceE",)}
 VALU_PROFILE = "r5_valu_per_cell.json"   # SQ_INSTS_VALU per kernel family (tools/gpu_steps.sh valu)
 

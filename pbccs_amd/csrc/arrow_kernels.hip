@@ -1152,9 +1152,7 @@ __device__ __forceinline__ void k_score_edge_body(DevBatch B, ScoreWork W, Score
 }
 __global__ void __launch_bounds__(64) k_score_edge(DevBatch B, ScoreWork W, ScoreScratch scratch)
 {
-    const long long wt0 = wave_t0(B.stats);
-    k_score_edge_body(B, W, scratch);
-    wave_ticks(B.stats, kWaveScore, wt0);
+    k_score_edge_body(B, W, scratch);   // (no wave stamp: roofline.occupancy's score family is k_score's)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1496,9 +1494,7 @@ __device__ __forceinline__ void k_score_ckpt_body(DevBatch B, ScoreWork W, CkptW
 }
 __global__ void __launch_bounds__(64) k_score_ckpt(DevBatch B, ScoreWork W, CkptWork C)
 {
-    const long long wt0 = wave_t0(B.stats);
     k_score_ckpt_body(B, W, C);
-    wave_ticks(B.stats, kWaveScore, wt0);
 }
 
 // Ordered reduction over reads with the fast-score break (MultiReadMutationScorer.cpp:352-362).

@@ -391,7 +391,7 @@ void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
         stats_[kKScore].bytes += (double)h[2 * kStatScore + 1];
         stats_[kKFill].waveTicks += (double)h[kWaveFill];
         stats_[kKFillTall].waveTicks += (double)h[kWaveFillTall];
-        stats_[kKScore].waveTicks += (double)h[kWaveScore];   // k_score, k_score_edge, k_score_ckpt
+        stats_[kKScore].waveTicks += (double)h[kWaveScore];   // k_score (its edge / checkpoint kernels do not stamp)
         stats_[kKSuffix].waveTicks += (double)h[kWaveSuffix];
         stats_[kKReduce].waveTicks += (double)h[kWaveReduce];
         static const bool trace = std::getenv("PBCCS_ROUND_TRACE") != nullptr;
