@@ -72,6 +72,11 @@ step() {
     mixed)    # configs[3] at 2000 ZMWs
       timeout -k 10 900 $BENCH --workload mixed --steps 1 --zmws-per-step 2000 --warmup 0 > $OUT/bench_mixed.json \
         2> $OUT/bench_mixed.err && summ $OUT/bench_mixed.json ;;
+    profmixed) # configs[3] at 2000 ZMWs on 8 slots under rocprofv3 (the line and its kernel summary in one run)
+      timeout -k 10 1000 rocprofv3 --kernel-trace --stats -f csv -d $OUT/profmixed -o run -- $BENCH --workload mixed \
+        --steps 1 --zmws-per-step 2000 --warmup 0 --streams 8 > $OUT/bench_mixed.json 2> $OUT/bench_mixed.err && \
+        summ $OUT/bench_mixed.json && \
+        cp "$(find $OUT/profmixed -name '*kernel_stats.csv' | head -1)" $OUT/mixed_kernel_stats.csv ;;
     cell2)    # configs[4]: two ranks sharing the one device (a rehearsal of the multi-rank queue), CELLN ZMWs
       PBCCS_BENCH_DEVICE=0 timeout -k 10 ${CELLTO:-1000} $BENCH --gpus 2 --workload smrtcell --steps 1 \
         --zmws-per-step ${CELLN:-10000} --warmup 0 --streams 4 > $OUT/bench_cell2.json 2> $OUT/bench_cell2.err && \
