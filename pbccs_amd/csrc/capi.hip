@@ -862,6 +862,12 @@ static double zmw_est_bytes(const pbccs_zmw_input& z)
         if (K > 0 && J >= minLen) tall = tall / K + pt * 2.0 * 8.0 * (kCkptTail + 1) * (I + 1);
         b += typical + tall;
     }
+    // the refine rounds' per-ZMW buffers beside the bands: ~9 unique single-base mutations per template base
+    // (Prepare's unique_mutation_count + 64), each with a code, a score, a flag and one delta per read (dDelta_:
+    // 43 MB for a 20 kb template with 30 reads, which the band-only estimate missed: 5 OOM retries in the 2000-ZMW
+    // configs[3] run, profiles/r5_mixed_2000_s8.json)
+    const double L = std::max(1, z.draft_len);
+    b += (9.0 * L + 64.0) * (8.0 * std::max(1, z.n_reads) + 13.0);
     return std::max(b, 4096.0);
 }
 
