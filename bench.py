@@ -543,17 +543,24 @@ def main():
         return report(args, rank, world, eng, slots, job_time, local_time, res, workload, scaling, total, qstats,
                       extra=extra, settings=settings)
 
-    # a step's ZMWs as BATCH_SPLIT device batches (the step is the workload's unit; the batch, the engine's)
-    def split(zs):
-        per = -(-len(zs) // max(1, args.batch_split))
-        return [zs[i:i + per] for i in range(0, len(zs), per)]
+    # the K steps as device batches of zmws_per_step / BATCH_SPLIT ZMWs, each made (pbccs_batch_create's per-ZMW
+    # setup and upload) and polished by a slot thread of the engine's queue (pbccs_polish_batch): batch creation
+    # is inside the timed region, pipelined with the other slots' polishes (made ahead it was
+    # 9% of the timed region, profiles/r5a_bench.json `prepare`)
+    import ctypes
+    from pbccs_amd import lib as L
+    from pbccs_amd.polish import _Marshalled
+    qset = pbccs_amd.ConsensusSettings(zmws_per_batch=-(-args.zmws_per_step // max(1, args.batch_split)))
+
+    def polish_queue(m):
+        opts = qset._c()
+        L.check(L.load().pbccs_polish_batch(eng._h, m._ins, len(m.zmws), ctypes.byref(opts), m._outs))
 
     # ---- warmup (untimed): W steps, concurrently over the slots like the timed ones ------------------
-    wb = [pbccs_amd.PreparedBatch(part, settings, eng) for w in range(args.warmup)
-          for part in split(synth.make_zmws(args.zmws_per_step, args.length, args.passes, seed=seed0 + 1000 + w))]
-    pbccs_amd.polish_many(wb)
-    for b in wb:
-        b.close()
+    wz = [z for w in range(args.warmup)
+          for z in synth.make_zmws(args.zmws_per_step, args.length, args.passes, seed=seed0 + 1000 + w)]
+    if wz:
+        polish_queue(_Marshalled(wz))
     log(rank, f"[bench] warmup done ({args.warmup} x {args.zmws_per_step} ZMWs over {slots} slots)")
 
     # ---- engine pools mapped before the timed region (a long run maps them once and reuses them) ----
@@ -563,27 +570,19 @@ def main():
         eng.reserve_pool(per_slot)
         log(rank, f"[bench] band pools: {per_slot / 2**30:.1f} GB mapped per slot x {slots}")
 
-    # ---- inputs resident in HBM before the timed region ------------------------------------------
-    # split three ways: the synthetic generation (Python strings: the stand-in for reading the subreads), the
-    # marshalling into the C structs of the boundary, and pbccs_batch_create (per ZMW the ArrowConfig's
-    # transition tables and expectations, the reverse-complement template, then the one-copy upload)
-    eng.counters(reset=True)
+    # ---- inputs before the timed region: the synthetic generation (Python strings: the stand-in for reading the
+    # subreads) and their marshalling into the C structs of the boundary (the stand-in for the reader's records)
     t_prep = time.perf_counter()
-    synth_s = 0.0
-    batches = []
+    zs_all = []
     for k in range(args.steps):
-        ts = time.perf_counter()
-        zs = synth.make_zmws(args.zmws_per_step, args.length, args.passes, seed=seed0 + k)
-        synth_s += time.perf_counter() - ts
-        batches.extend(pbccs_amd.PreparedBatch(part, settings, eng) for part in split(zs))
-    sync()
-    prep = {"synth_s": round(synth_s, 3), "marshal_s": round(sum(b.marshal_s for b in batches), 3),
-            "create_s": round(sum(b.create_s for b in batches), 3)}
+        zs_all.extend(synth.make_zmws(args.zmws_per_step, args.length, args.passes, seed=seed0 + k))
+    synth_s = time.perf_counter() - t_prep
+    tm = time.perf_counter()
+    marshalled = _Marshalled(zs_all)
+    prep = {"synth_s": round(synth_s, 3), "marshal_s": round(time.perf_counter() - tm, 3)}
     log(rank, f"[bench] prepared {args.steps} steps x {args.zmws_per_step} ZMWs in {time.perf_counter() - t_prep:.1f}s "
               f"{prep}")
-    c0 = eng.counters(reset=True)
-    prep["create_host_s"] = round(c0["create_host_ns"] / 1e9, 3)
-    prep["create_upload_s"] = round(c0["create_upload_ns"] / 1e9, 3)
+    eng.counters(reset=True)
     eng.kernel_stats(reset=True)
 
     # ---- timed region: exactly K steps --------------------------------------------------------
@@ -591,24 +590,24 @@ def main():
     sync()
     host = HostUsage()
     t0 = time.perf_counter()
-    pbccs_amd.polish_many(batches)   # the K steps, pipelined over the slots' HIP streams / host threads
+    polish_queue(marshalled)   # the K steps: batches made and polished by the slots' host threads / HIP streams
     sync()
     barrier()
     local_time = time.perf_counter() - t0
     log(rank, f"[bench] {args.steps} steps done t={local_time:.2f}s")
     job_time = max_over_ranks(local_time, world)
 
-    res = [r for b in batches for r in b.results()]
-    zs_all = [z for b in batches for z in b.zmws]
+    res = marshalled.results()
     hostu = host.report(len(res), world)
-    for b in batches:
-        b.close()
-    prep["create_frac_of_timed"] = round(prep["create_s"] / local_time, 4)
-    prep["note"] = ("outside the timed region (the reads resident in HBM when it starts): synth_s the synthetic "
-                    "subreads, marshal_s the C structs, create_s pbccs_batch_create (create_host_s of it the batch's "
-                    "copy of its inputs and the read pool, create_upload_s the reservations and the read upload).  "
-                    "Inside it: the per-ZMW setup of Consensus.h:437-453 (transition tables, expectations, "
-                    "reverse-complement template, descriptor arena), derive_thread_s_in_timed of slot-thread time")
+    c0 = eng.counters()
+    prep["create_thread_s_in_timed"] = round((c0["create_host_ns"] + c0["create_upload_ns"]) / 1e9, 3)
+    prep["create_host_s"] = round(c0["create_host_ns"] / 1e9, 3)
+    prep["create_upload_s"] = round(c0["create_upload_ns"] / 1e9, 3)
+    prep["note"] = ("outside the timed region: synth_s the synthetic subreads, marshal_s the boundary's C structs "
+                    "(the reader's part).  Inside it, on the slot threads: pbccs_batch_create per device batch "
+                    "(create_host_s the batch's copy of its inputs and the read pool, create_upload_s the "
+                    "reservations and the read upload) and the per-ZMW setup of Consensus.h:437-453 (transition "
+                    "tables, expectations, reverse-complement template, descriptor arena: derive_thread_s_in_timed)")
     workload = (f"configs[1]: synthetic {args.length} bp insert, {args.passes} full passes, "
                 f"{args.zmws_per_step} ZMWs per step")
     report(args, rank, world, eng, slots, job_time, local_time, res, workload, "weak", len(res) * world,
