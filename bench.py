@@ -35,11 +35,11 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # PMC HBM bytes per launch of each fill kind (tools/gpu_steps.sh traffic -> tools/pmc_traffic.py); used only while
 # the kernel sources still hash to the digest the profile was taken at
-TRAFFIC_PROFILES = {"k_fill_tall": "r4_traffic_fill_tall.json", "k_fill": "r4_traffic_fill.json",
-                    "k_score": "r4_traffic_score.json"}
+TRAFFIC_PROFILES = {"k_fill_tall": "r5_traffic_fill_tall.json", "k_fill": "r5_traffic_fill.json",
+                    "k_score": "r5_traffic_score.json"}
 # the same command on one workspace slot (--streams 1): the dominant kernel's launch duration there is not
 # time-shared with other batches' launches; used only while the kernel sources hash to its digest
-SINGLE_SLOT_PROFILE = "r4_streams1_bench.json"
+SINGLE_SLOT_PROFILE = "r5_streams1_bench.json"
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
 FLOP_PER_CELL = 11             # fill cell 6 mul + 3 add + <= 1 div, + the column rescale
 CHAIN_ROW_CYCLES = 21.5        # one band row of the tall fills' chain at 2 rows per lane (tools/ubench/chain_step.hip

@@ -30,6 +30,12 @@ step() {
         > $OUT/pytest_gpu.log 2>&1; local rc=$?; tail -3 $OUT/pytest_gpu.log; return $rc ;;
     smoke)
       timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && tail -1 $OUT/smoke.log ;;
+    evidence) # the round's committed inputs of the bench line, then the line: PMC traffic and VALU passes and the
+              # single-slot run of the final sources copied to profiles/ under the names bench.py reads, then the
+              # driver's command and the occupancy build's
+      step traffic && for k in fill_tall fill score; do cp $OUT/traffic_$k.json profiles/r5_traffic_$k.json; done && \
+        step valu && cp $OUT/valu_per_cell.json profiles/r5_valu_per_cell.json && \
+        step bench1 && cp $OUT/bench_streams1.json profiles/r5_streams1_bench.json && step bench && step occ ;;
     bench)    # the driver's command
       timeout -k 10 400 $BENCH --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err && summ $OUT/bench.json ;;
     bench5)
