@@ -1092,6 +1092,7 @@ WAVE_FAMILIES = {"k_fill": ("k_fill_coopILi16E",), "k_fill_tall": ("k_fill_coopI
                  "k_score": ("7k_scoreE",), "k_suffix": ("8k_suffixE",),
                  "k_reduce": ("8k_reduceE",)}
 VALU_PROFILE = "r5_valu_per_cell.json"   # SQ_INSTS_VALU per kernel family (tools/gpu_steps.sh valu)
+OCC_PROFILE = "r5_occupancy_bench.json"  # the driver's command on the occupancy build (tools/gpu_steps.sh occ)
 
 
 def occupancy_report(stats, local_time):
@@ -1194,6 +1195,14 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
 
     roofline = make_roofline(stats, local_time, workload)
     occ = occupancy_report(stats, local_time)
+    if occ is None and workload.startswith("configs[1]"):
+        # the default build has no wave stamps: the committed occupancy run of the same sources stands in
+        opath = os.path.join(ROOT, "profiles", OCC_PROFILE)
+        if os.path.exists(opath):
+            o = json.load(open(opath))
+            if o.get("roofline", {}).get("source_digest") == kernel_source_digest():
+                occ = dict(o["roofline"].get("occupancy") or {})
+                occ["source"] = f"profiles/{OCC_PROFILE} (the occupancy build, same kernel sources, same command)"
     if occ:
         roofline["occupancy"] = occ
         roofline["binding_measured"] = (
