@@ -347,16 +347,19 @@ def cpu_share_note():
             "vs_cpu_full_host: against that rate scaled linearly to all `nproc` hardware threads of the node")
 
 
+KERNEL_SOURCES = ("arrow_device.hpp", "arrow_kernels.hip", "arrow_kernels.hpp", "coop_chain.hpp", "fill_coop.hip")
+
+
 def kernel_source_digest():
-    """sha256 (16 hex) of the HIP/C++ sources of the engine: a PMC traffic profile is valid for the build it was
-    taken on, and stale once any kernel source changes."""
+    """sha256 (16 hex) of the Arrow path's device code (KERNEL_SOURCES): a committed PMC profile (traffic, VALU per
+    launch) or single-slot / occupancy run is valid for the kernels it was taken on, and stale once any of them
+    changes.  Host-side engine edits (engine.hip, capi.hip) do not change a launch's instructions or bytes."""
     import hashlib
     d = os.path.join(ROOT, "pbccs_amd", "csrc")
     h = hashlib.sha256()
-    for f in sorted(os.listdir(d)):
-        if f.endswith((".hip", ".hpp", ".cpp", ".h")):
-            h.update(f.encode())
-            h.update(open(os.path.join(d, f), "rb").read())
+    for f in KERNEL_SOURCES:
+        h.update(f.encode())
+        h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()[:16]
 
 
