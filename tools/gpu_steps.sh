@@ -42,7 +42,7 @@ step() {
       timeout -k 10 300 $BENCH --steps 5 --warmup 1 --cpu-sample 0 > $OUT/bench5.json 2> $OUT/bench5.err && summ $OUT/bench5.json ;;
     prof)     # rocprofv3 kernel summary of the driver's command
       timeout -k 10 500 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof -o run -- $BENCH --gpus 1 --steps 20 \
-        --warmup 5 --cpu-sample 0 > $OUT/bench_prof.json 2> $OUT/bench_prof.err && summ $OUT/bench_prof.json && \
+        --warmup 5 > $OUT/bench_prof.json 2> $OUT/bench_prof.err && summ $OUT/bench_prof.json && \
         cp "$(find $OUT/prof -name '*kernel_stats.csv' | head -1)" $OUT/kernel_stats.csv ;;
     prof1)    # single slot: kernel durations that are not time-shared
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof1 -o run -- $BENCH --streams 1 --steps 5 \
@@ -50,7 +50,7 @@ step() {
         summ $OUT/bench_streams1_prof.json && \
         cp "$(find $OUT/prof1 -name '*kernel_stats.csv' | head -1)" $OUT/streams1_kernel_stats.csv ;;
     bench1)   # single slot, no profiler
-      timeout -k 10 300 $BENCH --streams 1 --steps 5 --warmup 1 --cpu-sample 0 > $OUT/bench_streams1.json \
+      timeout -k 10 300 $BENCH --streams 1 --steps 5 --warmup 1 > $OUT/bench_streams1.json \
         2> $OUT/bench_streams1.err && summ $OUT/bench_streams1.json ;;
     trace)    # per-round trace of the driver's command (phase walls per batch round, fill launch sets)
       PBCCS_ROUND_TRACE=1 PBCCS_FILL_PATHS=1 timeout -k 10 400 $BENCH --gpus 1 --steps 20 --warmup 5 --cpu-sample 0 \
@@ -145,7 +145,7 @@ step() {
     occ)      # the driver's command on the occupancy build (wave stamps on: built by
               # AB_FLAGS="-DPBCCS_WAVE_STAMPS=1" AB_OUT=pbccs_amd/_lib_occ tools/build_ab.sh HEAD): roofline.occupancy
       PBCCS_LIB=pbccs_amd/_lib_occ/libpbccs_amd.so timeout -k 10 400 $BENCH --gpus 1 --steps 20 --warmup 5 \
-        --cpu-sample 0 > $OUT/bench_occ.json 2> $OUT/bench_occ.err && summ $OUT/bench_occ.json && \
+        > $OUT/bench_occ.json 2> $OUT/bench_occ.err && summ $OUT/bench_occ.json && \
         python3 -c "import json; d=json.load(open('$OUT/bench_occ.json')); print(json.dumps(d['roofline'].get('occupancy')))" ;;
     ab_tree)  # interleaved A/B of whole trees (git worktrees of older revisions under _ab/, built in-tree): TREES="a b"
       local k=0
