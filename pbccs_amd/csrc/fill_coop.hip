@@ -1037,7 +1037,7 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
 // and template window.
 // Group g of block b fills task 4b + g (G = 16) / task b (G = 64).  (A dynamic assignment -- a group that finished
 // its read taking the launch's next task from a counter, against the 36% idle group slots of lock-step waves,
-// profiles/r5c_fill_work_bench.json -- measured no faster, and its second inlined copy of the fill cost 5% of the
+// profiles/r5c_fill_work.json -- measured no faster, and its second inlined copy of the fill cost 5% of the
 // headline in instruction-cache footprint: removed)
 // ------------------------------------------------------------------------------------------------
 template <int G, int MINW, bool GC, int R>
