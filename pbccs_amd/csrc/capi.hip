@@ -995,6 +995,10 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
             } else if (r == PBCCS_EOOM) {
                 std::lock_guard<std::mutex> lk(deferMu);
                 deferred.emplace_back(start[b], start[b + 1]);
+                double est = 0.0;   // one line per deferred batch: what the plan expected, what ran out
+                for (const pbccs_zmw_input& z : bin) est += zmw_est_bytes(z);
+                std::fprintf(stderr, "[queue] batch %d (%d ZMWs, estimated %.1f GB) deferred on slot %d: %s\n", b,
+                             start[b + 1] - start[b], est / 1e9, slot, g_lastError.c_str());
             } else {
                 rc[slot] = r;
                 err[slot] = g_lastError;
