@@ -49,6 +49,9 @@ constexpr long long kTallFirstDiv = 25;
 constexpr int kCkptDefaultK = 8;
 constexpr int kCkptDefaultMinLen = 4000;
 constexpr int kCkptSlotsMax = 2048;   // k_score_ckpt persistent waves (2 per SIMD at its register budget)
+// the replay slots' memory per scoring launch: fewer persistent waves once the slots outgrow it (a 20 kb read's
+// exploded band asked 2048 slots x 2.9 MB = 5.8 GB beside full band pools: an OOM retry in configs[3])
+constexpr long long kCkptSlotBytes = 1ll << 30;
 int env_int(const char* name, int dflt)
 {
     const char* e = std::getenv(name);
@@ -1484,6 +1487,9 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
             sc.cap = dScratch_.cap;
             sc.overflow = dScratchOverflow_.ptr;
             if (ck.nTasks > 0) {
+                const long long fit = kCkptSlotBytes / std::max<long long>(1, ckSlotCap_ * (long long)sizeof(double));
+                ck.nSlots = (int)std::max<long long>(
+                    1, std::min<long long>(std::min<long long>(ck.nTasks, kCkptSlotsMax), std::max<long long>(64, fit)));
                 ws_->ckSlots.reserve((size_t)ck.nSlots * ckSlotCap_, false);
                 ck.slots = ws_->ckSlots.ptr;
                 ck.slotCap = ckSlotCap_;
