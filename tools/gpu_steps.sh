@@ -36,6 +36,11 @@ step() {
       step traffic && for k in fill_tall fill score; do cp $OUT/traffic_$k.json profiles/r5_traffic_$k.json; done && \
         step valu && cp $OUT/valu_per_cell.json profiles/r5_valu_per_cell.json && \
         step bench1 && cp $OUT/bench_streams1.json profiles/r5_streams1_bench.json && step bench && step occ ;;
+    apiccs)   # HIP API trace of the ccs stage (no counters): calls per API, e.g. no hipDeviceSynchronize in steady state
+      timeout -k 10 500 rocprofv3 --hip-trace --stats -f csv -d $OUT/apiccs -o run -- $BENCH --stage ccs --steps 5 \
+        --warmup 1 --cpu-sample 0 > $OUT/ccs_api.json 2> $OUT/ccs_api.err && \
+        cp "$(find $OUT/apiccs -name '*hip_api_stats.csv' | head -1)" $OUT/ccs_hip_api_stats.csv && \
+        grep -E "hipDeviceSynchronize|hipFree\"|hipMalloc\"|hipStreamSynchronize|hipMemcpyAsync" $OUT/ccs_hip_api_stats.csv | cut -c1-120 ;;
     bench)    # the driver's command
       timeout -k 10 400 $BENCH --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err && summ $OUT/bench.json ;;
     bench5)
