@@ -534,8 +534,9 @@ static int create_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, con
         b->n = n;
         b->slot = slot >= 0 ? slot : eng->nextSlot++ % std::max(1, eng->concurrency);
         b->inputs.assign(in, n);
-        // every batch gets its own streams (ArrowBatch's ownStreams)
-        b->B.reset(new ArrowBatch(eng->device, eng->Slot(b->slot), true));
+        // every batch gets its own streams (ArrowBatch's ownStreams); a batch made and polished on its slot's thread
+        // (slot >= 0: the queue, the ccs chunks, reruns) uses the slot's descriptor arena and read pool
+        b->B.reset(new ArrowBatch(eng->device, eng->Slot(b->slot), true, slot >= 0));
         b->B->SetProfiling(eng->profiling);
         ArrowOptions ao;
         ao.scoreDiff = b->o.score_diff;

@@ -170,15 +170,17 @@ void VmPool::map_to(size_t n, bool soft)
                         std::to_string(want >> 20) + " MB");
 }
 
-void VmPool::unmap_all()
+void VmPool::unmap_all(hipStream_t s)
 {
     if (!vmm_) {
+        if (s) (void)hipStreamSynchronize(s);
         fallback_.release();
         ptr = nullptr;
         cap = 0;
         return;
     }
-    (void)hipDeviceSynchronize();
+    if (s) (void)hipStreamSynchronize(s);
+    else (void)hipDeviceSynchronize();
     size_t off = 0;
     for (size_t k = 0; k < handles_.size(); ++k) {
         (void)hipMemUnmap(reinterpret_cast<char*>(ptr) + off, sizes_[k]);
@@ -239,7 +241,7 @@ void Workspace::EnsureStreams()
     PBCCS_HIP(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
 }
 
-ArrowBatch::ArrowBatch(int device, Workspace* shared, bool ownStreams)
+ArrowBatch::ArrowBatch(int device, Workspace* shared, bool ownStreams, bool wsBuffers)
     : device_(device),
       ownWs_(shared ? nullptr : new Workspace()),
       ws_(shared ? shared : ownWs_.get()),
@@ -254,7 +256,8 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared, bool ownStreams)
       dPosOff_(ws_->posOff), dQv_(ws_->qv), dList_(ws_->list), dEdge_(ws_->edge), dEdgeCount_(ws_->edgeCount),
       dDelta_(ws_->delta), dScore_(ws_->score), dFav_(ws_->fav), dScratch_(ws_->scratch),
       dScratchTop_(ws_->scratchTop), dScratchOverflow_(ws_->scratchOverflow), dStats_(ws_->stats),
-      eventPool_(ws_->eventPool)
+      eventPool_(ws_->eventPool), dDesc_(wsBuffers && shared ? ws_->desc : ownDesc_),
+      dSeq_(wsBuffers && shared ? ws_->seq : ownSeq_)
 {
     PBCCS_HIP(hipSetDevice(device_));
     // first value-region estimate per read (PBCCS_INITIAL_BAND_HEIGHT overrides it: tests use a tiny one

@@ -169,7 +169,8 @@ struct VmPool {
     void try_reserve(size_t n);
     // Unmap every granule; the next reserve maps afresh at a new address range (never at the addresses just
     // unmapped, see unmap_all).  Synchronises.
-    void unmap_all();
+    // s: the stream whose work last used the pool (synchronised instead of the whole device); nullptr: the device
+    void unmap_all(hipStream_t s = nullptr);
     size_t mapped_bytes() const { return vmm_ ? mappedBytes_ : cap * sizeof(double); }
     ~VmPool();
     VmPool() = default;
@@ -243,6 +244,7 @@ struct Workspace {
     DevVec<double> colScratch;
     DevVec<unsigned long long> bump;
     PinnedBuf hDesc;
+    DevVec<char> desc, seq;   // the descriptor arena and read pool of the slot's current batch (wsBuffers)
     DevVec<int2> ckPairs;
     DevVec<long long> ckStart;
     DevVec<double> rBaseline;
@@ -282,7 +284,10 @@ public:
     // out of memory (pools unmapped and mapped again) scored wrong (tools/oom_dbg.py: 23 of 26 ZMWs; cause not
     // found -- own streams, or own per-round buffers, each made it exact), and own streams measured +2.6% at the
     // driver's command (interleaved A/B).  The fine-grained scorers keep the workspace's.
-    explicit ArrowBatch(int device, Workspace* shared = nullptr, bool ownStreams = false);
+    // wsBuffers: the descriptor arena and read pool are the workspace's (a slot's batches made and polished one after
+    // another: no hipMalloc / hipFree per batch -- 13.5 ms each on a busy device, 508 per ccs run); otherwise the
+    // batch's own (batches made ahead, several alive per slot)
+    explicit ArrowBatch(int device, Workspace* shared = nullptr, bool ownStreams = false, bool wsBuffers = false);
     ~ArrowBatch();
     ArrowBatch(const ArrowBatch&) = delete;
     ArrowBatch& operator=(const ArrowBatch&) = delete;
@@ -424,7 +429,9 @@ private:
     // device state owned by the batch (inputs + descriptors).  The per-ZMW and per-read descriptors and the
     // template pool live in one device arena, filled by one copy from a page-locked staging buffer per
     // UploadDescriptors (UploadDescriptors sets the typed views below).
-    DevVec<char> dDesc_, dSeq_;
+    DevVec<char> ownDesc_, ownSeq_;
+    DevVec<char>& dDesc_;
+    DevVec<char>& dSeq_;
     PinnedBuf& hDesc_;
     int *pZFwd_ = nullptr, *pZRev_ = nullptr, *pZLen_ = nullptr, *pZReadBegin_ = nullptr, *pZNReads_ = nullptr;
     double* pZCtx_ = nullptr;

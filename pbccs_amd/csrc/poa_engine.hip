@@ -558,6 +558,7 @@ PoaRunner::~PoaRunner()
 void PoaRunner::Align(std::vector<AlignRequest>& reqs, std::vector<AlignResult>* out)
 {
     check(hipSetDevice(device_), "hipSetDevice");
+    const StreamScope bound(stream_);   // the runner's buffers grow stream-ordered (no device-wide sync)
     const int n = (int)reqs.size();
     out->assign(n, AlignResult());
     if (n == 0) return;

@@ -201,7 +201,7 @@ public:
     void SetPoolBudget(size_t bytes) { budget_ = bytes; }
     // Unmap the score-matrix pool (the address reservation stays): the polish that follows the POA in a
     // ccs run then has the device memory to itself.
-    void ReleasePool() { dPool_.unmap_all(); }
+    void ReleasePool() { dPool_.unmap_all(stream_); }   // only this runner's stream uses the pool
     size_t PoolMappedBytes() const { return dPool_.mapped_bytes(); }
     int HostThreads() const { return threads_; }
     void ParallelFor(int n, const std::function<void(int)>& f) { workers_->Run(n, f); }
