@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--ccs-chunk", type=int, default=0,
                     help="ccs stage: ZMWs per POA chunk / polish batch (0 = planned from free HBM)")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--one-stream", action="store_true",
+                    help="A/B: each batch on one HIP stream (the tall fills behind the 16-lane fill), PBCCS_ONE_STREAM")
     ap.add_argument("--stage", choices=["polish", "poa", "ccs", "quiver"], default="polish",
                     help="polish: the headline line (Consensus.h's Arrow polish, from the draft on); poa: the POA "
                          "draft step before it (SparsePoa over each ZMW's raw subreads, SURVEY.md §8(f) row 1) on "
@@ -89,7 +91,10 @@ def parse():
                          "ExtractMappedRead, polish), the POA of the next steps overlapping the polish; quiver: "
                          "the Quiver family (QV-feature reads, FP32 log-space recursions) through "
                          "pbccs_quiver_polish_batch on configs[1]-shaped ZMWs")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.one_stream:   # read by the engine when it makes a batch (before any HIP call here)
+        os.environ["PBCCS_ONE_STREAM"] = "1"
+    return a
 
 
 _JSON_OUT = None   # the process's real stdout while fd 1 is pointed at stderr (multi-rank runs)

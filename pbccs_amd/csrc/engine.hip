@@ -268,7 +268,11 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared, bool ownStreams, bool wsBu
     if (ownStreams) {
         ownStreams_ = true;
         PBCCS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-        PBCCS_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
+        // PBCCS_ONE_STREAM=1 (A/B): the tall fills queue behind the 16-lane fill on the batch's one stream, so twice
+        // the slots fit the hardware queues
+        static const bool oneStream = env_int("PBCCS_ONE_STREAM", 0) != 0;
+        if (oneStream) stream2_ = stream_;
+        else PBCCS_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
         PBCCS_HIP(hipEventCreateWithFlags(&evFork_, hipEventDisableTiming));
         PBCCS_HIP(hipEventCreateWithFlags(&evJoin_, hipEventDisableTiming));
     } else {
@@ -300,7 +304,7 @@ ArrowBatch::~ArrowBatch()
         if (ownStreams_) {
             (void)hipEventDestroy(evFork_);
             (void)hipEventDestroy(evJoin_);
-            (void)hipStreamDestroy(stream2_);
+            if (stream2_ != stream_) (void)hipStreamDestroy(stream2_);
             (void)hipStreamDestroy(stream_);
         }
     }
