@@ -41,6 +41,10 @@ step() {
         --warmup 1 --cpu-sample 0 > $OUT/ccs_api.json 2> $OUT/ccs_api.err && \
         cp "$(find $OUT/apiccs -name '*hip_api_stats.csv' | head -1)" $OUT/ccs_hip_api_stats.csv && \
         grep -E "hipDeviceSynchronize|hipFree\"|hipMalloc\"|hipStreamSynchronize|hipMemcpyAsync" $OUT/ccs_hip_api_stats.csv | cut -c1-120 ;;
+    bench2r)  # the headline on two self-launched ranks pinned to the one device (a rehearsal of --gpus N)
+      PBCCS_BENCH_DEVICE=0 timeout -k 10 400 $BENCH --gpus 2 --steps 4 --warmup 1 --streams 4 > $OUT/bench_2ranks.json \
+        2> $OUT/bench_2ranks.err && summ $OUT/bench_2ranks.json && \
+        python3 -c "import json; d=json.load(open('$OUT/bench_2ranks.json')); print(d['n_gpus'], d['scaling'], d.get('parity_sample', {}).get('ok'))" ;;
     bench)    # the driver's command
       timeout -k 10 400 $BENCH --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err && summ $OUT/bench.json ;;
     bench5)
