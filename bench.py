@@ -18,6 +18,7 @@ rank 0 prints one JSON line.
 """
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -182,6 +183,19 @@ def cpu_threads(args, n):
     return max(1, min(threads, n))
 
 
+def full_host(cb, threads):
+    """The node-wide CPU figure beside the measured one: this job's CPU share is `threads` of the host's
+    hardware threads (the boxes give one GPU's job 16 cores: OMP_NUM_THREADS / affinity), so the whole host's rate
+    is not measured here -- it is the measured rate scaled linearly to every hardware thread (an upper bound: SMT
+    siblings share cores), labelled as such in the line."""
+    nproc = os.cpu_count() or threads
+    cb["full_host_value"] = round(cb["value"] * nproc / threads, 4)
+    cb["full_host_method"] = (f"not measured: the {threads}-thread rate scaled linearly to all {nproc} hardware "
+                              f"threads (SMT siblings share cores, so an upper bound on the host's rate); "
+                              f"the job's affinity allows {len(os.sched_getaffinity(0))} threads")
+    return cb
+
+
 def oracle_record(z, settings):
     """Consensus.h:436-512 for one ZMW on the CPU restatement (oracle/arrow_oracle.cpp), with the gates the batch
     polish applies (capi.hip polish_one): AddRead of every read, MinPasses / MaxDropFraction, ZScores,
@@ -286,17 +300,51 @@ def sampled_cpu_baseline(args, settings, zs, res, idx, costs=None):
     else:
         c_s = sum(costs[i] for i in idx)
         mean_all = sum(costs) / len(costs)
-        core_s_per_zmw = (sum(secs) / c_s) * mean_all   # ratio estimator x the workload's mean cost
+        ratio_core_s = (sum(secs) / c_s) * mean_all   # ratio estimator x the workload's mean cost (linear in cost)
+        # CPU time grows faster than the cost model (the survey: 48x the time for 20x the cost), so the linear ratio
+        # estimator, fed by a capped sample, understates the expensive ZMWs.  The stratified sample spans the
+        # eligible cost range; a power law t = a c^alpha fitted to it by least squares in log-log predicts every
+        # timed ZMW's time (alpha floored at 1: never below the linear estimate)
+        fit = power_law_fit([costs[i] for i in idx], secs)
+        if fit is not None:
+            a, alpha = fit
+            alpha_used = max(1.0, alpha)
+            a_used = a if alpha >= 1.0 else math.log(sum(secs) / sum(costs[i] ** alpha_used for i in idx))
+            core_s_per_zmw = sum(math.exp(a_used) * c ** alpha_used for c in costs) / len(costs)
+        else:
+            alpha = alpha_used = None
+            core_s_per_zmw = ratio_core_s
         cb["value"] = round(threads / core_s_per_zmw, 4)
         cb["extrapolated"] = {"core_s_per_zmw": round(core_s_per_zmw, 3), "sample_core_s": round(sum(secs), 2),
                               "cost_sample_mean": c_s / n, "cost_workload_mean": mean_all,
-                              "method": "ratio estimator: the sample's CPU seconds per unit of cost (template length "
-                                        "x read bases) times the workload's mean cost, on `cores` threads"}
+                              "alpha_fitted": None if alpha is None else round(alpha, 3),
+                              "alpha_used": None if alpha_used is None else round(alpha_used, 3),
+                              "ratio_estimator_core_s_per_zmw": round(ratio_core_s, 3),
+                              "ratio_estimator_value": round(threads / ratio_core_s, 4),
+                              "method": "sample stratified by cost (template length x read bases) over the eligible "
+                                        "range; power law t = a cost^alpha fitted in log-log on the sample (alpha >= "
+                                        "1), summed over every timed ZMW's cost, on `cores` threads; the linear "
+                                        "ratio estimator beside it"}
         desc += "; the workload's rate extrapolated from it (BASELINE.md CPU-baseline plan)"
     cb["sample"] = desc
     # the host's whole thread count, if the pool scaled linearly to it (an upper bound: SMT threads share cores)
-    cb["full_host_value"] = round(cb["value"] * (os.cpu_count() or threads) / threads, 4)
+    full_host(cb, threads)
     return cb, parity
+
+
+def power_law_fit(costs, secs):
+    """Least squares of log t = a + alpha log c over the sample (ZMWs with positive cost and time); None when the
+    sample cannot determine a slope."""
+    pts = [(math.log(c), math.log(t)) for c, t in zip(costs, secs) if c > 0 and t > 0]
+    if len(pts) < 3:
+        return None
+    mx = sum(x for x, _ in pts) / len(pts)
+    my = sum(y for _, y in pts) / len(pts)
+    sxx = sum((x - mx) ** 2 for x, _ in pts)
+    if sxx <= 1e-12:
+        return None
+    alpha = sum((x - mx) * (y - my) for x, y in pts) / sxx
+    return my - alpha * mx, alpha
 
 
 SAMPLE_COST_CAP = 8.5e8   # zmw_cost of a 10 kb / 8-pass ZMW: the largest ZMW a bounded CPU sample polishes
@@ -311,9 +359,17 @@ def sample_indices(args, n_timed, costs=None):
     if costs is None:
         step = max(1, n_timed // n)
         return list(range(0, n_timed, step))[:n]
-    elig = [i for i in range(n_timed) if costs[i] <= SAMPLE_COST_CAP]
+    elig = sorted((i for i in range(n_timed) if 0 < costs[i] <= SAMPLE_COST_CAP), key=lambda i: (costs[i], i))
     rng = random.Random(args.seed + 99991)
-    return sorted(rng.sample(elig, min(n, len(elig))))
+    if len(elig) <= n:
+        return sorted(elig)
+    # stratified: the eligible ZMWs in cost order cut into n strata of equal count, one seeded draw
+    # from each -- the sample spans the eligible cost range instead of clustering where the cheap ZMWs are
+    out = []
+    for k in range(n):
+        lo, hi = len(elig) * k // n, len(elig) * (k + 1) // n
+        out.append(elig[rng.randrange(lo, hi)])
+    return sorted(out)
 
 
 def coverage(costs, idx_pool_cap=SAMPLE_COST_CAP):
@@ -650,7 +706,7 @@ def poa_cpu_baseline(args, steps_in, res, n):
           "sample": f"{n} of the timed ZMWs (every {max(1, len(flat_in) // n)}-th), oracle/poa_oracle.cpp SparsePoa "
                     f"(OrientAndAddRead per subread, FindConsensus) one ZMW per task on {threads} host threads, "
                     f"{dt:.1f} s wall"}
-    cb["full_host_value"] = round(cb["value"] * (os.cpu_count() or threads) / threads, 4)
+    full_host(cb, threads)
     parity = {"n": n, "draft_equal": n - len(bad), "mismatched_zmws": bad[:16], "ok": not bad,
               "checked": "GPU drafts, read keys and PoaAlignmentSummary extents of the timed run against "
                          "oracle/poa_oracle.cpp on the same subreads, bit-exact"}
@@ -768,7 +824,7 @@ def quiver_cpu_baseline(args, zs, res):
           "nproc": os.cpu_count(),
           "sample": f"{n} of the timed Quiver ZMWs (every {max(1, len(zs) // n)}-th), oracle/quiver_oracle.cpp AddRead + "
                     f"RefineConsensus + ConsensusQVs one ZMW per task on {threads} host threads, {dt:.1f} s wall"}
-    cb["full_host_value"] = round(cb["value"] * (os.cpu_count() or threads) / threads, 4)
+    full_host(cb, threads)
     parity = {"n": n, "consensus_equal": cons_eq, "counts_equal": counts_eq, "qvs_equal": qv_eq,
               "mismatched_zmws": bad[:16], "ok": not bad,
               "checked": "GPU records of the timed run against oracle/quiver_oracle.cpp on the same scorers: "
@@ -944,7 +1000,7 @@ def ccs_cpu_baseline(args, settings, work, res, n):
                     f"SparsePoa, ExtractMappedRead, oracle/arrow_oracle.cpp AddRead, the TooFewPasses / "
                     f"TooManyUnusable gates, RefineConsensus and ConsensusQVs of converged ZMWs, one ZMW per task on "
                     f"{threads} host threads, {dt:.1f} s wall"}
-    cb["full_host_value"] = round(cb["value"] * (os.cpu_count() or threads) / threads, 4)
+    full_host(cb, threads)
     parity = {"n": n, "record_equal": n - len(bad), "max_qv_diff": max_qv, "mismatched_zmws": bad[:16],
               "ok": not bad,
               "checked": "GPU records of the timed run against the CPU pipeline on the same subreads: status, "
@@ -1268,6 +1324,11 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
     if "prepare" in extra:
         out["prepare"] = extra["prepare"]
         out["prepare"]["derive_thread_s_in_timed"] = round(counters.get("derive_ns", 0) / 1e9, 3)
+        # the reader's share outside the timed region, as a fraction of it (in ccs reading overlaps the polish;
+        # here it is not pipelined: VERDICT r5 item 7)
+        timed_s = out.get("ms_per_step", 0.0) * out.get("steps", 0) / 1e3
+        if timed_s > 0 and "marshal_s" in out["prepare"]:
+            out["prepare"]["marshal_frac_of_timed"] = round(out["prepare"]["marshal_s"] / timed_s, 4)
     parity_ok = True
     # the CPU leg on rank 0 (one rank: its records are the run's; several ranks: rank 0 holds the whole cell's
     # records for the strong-scaling cell, its own for the weak-scaling lines)

@@ -536,7 +536,9 @@ static int create_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, con
         b->inputs.assign(in, n);
         // every batch gets its own streams (ArrowBatch's ownStreams); a batch made and polished on its slot's thread
         // (slot >= 0: the queue, the ccs chunks, reruns) uses the slot's descriptor arena and read pool
-        b->B.reset(new ArrowBatch(eng->device, eng->Slot(b->slot), true, slot >= 0));
+        // PBCCS_SLOT_STREAMS=1 (debug / A/B): the slot workspace's persistent streams instead
+        static const bool slotStreams = std::getenv("PBCCS_SLOT_STREAMS") && std::getenv("PBCCS_SLOT_STREAMS")[0] == '1';
+        b->B.reset(new ArrowBatch(eng->device, eng->Slot(b->slot), !slotStreams, slot >= 0));
         b->B->SetProfiling(eng->profiling);
         ArrowOptions ao;
         ao.scoreDiff = b->o.score_diff;
@@ -720,6 +722,9 @@ static int polish_retry(pbccs_engine* eng, int slot, const pbccs_zmw_input* in, 
                         pbccs_zmw_output* out)
 {
     std::vector<std::pair<int, int>> todo{{0, n}};
+    // the slot's outgrown buffers go back to the device before the rerun (nothing of the slot is queued: its batches
+    // were destroyed, and the pools were unmapped with the device synchronised)
+    eng->Slot(slot)->TrimRetired();
     while (!todo.empty()) {
         const std::pair<int, int> span = todo.back();
         todo.pop_back();
@@ -1011,6 +1016,8 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
     std::vector<std::thread> pool;
     for (int s = 0; s < std::min(slots, nb); ++s) pool.emplace_back(worker, s);
     for (std::thread& t : pool) t.join();
+    // every batch of the call is destroyed (its streams synchronised): the slots' outgrown buffers can go
+    for (int s = 0; s < slots; ++s) eng->Slot(s)->TrimRetired();
     for (int s = 0; s < slots; ++s)
         if (rc[s] != PBCCS_OK) return fail(rc[s], err[s].c_str());
     if (!deferred.empty()) {
@@ -2032,6 +2039,7 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
             for (int s = 0; s < std::min(slots, nb); ++s) pool.emplace_back(worker, s);
         }
         for (std::thread& t : pool) t.join();
+        for (int s = 0; s < slots; ++s) eng->Slot(s)->TrimRetired();   // every chunk's batch is destroyed
         for (poa::PoaRunner* r : eng->PoaRunners()) {
             r->ReleasePool();
             r->SetPoolBudget(0);

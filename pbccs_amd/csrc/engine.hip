@@ -232,6 +232,20 @@ Workspace::~Workspace()
     if (stream) (void)hipStreamDestroy(stream);
 }
 
+size_t Workspace::TrimRetired()
+{
+    size_t b = 0;
+    auto t = [&](auto& v) { b += v.trim(); };
+    t(selBase); t(nSel); t(colScratch); t(bump); t(desc); t(seq); t(ckPairs); t(ckStart); t(rBaseline); t(rFlips);
+    t(rStatus); t(usedA); t(usedB); t(maxH); t(wZmw); t(wNMut); t(wMutBase); t(wDeltaBase); t(wWaveStart);
+    t(wMutStart); t(wPosStart); t(wPosBase); t(wQvBase); t(stats); t(aRange); t(bRange); t(aOff); t(bOff); t(aLs);
+    t(bLs); t(aPre); t(bSuf); t(fVal); t(fLs); t(fPre); t(fRange); t(fOff); t(codes); t(posOff); t(qv); t(list);
+    t(edge); t(edgeCount); t(ckSlots); t(ckCounter); t(delta); t(score); t(fav); t(scratch); t(scratchTop);
+    t(scratchOverflow); t(sel); t(selCount); t(selScore); t(selCode); t(selRank); t(selTmp);
+    b += val.trim_fallback();
+    return b;
+}
+
 void Workspace::EnsureStreams()
 {
     if (stream) return;
@@ -283,6 +297,20 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared, bool ownStreams, bool wsBu
         evJoin_ = ws_->evJoin;
     }
     const StreamScope bound(stream_);   // stream-ordered DevVec growth for this batch's calls (engine.hpp)
+    // PBCCS_DBG_CLEAR=1 (debug): the workspace's per-round scratch zeroed at every batch's start (does a batch
+    // depend on what the slot's previous batch left there?)
+    if (shared && std::getenv("PBCCS_DBG_CLEAR") && std::getenv("PBCCS_DBG_CLEAR")[0] == '1') {
+        PBCCS_HIP(hipDeviceSynchronize());
+        auto z = [](auto& v) {
+            if (v.ptr) PBCCS_HIP(hipMemset(v.ptr, 0, v.cap * sizeof(*v.ptr)));
+        };
+        Workspace& w = *ws_;
+        z(w.selBase); z(w.nSel); z(w.colScratch); z(w.bump); z(w.ckPairs); z(w.ckStart); z(w.rBaseline);
+        z(w.rFlips); z(w.rStatus); z(w.usedA); z(w.usedB); z(w.maxH); z(w.wZmw); z(w.wNMut); z(w.wMutBase);
+        z(w.wDeltaBase); z(w.wWaveStart); z(w.wMutStart); z(w.wPosStart); z(w.wPosBase); z(w.wQvBase); z(w.stats);
+        if (w.hDesc.ptr) std::memset(w.hDesc.ptr, 0, w.hDesc.cap);
+        PBCCS_HIP(hipDeviceSynchronize());
+    }
     dScratch_.reserve(kInitialScratch, false);
     dScratchTop_.reserve(1, false);
     // the read pool starts with 16 bytes of padding (see UploadDescriptors: word loads of read bases)
@@ -327,8 +355,15 @@ template <class F>
 void ArrowBatch::Timed(KernelKind k, F&& launch, hipStream_t st)
 {
     if (!st) st = stream_;
+    // PBCCS_DBG_SYNC=1 (debug): every launch waits for both of the batch's streams to drain (no two device
+    // operations of a batch overlap, and nothing is left queued when the host goes on)
+    static const bool dbgSync = std::getenv("PBCCS_DBG_SYNC") && std::getenv("PBCCS_DBG_SYNC")[0] == '1';
     if (!profiling_) {
         launch();
+        if (dbgSync) {
+            PBCCS_HIP(hipStreamSynchronize(stream_));
+            PBCCS_HIP(hipStreamSynchronize(stream2_));
+        }
         return;
     }
     hipEvent_t ev[2];
@@ -1051,6 +1086,9 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         if (forked) {
             PBCCS_HIP(hipEventRecord(evJoin_, stream2_));
             PBCCS_HIP(hipStreamWaitEvent(stream_, evJoin_, 0));
+            // PBCCS_DBG_JOINSYNC=1 (debug): the host also waits for the tall stream itself before the downloads
+            static const bool joinSync = std::getenv("PBCCS_DBG_JOINSYNC") && std::getenv("PBCCS_DBG_JOINSYNC")[0] == '1';
+            if (joinSync) PBCCS_HIP(hipStreamSynchronize(stream2_));
         }
         std::vector<int> st, fl, ua, ub, mh;
         std::vector<double> bl;

@@ -96,7 +96,10 @@ struct DevVec {
             if (keep && ptr && cap &&
                 hipMemcpyAsync(p, ptr, cap * sizeof(T), hipMemcpyDeviceToDevice, st) != hipSuccess)
                 throw DeviceError("device copy failed");
-            if (ptr) retired_.push_back(ptr);
+            if (ptr) {
+                retired_.push_back(ptr);
+                retiredCap_.push_back(cap);
+            }
         } else {
             if (keep && ptr && cap) {
                 if (hipDeviceSynchronize() != hipSuccess ||
@@ -114,10 +117,30 @@ struct DevVec {
     void release()
     {
         if (ptr) (void)hipFree(ptr);
-        for (T* q : retired_) (void)hipFree(q);
-        retired_.clear();
+        trim();
         ptr = nullptr;
         cap = 0;
+    }
+    // Free the buffers stream-ordered growth retired.  Only where no queued work can still read them: the caller
+    // has synchronised every stream that used this buffer (a hipFree also waits for the whole device, so the
+    // engine does this where the device is idle anyway: after a multi-batch call's slots joined, before an
+    // out-of-memory rerun).  Returns the bytes freed.
+    size_t trim()
+    {
+        size_t b = 0;
+        for (size_t k = 0; k < retired_.size(); ++k) {
+            b += retiredCap_[k] * sizeof(T);
+            (void)hipFree(retired_[k]);
+        }
+        retired_.clear();
+        retiredCap_.clear();
+        return b;
+    }
+    size_t retired_bytes() const
+    {
+        size_t b = 0;
+        for (size_t c : retiredCap_) b += c * sizeof(T);
+        return b;
     }
     DevVec() = default;
     DevVec(const DevVec&) = delete;
@@ -125,7 +148,8 @@ struct DevVec {
     ~DevVec() { release(); }
 
 private:
-    std::vector<T*> retired_;   // outgrown buffers of stream-ordered growth (freed by release)
+    std::vector<T*> retired_;   // outgrown buffers of stream-ordered growth (freed by trim / release)
+    std::vector<size_t> retiredCap_;
 };
 
 // Page-locked host staging (grow-only): copies from it go to the DMA engines asynchronously, where a copy from
@@ -172,6 +196,7 @@ struct VmPool {
     // s: the stream whose work last used the pool (synchronised instead of the whole device); nullptr: the device
     void unmap_all(hipStream_t s = nullptr);
     size_t mapped_bytes() const { return vmm_ ? mappedBytes_ : cap * sizeof(double); }
+    size_t trim_fallback() { return fallback_.trim(); }   // the hipMalloc fallback's retired buffers (DevVec::trim)
     ~VmPool();
     VmPool() = default;
     VmPool(const VmPool&) = delete;
@@ -235,6 +260,9 @@ struct Workspace {
     Workspace(const Workspace&) = delete;
     Workspace& operator=(const Workspace&) = delete;
     void EnsureStreams();   // creates the streams and fork/join events once
+    // Free every buffer the slot's stream-ordered growth retired (DevVec::trim): call only with the slot's work
+    // drained.  Returns the bytes freed (outgrown buffers otherwise stayed mapped for the engine's life).
+    size_t TrimRetired();
     hipStream_t stream = nullptr, stream2 = nullptr;   // a batch's main stream; the tall fills' stream
     hipEvent_t evFork = nullptr, evJoin = nullptr;
     std::vector<hipEvent_t> eventPool;                 // timing events (profiling)

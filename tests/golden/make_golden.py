@@ -306,6 +306,37 @@ def make_poa_kats():
     return {"poa_consensus": cases, "sparse_poa": sparse}
 
 
+def make_matrixtester_multiread():
+    """MatrixTester::TestMultiReadScorer (MatrixTester.cpp:212-384): the reference's one real multi-read ZMW -- a
+    222 bp template, SNR (15.49, 8.79, 13.52, 14.96) and 54 subreads with their strands and (often non-spanning)
+    template windows, each AddRead at threshold 1.0, then Score(INSERTION 202 'C').  The demo prints the score
+    and asserts nothing, so the fixture holds inputs only (parity against the restatement, not pinned)."""
+    src = open(os.path.join(REF, "ConsensusCore/src/Demos/MatrixTester.cpp")).read()
+    body = src[src.index("int MatrixTester::TestMultiReadScorer()"):]
+    body = body[:body.index("return 0;")]
+    tpl = re.search(r'std::string temp = "([ACGT]+)"', body).group(1)
+    snr = [float(x) for x in re.search(r"SNR snr\(([^)]*)\)", body).group(1).split(",")]
+    seqs = {int(k): (n, s) for k, n, s in re.findall(r'ArrowRead r(\d+) = MakeRead\("([^"]*)","([ACGT]*)"\);', body)}
+    mapped = re.findall(r"MappedArrowRead mr(\d+)\(r(\d+), StrandEnum::(FORWARD|REVERSE)_STRAND, (\d+), (\d+), "
+                        r"(true|false), (true|false) \);", body)
+    adds = re.findall(r"scorer\.AddRead\(mr(\d+), ([0-9.]+)\);", body)
+    mut = re.search(r"Mutation m\(MutationType::(\w+), (\d+), '([ACGT])'\);", body)
+    by_mr = {int(m[0]): m for m in mapped}
+    reads = []
+    for k, thr in adds:
+        m = by_mr[int(k)]
+        name, seq = seqs[int(m[1])]
+        reads.append({"name": name, "seq": seq, "strand": 1 if m[2] == "REVERSE" else 0, "ts": int(m[3]),
+                      "te": int(m[4]), "pin_start": m[5] == "true", "pin_end": m[6] == "true",
+                      "threshold": float(thr)})
+    assert len(reads) == 54, len(reads)
+    return {"source": "ConsensusCore/src/Demos/MatrixTester.cpp:212-384 (TestMultiReadScorer)",
+            "tpl": tpl, "snr": snr, "reads": reads,
+            "mutation": {"type": mut.group(1), "start": int(mut.group(2)), "base": mut.group(3)},
+            "note": "inputs only: the demo prints Score(m) without an expected value (parity unpinned by the "
+                    "reference; the GPU test compares with oracle/arrow_oracle.cpp)"}
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference tree not present; fixtures are committed, nothing to regenerate")
@@ -317,7 +348,9 @@ def main():
         json.dump(make_quiver_kats(), f, indent=1)
     with open(os.path.join(HERE, "poa_kats.json"), "w") as f:
         json.dump(make_poa_kats(), f, indent=1)
-    print("wrote arrow_kats.json, zmw6251.json, quiver_kats.json, poa_kats.json")
+    with open(os.path.join(HERE, "matrixtester_multiread.json"), "w") as f:
+        json.dump(make_matrixtester_multiread(), f, indent=1)
+    print("wrote arrow_kats.json, zmw6251.json, quiver_kats.json, poa_kats.json, matrixtester_multiread.json")
 
 
 if __name__ == "__main__":

@@ -127,3 +127,29 @@ def test_occupancy_report_from_wave_stamps():
     assert occ["families"]["k_fill"]["vgprs_per_lane"] == alloc
     assert abs(occ["vgpr_file_frac"] - round(1024 * alloc / (1024 * 512), 4)) < 1e-9
     assert occ["wave_slot_frac"] == round(1 / 8, 4)
+
+
+def test_cpu_leg_sample_is_stratified_and_the_power_law_recovers_its_exponent():
+    """the heterogeneous workloads' CPU leg samples one ZMW per cost stratum of the eligible
+    range (not a simple random sample that clusters on the cheap ZMWs), and the extrapolation fits CPU time as a
+    power of the cost model instead of scaling linearly."""
+    sys.path.insert(0, ROOT)
+    import random
+    import types
+    import bench
+    rng = random.Random(3)
+    costs = [10 ** rng.uniform(6, 10) for _ in range(2000)]
+    args = types.SimpleNamespace(cpu_sample=32, seed=3)
+    idx = bench.sample_indices(args, len(costs), costs)
+    assert len(idx) == 32 and len(set(idx)) == 32
+    assert all(costs[i] <= bench.SAMPLE_COST_CAP for i in idx)
+    elig = sorted(c for c in costs if c <= bench.SAMPLE_COST_CAP)
+    picked = sorted(costs[i] for i in idx)
+    # one per stratum: the k-th smallest pick lies in the k-th 1/32 of the eligible ZMWs by cost
+    for k, c in enumerate(picked):
+        lo, hi = len(elig) * k // 32, len(elig) * (k + 1) // 32
+        assert elig[lo] <= c <= elig[hi - 1]
+    secs = [2e-9 * costs[i] ** 1.3 for i in idx]
+    a, alpha = bench.power_law_fit([costs[i] for i in idx], secs)
+    assert abs(alpha - 1.3) < 1e-9
+    assert bench.power_law_fit([1.0, 1.0, 1.0], [1.0, 2.0, 3.0]) is None

@@ -86,6 +86,46 @@ def test_every_mutation_score_matches_oracle(P, seed, length, passes):
         assert _close(vq, o.score(t, s, b, -12.5)), (t, s, b)
 
 
+@pytest.mark.parametrize("threshold", [1.0, float("nan")])
+def test_matrixtester_multiread_zmw_matches_oracle(P, threshold):
+    """MatrixTester.cpp:212-384 -- the reference's only real multi-read ZMW (54 subreads, real SNRs, non-spanning
+    windows on both strands; tests/golden/matrixtester_multiread.json).  At the demo's AddRead threshold 1.0 (the
+    z-score gate keeps 5 reads; the refine ends NonConvergent on an end-of-template oscillation) and with the gate off
+    (all 54 reads): AddRead results, per-read LLs, z-scores, every unique mutation's full and fast score, the demo's
+    Score(INSERTION 202 'C'), RefineConsensus (converged, nTested, nApplied, template) and ConsensusQVs."""
+    d = json.load(open(os.path.join(GOLD, "matrixtester_multiread.json")))
+    tpl, snr = d["tpl"], d["snr"]
+    g = P.ArrowMultiReadMutationScorer(P.ArrowConfig(snr), tpl)
+    o = O.Scorer(tpl, snr)
+    rg = [g.AddRead(r["seq"], r["strand"], r["ts"], r["te"], threshold) for r in d["reads"]]
+    ro = [o.add_read(r["seq"], r["strand"], r["ts"], r["te"], threshold) for r in d["reads"]]
+    assert rg == ro
+    ll = g.BaselineScores()
+    assert len(ll) == o.num_reads()
+    for r in range(len(ll)):
+        assert _close(ll[r], o.read_info(r)["ll"]), r
+    assert _close(g.BaselineScore(), o.baseline())
+    if math.isnan(threshold):   # every read added: the z-scores over real error profiles
+        (zg, za), zs = g.ZScores()
+        ozg, oza, ozs = o.zscores()
+        assert _close(zg, ozg) and _close(za, oza)
+        assert all(_close(a, b) for a, b in zip(zs, ozs))
+    m = d["mutation"]
+    mt = {"INSERTION": P.INSERTION, "DELETION": P.DELETION, "SUBSTITUTION": P.SUBSTITUTION}[m["type"]]
+    assert _close(g.Score(P.Mutation(mt, m["start"], m["base"])), o.score(mt, m["start"], m["base"]))
+    muts = O.unique_mutations(tpl)
+    gm = [P.Mutation(t, s, b) for (t, s, b) in muts]
+    for (t, s, b), vf, vq in zip(muts, g.ScoreMany(gm), g.ScoreMany(gm, -12.5)):
+        assert _close(vf, o.score(t, s, b)), (t, s, b)
+        assert _close(vq, o.score(t, s, b, -12.5)), (t, s, b)
+    conv, nt, na = P.RefineConsensus(g)
+    ref = o.refine()
+    assert (conv, nt, na) == (ref["converged"], ref["n_tested"], ref["n_applied"])
+    assert g.Template() == o.template()
+    qg, qo = P.ConsensusQVs(g), o.qvs()
+    assert len(qg) == len(qo) and max(abs(a - b) for a, b in zip(qg, qo)) <= 1
+
+
 def test_partial_windows_and_strands(P):
     from pbccs_amd import synth
     import numpy as np

@@ -6,6 +6,7 @@
   boost shim in the survey container: a cross-check of the restatement, not a parity pin by this tier's rules).
 """
 import json
+import math
 import os
 
 import pytest
@@ -105,3 +106,20 @@ def test_polish_fixture_inputs_regenerate():
     fx = json.load(open(os.path.join(gold, "polish_10kb.json")))
     zs = synth.make_zmws(2, 10000, 8, seed=82)
     assert [digest(z) for z in zs] == [e["digest"] for e in fx["zmws"]]
+
+
+def test_matrixtester_multiread_fixture_runs_on_the_restatement():
+    """MatrixTester.cpp:212-384 (TestMultiReadScorer): the reference's only real multi-read ZMW -- 54 subreads,
+    real SNRs, non-spanning windows on both strands.  The demo asserts nothing, so this pins the fixture's shape
+    and that the restatement takes every read (the GPU comparison is test_gpu_parity's)."""
+    d = json.load(open(os.path.join(GOLD, "matrixtester_multiread.json")))
+    assert len(d["tpl"]) == 223 and len(d["reads"]) == 54
+    assert {r["strand"] for r in d["reads"]} == {0, 1}
+    assert sum(1 for r in d["reads"] if r["ts"] > 0 or r["te"] < len(d["tpl"])) >= 20   # non-spanning windows
+    o = O.Scorer(d["tpl"], d["snr"])
+    res = [o.add_read(r["seq"], r["strand"], r["ts"], r["te"], r["threshold"]) for r in d["reads"]]
+    assert set(res) <= {0, 1, 3}   # SUCCESS / ALPHABETAMISMATCH / POOR_ZSCORE at the demo's threshold 1.0
+    assert res.count(0) > 0
+    m = d["mutation"]
+    v = o.score(O.INSERTION if m["type"] == "INSERTION" else O.SUBSTITUTION, m["start"], m["base"])
+    assert math.isfinite(v)

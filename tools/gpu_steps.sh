@@ -87,6 +87,21 @@ step() {
     mixed)    # configs[3] at 2000 ZMWs
       timeout -k 10 900 $BENCH --workload mixed --steps 1 --zmws-per-step 2000 --warmup 0 > $OUT/bench_mixed.json \
         2> $OUT/bench_mixed.err && summ $OUT/bench_mixed.json ;;
+    abmixed)  # configs[3] at MIXN ZMWs under each "VAR=x VAR2=y" variant of VARIANTS (";"-separated), no profiler
+      local k=0
+      IFS=';' read -ra VS <<< "${VARIANTS:-NONE=1}"
+      for v in "${VS[@]}"; do
+        k=$((k+1))
+        eval "$v timeout -k 10 600 $BENCH --workload mixed --steps 1 --zmws-per-step ${MIXN:-1000} --warmup 0 --streams 8" \
+          > $OUT/abmixed_$k.json 2> $OUT/abmixed_$k.err || { echo "variant $k ($v) failed"; tail -3 $OUT/abmixed_$k.err; return 1; }
+        echo "[$v] $(summ $OUT/abmixed_$k.json) $(python3 -c "import json; d=json.load(open('$OUT/abmixed_$k.json')); print('polished', d['polished'], 'parity', d.get('parity_sample', {}).get('ok'))")"
+      done ;;
+    apimixed) # configs[3] HIP API trace: which calls block a slot thread between its kernels (tools/api_gaps.py)
+      timeout -k 10 1000 rocprofv3 --hip-trace --kernel-trace --stats -f csv -d $OUT/apimixed -o run -- $BENCH \
+        --workload mixed --steps 1 --zmws-per-step ${MIXN:-2000} --warmup 0 --streams 8 --cpu-sample 0 \
+        > $OUT/bench_mixed_api.json 2> $OUT/bench_mixed_api.err && summ $OUT/bench_mixed_api.json && \
+        python3 tools/api_gaps.py "$(find $OUT/apimixed -name '*hip_api_trace.csv' | head -1)" 200 > $OUT/api_gaps.json && \
+        head -60 $OUT/api_gaps.json && rm -f "$(find $OUT/apimixed -name '*hip_api_trace.csv' | head -1)" ;;
     profmixed) # configs[3] at 2000 ZMWs on 8 slots under rocprofv3 (the line and its kernel summary in one run)
       timeout -k 10 1000 rocprofv3 --kernel-trace --stats -f csv -d $OUT/profmixed -o run -- $BENCH --workload mixed \
         --steps 1 --zmws-per-step 2000 --warmup 0 --streams 8 > $OUT/bench_mixed.json 2> $OUT/bench_mixed.err && \
