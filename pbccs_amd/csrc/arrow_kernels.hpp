@@ -85,6 +85,7 @@ struct CoopFill {
     size_t groupBytes = 0;   // coop_group_bytes(hcap, readWords, tplWords)
     bool prio = false;       // waves at raised issue priority (the tall paths: each round's critical path)
     bool chainExit = true;   // G = 64 serial chain leaves a chunk early once its stop row is final
+    bool scan = false;       // G = 64: the reassociated (scan) chain, certified against a bound
     int rows = 1;            // band rows per lane (a chunk is G x rows rows)
     // relative width of the band around the row threshold pm / sdn in which the fill divides (thr_ge, 2^-50 x 3
     // roundings); tests widen it (PBCCS_FILL_THR_MARGIN) so that the division path runs on most rows

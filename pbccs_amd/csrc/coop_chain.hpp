@@ -212,5 +212,57 @@ __device__ __forceinline__ double insertion_chain64_exit(double m, double k, dou
     return x;
 }
 
+// ---- reassociated chain (the certified fast path of the tall fills) -----------------------
+// x_i = k_i x_{i-1} + c_i with c_i = m_i + d_i is an affine recurrence: each lane folds its R rows into one map
+// x -> A x + B, a Kogge-Stone scan over the 64 lanes composes the maps of the lanes below (6 DPP levels: row_shr
+// 1/2/4/8, row_bcast 15/31, as prefix_max), and each lane applies the exclusive prefix to the chunk's carry and
+// then runs its own R rows.  A chunk costs ~6 dependent levels instead of 64 hand-offs.  The sums are
+// reassociated, so the values are not the reference's bit for bit: every value is within a tracked relative
+// bound of it (all terms are non-negative), and the caller certifies each decision against that bound.
+// compose (A, B) := (A, B) o (Av, Bv), i.e. x -> A (Av x + Bv) + B; lanes without a source see the identity (1, 0)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void affine_step(double& A, double& B)
+{
+    const double Av = dpp_d<CTRL, ROWMASK, false>(1.0, A);
+    const double Bv = dpp_d<CTRL, ROWMASK, false>(0.0, B);
+    B = A * Bv + B;
+    A = A * Av;
+}
+// inclusive scan over the wavefront's 64 lanes: lane l ends with the composition of lanes 0..l
+__device__ __forceinline__ void affine_scan64(double& A, double& B)
+{
+    affine_step<0x111, 0xF>(A, B);   // row_shr:1
+    affine_step<0x112, 0xF>(A, B);   // row_shr:2
+    affine_step<0x114, 0xF>(A, B);   // row_shr:4
+    affine_step<0x118, 0xF>(A, B);   // row_shr:8
+    affine_step<0x142, 0xA>(A, B);   // row_bcast:15 (rows 1, 3)
+    affine_step<0x143, 0xC>(A, B);   // row_bcast:31 (rows 2, 3)
+}
+// The chunk's R x 64 rows by the scan: x[r] of lane l is row l R + r; lane 0's predecessor is `carry`.
+template <int R>
+__device__ __forceinline__ void scan_chain64(const double (&m)[R], const double (&k)[R], const double (&d)[R],
+                                             double carry, double (&x)[R])
+{
+    double c[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) c[r] = m[r] + d[r];
+    double A = k[0], B = c[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+        B = k[r] * B + c[r];
+        A = k[r] * A;
+    }
+    affine_scan64(A, B);
+    // exclusive prefix: the map of the lanes below (lane 0: the identity)
+    const double Ae = dpp_d<0x138, 0xF, false>(1.0, A);   // wave_shr:1
+    const double Be = dpp_d<0x138, 0xF, false>(0.0, B);
+    double up = Ae * carry + Be;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        x[r] = k[r] * up + c[r];
+        up = x[r];
+    }
+}
+
 }  // namespace coop
 }  // namespace pbccs

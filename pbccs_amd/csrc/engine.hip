@@ -67,11 +67,26 @@ void upload(DevVec<T>& d, const std::vector<T>& h, hipStream_t s)
     if (!h.empty()) PBCCS_HIP(hipMemcpyAsync(d.ptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
 }
 
+// Device-to-host copy into pageable memory.  The runtime stages a pageable copy through a pinned buffer it shares
+// between all streams of the device and holds that buffer until the copy has run -- i.e. until every kernel queued
+// before it on its stream has finished.  Queued behind a multi-second tall fill, one slot's download stalled every
+// other slot's pageable copies for seconds (configs[3]: 451 s of hipMemcpyAsync blocking over a 90 s run, 32% of
+// the slots' time with none of their kernels on the device; profiles/r9b_api_gaps.json, r9a_slot_gaps.json).  So
+// the stream is drained first (the caller waits for the result anyway) and the copy runs at once.
+// PBCCS_D2H_DRAIN=0 (A/B): the copy queued behind the stream's work as before.
+void d2h(void* dst, const void* src, size_t bytes, hipStream_t s)
+{
+    static const bool drain = env_int("PBCCS_D2H_DRAIN", 1) != 0;
+    if (!bytes) return;
+    if (drain) PBCCS_HIP(hipStreamSynchronize(s));
+    PBCCS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+}
+
 template <class T>
 void download(std::vector<T>& h, const DevVec<T>& d, size_t n, hipStream_t s)
 {
     h.resize(n);
-    if (n) PBCCS_HIP(hipMemcpyAsync(h.data(), d.ptr, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    d2h(h.data(), d.ptr, n * sizeof(T), s);
 }
 
 }  // namespace
@@ -404,7 +419,7 @@ const Counters& ArrowBatch::counters()
     const StreamScope bound(stream_);
     if (dFillWork_.ptr) {   // PBCCS_FILL_WORK diagnostics: fold the device counters in and clear them
         unsigned long long h[16];
-        PBCCS_HIP(hipMemcpyAsync(h, dFillWork_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
+        d2h(h, dFillWork_.ptr, sizeof(h), stream_);
         PBCCS_HIP(hipMemsetAsync(dFillWork_.ptr, 0, sizeof(h), stream_));
         PBCCS_HIP(hipStreamSynchronize(stream_));
         for (int k = 0; k < 16; ++k) counters_.fillWork[k] += (long long)h[k];
@@ -426,7 +441,7 @@ void ArrowBatch::CollectProfile(KernelStat out[kKernelKinds])
     ResolveEvents();
     if (profiling_) {
         unsigned long long h[16];
-        PBCCS_HIP(hipMemcpyAsync(h, dStats_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
+        d2h(h, dStats_.ptr, sizeof(h), stream_);
         PBCCS_HIP(hipStreamSynchronize(stream_));
         stats_[kKFill].cells += (double)h[2 * kStatFill];
         stats_[kKFill].bytes += (double)h[2 * kStatFill + 1];
@@ -1048,6 +1063,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             const int G = p == 1 ? narrowG : tallG;
             F.rows = p == 1 ? narrowRows : tallRows;
             F.prio = p >= 2;   // (neutral in an A/B against no priority, profiles/r4k_tall_prio_slots.txt)
+            static const bool scanProbe = env_int("PBCCS_TALL_SCAN_PROBE", 0) != 0;   // speed probe, uncertified
+            F.scan = p >= 2 && scanProbe;
             if (const char* e = std::getenv("PBCCS_FILL_THR_MARGIN"))   // test hook, read per launch
                 F.thrMargin = std::max(0x1p-50, std::atof(e));
             F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);
@@ -1099,7 +1116,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         download(ua, dUsedA_, R, stream_);
         download(ub, dUsedB_, R, stream_);
         unsigned long long bump = (unsigned long long)valTop_;
-        if (grow) PBCCS_HIP(hipMemcpyAsync(&bump, dBump_.ptr, sizeof(bump), hipMemcpyDeviceToHost, stream_));
+        if (grow) d2h(&bump, dBump_.ptr, sizeof(bump), stream_);
         PBCCS_HIP(hipStreamSynchronize(stream_));
         if (grow && bump != (unsigned long long)valTop_) {
             // some reads moved to larger regions: adopt the device's descriptors (host mirrors stay exact)
@@ -1107,9 +1124,9 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             va.resize(R);
             vb.resize(R);
             vc.resize(R);
-            PBCCS_HIP(hipMemcpyAsync(va.data(), pRValA_, R * sizeof(long long), hipMemcpyDeviceToHost, stream_));
-            PBCCS_HIP(hipMemcpyAsync(vb.data(), pRValB_, R * sizeof(long long), hipMemcpyDeviceToHost, stream_));
-            PBCCS_HIP(hipMemcpyAsync(vc.data(), pRValCap_, R * sizeof(long long), hipMemcpyDeviceToHost, stream_));
+            d2h(va.data(), pRValA_, R * sizeof(long long), stream_);
+            d2h(vb.data(), pRValB_, R * sizeof(long long), stream_);
+            d2h(vc.data(), pRValCap_, R * sizeof(long long), stream_);
             PBCCS_HIP(hipStreamSynchronize(stream_));
             for (auto& v : todo)
                 for (int r : v) {
@@ -1544,9 +1561,9 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
             PBCCS_HIP(hipGetLastError());
             int ovf = 0;
             unsigned long long ckNeed = 0;
-            PBCCS_HIP(hipMemcpyAsync(&ovf, dScratchOverflow_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream_));
+            d2h(&ovf, dScratchOverflow_.ptr, sizeof(int), stream_);
             if (ck.nTasks > 0)
-                PBCCS_HIP(hipMemcpyAsync(&ckNeed, ck.need, sizeof(ckNeed), hipMemcpyDeviceToHost, stream_));
+                d2h(&ckNeed, ck.need, sizeof(ckNeed), stream_);
             PBCCS_HIP(hipStreamSynchronize(stream_));
             if (ckNeed >= kCkptBadGeometry) throw DeviceError("checkpoint replay: block outgrew its column tables");
             if (ckNeed > 0) {
@@ -1960,7 +1977,7 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
         });
         PBCCS_HIP(hipGetLastError());
         long long cnt[2] = {0, 0};
-        PBCCS_HIP(hipMemcpyAsync(cnt, dCount.ptr, 2 * sizeof(long long), hipMemcpyDeviceToHost, stream_));
+        d2h(cnt, dCount.ptr, 2 * sizeof(long long), stream_);
         PBCCS_HIP(hipStreamSynchronize(stream_));
         std::vector<long long> sel;
         std::vector<double> selScore;

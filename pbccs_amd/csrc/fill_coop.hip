@@ -50,6 +50,7 @@ struct Task {
     bool gcol;
     int ckK;               // checkpoint interval: 0 keeps every column's values, else only ckpt_col_a/b columns
     bool chainExit;            // G = 64 serial steps with the early exit (insertion_chain64_exit)
+    bool scan;                 // G = 64, R > 1: the reassociated chain (scan_chain64)
     int slackDiv;              // regrow_bands slack: need / slackDiv
     double prNot, prThird, sdn;
     double sdnInvLow;   // a double strictly below 1 / sdn (early-exit test of the 64-lane chain)
@@ -364,8 +365,14 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                             return T.g.bits(st);
                         };
                         const int firstRow = min(reqEnd, I) - 1 - i0;   // the first chunk row the loop may stop at
-                        insertion_chain_rows<G, R>(m, k, d, carry, x, firstRow < 0 ? 0 : firstRow / R, T.chainExit,
-                                                   startLane, maybe_stop);
+                        if constexpr (G == 64) {
+                            if (T.scan) scan_chain64<R>(m, k, d, carry, x);
+                            else insertion_chain_rows<G, R>(m, k, d, carry, x, firstRow < 0 ? 0 : firstRow / R,
+                                                            T.chainExit, startLane, maybe_stop);
+                        } else {
+                            insertion_chain_rows<G, R>(m, k, d, carry, x, firstRow < 0 ? 0 : firstRow / R, T.chainExit,
+                                                       startLane, maybe_stop);
+                        }
                     }
                 }
                 // the reference loop's running maximum at each row, its threshold and continue test (:110-112)
@@ -645,8 +652,14 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                             return T.g.bits(st);
                         };
                         const int firstOff = e - 1 - max(1, reqBegin) - c * CH;   // the first chunk offset that may stop
-                        insertion_chain_rows<G, R>(m, k, d, carry, x, firstOff < 0 ? 0 : firstOff / R, T.chainExit,
-                                                   startLane, maybe_stop);
+                        if constexpr (G == 64) {
+                            if (T.scan) scan_chain64<R>(m, k, d, carry, x);
+                            else insertion_chain_rows<G, R>(m, k, d, carry, x, firstOff < 0 ? 0 : firstOff / R,
+                                                            T.chainExit, startLane, maybe_stop);
+                        } else {
+                            insertion_chain_rows<G, R>(m, k, d, carry, x, firstOff < 0 ? 0 : firstOff / R, T.chainExit,
+                                                       startLane, maybe_stop);
+                        }
                     }
                 }
                 double pmR[R];
@@ -869,6 +882,7 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
     T.rowsCap = GC ? F.hcap + F.gRows : F.hcap;
     T.gcol = GC;
     T.chainExit = F.chainExit;
+    T.scan = G == 64 && R > 1 && F.scan;
     T.ckK = B.rCkpt ? B.rCkpt[r] : 0;
     T.slackDiv = max(1, F.regrowSlackDiv);
     T.prNot = B.prNot;
