@@ -1314,6 +1314,13 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
         "band_memory_gb": {k: round(counters[k] / 2**30, 3) for k in
                            ("band_top_bytes", "band_region_bytes", "band_used_bytes", "pool_mapped_bytes")},
         "oom_retries": counters["oom_retries"],
+        # the certified fast path: tall reads filled by the reassociated chain, reads re-run exactly
+        # for an uncertain fill decision or AddRead gate, ZMW rounds re-scored on exact bands for an uncertain score
+        # decision (PBCCS_CERTIFIED_SCAN=0 turns the path off)
+        "certified_scan": {"scan_reads": counters.get("scan_reads", 0),
+                           "uncertain_reads": counters.get("uncertain_reads", 0),
+                           "exact_rounds": counters.get("exact_rounds", 0),
+                           "on": os.environ.get("PBCCS_CERTIFIED_SCAN", "1") != "0"},
     }
     if qstats:   # configs[4]: records stream to rank 0 per chunk; tail_ms = rank 0's wait after its last chunk
         out["queue"] = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in qstats.items()}

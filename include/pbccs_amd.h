@@ -233,6 +233,9 @@ typedef struct {
                                     [8 k + ...]: counted cells, cells thrown away by a tall abort, count-only
                                     regrow cells, count-only overflow cells, group chunk steps, wave chunk issues,
                                     reads, counted passes */
+    long long scan_reads;        /* certified fast path: reads its tall fills took */
+    long long uncertain_reads;   /* ... reads re-run exactly (a fill decision or the AddRead gate within the bound) */
+    long long exact_rounds;      /* ... ZMW rounds re-scored on exact bands (a score decision within the bound) */
 } pbccs_counters;
 int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset);
 

@@ -32,7 +32,12 @@ enum MutType : int { kIns = 0, kDel = 1, kSub = 2 };   // Mutation.hpp:50-53
 enum Strand : int { kFwd = 0, kRev = 1 };
 
 // kFillTall: a column did not fit the cooperative fill's LDS buffer (re-run on a wider path)
-enum FillStatus : int { kFillOk = 0, kFillMismatch = 1, kFillOverflow = 2, kFillBadInput = 3, kFillTall = 4 };
+// kFillUncertain: the certified fast path (reassociated chain) could not prove one of the fill's
+// decisions equal to the reference's (a band end, a begin hint or a flip-flop test within the deviation bound of
+// its threshold): the host re-runs the read on the exact path
+enum FillStatus : int { kFillOk = 0, kFillMismatch = 1, kFillOverflow = 2, kFillBadInput = 3, kFillTall = 4,
+                        kFillUncertain = 5 };
+constexpr double kUnitRoundoff = 0x1p-53;   // u: |fl(x) - x| <= u |x| for a normal result
 
 // Mutation code: pos << 4 | type << 2 | base(0..3).  Single-base mutations only (what ccs enumerates).
 __host__ __device__ inline int mut_code(int pos, int type, int base) { return (pos << 4) | (type << 2) | base; }
@@ -95,6 +100,9 @@ struct DevBatch {
     double* valPool;
     // per read results of the last fill
     double* rBaseline;        // MutationScorer::Score() = log(beta(0,0)) + sum(beta log-scales)
+    // per read: a bound on |LL - LL_reference| of the last fill's alpha and beta bands (their log-likelihoods and log-
+    // scale sums): 0 for the exact paths, > 0 for a read the certified fast path filled
+    double* rDev;
     int* rFlips;
     int* rStatus;
     // model constants

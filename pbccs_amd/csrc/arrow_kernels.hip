@@ -144,6 +144,7 @@ __global__ void __launch_bounds__(64) k_fill(DevBatch B, FillScratch F, const in
     const double mism = fabs(1.0 - av / bv);
     B.rFlips[r] = flips;
     B.rBaseline[r] = bv;
+    B.rDev[r] = 0.0;   // exact path
     F.usedA[r] = (int)ua;
     F.usedB[r] = (int)ub;
     B.rStatus[r] = (mism > kAlphaBetaTol) ? kFillMismatch : kFillOk;
@@ -1518,13 +1519,17 @@ __device__ __forceinline__ void k_reduce_body(DevBatch B, ScoreWork W, double fa
     const int rb = B.zReadBegin[z], nr = B.zNReads[z];
     const double* d = W.delta + W.deltaBase[k] + m;
     double sum = 0.0;
+    const double e = W.dev ? W.dev[k] : 0.0;   // certified fast path: the bound of this item's sums
+    bool amb = false;
     for (int rr = 0; rr < nr; ++rr) {
         const int r = rb + rr;
         if (B.rActive[r] && read_scores(B.rTs[r], B.rTe[r], type, pos, me)) sum += d[(long long)rr * M];
+        if (e > 0.0) amb = amb || fabs(sum - fastThr) <= e + 1e-12 * fabs(fastThr);
         if (sum < fastThr) break;
     }
     score[W.mutBase[k] + m] = sum;
     fav[W.mutBase[k] + m] = (sum > 0.04) ? 1 : 0;   // MIN_FAVORABLE_SCOREDIFF, MultiReadMutationScorer.cpp:56
+    if (e > 0.0 && (amb || fabs(sum - 0.04) <= e)) W.amb[k] = 1;   // the item's round is re-scored on exact bands
 }
 __global__ void __launch_bounds__(256) k_reduce(DevBatch B, ScoreWork W, double fastThr, double* __restrict__ score,
                                                 unsigned char* __restrict__ fav)

@@ -32,6 +32,12 @@ struct ScoreWork {
     const long long* sel = nullptr;
     const long long* selBase = nullptr;
     const int* nSel = nullptr;
+    // Certified fast path: per item a bound on how far any of its summed mutation scores may lie from
+    // the reference's (3x the reads' LL bounds: the mutated read, its baseline and the bands' prefix / suffix sums);
+    // k_reduce sets amb[k] when the fast-score break or the favourable test of a mutation lies within it.
+    // nullptr: every read of the round was filled exactly.
+    const double* dev = nullptr;
+    int* amb = nullptr;
 };
 
 // Scoring of reads with checkpointed bands (k_score_ckpt): a persistent grid of nSlots waves, each with a
@@ -86,6 +92,8 @@ struct CoopFill {
     bool prio = false;       // waves at raised issue priority (the tall paths: each round's critical path)
     bool chainExit = true;   // G = 64 serial chain leaves a chunk early once its stop row is final
     bool scan = false;       // G = 64: the reassociated (scan) chain, certified against a bound
+    double devScale = 1.0;   // test hook (PBCCS_SCAN_DEV_SCALE): the certified path's bounds inflated, so its exact
+                             // re-runs and re-scored rounds are exercised
     int rows = 1;            // band rows per lane (a chunk is G x rows rows)
     // relative width of the band around the row threshold pm / sdn in which the fill divides (thr_ge, 2^-50 x 3
     // roundings); tests widen it (PBCCS_FILL_THR_MARGIN) so that the division path runs on most rows

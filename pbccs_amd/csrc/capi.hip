@@ -272,6 +272,9 @@ int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset)
     out->create_upload_ns = eng->createUploadNs;
     out->derive_ns = eng->counters.deriveNs;
     for (int k = 0; k < 16; ++k) out->fill_work[k] = eng->counters.fillWork[k];
+    out->scan_reads = eng->counters.scanReads;
+    out->uncertain_reads = eng->counters.uncertainReads;
+    out->exact_rounds = eng->counters.exactRounds;
     if (reset) {
         eng->counters = Counters();
         eng->oomRetries = 0;
@@ -508,6 +511,9 @@ static void merge_engine_stats(pbccs_engine* eng, ArrowBatch& B)
         eng->counters.scoreTasks += c.scoreTasks;
         eng->counters.mutations += c.mutations;
         eng->counters.deriveNs += c.deriveNs;
+        eng->counters.scanReads += c.scanReads;
+        eng->counters.uncertainReads += c.uncertainReads;
+        eng->counters.exactRounds += c.exactRounds;
         for (int k = 0; k < 16; ++k) eng->counters.fillWork[k] += c.fillWork[k];
         eng->counters.bandTopBytes = std::max(eng->counters.bandTopBytes, c.bandTopBytes);
         eng->counters.bandRegionBytes = std::max(eng->counters.bandRegionBytes, c.bandRegionBytes);
@@ -619,7 +625,12 @@ static int polish_one(pbccs_batch* b, pbccs_zmw_output* out)
         const char* reclaimEnv = std::getenv("PBCCS_RECLAIM");
         const bool reclaim = reclaimEnv && std::strcmp(reclaimEnv, "1") == 0;
         B.SetReclaim(reclaim);
+        // the certified fast path for the batch's tall reads; PBCCS_CERTIFIED_SCAN=0: exact fills only
+        const char* ce = std::getenv("PBCCS_CERTIFIED_SCAN");   // read per batch: tests switch it at run time
+        const bool certified = !ce || ce[0] != '0';
+        B.SetCertifiedScan(certified);
         B.FillReads(b->allReads);
+        B.CertifyAddReads(b->allReads, o.min_zscore);
         std::vector<int> refineZ, refineIdx, dropZ;
         for (int i = 0; i < n; ++i) {
             if (b->zOf[i] < 0) continue;
@@ -946,7 +957,9 @@ int pbccs_polish_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, cons
         // every slot polishes at once: split what is free beyond the growth margin between them (the slots'
         // mapped band pools count as free: a batch on the slot reuses them)
         const double spare = std::max(0.0, (double)freeB + (double)slot_pool_bytes(eng) - (double)kQueueMargin);
-        const double budget = std::max(1.0 * (1 << 30), 0.9 * spare / slots);
+        // PBCCS_QUEUE_BUDGET_SCALE (A/B): the per-slot budget against the planner's per-ZMW estimates
+        const char* bs = std::getenv("PBCCS_QUEUE_BUDGET_SCALE");
+        const double budget = std::max(1.0 * (1 << 30), 0.9 * spare / slots) * (bs ? std::max(0.1, std::atof(bs)) : 1.0);
         int rc = pbccs_plan_batches(in, n, budget, kQueueMaxZmws, 1.5, order.data(), start.data(), nullptr, &nb);
         if (rc != PBCCS_OK) return rc;
         // a last wave with fewer batches than slots leaves slots idle through its whole polish: cap the batch

@@ -252,6 +252,7 @@ size_t Workspace::TrimRetired()
     size_t b = 0;
     auto t = [&](auto& v) { b += v.trim(); };
     t(selBase); t(nSel); t(colScratch); t(bump); t(desc); t(seq); t(ckPairs); t(ckStart); t(rBaseline); t(rFlips);
+    t(rDev); t(wDev); t(wAmb);
     t(rStatus); t(usedA); t(usedB); t(maxH); t(wZmw); t(wNMut); t(wMutBase); t(wDeltaBase); t(wWaveStart);
     t(wMutStart); t(wPosStart); t(wPosBase); t(wQvBase); t(stats); t(aRange); t(bRange); t(aOff); t(bOff); t(aLs);
     t(bLs); t(aPre); t(bSuf); t(fVal); t(fLs); t(fPre); t(fRange); t(fOff); t(codes); t(posOff); t(qv); t(list);
@@ -276,6 +277,7 @@ ArrowBatch::ArrowBatch(int device, Workspace* shared, bool ownStreams, bool wsBu
       ws_(shared ? shared : ownWs_.get()),
       dSelBase_(ws_->selBase), dNSel_(ws_->nSel), dColScratch_(ws_->colScratch), dBump_(ws_->bump),
       hDesc_(ws_->hDesc), dCkPairs_(ws_->ckPairs), dCkStart_(ws_->ckStart), dRBaseline_(ws_->rBaseline),
+      dRDev_(ws_->rDev),
       dRFlips_(ws_->rFlips), dRStatus_(ws_->rStatus), dUsedA_(ws_->usedA), dUsedB_(ws_->usedB), dMaxH_(ws_->maxH),
       dWZmw_(ws_->wZmw), dWNMut_(ws_->wNMut), dWMutBase_(ws_->wMutBase), dWDeltaBase_(ws_->wDeltaBase),
       dWWaveStart_(ws_->wWaveStart), dWMutStart_(ws_->wMutStart), dWPosStart_(ws_->wPosStart),
@@ -802,6 +804,7 @@ void ArrowBatch::UploadDescriptors()
     dBSuf_.reserve(cols, true);
     dVal_.reserve(std::max<long long>(valTop_, 1), true);
     dRBaseline_.reserve(std::max(R, 1), true);
+    dRDev_.reserve(std::max(R, 1), true);
     dRFlips_.reserve(std::max(R, 1), true);
     dRStatus_.reserve(std::max(R, 1), true);
     PBCCS_HIP(hipStreamSynchronize(stream_));   // host vectors above are temporaries
@@ -841,6 +844,7 @@ DevBatch ArrowBatch::View() const
     b.bSuf = dBSuf_.ptr;
     b.valPool = dVal_.ptr;
     b.rBaseline = dRBaseline_.ptr;
+    b.rDev = dRDev_.ptr;
     b.rFlips = dRFlips_.ptr;
     b.rStatus = dRStatus_.ptr;
     b.prNot = 1.0 - kMismatchProbability;
@@ -932,7 +936,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             return room >= want ? (int)want : 0;
         }
         // hybrid: as many LDS rows as fit, up to kHybridRows (the rest of a column goes to global memory)
-        const long long want = std::min(std::min(full, room), (long long)kHybridRows);
+        // PBCCS_HYBRID_LDS_KB / PBCCS_HYBRID_ROWS (A/B): the hybrid path's LDS budget per read and its row cap
+        static const long long hybLds = (long long)env_int("PBCCS_HYBRID_LDS_KB", (int)(kCoopLdsBytes >> 10)) << 10;
+        static const long long hybRows = env_int("PBCCS_HYBRID_ROWS", kHybridRows);
+        const long long hroom = (std::min<long long>(hybLds, 160 << 10) - (long long)coop_group_bytes(0, w, 0)) / 16 / 64 * 64;
+        const long long want = std::min(std::min(full, hroom), hybRows);
         return want >= 64 ? (int)want : 0;
     };
     // PBCCS_FILL_PATHS=1: one stderr line per launch set (reads per path, wall ms, reads re-routed / regrown)
@@ -998,6 +1006,11 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                     descDirty_ = true;
                 }
             }
+        // the certified fast path (scan_): the LDS-only tall path's reads with full bands fill with the reassociated
+        // chain, listed first; a read whose last certified fill met an uncertain decision runs exactly
+        auto scannable = [&](int r) { return scan_ && !reads_[r].exact && reads_[r].ckpt == 0; };
+        std::stable_partition(todo[2].begin(), todo[2].end(), scannable);
+        const int nScan2 = (int)std::count_if(todo[2].begin(), todo[2].end(), scannable);
         UploadDescriptors();
         const size_t R = reads_.size();
         dUsedA_.reserve(std::max<size_t>(R, 1), true);
@@ -1063,8 +1076,6 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             const int G = p == 1 ? narrowG : tallG;
             F.rows = p == 1 ? narrowRows : tallRows;
             F.prio = p >= 2;   // (neutral in an A/B against no priority, profiles/r4k_tall_prio_slots.txt)
-            static const bool scanProbe = env_int("PBCCS_TALL_SCAN_PROBE", 0) != 0;   // speed probe, uncertified
-            F.scan = p >= 2 && scanProbe;
             if (const char* e = std::getenv("PBCCS_FILL_THR_MARGIN"))   // test hook, read per launch
                 F.thrMargin = std::max(0x1p-50, std::atof(e));
             F.groupBytes = coop_group_bytes(F.hcap, F.readWords, F.tplWords);
@@ -1095,9 +1106,24 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 PBCCS_HIP(hipMemsetAsync(dCoopTrace_[p].ptr, 0, sizeof(long long) * 6 * n, st));
                 F.trace = dCoopTrace_[p].ptr;
             }
-            Timed(p == 1 ? kKFill : kKFillTall, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
-            PBCCS_HIP(hipGetLastError());
-            counters_.fillLaunches += 1;
+            if (p == 2 && nScan2 > 0) {   // certified scan launch over the first nScan2 reads, the exact rest after it
+                CoopFill FS = F;
+                FS.scan = true;
+                if (const char* e = std::getenv("PBCCS_SCAN_DEV_SCALE")) FS.devScale = std::max(1.0, std::atof(e));
+                Timed(kKFillTall, [&] { launch_fill_coop(G, B, FS, lp, nScan2, st); }, st);
+                PBCCS_HIP(hipGetLastError());
+                counters_.fillLaunches += 1;
+                counters_.scanReads += nScan2;
+                if (n > nScan2) {
+                    Timed(kKFillTall, [&] { launch_fill_coop(G, B, F, lp + nScan2, n - nScan2, st); }, st);
+                    PBCCS_HIP(hipGetLastError());
+                    counters_.fillLaunches += 1;
+                }
+            } else {
+                Timed(p == 1 ? kKFill : kKFillTall, [&] { launch_fill_coop(G, B, F, lp, n, st); }, st);
+                PBCCS_HIP(hipGetLastError());
+                counters_.fillLaunches += 1;
+            }
             off += n;
         }
         if (forked) {
@@ -1108,8 +1134,9 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             if (joinSync) PBCCS_HIP(hipStreamSynchronize(stream2_));
         }
         std::vector<int> st, fl, ua, ub, mh;
-        std::vector<double> bl;
+        std::vector<double> bl, dv;
         download(mh, dMaxH_, R, stream_);
+        if (nScan2 > 0) download(dv, dRDev_, R, stream_);
         download(st, dRStatus_, R, stream_);
         download(fl, dRFlips_, R, stream_);
         download(bl, dRBaseline_, R, stream_);
@@ -1182,6 +1209,12 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                     else next[q].push_back(r);
                     continue;
                 }
+                if (st[r] == kFillUncertain) {   // re-run on the exact path (same path, the exact launch)
+                    h.exact = true;
+                    counters_.uncertainReads += 1;
+                    next[p].push_back(r);
+                    continue;
+                }
                 if (st[r] == kFillOverflow) {
                     const long long need = std::max(ua[r], ub[r]);
                     h.valCap = std::max(need + need / 16 + 64, h.valCap + 1);
@@ -1195,6 +1228,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 h.status = st[r];
                 h.flips = fl[r];
                 h.baseline = bl[r];
+                h.dev = (p == 2 && !dv.empty()) ? dv[r] : 0.0;
                 h.filled = true;
                 h.usedA = ua[r];
                 h.usedB = ub[r];
@@ -1289,6 +1323,7 @@ void ArrowBatch::FillReadsSerial(const std::vector<int>& readsIn)
                 h.status = st[r];
                 h.flips = fl[r];
                 h.baseline = bl[r];
+                h.dev = 0.0;   // the lane-serial fill is exact
                 h.filled = true;
                 h.usedA = ua[r];
                 h.usedB = ub[r];
@@ -1357,6 +1392,30 @@ void ArrowBatch::MeanVar(const HZmw& z, int strand, int ts, int te, double* mean
     }
     *mean = m;
     *var = v;
+}
+
+void ArrowBatch::CertifyAddReads(const std::vector<int>& readsIn, double threshold)
+{
+    if (std::isnan(threshold)) return;
+    std::vector<int> redo;
+    for (int ri : readsIn) {
+        HRead& r = reads_[ri];
+        if (r.dev <= 0.0 || r.status != kFillOk || !std::isfinite(r.baseline)) continue;
+        double mean = 0.0, var = 0.0;
+        MeanVar(zmws_[r.zmw], r.strand, r.ts, r.te, &mean, &var);
+        const double sd = std::sqrt(var);
+        const double z = (r.baseline - mean) / sd;
+        // the reference's z lies within (dev + the rounding of (ll - mean) / sd) / sd of this one
+        if (!std::isfinite(z) || std::fabs(z - threshold) <= (r.dev + 4.0 * kUnitRoundoff * (std::fabs(r.baseline) +
+                                                                                          std::fabs(mean))) / sd +
+                                                                  8.0 * kUnitRoundoff * std::fabs(z)) {
+            r.exact = true;
+            redo.push_back(ri);
+        }
+    }
+    if (redo.empty()) return;
+    counters_.uncertainReads += (long long)redo.size();
+    FillReads(redo);
 }
 
 int ArrowBatch::FinishAddRead(int ri, double threshold)
@@ -1482,6 +1541,29 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
     W.posStart = dWPosStart_.ptr;
     W.codes = dCodes_.ptr;
     W.delta = dDelta_.ptr;
+    // certified fast path: per item the bound of its summed scores -- each active read contributes 3x its LL bound
+    // (the mutated read's LL, its baseline, and the prefix / suffix log-scale sums of its bands)
+    {
+        std::vector<double> dev(n, 0.0);
+        bool any = false;
+        for (int k = 0; k < n; ++k) {
+            const HZmw& z = zmws_[zl[k]];
+            for (int q = 0; q < z.nReads; ++q) {
+                const HRead& h = reads_[z.readBegin + q];
+                if (h.active && h.dev > 0.0) dev[k] += 3.0 * h.dev;
+            }
+            any = any || dev[k] > 0.0;
+        }
+        rDevItem_ = dev;
+        if (any) {
+            upload(ws_->wDev, dev, stream_);
+            ws_->wAmb.reserve(std::max(n, 1), false);
+            PBCCS_HIP(hipMemsetAsync(ws_->wAmb.ptr, 0, std::max(n, 1) * sizeof(int), stream_));
+            W.dev = ws_->wDev.ptr;
+            W.amb = ws_->wAmb.ptr;
+        }
+        rAmbOn_ = any;
+    }
     // k_score_edge list: tasks within 3 columns of a window end; bound = 80 per (work item, read)
     long long edgeCap = 0;
     for (int k = 0; k < n; ++k) edgeCap += 80LL * zmws_[zl[k]].nReads;
@@ -1755,6 +1837,42 @@ std::vector<Scored> best_subset(std::vector<Scored> in, int sep)   // Consensus-
     return out;
 }
 
+// Certified fast path: does BestSubset (Consensus-inl.hpp:98-118, first maximum of the float-cast
+// scores) pick the same entries for every set of double scores within e of `sc`?  The casts of a score within e lie
+// in [(float)(s - e), (float)(s + e)] (round to nearest is monotone).  Each pick is certain when the nominal winner's
+// lowest cast beats every remaining entry's highest, or both casts are fixed and equal with the winner first.
+bool best_subset_certain(const std::vector<Scored>& in, const std::vector<double>& sc, double e, int sep)
+{
+    const size_t n = in.size();
+    if (n == 0 || e <= 0.0) return true;
+    std::vector<float> lo(n), hi(n);
+    for (size_t i = 0; i < n; ++i) {
+        const double w = e + 4.0 * kUnitRoundoff * std::fabs(sc[i]);
+        lo[i] = (float)(sc[i] - w);
+        hi[i] = (float)(sc[i] + w);
+    }
+    std::vector<char> alive(n, 1);
+    for (;;) {
+        size_t best = n;
+        for (size_t k = 0; k < n; ++k)
+            if (alive[k] && (best == n || in[best].score < in[k].score)) best = k;
+        if (best == n) return true;
+        for (size_t k = 0; k < n; ++k) {
+            if (!alive[k] || k == best) continue;
+            if (hi[k] < lo[best]) continue;
+            const bool fixedTie = lo[k] == hi[k] && lo[best] == hi[best] && lo[k] == lo[best] && k > best;
+            if (!fixedTie) return false;
+        }
+        const int bp = mut_pos(in[best].code);
+        if (sep == 0) {
+            alive[best] = 0;
+            continue;
+        }
+        for (size_t k = 0; k < n; ++k)
+            if (alive[k] && bp - sep <= mut_pos(in[k].code) && mut_pos(in[k].code) <= bp + sep) alive[k] = 0;
+    }
+}
+
 }  // namespace
 
 void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std::vector<int>* converged,
@@ -1932,70 +2050,124 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
         for (size_t a = 0; a < act.size(); ++a) (*nTested)[idx[a]] += rNMut_[a];
         const Clock::time_point t1 = Clock::now();
 
-        // favourable mutations, compacted on the device in list order
-        DevVec<long long>& dSel = ws_->sel;
-        DevVec<double>& dSelScore = ws_->selScore;
-        DevVec<long long>& dCount = ws_->selCount;
-        dSel.reserve(std::max<long long>(rTotalMut_, 1), false);
-        dSelScore.reserve(std::max<long long>(rTotalMut_, 1), false);
-        dCount.reserve(2, false);
-        size_t tmpBytes = 0, tmpBytes2 = 0;
-        hipcub::CountingInputIterator<long long> it(0);
-        PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmpBytes, it, dFav_.ptr, dSel.ptr, dCount.ptr,
-                                                (int)rTotalMut_, stream_));
-        PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmpBytes2, dScore_.ptr, dFav_.ptr, dSelScore.ptr,
-                                                dCount.ptr + 1, (int)rTotalMut_, stream_));
-        DevVec<unsigned char>& tmp = ws_->selTmp;
-        tmp.reserve(std::max<size_t>(std::max(tmpBytes, tmpBytes2), 1), false);
-        PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tmpBytes, it, dFav_.ptr, dSel.ptr, dCount.ptr,
-                                                (int)rTotalMut_, stream_));
-        PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tmpBytes2, dScore_.ptr, dFav_.ptr, dSelScore.ptr,
-                                                dCount.ptr + 1, (int)rTotalMut_, stream_));
-        // the codes of the favourable entries (round 0's exist only on the device; later rounds' were uploaded)
-        DevVec<int>& dSelCode = ws_->selCode;
-        dSelCode.reserve(std::max<long long>(rTotalMut_, 1), false);
-        size_t tb = 0;
-        PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,
-                                                (int)rTotalMut_, stream_));
-        tmp.reserve(std::max<size_t>(tb, 1), false);
-        PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,
-                                                (int)rTotalMut_, stream_));
-        // BestSubset on the device: per ZMW its range of the compacted list, then one wavefront per ZMW
-        const int nAct = (int)act.size();
-        dSelBase_.reserve(std::max(nAct, 1), false);
-        dNSel_.reserve(std::max(nAct, 1), false);
-        DevVec<int>& dSelRank = ws_->selRank;
-        dSelRank.reserve(std::max<long long>(rTotalMut_, 1), false);
-        ScoreWork SW;
-        SW.nWork = nAct;
-        SW.mutStart = dWMutStart_.ptr;
-        launch_sel_ranges(SW, dSel.ptr, dCount.ptr, dSelBase_.ptr, dNSel_.ptr, stream_);
-        const char* capEnv = std::getenv("PBCCS_BEST_LDS");   // tests: force the HBM path of long lists
-        Timed(kKSelect, [&] {
-            launch_best_subset(nAct, dSelBase_.ptr, dNSel_.ptr, dSelCode.ptr, dSelScore.ptr, ro.mutationSeparation,
-                               capEnv ? std::atoi(capEnv) : -1, dSelRank.ptr, stream_);
-        });
-        PBCCS_HIP(hipGetLastError());
-        long long cnt[2] = {0, 0};
-        d2h(cnt, dCount.ptr, 2 * sizeof(long long), stream_);
-        PBCCS_HIP(hipStreamSynchronize(stream_));
-        std::vector<long long> sel;
-        std::vector<double> selScore;
-        std::vector<int> selCode, selRank;
-        download(sel, dSel, cnt[0], stream_);
-        download(selScore, dSelScore, cnt[0], stream_);
-        download(selCode, dSelCode, cnt[0], stream_);
-        download(selRank, dSelRank, cnt[0], stream_);
-        PBCCS_HIP(hipStreamSynchronize(stream_));
+        // the favourable list of each listed ZMW of the last RunRound, compacted on the device in list order, with the
+        // device BestSubset's picks (rank, entry) and the double scores (the certified path checks the float casts)
+        auto select_round = [&](const std::vector<int>& actL, std::vector<std::vector<Scored>>& favL,
+                                std::vector<std::vector<std::pair<int, Scored>>>& pickedL,
+                                std::vector<std::vector<double>>& favD) {
+            // favourable mutations, compacted on the device in list order
+            DevVec<long long>& dSel = ws_->sel;
+            DevVec<double>& dSelScore = ws_->selScore;
+            DevVec<long long>& dCount = ws_->selCount;
+            dSel.reserve(std::max<long long>(rTotalMut_, 1), false);
+            dSelScore.reserve(std::max<long long>(rTotalMut_, 1), false);
+            dCount.reserve(2, false);
+            size_t tmpBytes = 0, tmpBytes2 = 0;
+            hipcub::CountingInputIterator<long long> it(0);
+            PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmpBytes, it, dFav_.ptr, dSel.ptr, dCount.ptr,
+                                                    (int)rTotalMut_, stream_));
+            PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmpBytes2, dScore_.ptr, dFav_.ptr, dSelScore.ptr,
+                                                    dCount.ptr + 1, (int)rTotalMut_, stream_));
+            DevVec<unsigned char>& tmp = ws_->selTmp;
+            tmp.reserve(std::max<size_t>(std::max(tmpBytes, tmpBytes2), 1), false);
+            PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tmpBytes, it, dFav_.ptr, dSel.ptr, dCount.ptr,
+                                                    (int)rTotalMut_, stream_));
+            PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tmpBytes2, dScore_.ptr, dFav_.ptr, dSelScore.ptr,
+                                                    dCount.ptr + 1, (int)rTotalMut_, stream_));
+            // the codes of the favourable entries (round 0's exist only on the device; later rounds' were uploaded)
+            DevVec<int>& dSelCode = ws_->selCode;
+            dSelCode.reserve(std::max<long long>(rTotalMut_, 1), false);
+            size_t tb = 0;
+            PBCCS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,
+                                                    (int)rTotalMut_, stream_));
+            tmp.reserve(std::max<size_t>(tb, 1), false);
+            PBCCS_HIP(hipcub::DeviceSelect::Flagged(tmp.ptr, tb, dCodes_.ptr, dFav_.ptr, dSelCode.ptr, dCount.ptr + 1,
+                                                    (int)rTotalMut_, stream_));
+            // BestSubset on the device: per ZMW its range of the compacted list, then one wavefront per ZMW
+            const int nAct = (int)actL.size();
+            dSelBase_.reserve(std::max(nAct, 1), false);
+            dNSel_.reserve(std::max(nAct, 1), false);
+            DevVec<int>& dSelRank = ws_->selRank;
+            dSelRank.reserve(std::max<long long>(rTotalMut_, 1), false);
+            ScoreWork SW;
+            SW.nWork = nAct;
+            SW.mutStart = dWMutStart_.ptr;
+            launch_sel_ranges(SW, dSel.ptr, dCount.ptr, dSelBase_.ptr, dNSel_.ptr, stream_);
+            const char* capEnv = std::getenv("PBCCS_BEST_LDS");   // tests: force the HBM path of long lists
+            Timed(kKSelect, [&] {
+                launch_best_subset(nAct, dSelBase_.ptr, dNSel_.ptr, dSelCode.ptr, dSelScore.ptr, ro.mutationSeparation,
+                                   capEnv ? std::atoi(capEnv) : -1, dSelRank.ptr, stream_);
+            });
+            PBCCS_HIP(hipGetLastError());
+            long long cnt[2] = {0, 0};
+            d2h(cnt, dCount.ptr, 2 * sizeof(long long), stream_);
+            PBCCS_HIP(hipStreamSynchronize(stream_));
+            std::vector<long long> sel;
+            std::vector<double> selScore;
+            std::vector<int> selCode, selRank;
+            download(sel, dSel, cnt[0], stream_);
+            download(selScore, dSelScore, cnt[0], stream_);
+            download(selCode, dSelCode, cnt[0], stream_);
+            download(selRank, dSelRank, cnt[0], stream_);
+            PBCCS_HIP(hipStreamSynchronize(stream_));
 
-        std::vector<std::vector<Scored>> fav(act.size());
-        std::vector<std::vector<std::pair<int, Scored>>> picked(act.size());   // (rank, entry)
-        for (size_t q = 0; q < sel.size(); ++q) {
-            const long long g = sel[q];
-            const size_t a = std::upper_bound(rMutStart_.begin(), rMutStart_.end(), g) - rMutStart_.begin() - 1;
-            const Scored e{selCode[q], (float)selScore[q]};
-            fav[a].push_back(e);
-            if (selRank[q] > 0) picked[a].emplace_back(selRank[q], e);
+            favL.assign(actL.size(), {});
+            pickedL.assign(actL.size(), {});
+            favD.assign(actL.size(), {});
+            for (size_t q = 0; q < sel.size(); ++q) {
+                const long long g = sel[q];
+                const size_t a = std::upper_bound(rMutStart_.begin(), rMutStart_.end(), g) - rMutStart_.begin() - 1;
+                const Scored e{selCode[q], (float)selScore[q]};
+                favL[a].push_back(e);
+                favD[a].push_back(selScore[q]);
+                if (selRank[q] > 0) pickedL[a].emplace_back(selRank[q], e);
+            }
+        };
+        std::vector<std::vector<Scored>> fav;
+        std::vector<std::vector<std::pair<int, Scored>>> picked;   // (rank, entry)
+        std::vector<std::vector<double>> favD;
+        select_round(act, fav, picked, favD);
+        // Certified fast path: a ZMW whose round took a decision within its score bound -- k_reduce's
+        // favourable test or fast-score break, or a BestSubset pick among float casts that the bound could reorder --
+        // has its reads re-filled exactly and its round scored again on exact bands (its later rounds stay exact).
+        if (rAmbOn_) {
+            std::vector<int> ambFlag;
+            download(ambFlag, ws_->wAmb, act.size(), stream_);
+            PBCCS_HIP(hipStreamSynchronize(stream_));
+            std::vector<int> redo;   // positions in act
+            for (size_t a = 0; a < act.size(); ++a) {
+                const double e = rDevItem_[a];
+                if (e <= 0.0) continue;
+                if (ambFlag[a] || !best_subset_certain(fav[a], favD[a], e, ro.mutationSeparation)) redo.push_back((int)a);
+            }
+            if (!redo.empty()) {
+                std::vector<int> actR, readsR;
+                std::vector<std::vector<int>> listsR;
+                for (int a : redo) {
+                    actR.push_back(act[a]);
+                    if (round > 0) listsR.push_back(lists[a]);
+                    const HZmw& z = zmws_[act[a]];
+                    for (int q = 0; q < z.nReads; ++q) {
+                        HRead& h = reads_[z.readBegin + q];
+                        h.exact = true;
+                        if (h.active) readsR.push_back(z.readBegin + q);
+                    }
+                }
+                counters_.exactRounds += (long long)redo.size();
+                FillReads(readsR);   // the same template and windows, now on the exact paths: the reference's bands
+                for (int r : readsR)
+                    if (reads_[r].status != kFillOk) reads_[r].active = false;
+                descDirty_ = true;
+                RunRound(actR, round == 0 ? nullptr : &listsR, fastThr, false, true);
+                std::vector<std::vector<Scored>> favR;
+                std::vector<std::vector<std::pair<int, Scored>>> pickedR;
+                std::vector<std::vector<double>> favDR;
+                select_round(actR, favR, pickedR, favDR);
+                for (size_t i = 0; i < redo.size(); ++i) {
+                    fav[redo[i]] = std::move(favR[i]);
+                    picked[redo[i]] = std::move(pickedR[i]);
+                }
+            }
         }
         // PBCCS_CHECK_BEST_SUBSET=1: the host restatement beside the device select, any difference fatal
         const bool checkBest = std::getenv("PBCCS_CHECK_BEST_SUBSET") != nullptr;

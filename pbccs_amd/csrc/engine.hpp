@@ -223,6 +223,9 @@ struct Counters {   // work counters for the roofline report (bench.py)
     // bump top (everything ever handed out), current regions (2 x capacity per read), cells in use
     long long bandTopBytes = 0, bandRegionBytes = 0, bandUsedBytes = 0;
     long long deriveNs = 0;      // DeriveZmws: the per-ZMW setup of Consensus.h:437-453 (host)
+    // certified fast path: reads it filled, reads re-run exactly (an uncertain fill decision or
+    // AddRead gate), ZMW rounds re-scored on exact bands (an uncertain score decision)
+    long long scanReads = 0, uncertainReads = 0, exactRounds = 0;
     long long fillWork[16] = {}; // PBCCS_FILL_WORK=1: CoopFill::work summed (2 kinds x kFillWorkSlots)
 };
 
@@ -275,7 +278,9 @@ struct Workspace {
     DevVec<char> desc, seq;   // the descriptor arena and read pool of the slot's current batch (wsBuffers)
     DevVec<int2> ckPairs;
     DevVec<long long> ckStart;
-    DevVec<double> rBaseline;
+    DevVec<double> rBaseline, rDev;
+    DevVec<double> wDev;   // per scoring work item: the bound on its mutations' summed score deviations (certified path)
+    DevVec<int> wAmb;      // per scoring work item: a decision of k_reduce lay within that bound
     DevVec<int> rFlips, rStatus, usedA, usedB, maxH;
     DevVec<int> wZmw, wNMut;
     DevVec<long long> wMutBase, wDeltaBase, wWaveStart, wMutStart, wPosStart, wPosBase, wQvBase;
@@ -347,6 +352,14 @@ public:
     // afresh from offset 0, each region sized from the read's last band.  Live = filled, active
     // and not retired; the caller retires the ZMWs whose bands it will not read again.
     void SetReclaim(bool on) { reclaim_ = on; }
+    // The certified fast path: tall reads on the LDS-only 64-lane path fill with the reassociated
+    // chain, every fill decision certified against a deviation bound (uncertain reads re-run exactly), and every
+    // score decision the refine loop takes certified the same way (an uncertain ZMW round re-runs on exact bands).
+    // Only for whole-batch polish: the fine-grained scorer API keeps every value the reference's bit for bit.
+    void SetCertifiedScan(bool on) { scan_ = on; }
+    // AddRead's z-score gate (MultiReadMutationScorer.cpp:296-318) certified: reads whose z-score lies within their
+    // LL bound of `threshold` are re-filled exactly before FinishAddRead decides.
+    void CertifyAddReads(const std::vector<int>& reads, double threshold);
     void Retire(const std::vector<int>& zmws);
     // ConsensusQVs for the listed ZMWs.
     void QVs(const std::vector<int>& zmws, std::vector<std::vector<int>>* qvs);
@@ -412,6 +425,8 @@ private:
         long long usedA = 0, usedB = 0;   // band values the last fill kept (its region need)
         int maxH = 0;                       // the last cooperative fill's tallest column (rows)
         int ckpt = 0;   // checkpoint interval of the bands (0: every column's values kept)
+        double dev = 0.0;     // bound on |LL - the reference's| of the last fill (0: exact path)
+        bool exact = false;   // the certified fast path may not fill this read (an uncertain decision was met)
     };
 
     void EnsureZmwUploaded();
@@ -474,6 +489,8 @@ private:
     int ckptK_ = 0, ckptMinLen_ = 0, ckptAll_ = 0;
     long long ckSlotCap_ = 0;
     DevVec<double>& dRBaseline_;
+    DevVec<double>& dRDev_;
+    bool scan_ = false;
     DevVec<int>& dRFlips_, &dRStatus_, &dUsedA_, &dUsedB_, &dMaxH_;
     DevVec<int>& dWZmw_, &dWNMut_;
     DevVec<long long>& dWMutBase_, &dWDeltaBase_, &dWWaveStart_, &dWMutStart_, &dWPosStart_, &dWPosBase_,
@@ -503,6 +520,8 @@ private:
     // last round bookkeeping (host)
     std::vector<long long> rMutStart_, rPosStart_, rDeltaBase_;
     std::vector<int> rNMut_;
+    std::vector<double> rDevItem_;   // the last round's per-item score bounds (certified fast path; 0: exact)
+    bool rAmbOn_ = false;            // the last round's k_reduce flagged uncertain items into ws_->wAmb
     long long rTotalMut_ = 0, rTotalPos_ = 0, rTotalDelta_ = 0;
     Counters counters_;
     // profiling

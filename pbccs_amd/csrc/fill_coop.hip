@@ -50,11 +50,11 @@ struct Task {
     bool gcol;
     int ckK;               // checkpoint interval: 0 keeps every column's values, else only ckpt_col_a/b columns
     bool chainExit;            // G = 64 serial steps with the early exit (insertion_chain64_exit)
-    bool scan;                 // G = 64, R > 1: the reassociated chain (scan_chain64)
     int slackDiv;              // regrow_bands slack: need / slackDiv
     double prNot, prThird, sdn;
     double sdnInvLow;   // a double strictly below 1 / sdn (early-exit test of the 64-lane chain)
     double sdnInvHigh;  // a double strictly above 1 / sdn (thr_ge)
+    double devScale;    // SCAN: CoopFill::devScale (test hook: the bounds inflated)
     // in-kernel band growth (CoopFill::valBump): pool, bump pointer, mapped limit, descriptor arrays
     int r;
     double* pool;
@@ -105,6 +105,8 @@ struct PassOut {
     bool changed;     // some column's [begin, end) differs from the previous pass of this matrix
     bool regrow;      // the pass outgrew its region and ran to its end counting only: `used` is its exact need
     int maxH;         // the pass's tallest column (rows)
+    double dev;       // SCAN: bound on |log-likelihood - the reference's| of this pass (last + sumL), 0 when exact
+    bool unc;         // SCAN: some band decision lay within the deviation bound of its threshold
 };
 
 // PBCCS_FILL_WORK diagnostics (CoopFill::work): the group's chunk steps and, per lane, the chunk bodies this lane
@@ -143,6 +145,23 @@ __device__ __forceinline__ bool thr_ge(double x, double pm, double lo, double hi
     const bool lt = x < pm * lo;
     amb = pm != 0.0 && (pm < 0x1p-960 || (!ge && !lt));
     return ge || pm == 0.0;
+}
+
+// ---- the certified fast path (SCAN) ------------------------------------------------
+// With the reassociated chain (scan_chain64) a cell's value is not the reference's bit for bit.  Both are within
+// a relative distance of the exact real-arithmetic value of the same recursion (all terms are non-negative), which
+// a pass tracks as D: per column the reference's serial chain adds at most 3 u per row it runs (a mul and two adds
+// on the dependent path, propagated with weight <= 1), the scan at most 29 u per chunk (the lane fold, six
+// composition levels and the carry, R = 2) plus the chunk-to-chunk carry, the inputs m and d 3 u, the column scale
+// u; D accumulates over the pass's columns.  A decision (x >= threshold) is certain when x and the threshold are
+// further apart than 2 D + 4 u of the larger; otherwise the read is re-run on the exact path (kFillUncertain).
+__device__ __forceinline__ double scan_col_dev(double D, int chunks, int rowsPerChunk)
+{
+    return D + (3.0 * (double)chunks * (double)rowsPerChunk + 29.0 * (double)chunks + 8.0) * kUnitRoundoff;
+}
+__device__ __forceinline__ bool near_thr(double x, double t, double margin)
+{
+    return fabs(x - t) <= margin * fmax(x, t);
 }
 
 // ---- band growth ---------------------------------------------------------------------------------
@@ -223,14 +242,15 @@ __device__ double finish_log_scales(const Task<G>& T, const Band& m, int J)
 // ---- FillAlpha (SimpleRecursor.cpp:60-181) --------------------------------------------------------
 // A column's rows run in chunks of CH = G x R rows, R consecutive rows per lane (lane l: rows i0 + l R ..
 // i0 + l R + R - 1); R > 1 hands the chain on once per R rows (insertion_chain_rows).
-template <int G, int R>
+// SCAN (G = 64, R > 1): the reassociated chain and its certification.
+template <int G, int R, bool SCAN>
 __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO,
                               Work& W)
 {
     constexpr int CH = G * R;
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1};
+    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1, 0.0, false};
     bool counting = false;   // outgrew the region: finish the pass without stores (regrow_bands)
     (void)keepO;
     if (a.cap < 1) ovf = true;
@@ -243,6 +263,8 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     int prev = 0, cur = 1;   // column buffers
     if (lane == 0) T.cset(prev, 0, 1.0);
     int pb = 0, pe = 1;
+    double D = 0.0;     // SCAN: the pass's relative deviation bound so far (scan_col_dev)
+    bool unc = false;   // SCAN: an uncertain decision was met
     long long used = 1, stored = 1;   // cells computed / values kept (column 0 is always kept)
     int hb = 1, he = 1;
     int prevCtx = kCtxZero;
@@ -365,10 +387,8 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                             return T.g.bits(st);
                         };
                         const int firstRow = min(reqEnd, I) - 1 - i0;   // the first chunk row the loop may stop at
-                        if constexpr (G == 64) {
-                            if (T.scan) scan_chain64<R>(m, k, d, carry, x);
-                            else insertion_chain_rows<G, R>(m, k, d, carry, x, firstRow < 0 ? 0 : firstRow / R,
-                                                            T.chainExit, startLane, maybe_stop);
+                        if constexpr (SCAN) {
+                            scan_chain64<R>(m, k, d, carry, x);
                         } else {
                             insertion_chain_rows<G, R>(m, k, d, carry, x, firstRow < 0 ? 0 : firstRow / R, T.chainExit,
                                                        startLane, maybe_stop);
@@ -415,6 +435,19 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
 #pragma unroll
                 for (int r = 0; r < R - 1; ++r)
                     if (r == fs) pmAt = pmR[r];
+                if constexpr (SCAN) {   // every threshold test up to the stop row, with the chunk's margin
+                    const double mg = T.devScale * (2.0 * scan_col_dev(D, nc + 1, CH) + 4.0 * kUnitRoundoff);
+                    const int rsStop = stop ? T.g.bcast(fs, lastLane) : R;
+                    bool u = false;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int i = ib + r;
+                        const bool matters = (i + 1 < I) && (i + 1 >= reqEnd);
+                        const bool upto = !stop || lane < lastLane || (lane == lastLane && r <= rsStop);
+                        u = u || (matters && upto && near_thr(x[r], pmR[r] / T.sdn, mg));
+                    }
+                    unc = unc || T.g.bits(u) != 0;
+                }
                 mx = T.g.bcast(pmAt, lastLane);
                 ++nc;
                 if (stop) {
@@ -441,10 +474,12 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhb = e;
         bool found = false;
+        const double mh = SCAN ? T.devScale * (3.0 * scan_col_dev(D, nc, CH) + 4.0 * kUnitRoundoff) : 0.0;   // hint margin
         // two chunks per iteration: their divisions and LDS round trips overlap (tall columns have many chunks)
 #pragma unroll 2
         for (int c = 0; c < nc; ++c) {
             int fh = R;   // the lane's first row at or above the scaled threshold
+            bool nearH[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int kk = c * CH + lane * R + r;
@@ -456,14 +491,26 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                     if (store && stored + kk < a.cap) a.V(stored + kk) = v;
                 }
                 if (fh == R && ok && !(v < thrF)) fh = r;
+                nearH[r] = SCAN && ok && near_thr(v, thrF, mh);
             }
             const unsigned long long hit = T.g.bits(fh < R);
+            if constexpr (SCAN) {   // the tests up to the hint row (the first hit) decide it
+                if (!found) {
+                    const int hl = hit ? __ffsll((long long)hit) - 1 : G;
+                    const int fhl = hit ? T.g.bcast(fh, hl) : R;
+                    bool u = false;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) u = u || (nearH[r] && (lane < hl || (lane == hl && r <= fhl)));
+                    unc = unc || T.g.bits(u) != 0;
+                }
+            }
             if (!found && hit) {
                 const int hl = __ffsll((long long)hit) - 1;
                 nhb = b + c * CH + hl * R + (R == 1 ? 0 : T.g.bcast(fh, hl));
                 found = true;
             }
         }
+        if constexpr (SCAN) D = scan_col_dev(D, nc, CH) + kUnitRoundoff;   // the column's rows and its scale
         if (!counting && stored + add > a.cap) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
         out.maxH = max(out.maxH, e - b);
@@ -513,18 +560,23 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     out.stored = stored + 1;
     out.last = v;
     if (!counting) out.sumL = finish_log_scales<G>(T, a, J);
+    if constexpr (SCAN) {   // log(last) + sumL: the mass's deviation plus both sides' log and summation roundings
+        out.dev = T.devScale * (1.01 * (D + 4.0 * kUnitRoundoff) +
+                                2.0 * (double)(J + 4) * kUnitRoundoff * (fabs(out.sumL) + fabs(log(fmax(v, 1e-300))) + 64.0));
+        out.unc = unc;
+    }
     return out;
 }
 
 // ---- FillBeta (SimpleRecursor.cpp:183-296); rows run bottom-up, stored bottom-up --------------------
-template <int G, int R>
+template <int G, int R, bool SCAN>
 __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO,
                              Work& W)
 {
     constexpr int CH = G * R;
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1};
+    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1, 0.0, false};
     bool counting = false;   // outgrew the region: finish the pass without stores (regrow_bands)
     (void)keepO;
     if (bm.cap < 1) ovf = true;
@@ -538,6 +590,8 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     int nxt = 0, cur = 1;   // column buffers
     if (lane == 0) T.cset(nxt, 0, 1.0);
     int pb = I, pe = I + 1;
+    double D = 0.0;     // SCAN: the pass's relative deviation bound so far (scan_col_dev)
+    bool unc = false;   // SCAN: an uncertain decision was met
     long long used = 1, stored = 1;   // cells computed / values kept (column J is always kept)
     int hb = I, he = I;
     int nextBase = T.TBase(J - 1);
@@ -652,10 +706,8 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                             return T.g.bits(st);
                         };
                         const int firstOff = e - 1 - max(1, reqBegin) - c * CH;   // the first chunk offset that may stop
-                        if constexpr (G == 64) {
-                            if (T.scan) scan_chain64<R>(m, k, d, carry, x);
-                            else insertion_chain_rows<G, R>(m, k, d, carry, x, firstOff < 0 ? 0 : firstOff / R,
-                                                            T.chainExit, startLane, maybe_stop);
+                        if constexpr (SCAN) {
+                            scan_chain64<R>(m, k, d, carry, x);
                         } else {
                             insertion_chain_rows<G, R>(m, k, d, carry, x, firstOff < 0 ? 0 : firstOff / R, T.chainExit,
                                                        startLane, maybe_stop);
@@ -701,6 +753,19 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 #pragma unroll
                 for (int r = 0; r < R - 1; ++r)
                     if (r == fs) pmAt = pmR[r];
+                if constexpr (SCAN) {   // every threshold test up to the stop row, with the chunk's margin
+                    const double mg = T.devScale * (2.0 * scan_col_dev(D, nc + 1, CH) + 4.0 * kUnitRoundoff);
+                    const int rsStop = stop ? T.g.bcast(fs, lastLane) : R;
+                    bool u = false;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int i = e - 1 - ob - r;
+                        const bool matters = (i - 1 > 0) && (i - 1 < reqBegin);
+                        const bool upto = !stop || lane < lastLane || (lane == lastLane && r <= rsStop);
+                        u = u || (matters && upto && near_thr(x[r], pmR[r] / T.sdn, mg));
+                    }
+                    unc = unc || T.g.bits(u) != 0;
+                }
                 mx = T.g.bcast(pmAt, lastLane);
                 ++nc;
                 if (stop) {
@@ -726,9 +791,11 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         const bool scale = (mx != 0.0 && mx != 1.0);
         int nhe = b;
         bool found = false;
+        const double mh = SCAN ? T.devScale * (3.0 * scan_col_dev(D, nc, CH) + 4.0 * kUnitRoundoff) : 0.0;   // hint margin
 #pragma unroll 2
         for (int c = 0; c < nc; ++c) {
             int fh = R;
+            bool nearH[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int off = c * CH + lane * R + r;
@@ -740,14 +807,26 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                     if (store && stored + off < bm.cap) bm.V(stored + off) = v;
                 }
                 if (fh == R && ok && !(v < thrF)) fh = r;
+                nearH[r] = SCAN && ok && near_thr(v, thrF, mh);
             }
             const unsigned long long hit = T.g.bits(fh < R);
+            if constexpr (SCAN) {   // the tests up to the hint row (the first hit) decide it
+                if (!found) {
+                    const int hl = hit ? __ffsll((long long)hit) - 1 : G;
+                    const int fhl = hit ? T.g.bcast(fh, hl) : R;
+                    bool u = false;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) u = u || (nearH[r] && (lane < hl || (lane == hl && r <= fhl)));
+                    unc = unc || T.g.bits(u) != 0;
+                }
+            }
             if (!found && hit) {
                 const int hl = __ffsll((long long)hit) - 1;
                 nhe = e - (c * CH + hl * R + (R == 1 ? 0 : T.g.bcast(fh, hl)));
                 found = true;
             }
         }
+        if constexpr (SCAN) D = scan_col_dev(D, nc, CH) + kUnitRoundoff;   // the column's rows and its scale
         if (!counting && stored + add > bm.cap) ovf = true;
         out.changed = out.changed || b != sx || e != sy;
         out.maxH = max(out.maxH, e - b);
@@ -791,6 +870,11 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     out.stored = stored + 1;
     out.last = v;
     if (!counting) out.sumL = finish_log_scales<G>(T, bm, J);
+    if constexpr (SCAN) {   // as coop_alpha's
+        out.dev = T.devScale * (1.01 * (D + 4.0 * kUnitRoundoff) +
+                                2.0 * (double)(J + 4) * kUnitRoundoff * (fabs(out.sumL) + fabs(log(fmax(v, 1e-300))) + 64.0));
+        out.unc = unc;
+    }
     return out;
 }
 
@@ -802,7 +886,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 // and template window.
 // ------------------------------------------------------------------------------------------------
 // One listed read's FillAlphaBeta by the G-lane group whose LDS slot starts at gbase (task t of the launch).
-template <int G, bool GC, int R>
+template <int G, bool GC, int R, bool SCAN>
 __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, const int* __restrict__ reads, int n,
                                           int t, unsigned char* gbase)
 {
@@ -882,7 +966,6 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
     T.rowsCap = GC ? F.hcap + F.gRows : F.hcap;
     T.gcol = GC;
     T.chainExit = F.chainExit;
-    T.scan = G == 64 && R > 1 && F.scan;
     T.ckK = B.rCkpt ? B.rCkpt[r] : 0;
     T.slackDiv = max(1, F.regrowSlackDiv);
     T.prNot = B.prNot;
@@ -890,6 +973,7 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
     T.sdn = B.sdn;
     T.sdnInvLow = (1.0 / B.sdn) * (1.0 - F.thrMargin);
     T.sdnInvHigh = (1.0 / B.sdn) * (1.0 + F.thrMargin);
+    T.devScale = F.devScale;
     T.r = r;
     T.pool = B.valPool;
     T.bump = F.valBump;
@@ -927,12 +1011,13 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
     // its own previous pass (hint), never on previous values.  Once an alpha pass and the beta pass after
     // it both reproduce their predecessors' ranges, every later pass repeats them bit for bit, so the
     // remaining flip-flops are skipped and only the count the reference reports is kept.
-    PassOut pa{0, 0, 0.0, 0.0, false, false, false, 0}, pb{0, 0, 0.0, 0.0, false, false, false, 0};
+    PassOut pa{0, 0, 0.0, 0.0, false, false, false, 0, 0.0, false}, pb{0, 0, 0.0, 0.0, false, false, false, 0, 0.0, false};
     int maxH = 0;
     long long ua = 0, ub = 0;   // cells of the last alpha / beta pass (the reband test)
     long long sa = 0, sb = 0;   // values they keep (region sizes)
     const int maxSize = (int)(0.5 + kRebandFrac * (I + 1) * (J + 1));
     bool mismatched = false;
+    bool uncAny = false;   // SCAN: some decision of the fill could not be certified (kFillUncertain)
     int unchanged = 0;
     int regrows = 0;
     for (int step = 0;; ++step) {
@@ -944,7 +1029,11 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
         } else doAlpha = step == 2 || step == 4;
         if (step == 5) {
             if (flips == 0 || flips == 3) {   // first entry into the flip-flop loop
-                mismatched = fabs((log(pa.last) + pa.sumL) - (log(pb.last) + pb.sumL)) > kAlphaBetaTol;
+                const double la = log(pa.last) + pa.sumL, lb = log(pb.last) + pb.sumL;
+                mismatched = fabs(la - lb) > kAlphaBetaTol;
+                if constexpr (SCAN)
+                    uncAny = uncAny || fabs(fabs(la - lb) - kAlphaBetaTol) <=
+                                           pa.dev + pb.dev + 8.0 * kUnitRoundoff * fmax(fabs(la), fabs(lb));
             }
         }
         if (step >= 5) {
@@ -953,8 +1042,9 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
         }
         const bool guided = step > 0, self = step > 1;
         PassOut o;
-        if (doAlpha) o = coop_alpha<G, R>(T, a, bm, guided, self, ovf, ub, W);
-        else o = coop_beta<G, R>(T, bm, a, guided, self, ovf, ua, W);
+        if (doAlpha) o = coop_alpha<G, R, SCAN>(T, a, bm, guided, self, ovf, ub, W);
+        else o = coop_beta<G, R, SCAN>(T, bm, a, guided, self, ovf, ua, W);
+        uncAny = uncAny || o.unc;
         if (o.tall) {   // every cell so far is thrown away: the read restarts on the 64-lane path
             tallAbort = true;
             abortCells = cells + (unsigned long long)o.used;
@@ -1014,14 +1104,19 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
     const double av = log(pa.last) + pa.sumL;
     const double bv = log(pb.last) + pb.sumL;
     const double mism = fabs(1.0 - av / bv);
+    if constexpr (SCAN)   // the AlphaBetaMismatch test (SimpleRecursor.cpp:682-688) within the bound of its threshold
+        uncAny = uncAny || fabs(mism - kAlphaBetaTol) <= (pa.dev + fabs(av / bv) * pb.dev) / fabs(bv) + 8.0 * kUnitRoundoff;
     if (lane == 0) {
         if (ovf) {
             B.rStatus[r] = kFillOverflow;
             F.usedA[r] = (int)needA;
             F.usedB[r] = (int)needB;
+        } else if (SCAN && uncAny) {
+            B.rStatus[r] = kFillUncertain;   // the host re-runs the read on the exact path
         } else {
             B.rFlips[r] = flips;
             B.rBaseline[r] = bv;
+            B.rDev[r] = SCAN ? fmax(pa.dev, pb.dev) : 0.0;
             F.usedA[r] = (int)sa;   // region sizes: the values the bands keep
             F.usedB[r] = (int)sb;
             if (F.maxH) F.maxH[r] = maxH;
@@ -1054,7 +1149,7 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
 // profiles/r5c_fill_work.json -- measured no faster, and its second inlined copy of the fill cost 5% of the
 // headline in instruction-cache footprint: removed)
 // ------------------------------------------------------------------------------------------------
-template <int G, int MINW, bool GC, int R>
+template <int G, int MINW, bool GC, int R, bool SCAN>
 __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, const int* __restrict__ reads, int n)
 {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -1064,7 +1159,7 @@ __global__ void __launch_bounds__(64, MINW) k_fill_coop(DevBatch B, CoopFill F, 
     if (F.prio) __builtin_amdgcn_s_setprio(3);
     const int grp = threadIdx.x / G;
     unsigned char* gbase = smem + (size_t)grp * F.groupBytes;
-    fill_read<G, GC, R>(B, F, reads, n, blockIdx.x * (64 / G) + grp, gbase);
+    fill_read<G, GC, R, SCAN>(B, F, reads, n, blockIdx.x * (64 / G) + grp, gbase);
     wave_ticks(B.stats, G == 64 ? kWaveFillTall : kWaveFill, wt0);
 }
 
@@ -1097,18 +1192,22 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
     const int R = gc ? std::min(F.rows, 2) : F.rows;
     struct Entry {
         int g, r;
-        bool gc;
+        bool gc, scan;
         K k;
         bool attr;
     };
+    // the certified fast path (scan) exists for the LDS-only tall path with two rows per lane
     static Entry ks[] = {
-        {16, 1, false, (K)k_fill_coop<16, PBCCS_NARROW_MINW, false, 1>, false},
-        {64, 1, false, (K)k_fill_coop<64, 2, false, 1>, false},
-        {64, 2, false, (K)k_fill_coop<64, 2, false, 2>, false},
-        {64, 1, true, (K)k_fill_coop<64, 2, true, 1>, false},   {64, 2, true, (K)k_fill_coop<64, 2, true, 2>, false}};
+        {16, 1, false, false, (K)k_fill_coop<16, PBCCS_NARROW_MINW, false, 1, false>, false},
+        {64, 1, false, false, (K)k_fill_coop<64, 2, false, 1, false>, false},
+        {64, 2, false, false, (K)k_fill_coop<64, 2, false, 2, false>, false},
+        {64, 2, false, true, (K)k_fill_coop<64, 2, false, 2, true>, false},
+        {64, 1, true, false, (K)k_fill_coop<64, 2, true, 1, false>, false},
+        {64, 2, true, false, (K)k_fill_coop<64, 2, true, 2, false>, false}};
+    const bool scan = F.scan && G == 64 && R == 2 && !gc;
     Entry* e = nullptr;
     for (Entry& x : ks)
-        if (x.g == G && x.r == R && x.gc == gc) e = &x;
+        if (x.g == G && x.r == R && x.gc == gc && x.scan == scan) e = &x;
     if (!e) throw std::runtime_error("no fill kernel for this group size / rows per lane / column buffer");
     if (R > 1 && ((gc ? (F.hcap + F.gRows) : F.hcap) % (G * R) != 0 || F.hcap % 2 != 0))
         throw std::runtime_error("fill column buffers must hold whole chunks of G x rows rows (and even LDS rows)");

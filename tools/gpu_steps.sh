@@ -92,8 +92,9 @@ step() {
       IFS=';' read -ra VS <<< "${VARIANTS:-NONE=1}"
       for v in "${VS[@]}"; do
         k=$((k+1))
-        eval "$v timeout -k 10 600 $BENCH --workload mixed --steps 1 --zmws-per-step ${MIXN:-1000} --warmup 0 --streams 8" \
-          > $OUT/abmixed_$k.json 2> $OUT/abmixed_$k.err || { echo "variant $k ($v) failed"; tail -3 $OUT/abmixed_$k.err; return 1; }
+        ( eval "export $v"; timeout -k 10 600 $BENCH --workload mixed --steps 1 --zmws-per-step ${MIXN:-1000} --warmup 0 \
+          --streams ${MIXSTREAMS:-8} ) > $OUT/abmixed_$k.json 2> $OUT/abmixed_$k.err || \
+          { echo "variant $k ($v) failed"; tail -3 $OUT/abmixed_$k.err; return 1; }
         echo "[$v] $(summ $OUT/abmixed_$k.json) $(python3 -c "import json; d=json.load(open('$OUT/abmixed_$k.json')); print('polished', d['polished'], 'parity', d.get('parity_sample', {}).get('ok'))")"
       done ;;
     apimixed) # configs[3] HIP API trace: which calls block a slot thread between its kernels (tools/api_gaps.py)

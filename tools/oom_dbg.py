@@ -35,7 +35,8 @@ def main():
     zs = synth.make_zmws(24, 2000, 10, seed=31)
     small = synth.make_zmws(2, 600, 6, seed=32)
     ref = pbccs_amd.polish_zmws(zs + small, engine=pbccs_amd.Engine(0))
-    os.environ["PBCCS_POOL_CAP_MB"] = "200"
+    if os.environ.get("OOM_DBG_NO_CAP") != "1":   # OOM_DBG_NO_CAP=1: no capped pool, so no batch runs out of memory
+        os.environ["PBCCS_POOL_CAP_MB"] = "200"
     eng = pbccs_amd.Engine(0)
     eng.set_concurrency(2)
     got = pbccs_amd.polish_stream(zs + small, pbccs_amd.ConsensusSettings(zmws_per_batch=24), eng)
