@@ -1320,6 +1320,8 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
         "certified_scan": {"scan_reads": counters.get("scan_reads", 0),
                            "uncertain_reads": counters.get("uncertain_reads", 0),
                            "exact_rounds": counters.get("exact_rounds", 0),
+                           "uncertain_why": dict(zip(("band_end", "begin_hint", "loop_entry", "final_mismatch"),
+                                                     counters.get("uncertain_why", [0] * 4))),
                            "on": os.environ.get("PBCCS_CERTIFIED_SCAN", "1") != "0"},
     }
     if qstats:   # configs[4]: records stream to rank 0 per chunk; tail_ms = rank 0's wait after its last chunk

@@ -236,6 +236,7 @@ typedef struct {
     long long scan_reads;        /* certified fast path: reads its tall fills took */
     long long uncertain_reads;   /* ... reads re-run exactly (a fill decision or the AddRead gate within the bound) */
     long long exact_rounds;      /* ... ZMW rounds re-scored on exact bands (a score decision within the bound) */
+    long long uncertain_why[4];  /* ... uncertain fills by decision: band end, begin hint, loop entry, final mismatch */
 } pbccs_counters;
 int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset);
 

@@ -109,7 +109,8 @@ class Engine:
     def counters(self, reset=False):
         c = _lib_mod.CCounters()
         _lib_mod.check(load().pbccs_engine_counters(self._h, ctypes.byref(c), 1 if reset else 0))
-        return {k: (list(getattr(c, k)) if k == "fill_work" else getattr(c, k)) for k, _ in _lib_mod.CCounters._fields_}
+        return {k: (list(getattr(c, k)) if k in ("fill_work", "uncertain_why") else getattr(c, k))
+                for k, _ in _lib_mod.CCounters._fields_}
 
 
 _default_engine = None

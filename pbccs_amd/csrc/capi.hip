@@ -275,6 +275,7 @@ int pbccs_engine_counters(pbccs_engine* eng, pbccs_counters* out, int reset)
     out->scan_reads = eng->counters.scanReads;
     out->uncertain_reads = eng->counters.uncertainReads;
     out->exact_rounds = eng->counters.exactRounds;
+    for (int k = 0; k < 4; ++k) out->uncertain_why[k] = eng->counters.uncertainWhy[k];
     if (reset) {
         eng->counters = Counters();
         eng->oomRetries = 0;
@@ -514,6 +515,7 @@ static void merge_engine_stats(pbccs_engine* eng, ArrowBatch& B)
         eng->counters.scanReads += c.scanReads;
         eng->counters.uncertainReads += c.uncertainReads;
         eng->counters.exactRounds += c.exactRounds;
+        for (int k = 0; k < 4; ++k) eng->counters.uncertainWhy[k] += c.uncertainWhy[k];
         for (int k = 0; k < 16; ++k) eng->counters.fillWork[k] += c.fillWork[k];
         eng->counters.bandTopBytes = std::max(eng->counters.bandTopBytes, c.bandTopBytes);
         eng->counters.bandRegionBytes = std::max(eng->counters.bandRegionBytes, c.bandRegionBytes);

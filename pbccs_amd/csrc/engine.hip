@@ -1212,6 +1212,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 if (st[r] == kFillUncertain) {   // re-run on the exact path (same path, the exact launch)
                     h.exact = true;
                     counters_.uncertainReads += 1;
+                    for (int bit = 0; bit < 4; ++bit) counters_.uncertainWhy[bit] += (fl[r] >> bit) & 1;
                     next[p].push_back(r);
                     continue;
                 }

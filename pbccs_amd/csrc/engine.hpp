@@ -226,6 +226,7 @@ struct Counters {   // work counters for the roofline report (bench.py)
     // certified fast path: reads it filled, reads re-run exactly (an uncertain fill decision or
     // AddRead gate), ZMW rounds re-scored on exact bands (an uncertain score decision)
     long long scanReads = 0, uncertainReads = 0, exactRounds = 0;
+    long long uncertainWhy[4] = {};   // uncertain fills by decision: band end, begin hint, loop entry, final mismatch
     long long fillWork[16] = {}; // PBCCS_FILL_WORK=1: CoopFill::work summed (2 kinds x kFillWorkSlots)
 };
 

@@ -55,6 +55,7 @@ struct Task {
     double sdnInvLow;   // a double strictly below 1 / sdn (early-exit test of the 64-lane chain)
     double sdnInvHigh;  // a double strictly above 1 / sdn (thr_ge)
     double devScale;    // SCAN: CoopFill::devScale (test hook: the bounds inflated)
+    double sdnInv;      // SCAN: fl(1 / sdn) -- pm * sdnInv is within 2 u of fl(pm / sdn) (the margins hold 8 u)
     // in-kernel band growth (CoopFill::valBump): pool, bump pointer, mapped limit, descriptor arrays
     int r;
     double* pool;
@@ -106,7 +107,8 @@ struct PassOut {
     bool regrow;      // the pass outgrew its region and ran to its end counting only: `used` is its exact need
     int maxH;         // the pass's tallest column (rows)
     double dev;       // SCAN: bound on |log-likelihood - the reference's| of this pass (last + sumL), 0 when exact
-    bool unc;         // SCAN: some band decision lay within the deviation bound of its threshold
+    int unc;          // SCAN: decisions that lay within the deviation bound of their threshold (bit 0: a band end,
+                      // bit 1: a begin hint)
 };
 
 // PBCCS_FILL_WORK diagnostics (CoopFill::work): the group's chunk steps and, per lane, the chunk bodies this lane
@@ -149,19 +151,25 @@ __device__ __forceinline__ bool thr_ge(double x, double pm, double lo, double hi
 
 // ---- the certified fast path (SCAN) ------------------------------------------------
 // With the reassociated chain (scan_chain64) a cell's value is not the reference's bit for bit.  Both are within
-// a relative distance of the exact real-arithmetic value of the same recursion (all terms are non-negative), which
-// a pass tracks as D: per column the reference's serial chain adds at most 3 u per row it runs (a mul and two adds
-// on the dependent path, propagated with weight <= 1), the scan at most 29 u per chunk (the lane fold, six
-// composition levels and the carry, R = 2) plus the chunk-to-chunk carry, the inputs m and d 3 u, the column scale
-// u; D accumulates over the pass's columns.  A decision (x >= threshold) is certain when x and the threshold are
-// further apart than 2 D + 4 u of the larger; otherwise the read is re-run on the exact path (kFillUncertain).
+// a relative distance of the exact real-arithmetic value of the same recursion (all terms are non-negative: a sum's
+// relative error is at most its terms' largest plus u, a product's the sum of its factors' plus u), which a pass
+// tracks as D.  Per column: the reference's serial chain adds at most 3 u per row it runs (a mul and two adds on the
+// dependent path, propagated with weight <= 1); the scan forms each cell from products of up to a chunk's k's (a
+// product of n factors carries at most n - 1 roundings in any order) and sums over six composition levels, so it adds
+// at most (rows of the chunk + 40) u per chunk, the carry's error propagating with weight <= 1; the inputs m and d
+// add 3 u and the column scale u.  D accumulates over the pass's columns.  A decision (x >= threshold) is certain when
+// x and the threshold are further apart than 2 D + 4 u of the larger; otherwise the read is re-run on the exact path
+// (kFillUncertain).
 __device__ __forceinline__ double scan_col_dev(double D, int chunks, int rowsPerChunk)
 {
-    return D + (3.0 * (double)chunks * (double)rowsPerChunk + 29.0 * (double)chunks + 8.0) * kUnitRoundoff;
+    return D + (4.0 * (double)chunks * (double)rowsPerChunk + 40.0 * (double)chunks + 8.0) * kUnitRoundoff;
 }
+// Exact zeros are exact on both paths (a cell is 0 only when every term reaching it is, whatever the association),
+// so 0 against a 0 threshold (the running maximum of leading zero rows) is the reference's decision, not an uncertain one.
 __device__ __forceinline__ bool near_thr(double x, double t, double margin)
 {
-    return fabs(x - t) <= margin * fmax(x, t);
+    const double mx = fmax(x, t);
+    return mx > 0.0 && fabs(x - t) <= margin * mx;
 }
 
 // ---- band growth ---------------------------------------------------------------------------------
@@ -250,7 +258,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     constexpr int CH = G * R;
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1, 0.0, false};
+    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1, 0.0, 0};
     bool counting = false;   // outgrew the region: finish the pass without stores (regrow_bands)
     (void)keepO;
     if (a.cap < 1) ovf = true;
@@ -264,7 +272,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     if (lane == 0) T.cset(prev, 0, 1.0);
     int pb = 0, pe = 1;
     double D = 0.0;     // SCAN: the pass's relative deviation bound so far (scan_col_dev)
-    bool unc = false;   // SCAN: an uncertain decision was met
+    int unc = 0;   // SCAN: the uncertain decisions met (PassOut::unc)
     long long used = 1, stored = 1;   // cells computed / values kept (column 0 is always kept)
     int hb = 1, he = 1;
     int prevCtx = kCtxZero;
@@ -435,8 +443,10 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
 #pragma unroll
                 for (int r = 0; r < R - 1; ++r)
                     if (r == fs) pmAt = pmR[r];
-                if constexpr (SCAN) {   // every threshold test up to the stop row, with the chunk's margin
-                    const double mg = T.devScale * (2.0 * scan_col_dev(D, nc + 1, CH) + 4.0 * kUnitRoundoff);
+                // every threshold test up to the stop row, with the chunk's margin (none is read in a chunk that ends
+                // before reqEnd: its rows continue unconditionally)
+                if (SCAN && i0 + CH >= reqEnd) {
+                    const double mg = T.devScale * (2.0 * scan_col_dev(D, nc + 1, CH) + 8.0 * kUnitRoundoff);
                     const int rsStop = stop ? T.g.bcast(fs, lastLane) : R;
                     bool u = false;
 #pragma unroll
@@ -444,9 +454,9 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                         const int i = ib + r;
                         const bool matters = (i + 1 < I) && (i + 1 >= reqEnd);
                         const bool upto = !stop || lane < lastLane || (lane == lastLane && r <= rsStop);
-                        u = u || (matters && upto && near_thr(x[r], pmR[r] / T.sdn, mg));
+                        u = u || (matters && upto && near_thr(x[r], pmR[r] * T.sdnInv, mg));
                     }
-                    unc = unc || T.g.bits(u) != 0;
+                    if (T.g.bits(u) != 0) unc |= 1;
                 }
                 mx = T.g.bcast(pmAt, lastLane);
                 ++nc;
@@ -479,7 +489,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
 #pragma unroll 2
         for (int c = 0; c < nc; ++c) {
             int fh = R;   // the lane's first row at or above the scaled threshold
-            bool nearH[R];
+            double vv[R];   // SCAN: the chunk's scaled values (-1: outside the band), for the hint's certification
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int kk = c * CH + lane * R + r;
@@ -491,7 +501,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                     if (store && stored + kk < a.cap) a.V(stored + kk) = v;
                 }
                 if (fh == R && ok && !(v < thrF)) fh = r;
-                nearH[r] = SCAN && ok && near_thr(v, thrF, mh);
+                vv[r] = ok ? v : -1.0;
             }
             const unsigned long long hit = T.g.bits(fh < R);
             if constexpr (SCAN) {   // the tests up to the hint row (the first hit) decide it
@@ -500,8 +510,9 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                     const int fhl = hit ? T.g.bcast(fh, hl) : R;
                     bool u = false;
 #pragma unroll
-                    for (int r = 0; r < R; ++r) u = u || (nearH[r] && (lane < hl || (lane == hl && r <= fhl)));
-                    unc = unc || T.g.bits(u) != 0;
+                    for (int r = 0; r < R; ++r)
+                        u = u || (vv[r] >= 0.0 && (lane < hl || (lane == hl && r <= fhl)) && near_thr(vv[r], thrF, mh));
+                    if (T.g.bits(u) != 0) unc |= 2;
                 }
             }
             if (!found && hit) {
@@ -541,7 +552,8 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     }
     // pinned final match (:169-179)
     const double em = (T.RB(I - 1) == T.TBase(J - 1)) ? T.prNot : T.prThird;
-    const double lik = ((I - 1 >= pb && I - 1 < pe) ? T.cget(prev, I - 1 - pb) : 0.0) * em;
+    const bool lastIn = I - 1 >= pb && I - 1 < pe;
+    const double lik = (lastIn ? T.cget(prev, I - 1 - pb) : 0.0) * em;
     const double c = (0.0 < lik) ? lik : 0.0;
     double v = lik, ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = lik / c; ls = log(c); }
@@ -563,7 +575,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
     if constexpr (SCAN) {   // log(last) + sumL: the mass's deviation plus both sides' log and summation roundings
         out.dev = T.devScale * (1.01 * (D + 4.0 * kUnitRoundoff) +
                                 2.0 * (double)(J + 4) * kUnitRoundoff * (fabs(out.sumL) + fabs(log(fmax(v, 1e-300))) + 64.0));
-        out.unc = unc;
+        out.unc = unc | ((lastIn && v == 0.0) ? 1 : 0);   // a zero inside the band: an underflow, not a structure
     }
     return out;
 }
@@ -576,7 +588,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     constexpr int CH = G * R;
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
-    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1, 0.0, false};
+    PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1, 0.0, 0};
     bool counting = false;   // outgrew the region: finish the pass without stores (regrow_bands)
     (void)keepO;
     if (bm.cap < 1) ovf = true;
@@ -591,7 +603,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     if (lane == 0) T.cset(nxt, 0, 1.0);
     int pb = I, pe = I + 1;
     double D = 0.0;     // SCAN: the pass's relative deviation bound so far (scan_col_dev)
-    bool unc = false;   // SCAN: an uncertain decision was met
+    int unc = 0;   // SCAN: the uncertain decisions met (PassOut::unc)
     long long used = 1, stored = 1;   // cells computed / values kept (column J is always kept)
     int hb = I, he = I;
     int nextBase = T.TBase(J - 1);
@@ -753,8 +765,9 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 #pragma unroll
                 for (int r = 0; r < R - 1; ++r)
                     if (r == fs) pmAt = pmR[r];
-                if constexpr (SCAN) {   // every threshold test up to the stop row, with the chunk's margin
-                    const double mg = T.devScale * (2.0 * scan_col_dev(D, nc + 1, CH) + 4.0 * kUnitRoundoff);
+                // every threshold test up to the stop row (none is read in a chunk whose lowest row is >= reqBegin + 1)
+                if (SCAN && e - (c + 1) * CH - 1 < reqBegin) {
+                    const double mg = T.devScale * (2.0 * scan_col_dev(D, nc + 1, CH) + 8.0 * kUnitRoundoff);
                     const int rsStop = stop ? T.g.bcast(fs, lastLane) : R;
                     bool u = false;
 #pragma unroll
@@ -762,9 +775,9 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                         const int i = e - 1 - ob - r;
                         const bool matters = (i - 1 > 0) && (i - 1 < reqBegin);
                         const bool upto = !stop || lane < lastLane || (lane == lastLane && r <= rsStop);
-                        u = u || (matters && upto && near_thr(x[r], pmR[r] / T.sdn, mg));
+                        u = u || (matters && upto && near_thr(x[r], pmR[r] * T.sdnInv, mg));
                     }
-                    unc = unc || T.g.bits(u) != 0;
+                    if (T.g.bits(u) != 0) unc |= 1;
                 }
                 mx = T.g.bcast(pmAt, lastLane);
                 ++nc;
@@ -795,7 +808,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
 #pragma unroll 2
         for (int c = 0; c < nc; ++c) {
             int fh = R;
-            bool nearH[R];
+            double vv[R];   // SCAN: the chunk's scaled values (-1: outside the band), for the hint's certification
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int off = c * CH + lane * R + r;
@@ -807,7 +820,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                     if (store && stored + off < bm.cap) bm.V(stored + off) = v;
                 }
                 if (fh == R && ok && !(v < thrF)) fh = r;
-                nearH[r] = SCAN && ok && near_thr(v, thrF, mh);
+                vv[r] = ok ? v : -1.0;
             }
             const unsigned long long hit = T.g.bits(fh < R);
             if constexpr (SCAN) {   // the tests up to the hint row (the first hit) decide it
@@ -816,8 +829,9 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                     const int fhl = hit ? T.g.bcast(fh, hl) : R;
                     bool u = false;
 #pragma unroll
-                    for (int r = 0; r < R; ++r) u = u || (nearH[r] && (lane < hl || (lane == hl && r <= fhl)));
-                    unc = unc || T.g.bits(u) != 0;
+                    for (int r = 0; r < R; ++r)
+                        u = u || (vv[r] >= 0.0 && (lane < hl || (lane == hl && r <= fhl)) && near_thr(vv[r], thrF, mh));
+                    if (T.g.bits(u) != 0) unc |= 2;
                 }
             }
             if (!found && hit) {
@@ -851,7 +865,8 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         tA = tC;
     }
     const double em = (T.TBase(0) == T.RB(0)) ? T.prNot : T.prThird;
-    const double raw = em * ((1 >= pb && 1 < pe) ? T.cget(nxt, pe - 2) : 0.0);
+    const bool lastIn = 1 >= pb && 1 < pe;
+    const double raw = em * (lastIn ? T.cget(nxt, pe - 2) : 0.0);
     const double c = (0.0 < raw) ? raw : 0.0;
     double v = raw, ls = 0.0;
     if (c != 0.0 && c != 1.0) { v = raw / c; ls = log(c); }
@@ -873,7 +888,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
     if constexpr (SCAN) {   // as coop_alpha's
         out.dev = T.devScale * (1.01 * (D + 4.0 * kUnitRoundoff) +
                                 2.0 * (double)(J + 4) * kUnitRoundoff * (fabs(out.sumL) + fabs(log(fmax(v, 1e-300))) + 64.0));
-        out.unc = unc;
+        out.unc = unc | ((lastIn && v == 0.0) ? 1 : 0);   // a zero inside the band: an underflow, not a structure
     }
     return out;
 }
@@ -974,6 +989,7 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
     T.sdnInvLow = (1.0 / B.sdn) * (1.0 - F.thrMargin);
     T.sdnInvHigh = (1.0 / B.sdn) * (1.0 + F.thrMargin);
     T.devScale = F.devScale;
+    T.sdnInv = 1.0 / B.sdn;
     T.r = r;
     T.pool = B.valPool;
     T.bump = F.valBump;
@@ -1011,13 +1027,14 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
     // its own previous pass (hint), never on previous values.  Once an alpha pass and the beta pass after
     // it both reproduce their predecessors' ranges, every later pass repeats them bit for bit, so the
     // remaining flip-flops are skipped and only the count the reference reports is kept.
-    PassOut pa{0, 0, 0.0, 0.0, false, false, false, 0, 0.0, false}, pb{0, 0, 0.0, 0.0, false, false, false, 0, 0.0, false};
+    PassOut pa{0, 0, 0.0, 0.0, false, false, false, 0, 0.0, 0}, pb{0, 0, 0.0, 0.0, false, false, false, 0, 0.0, 0};
     int maxH = 0;
     long long ua = 0, ub = 0;   // cells of the last alpha / beta pass (the reband test)
     long long sa = 0, sb = 0;   // values they keep (region sizes)
     const int maxSize = (int)(0.5 + kRebandFrac * (I + 1) * (J + 1));
     bool mismatched = false;
-    bool uncAny = false;   // SCAN: some decision of the fill could not be certified (kFillUncertain)
+    int uncAny = 0;   // SCAN: the decisions of the fill that could not be certified (kFillUncertain): bits 0-1 a pass's
+                      // (PassOut::unc), bit 2 the flip-flop loop's entry test, bit 3 the final mismatch test
     int unchanged = 0;
     int regrows = 0;
     for (int step = 0;; ++step) {
@@ -1031,9 +1048,12 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
             if (flips == 0 || flips == 3) {   // first entry into the flip-flop loop
                 const double la = log(pa.last) + pa.sumL, lb = log(pb.last) + pb.sumL;
                 mismatched = fabs(la - lb) > kAlphaBetaTol;
+                // (an infinite LL is an exact zero final cell -- zeros are exact on both paths -- so its test is
+                // certain; only finite LLs within the bound of the tolerance are not)
                 if constexpr (SCAN)
-                    uncAny = uncAny || fabs(fabs(la - lb) - kAlphaBetaTol) <=
-                                           pa.dev + pb.dev + 8.0 * kUnitRoundoff * fmax(fabs(la), fabs(lb));
+                    if (isfinite(la) && isfinite(lb) &&
+                        fabs(fabs(la - lb) - kAlphaBetaTol) <= pa.dev + pb.dev + 8.0 * kUnitRoundoff * fmax(fabs(la), fabs(lb)))
+                        uncAny |= 4;
             }
         }
         if (step >= 5) {
@@ -1044,7 +1064,7 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
         PassOut o;
         if (doAlpha) o = coop_alpha<G, R, SCAN>(T, a, bm, guided, self, ovf, ub, W);
         else o = coop_beta<G, R, SCAN>(T, bm, a, guided, self, ovf, ua, W);
-        uncAny = uncAny || o.unc;
+        uncAny |= o.unc;
         if (o.tall) {   // every cell so far is thrown away: the read restarts on the 64-lane path
             tallAbort = true;
             abortCells = cells + (unsigned long long)o.used;
@@ -1105,7 +1125,9 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
     const double bv = log(pb.last) + pb.sumL;
     const double mism = fabs(1.0 - av / bv);
     if constexpr (SCAN)   // the AlphaBetaMismatch test (SimpleRecursor.cpp:682-688) within the bound of its threshold
-        uncAny = uncAny || fabs(mism - kAlphaBetaTol) <= (pa.dev + fabs(av / bv) * pb.dev) / fabs(bv) + 8.0 * kUnitRoundoff;
+        if (isfinite(av) && isfinite(bv) && isfinite(mism) &&
+            fabs(mism - kAlphaBetaTol) <= (pa.dev + fabs(av / bv) * pb.dev) / fabs(bv) + 8.0 * kUnitRoundoff)
+            uncAny |= 8;
     if (lane == 0) {
         if (ovf) {
             B.rStatus[r] = kFillOverflow;
@@ -1113,6 +1135,7 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
             F.usedB[r] = (int)needB;
         } else if (SCAN && uncAny) {
             B.rStatus[r] = kFillUncertain;   // the host re-runs the read on the exact path
+            B.rFlips[r] = uncAny;            // (which decisions: diagnostics)
         } else {
             B.rFlips[r] = flips;
             B.rBaseline[r] = bv;

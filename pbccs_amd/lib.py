@@ -69,7 +69,8 @@ class CCounters(ctypes.Structure):
                 ("oom_retries", ctypes.c_longlong), ("create_host_ns", ctypes.c_longlong),
                 ("create_upload_ns", ctypes.c_longlong), ("derive_ns", ctypes.c_longlong),
                 ("fill_work", ctypes.c_longlong * 16), ("scan_reads", ctypes.c_longlong),
-                ("uncertain_reads", ctypes.c_longlong), ("exact_rounds", ctypes.c_longlong)]
+                ("uncertain_reads", ctypes.c_longlong), ("exact_rounds", ctypes.c_longlong),
+                ("uncertain_why", ctypes.c_longlong * 4)]
 
 
 class CQvModelParams(ctypes.Structure):
