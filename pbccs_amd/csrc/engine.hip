@@ -1006,11 +1006,20 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                     descDirty_ = true;
                 }
             }
-        // the certified fast path (scan_): the LDS-only tall path's reads with full bands fill with the reassociated
-        // chain, listed first; a read whose last certified fill met an uncertain decision runs exactly
-        auto scannable = [&](int r) { return scan_ && !reads_[r].exact && reads_[r].ckpt == 0; };
-        std::stable_partition(todo[2].begin(), todo[2].end(), scannable);
-        const int nScan2 = (int)std::count_if(todo[2].begin(), todo[2].end(), scannable);
+        // the certified fast path (scan_): the LDS-only tall path's reads (checkpointed or not) fill with the
+        // reassociated chain, listed first; a read whose last certified fill met an uncertain decision runs exactly.
+        // PBCCS_SCAN_PATHS (read per batch): bit 0 the LDS-only path, bit 1 the hybrid one -- certified and tested
+        // too, but off by default: its fills ran no faster per cell and its longer reads' wider bounds sent 16 ZMW
+        // rounds to the exact re-run instead of 3 (configs[3] 12.2 vs 13.6 ZMWs/s, profiles/r9o_hybrid_scan_ab.txt).
+        const int scanPaths = env_int("PBCCS_SCAN_PATHS", 1);
+        auto scannable = [&](int r) { return scan_ && !reads_[r].exact; };
+        int nScan[kPaths] = {};
+        for (int p = 2; p < kPaths; ++p) {
+            if (!((scanPaths >> (p - 2)) & 1)) continue;
+            std::stable_partition(todo[p].begin(), todo[p].end(), scannable);
+            nScan[p] = (int)std::count_if(todo[p].begin(), todo[p].end(), scannable);
+        }
+        const bool anyScan = nScan[2] + nScan[3] > 0;
         UploadDescriptors();
         const size_t R = reads_.size();
         dUsedA_.reserve(std::max<size_t>(R, 1), true);
@@ -1106,7 +1115,8 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 PBCCS_HIP(hipMemsetAsync(dCoopTrace_[p].ptr, 0, sizeof(long long) * 6 * n, st));
                 F.trace = dCoopTrace_[p].ptr;
             }
-            if (p == 2 && nScan2 > 0) {   // certified scan launch over the first nScan2 reads, the exact rest after it
+            const int nScan2 = nScan[p];
+            if (nScan2 > 0) {   // certified scan launch over the first nScan2 reads, the exact rest after it
                 CoopFill FS = F;
                 FS.scan = true;
                 if (const char* e = std::getenv("PBCCS_SCAN_DEV_SCALE")) FS.devScale = std::max(1.0, std::atof(e));
@@ -1136,7 +1146,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         std::vector<int> st, fl, ua, ub, mh;
         std::vector<double> bl, dv;
         download(mh, dMaxH_, R, stream_);
-        if (nScan2 > 0) download(dv, dRDev_, R, stream_);
+        if (anyScan) download(dv, dRDev_, R, stream_);
         download(st, dRStatus_, R, stream_);
         download(fl, dRFlips_, R, stream_);
         download(bl, dRBaseline_, R, stream_);
@@ -1229,7 +1239,7 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
                 h.status = st[r];
                 h.flips = fl[r];
                 h.baseline = bl[r];
-                h.dev = (p == 2 && !dv.empty()) ? dv[r] : 0.0;
+                h.dev = !dv.empty() ? dv[r] : 0.0;   // every cooperative fill writes it (0 when exact)
                 h.filled = true;
                 h.usedA = ua[r];
                 h.usedB = ub[r];

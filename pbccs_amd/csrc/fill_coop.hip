@@ -251,7 +251,7 @@ __device__ double finish_log_scales(const Task<G>& T, const Band& m, int J)
 // A column's rows run in chunks of CH = G x R rows, R consecutive rows per lane (lane l: rows i0 + l R ..
 // i0 + l R + R - 1); R > 1 hands the chain on once per R rows (insertion_chain_rows).
 // SCAN (G = 64, R > 1): the reassociated chain and its certification.
-template <int G, int R, bool SCAN>
+template <int G, int R, bool SCAN, bool GC>
 __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO,
                               Work& W)
 {
@@ -329,6 +329,18 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         int e = b, nc = 0;
         if (b < I) {
             double carry = 0.0;
+            // the previous column's rows of a chunk: diag and left of the lane's rows (ibx - 1 .. ibx + R - 1).  GC (the
+            // hybrid path, rows past the LDS buffer in global memory): loaded one chunk ahead into pvN, so a global
+            // row's latency overlaps the chunk before it (the loads precede the chunk's stores to the other buffer)
+            auto load_prev = [&](int ibx, double (&dst)[R + 1]) {
+#pragma unroll
+                for (int q = 0; q <= R; ++q) {
+                    const int row = ibx - 1 + q;
+                    dst[q] = (row >= pb && row < pe) ? T.cget(prev, row - pb) : 0.0;
+                }
+            };
+            double pvN[R + 1];
+            if constexpr (GC) load_prev(b + lane * R, pvN);
             for (int i0 = b;; i0 += CH) {
                 if ((nc + 1) * CH > T.rowsCap) {
                     out.tall = true;
@@ -341,10 +353,12 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                 double m[R], k[R], d[R], x[R];
                 {
                     double pv[R + 1];   // scaled previous column at rows ib - 1 .. ib + R - 1 (diag, left)
+                    if constexpr (GC) {
 #pragma unroll
-                    for (int q = 0; q <= R; ++q) {
-                        const int row = ib - 1 + q;
-                        pv[q] = (row >= pb && row < pe) ? T.cget(prev, row - pb) : 0.0;
+                        for (int q = 0; q <= R; ++q) pv[q] = pvN[q];
+                        load_prev(ib + CH, pvN);
+                    } else {
+                        load_prev(ib, pv);
                     }
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
@@ -486,15 +500,30 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
         bool found = false;
         const double mh = SCAN ? T.devScale * (3.0 * scan_col_dev(D, nc, CH) + 4.0 * kUnitRoundoff) : 0.0;   // hint margin
         // two chunks per iteration: their divisions and LDS round trips overlap (tall columns have many chunks)
+        // GC: the next chunk's values are loaded before this chunk's stores (its global rows' latency overlaps)
+        auto load_cur = [&](int cx, double (&dst)[R]) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) dst[r] = (cx == nc - 1) ? aLast[r] : T.cget(cur, cx * CH + lane * R + r);
+        };
+        double xN[R];
+        if constexpr (GC) load_cur(0, xN);
 #pragma unroll 2
         for (int c = 0; c < nc; ++c) {
             int fh = R;   // the lane's first row at or above the scaled threshold
             double vv[R];   // SCAN: the chunk's scaled values (-1: outside the band), for the hint's certification
+            double xc[R];
+            if constexpr (GC) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) xc[r] = xN[r];
+                if (c + 1 < nc) load_cur(c + 1, xN);
+            } else {
+                load_cur(c, xc);
+            }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int kk = c * CH + lane * R + r;
                 const bool ok = b + kk < e;
-                const double x = (c == nc - 1) ? aLast[r] : T.cget(cur, kk);
+                const double x = xc[r];
                 const double v = scale ? x / mx : x;
                 if (ok) {
                     T.cset(cur, kk, v);
@@ -581,7 +610,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
 }
 
 // ---- FillBeta (SimpleRecursor.cpp:183-296); rows run bottom-up, stored bottom-up --------------------
-template <int G, int R, bool SCAN>
+template <int G, int R, bool SCAN, bool GC>
 __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO,
                              Work& W)
 {
@@ -652,6 +681,16 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         int b = e, nc = 0;
         if (e - 1 > 0) {
             double carry = 0.0;
+            // the next column's rows of a chunk (rows e - obx .. e - obx - R); GC: one chunk ahead (see coop_alpha)
+            auto load_next = [&](int obx, double (&dst)[R + 1]) {
+#pragma unroll
+                for (int q = 0; q <= R; ++q) {
+                    const int row = e - obx - q;
+                    dst[q] = (row >= pb && row < pe) ? T.cget(nxt, pe - 1 - row) : 0.0;
+                }
+            };
+            double pvN[R + 1];
+            if constexpr (GC) load_next(lane * R, pvN);
             for (int c = 0;; ++c) {
                 if ((c + 1) * CH > T.rowsCap) {
                     out.tall = true;
@@ -664,10 +703,12 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                 double m[R], k[R], d[R], x[R];
                 {
                     double pv[R + 1];   // scaled next column at rows e - ob .. e - ob - R (diag, left)
+                    if constexpr (GC) {
 #pragma unroll
-                    for (int q = 0; q <= R; ++q) {
-                        const int row = e - ob - q;
-                        pv[q] = (row >= pb && row < pe) ? T.cget(nxt, pe - 1 - row) : 0.0;
+                        for (int q = 0; q <= R; ++q) pv[q] = pvN[q];
+                        load_next(ob + CH, pvN);
+                    } else {
+                        load_next(ob, pv);
                     }
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
@@ -805,15 +846,29 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
         int nhe = b;
         bool found = false;
         const double mh = SCAN ? T.devScale * (3.0 * scan_col_dev(D, nc, CH) + 4.0 * kUnitRoundoff) : 0.0;   // hint margin
+        auto load_cur = [&](int cx, double (&dst)[R]) {   // GC: one chunk ahead (see coop_alpha)
+#pragma unroll
+            for (int r = 0; r < R; ++r) dst[r] = (cx == nc - 1) ? aLast[r] : T.cget(cur, cx * CH + lane * R + r);
+        };
+        double xN[R];
+        if constexpr (GC) load_cur(0, xN);
 #pragma unroll 2
         for (int c = 0; c < nc; ++c) {
             int fh = R;
             double vv[R];   // SCAN: the chunk's scaled values (-1: outside the band), for the hint's certification
+            double xc[R];
+            if constexpr (GC) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) xc[r] = xN[r];
+                if (c + 1 < nc) load_cur(c + 1, xN);
+            } else {
+                load_cur(c, xc);
+            }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int off = c * CH + lane * R + r;
                 const bool ok = e - 1 - off >= b;
-                const double x = (c == nc - 1) ? aLast[r] : T.cget(cur, off);
+                const double x = xc[r];
                 const double v = scale ? x / mx : x;
                 if (ok) {
                     T.cset(cur, off, v);
@@ -1062,8 +1117,8 @@ __device__ __forceinline__ void fill_read(const DevBatch& B, const CoopFill& F, 
         }
         const bool guided = step > 0, self = step > 1;
         PassOut o;
-        if (doAlpha) o = coop_alpha<G, R, SCAN>(T, a, bm, guided, self, ovf, ub, W);
-        else o = coop_beta<G, R, SCAN>(T, bm, a, guided, self, ovf, ua, W);
+        if (doAlpha) o = coop_alpha<G, R, SCAN, GC>(T, a, bm, guided, self, ovf, ub, W);
+        else o = coop_beta<G, R, SCAN, GC>(T, bm, a, guided, self, ovf, ua, W);
         uncAny |= o.unc;
         if (o.tall) {   // every cell so far is thrown away: the read restarts on the 64-lane path
             tallAbort = true;
@@ -1219,15 +1274,18 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
         K k;
         bool attr;
     };
-    // the certified fast path (scan) exists for the LDS-only tall path with two rows per lane
+    // the certified fast path (scan) exists for the tall paths with two rows per lane
     static Entry ks[] = {
         {16, 1, false, false, (K)k_fill_coop<16, PBCCS_NARROW_MINW, false, 1, false>, false},
         {64, 1, false, false, (K)k_fill_coop<64, 2, false, 1, false>, false},
         {64, 2, false, false, (K)k_fill_coop<64, 2, false, 2, false>, false},
         {64, 2, false, true, (K)k_fill_coop<64, 2, false, 2, true>, false},
-        {64, 1, true, false, (K)k_fill_coop<64, 2, true, 1, false>, false},
-        {64, 2, true, false, (K)k_fill_coop<64, 2, true, 2, false>, false}};
-    const bool scan = F.scan && G == 64 && R == 2 && !gc;
+        // (the hybrid kernels -- their loads one chunk ahead -- need more than the 256 registers of two waves per
+        // SIMD: one wave per SIMD, where their 60 KB of LDS per read already allows only two reads per CU)
+        {64, 1, true, false, (K)k_fill_coop<64, 1, true, 1, false>, false},
+        {64, 2, true, false, (K)k_fill_coop<64, 1, true, 2, false>, false},
+        {64, 2, true, true, (K)k_fill_coop<64, 1, true, 2, true>, false}};
+    const bool scan = F.scan && G == 64 && R == 2;
     Entry* e = nullptr;
     for (Entry& x : ks)
         if (x.g == G && x.r == R && x.gc == gc && x.scan == scan) e = &x;

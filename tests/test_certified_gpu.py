@@ -83,3 +83,21 @@ def test_certified_scan_equals_exact_path(batch2kb, monkeypatch):
             assert a[k] == b[k], k
         assert len(a["qvs"]) == len(b["qvs"]) and all(abs(x - y) <= 1 for x, y in zip(a["qvs"], b["qvs"]))
         assert all(_close(x, y) for x, y in zip(a["zscores"], b["zscores"]))
+
+
+@pytest.mark.parametrize("ckpt_k", ["8", "0"])
+def test_certified_scan_equals_exact_path_on_10kb_hybrid(ckpt_k, monkeypatch):
+    """10 kb reads: their columns overflow the LDS buffers, so they fill on the hybrid path (rows past the LDS buffer in
+    global scratch), checkpointed (PBCCS_CKPT_K=8: every 8th column kept, the rest replayed by k_score_ckpt) or with full
+    bands (0).  The certified fast path -- on the hybrid path too (PBCCS_SCAN_PATHS=3; off by default) -- must give the
+    exact path's records."""
+    from pbccs_amd import synth
+    zs = synth.make_zmws(3, 10000, 8, seed=67)
+    fast, cf = _polish(zs, monkeypatch, PBCCS_CKPT_K=ckpt_k, PBCCS_SCAN_PATHS="3")
+    exact, ce = _polish(zs, monkeypatch, PBCCS_CKPT_K=ckpt_k, PBCCS_CERTIFIED_SCAN="0")
+    assert cf["scan_reads"] > 0 and ce["scan_reads"] == 0
+    for a, b in zip(fast, exact):
+        for k in ("status", "consensus", "n_tested", "n_applied", "add_read_results", "n_passes"):
+            assert a[k] == b[k], k
+        assert len(a["qvs"]) == len(b["qvs"]) and all(abs(x - y) <= 1 for x, y in zip(a["qvs"], b["qvs"]))
+        assert all(_close(x, y) for x, y in zip(a["zscores"], b["zscores"]))

@@ -93,7 +93,7 @@ step() {
       for v in "${VS[@]}"; do
         k=$((k+1))
         ( eval "export $v"; timeout -k 10 600 $BENCH --workload mixed --steps 1 --zmws-per-step ${MIXN:-1000} --warmup 0 \
-          --streams ${MIXSTREAMS:-8} ) > $OUT/abmixed_$k.json 2> $OUT/abmixed_$k.err || \
+          --streams ${MIXSTREAMS:-8} ${MIXARGS:-} ) > $OUT/abmixed_$k.json 2> $OUT/abmixed_$k.err || \
           { echo "variant $k ($v) failed"; tail -3 $OUT/abmixed_$k.err; return 1; }
         echo "[$v] $(summ $OUT/abmixed_$k.json) $(python3 -c "import json; d=json.load(open('$OUT/abmixed_$k.json')); print('polished', d['polished'], 'parity', d.get('parity_sample', {}).get('ok'))")"
       done ;;
@@ -142,6 +142,14 @@ step() {
         || { echo "valu pass failed"; return 1; }
       python3 tools/valu_per_cell.py "$(find $OUT/valu -name '*counter_collection.csv' | head -1)" $OUT/valu.json \
         $OUT/valu_per_cell.json "$(python3 -c 'import bench; print(bench.kernel_source_digest())')" ;;
+    binding)  # wave-cycle decomposition per kernel family (issuing / issue-stalled / parked), CU busy, L2 hit rate:
+              # one pass of 8 SQ + 1 GRBM + 2 TCC counters (tools/binding.py)
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY \
+        SQ_ACTIVE_INST_VALU SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum \
+        -f csv -d $OUT/binding -o pmc -- $BENCH --cpu-sample 0 --steps 3 --warmup 1 > $OUT/binding.json \
+        2> $OUT/binding.err || { echo "binding pass failed"; tail -5 $OUT/binding.err; return 1; }
+      python3 tools/binding.py "$(find $OUT/binding -name '*counter_collection.csv' | head -1)" $OUT/binding_summary.json \
+        "$(python3 -c 'import bench; print(bench.kernel_source_digest())')" ;;
     work)     # where the fills' computed cells go (PBCCS_FILL_WORK=1 in-kernel counters), the driver's shape, 5 steps
       PBCCS_FILL_WORK=1 timeout -k 10 300 $BENCH --steps 5 --warmup 1 --cpu-sample 0 > $OUT/work.json 2> $OUT/work.err && \
         python3 -c "import json; d=json.load(open('$OUT/work.json')); print(d['value'], json.dumps(d.get('fill_work')))" ;;
