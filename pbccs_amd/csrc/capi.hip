@@ -545,7 +545,8 @@ static int create_batch(pbccs_engine* eng, const pbccs_zmw_input* in, int n, con
         // every batch gets its own streams (ArrowBatch's ownStreams); a batch made and polished on its slot's thread
         // (slot >= 0: the queue, the ccs chunks, reruns) uses the slot's descriptor arena and read pool
         // PBCCS_SLOT_STREAMS=1 (debug / A/B): the slot workspace's persistent streams instead
-        static const bool slotStreams = std::getenv("PBCCS_SLOT_STREAMS") && std::getenv("PBCCS_SLOT_STREAMS")[0] == '1';
+        // (read per batch: a test switches it at run time)
+        const bool slotStreams = std::getenv("PBCCS_SLOT_STREAMS") && std::getenv("PBCCS_SLOT_STREAMS")[0] == '1';
         b->B.reset(new ArrowBatch(eng->device, eng->Slot(b->slot), !slotStreams, slot >= 0));
         b->B->SetProfiling(eng->profiling);
         ArrowOptions ao;

@@ -106,12 +106,24 @@ void VmPool::reserve(size_t n, bool keep)
     if (!tried_ && allowVmm) {
         tried_ = true;
         void* va = nullptr;
-        vmm_ = hipMemAddressReserve(&va, kVaBytes, 0, nullptr, 0) == hipSuccess && va != nullptr;
-        if (vmm_) ptr = static_cast<double*>(va);
-        else (void)hipGetLastError();
-        if (oldVa_) {   // the reservation unmap_all left: the new one is taken, so it cannot come back as this one
-            (void)hipMemAddressFree(oldVa_, kVaBytes);
-            oldVa_ = nullptr;
+        static const bool dbgVa = env_int("PBCCS_DBG_VA", 0) != 0;   // debug: every reservation and unmap
+        // a range this pool mapped before must never be mapped by it again (same-VA remap, unmap_all): the ranges it
+        // unmapped stay reserved (oldVas_), and one the allocator still hands back (past kKeptVas) is parked there too
+        for (int attempt = 0;; ++attempt) {
+            vmm_ = hipMemAddressReserve(&va, kVaBytes, 0, nullptr, 0) == hipSuccess && va != nullptr;
+            if (!vmm_) {
+                (void)hipGetLastError();
+                break;
+            }
+            if (dbgVa) std::fprintf(stderr, "[vmpool %p] reserve va=%p (%zu kept)\n", (void*)this, va, oldVas_.size());
+            if (std::find(usedVas_.begin(), usedVas_.end(), va) == usedVas_.end()) break;
+            reusedVas_ += 1;
+            oldVas_.push_back(va);
+            if (attempt == 3) throw DeviceError("band pool: no address range this pool has not mapped before");
+        }
+        if (vmm_) {
+            ptr = static_cast<double*>(va);
+            usedVas_.push_back(va);
         }
     }
     if (!vmm_) {
@@ -196,6 +208,8 @@ void VmPool::unmap_all(hipStream_t s)
     }
     if (s) (void)hipStreamSynchronize(s);
     else (void)hipDeviceSynchronize();
+    static const bool dbgVa = env_int("PBCCS_DBG_VA", 0) != 0;
+    if (dbgVa) std::fprintf(stderr, "[vmpool %p] unmap_all va=%p mapped=%zu MB\n", (void*)this, (void*)ptr, mappedBytes_ >> 20);
     size_t off = 0;
     for (size_t k = 0; k < handles_.size(); ++k) {
         (void)hipMemUnmap(reinterpret_cast<char*>(ptr) + off, sizes_[k]);
@@ -206,11 +220,17 @@ void VmPool::unmap_all(hipStream_t s)
     sizes_.clear();
     mappedBytes_ = 0;
     cap = 0;
-    // The next mapping takes a fresh address range: mapping new granules at the addresses just unmapped gave
-    // wrong POA drafts (a POA pool released and mapped again between calls, every kernel serialised -- not a
-    // race; a fresh range fixed it, tools/ccs_draft_dbg.py).  This range is freed once the next
-    // one is reserved, so the two differ.
-    oldVa_ = ptr;
+    // Same-VA remap: new granules mapped at an address range this pool had mapped and unmapped, with
+    // the streams that used the old mapping still alive, gave wrong results -- POA drafts after a pool release,
+    // and an out-of-memory rerun on slot-shared streams (its range was the one unmapped two reservations before,
+    // PBCCS_DBG_VA=1 logs in profiles/r9s_same_va_oom.txt; with per-batch streams the same reuse was harmless).
+    // So the range stays reserved: the next reservation cannot return it.  Beyond kKeptVas the oldest is freed,
+    // and reserve parks it should the allocator hand it back.
+    oldVas_.push_back(ptr);
+    if (oldVas_.size() > kKeptVas) {
+        (void)hipMemAddressFree(oldVas_.front(), kVaBytes);
+        oldVas_.erase(oldVas_.begin());
+    }
     ptr = nullptr;
     tried_ = false;
     vmm_ = false;
@@ -218,7 +238,7 @@ void VmPool::unmap_all(hipStream_t s)
 
 VmPool::~VmPool()
 {
-    if (oldVa_) (void)hipMemAddressFree(oldVa_, kVaBytes);
+    for (void* va : oldVas_) (void)hipMemAddressFree(va, kVaBytes);
     if (!vmm_) return;
     (void)hipDeviceSynchronize();
     size_t off = 0;

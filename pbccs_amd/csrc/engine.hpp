@@ -191,8 +191,8 @@ struct VmPool {
     // Best effort: map granules towards n doubles until the device runs out of memory (no throw).
     // Only meaningful on the VMM path (the hipMalloc fallback would have to copy): there it is a no-op.
     void try_reserve(size_t n);
-    // Unmap every granule; the next reserve maps afresh at a new address range (never at the addresses just
-    // unmapped, see unmap_all).  Synchronises.
+    // Unmap every granule; the next reserve maps afresh at a new address range (never at addresses this pool has
+    // mapped before, see unmap_all).  Synchronises.
     // s: the stream whose work last used the pool (synchronised instead of the whole device); nullptr: the device
     void unmap_all(hipStream_t s = nullptr);
     size_t mapped_bytes() const { return vmm_ ? mappedBytes_ : cap * sizeof(double); }
@@ -206,7 +206,15 @@ private:
     static constexpr size_t kVaBytes = 1ull << 39;      // 512 GB of address space
     static constexpr size_t kChunkBytes = 1ull << 30;   // mapping granule
     bool tried_ = false, vmm_ = false;
-    void* oldVa_ = nullptr;   // an unmapped reservation, freed once the next one is taken (unmap_all)
+    // The ranges this pool mapped and unmapped, kept reserved so the address allocator cannot hand one back: a
+    // range mapped again while the streams that used it live on reads wrong values ("same-VA remap").
+    // Freed with the pool, or oldest first beyond kKeptVas (reserve then parks it, should it come back).
+    static constexpr size_t kKeptVas = 64;
+    std::vector<void*> oldVas_;
+    std::vector<void*> usedVas_;   // every range this pool has mapped (reserve's check)
+public:
+    long long reusedVas_ = 0;      // reservations that returned such a range (parked, not mapped)
+private:
     size_t mappedBytes_ = 0;
     std::vector<hipMemGenericAllocationHandle_t> handles_;
     std::vector<size_t> sizes_;

@@ -251,11 +251,20 @@ __device__ double finish_log_scales(const Task<G>& T, const Band& m, int J)
 // A column's rows run in chunks of CH = G x R rows, R consecutive rows per lane (lane l: rows i0 + l R ..
 // i0 + l R + R - 1); R > 1 hands the chain on once per R rows (insertion_chain_rows).
 // SCAN (G = 64, R > 1): the reassociated chain and its certification.
+#ifndef PBCCS_TALL_PREFETCH   // A/B builds
+#define PBCCS_TALL_PREFETCH 1
+#endif
 template <int G, int R, bool SCAN, bool GC>
 __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, bool selfValid, bool& ovf, long long keepO,
                               Work& W)
 {
     constexpr int CH = G * R;
+    // loads one chunk ahead (the previous column's rows in the chunk loop, this column's in the scale loop): the
+    // hybrid path (global rows) and, with PBCCS_TALL_PREFETCH, the LDS-only tall path too -- its waves spent 35% of
+    // their cycles parked on waitcnt (SQ_WAIT_ANY, profiles/r9p_binding_summary.json)
+    constexpr bool PF = GC || (G == 64 && PBCCS_TALL_PREFETCH && !SCAN);   // the chunk loop's (no room for it in
+                                                                           // the scan kernel's registers)
+    constexpr bool PFS = GC || (G == 64 && PBCCS_TALL_PREFETCH);            // the scale loop's
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
     PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1, 0.0, 0};
@@ -340,7 +349,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                 }
             };
             double pvN[R + 1];
-            if constexpr (GC) load_prev(b + lane * R, pvN);
+            if constexpr (PF) load_prev(b + lane * R, pvN);
             for (int i0 = b;; i0 += CH) {
                 if ((nc + 1) * CH > T.rowsCap) {
                     out.tall = true;
@@ -353,7 +362,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                 double m[R], k[R], d[R], x[R];
                 {
                     double pv[R + 1];   // scaled previous column at rows ib - 1 .. ib + R - 1 (diag, left)
-                    if constexpr (GC) {
+                    if constexpr (PF) {
 #pragma unroll
                         for (int q = 0; q <= R; ++q) pv[q] = pvN[q];
                         load_prev(ib + CH, pvN);
@@ -506,13 +515,13 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
             for (int r = 0; r < R; ++r) dst[r] = (cx == nc - 1) ? aLast[r] : T.cget(cur, cx * CH + lane * R + r);
         };
         double xN[R];
-        if constexpr (GC) load_cur(0, xN);
+        if constexpr (PFS) load_cur(0, xN);
 #pragma unroll 2
         for (int c = 0; c < nc; ++c) {
             int fh = R;   // the lane's first row at or above the scaled threshold
             double vv[R];   // SCAN: the chunk's scaled values (-1: outside the band), for the hint's certification
             double xc[R];
-            if constexpr (GC) {
+            if constexpr (PFS) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) xc[r] = xN[r];
                 if (c + 1 < nc) load_cur(c + 1, xN);
@@ -615,6 +624,12 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                              Work& W)
 {
     constexpr int CH = G * R;
+    // loads one chunk ahead (the previous column's rows in the chunk loop, this column's in the scale loop): the
+    // hybrid path (global rows) and, with PBCCS_TALL_PREFETCH, the LDS-only tall path too -- its waves spent 35% of
+    // their cycles parked on waitcnt (SQ_WAIT_ANY, profiles/r9p_binding_summary.json)
+    constexpr bool PF = GC || (G == 64 && PBCCS_TALL_PREFETCH && !SCAN);   // the chunk loop's (no room for it in
+                                                                           // the scan kernel's registers)
+    constexpr bool PFS = GC || (G == 64 && PBCCS_TALL_PREFETCH);            // the scale loop's
     const Band* guide = guided ? &o : nullptr;
     const int I = T.I, J = T.J, lane = T.g.lane;
     PassOut out{0, 0, 0.0, 0.0, false, !selfValid, false, 1, 0.0, 0};
@@ -690,7 +705,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                 }
             };
             double pvN[R + 1];
-            if constexpr (GC) load_next(lane * R, pvN);
+            if constexpr (PF) load_next(lane * R, pvN);
             for (int c = 0;; ++c) {
                 if ((c + 1) * CH > T.rowsCap) {
                     out.tall = true;
@@ -703,7 +718,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                 double m[R], k[R], d[R], x[R];
                 {
                     double pv[R + 1];   // scaled next column at rows e - ob .. e - ob - R (diag, left)
-                    if constexpr (GC) {
+                    if constexpr (PF) {
 #pragma unroll
                         for (int q = 0; q <= R; ++q) pv[q] = pvN[q];
                         load_next(ob + CH, pvN);
@@ -851,13 +866,13 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
             for (int r = 0; r < R; ++r) dst[r] = (cx == nc - 1) ? aLast[r] : T.cget(cur, cx * CH + lane * R + r);
         };
         double xN[R];
-        if constexpr (GC) load_cur(0, xN);
+        if constexpr (PFS) load_cur(0, xN);
 #pragma unroll 2
         for (int c = 0; c < nc; ++c) {
             int fh = R;
             double vv[R];   // SCAN: the chunk's scaled values (-1: outside the band), for the hint's certification
             double xc[R];
-            if constexpr (GC) {
+            if constexpr (PFS) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) xc[r] = xN[r];
                 if (c + 1 < nc) load_cur(c + 1, xN);

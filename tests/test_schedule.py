@@ -169,3 +169,40 @@ def test_out_of_memory_batches_are_rerun_with_identical_results(monkeypatch):
     got = pbccs_amd.polish_stream(zs + small, pbccs_amd.ConsensusSettings(zmws_per_batch=24), eng)
     _same_records(got, ref + ref_small)
     assert eng.counters()["oom_retries"] >= 1
+
+
+@pytest.mark.gpu
+def test_out_of_memory_rerun_on_slot_streams_after_same_va_remap(monkeypatch):
+    """The round-5 failure (same-VA remap): the work queue's out-of-memory rerun on the slots' persistent
+    streams (PBCCS_SLOT_STREAMS=1) returned unpolished drafts for 22-23 of 24 ZMWs, with most of the device held
+    elsewhere (as earlier tests' engines hold it in a full GPU run).  Its pool had been handed back the address range
+    it had mapped and unmapped two reservations before; pools now keep such ranges reserved, so the rerun maps fresh
+    addresses and every record equals the uncapped polish."""
+    import ctypes
+    import pbccs_amd
+    zs = synth.make_zmws(24, 2000, 10, seed=31)
+    small = synth.make_zmws(2, 600, 6, seed=32)
+    ref = pbccs_amd.polish_zmws(zs + small, engine=pbccs_amd.Engine(0))
+    # the HIP runtime the engine library uses (torch bundles another one, which need not see the device here)
+    hip = ctypes.CDLL("libamdhip64.so")
+    free, total = ctypes.c_size_t(), ctypes.c_size_t()
+    assert hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) == 0
+    hold = max(0, free.value - (20 << 30))   # leave 20 GB: the fills take no in-kernel growth headroom
+    blocks = []
+    try:
+        while hold > (1 << 30):
+            n = min(hold, 16 << 30)
+            p = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(n)) == 0
+            blocks.append(p)
+            hold -= n
+        monkeypatch.setenv("PBCCS_POOL_CAP_MB", "200")
+        monkeypatch.setenv("PBCCS_SLOT_STREAMS", "1")
+        eng = pbccs_amd.Engine(0)
+        eng.set_concurrency(2)
+        got = pbccs_amd.polish_stream(zs + small, pbccs_amd.ConsensusSettings(zmws_per_batch=24), eng)
+        assert eng.counters()["oom_retries"] >= 2
+        _same_records(got, ref)
+    finally:
+        for p in blocks:
+            hip.hipFree(p)
