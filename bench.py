@@ -36,11 +36,11 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # the boxes export
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # PMC HBM bytes per launch of each fill kind (tools/gpu_steps.sh traffic -> tools/pmc_traffic.py); used only while
 # the kernel sources still hash to the digest the profile was taken at
-TRAFFIC_PROFILES = {"k_fill_tall": "r5_traffic_fill_tall.json", "k_fill": "r5_traffic_fill.json",
-                    "k_score": "r5_traffic_score.json"}
+TRAFFIC_PROFILES = {"k_fill_tall": "r6_traffic_fill_tall.json", "k_fill": "r6_traffic_fill.json",
+                    "k_score": "r6_traffic_score.json"}
 # the same command on one workspace slot (--streams 1): the dominant kernel's launch duration there is not
 # time-shared with other batches' launches; used only while the kernel sources hash to its digest
-SINGLE_SLOT_PROFILE = "r5_streams1_bench.json"
+SINGLE_SLOT_PROFILE = "r6_streams1_bench.json"
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
 FLOP_PER_CELL = 11             # fill cell 6 mul + 3 add + <= 1 div, + the column rescale
 CHAIN_ROW_CYCLES = 21.5        # one band row of the tall fills' chain at 2 rows per lane (tools/ubench/chain_step.hip
@@ -1137,13 +1137,14 @@ def make_roofline(stats, local_time, workload):
             "fp64_valu": {"achieved": round(fp64_tf, 4), "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": round(fp64_tf / FP64_VALU_PEAK_TFLOPS, 6),
                           "note": f"{FLOP_PER_CELL} FLOP per DP cell-update over the timed region's wall time"},
-            "binding": f"device-wide: with eight slots of 1000-ZMW batches the device is saturated (five and six slots "
-                       f"ran at the same rate, profiles/r4k_tall_prio_slots.txt; ten and twelve slots lose, "
-                       f"profiles/r4u_batch_shape.txt), so the line follows the device's total work per ZMW; the "
-                       f"tall fill itself is latency-bound on the serial insertion chain (a dependent mul + add + add per "
-                       f"band row, a DPP hand-off per two rows, ~{CHAIN_ROW_CYCLES} cycles per row, "
-                       f"tools/ubench/chain_step.hip) and its per-chunk band-end logic (DESIGN.md §6); neither HBM nor "
-                       f"FP64 VALU",
+            "bound_note": "the roofline axis the contract names (HBM bytes); not the binding resource, see binding",
+            "binding": "no device resource saturates: VALU issue ~0.55 of the SIMDs' cycles, ~0.27 of the wave slots "
+                       "and ~0.66 of the VGPR file held (occupancy), HBM < 0.1; more slots do not help (ten and twelve "
+                       "lose, profiles/r4u_batch_shape.txt).  Each family is bound inside its own wavefronts: the fills "
+                       "issue on ~0.6 of their wave cycles and are parked on LDS / memory waits ~0.35, with ~0.04 "
+                       "dependency stalls -- per-wave instruction issue, the tall fill a lone wave on its SIMD -- and "
+                       "k_score is parked on memory ~0.64 of its wave cycles (wave_cycles, tools/binding.py; "
+                       "DESIGN.md section 6)",
             "source_digest": digest}
 
 
@@ -1155,8 +1156,9 @@ SIMDS, WAVE_SLOTS_PER_SIMD, VGPRS_PER_SIMD_LANE, VALU_CYCLES_PER_INST, ENGINE_HZ
 WAVE_FAMILIES = {"k_fill": ("k_fill_coopILi16E",), "k_fill_tall": ("k_fill_coopILi64E",),
                  "k_score": ("7k_scoreE",), "k_suffix": ("8k_suffixE",),
                  "k_reduce": ("8k_reduceE",)}
-VALU_PROFILE = "r5_valu_per_cell.json"   # SQ_INSTS_VALU per kernel family (tools/gpu_steps.sh valu)
-OCC_PROFILE = "r5_occupancy_bench.json"  # the driver's command on the occupancy build (tools/gpu_steps.sh occ)
+VALU_PROFILE = "r6_valu_per_cell.json"
+BINDING_PROFILE = "r6_binding_summary.json"   # wave-cycle decomposition per family (tools/gpu_steps.sh binding)   # SQ_INSTS_VALU per kernel family (tools/gpu_steps.sh valu)
+OCC_PROFILE = "r6_occupancy_bench.json"  # the driver's command on the occupancy build (tools/gpu_steps.sh occ)
 
 
 def occupancy_report(stats, local_time):
@@ -1273,6 +1275,30 @@ def report(args, rank, world, eng, slots, job_time, local_time, res, workload, s
             f"over the timed region {occ['waves_per_simd']} waves resident per SIMD ({occ['wave_slot_frac']} of the "
             f"wave slots), holding {occ['vgpr_file_frac']} of the VGPR file; VALU issue "
             f"{occ.get('valu_issue_frac', 'n/a')} of the SIMDs' cycles (roofline.occupancy)")
+        tw = (occ.get("families", {}).get("k_fill_tall") or {}).get("resident_waves")
+        tall = stats.get("k_fill_tall")
+        if tw and tall and local_time > 0:   # the tall fill against its own serial-chain bound
+            bound = tw * ENGINE_HZ / CHAIN_ROW_CYCLES
+            got = tall["cells"] / local_time
+            roofline["chain_bound"] = {
+                "achieved_cells_per_s": round(got / 1e9, 3), "bound_cells_per_s": round(bound / 1e9, 3),
+                "unit": "G cells/s", "frac": round(got / bound, 4), "resident_tall_waves": tw,
+                "cycles_per_row": CHAIN_ROW_CYCLES,
+                "note": "resident tall waves x clock / the exact chain's cycles per band row (tools/ubench/"
+                        "chain_step.hip); the certified scan path (DESIGN.md 3.12) has no per-row chain, so its "
+                        "reads can exceed this bound"}
+    bpath = os.path.join(ROOT, "profiles", BINDING_PROFILE)
+    if workload.startswith("configs[1]") and os.path.exists(bpath):
+        bp = json.load(open(bpath))
+        if bp.get("source_digest") == kernel_source_digest():
+            roofline["wave_cycles"] = {k: {x: v.get(x) for x in ("issuing_frac", "issue_stalled_frac",
+                                                                 "waitcnt_parked_frac", "valu_issuing_frac",
+                                                                 "l2_hit_frac")}
+                                       for k, v in bp.get("kernels", {}).items()}
+            roofline["wave_cycles_source"] = (f"profiles/{BINDING_PROFILE} (rocprofv3 --pmc SQ_WAVE_CYCLES, "
+                                              f"SQ_ACTIVE_INST_ANY, SQ_WAIT_INST_ANY, SQ_WAIT_ANY, ...; same sources)")
+        else:
+            roofline["wave_cycles_source"] = f"profiles/{BINDING_PROFILE} is stale: sources {bp.get('source_digest')}"
     out = {
         "metric": "CCS ZMWs/sec (and GCUPS) at 1/2/4/8 MI355X vs host-CPU ccs",
         "stage": "polish: Consensus.h:436-552 from the POA draft on (AddRead gates, RefineConsensus, "

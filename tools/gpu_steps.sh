@@ -33,9 +33,11 @@ step() {
     evidence) # the round's committed inputs of the bench line, then the line: PMC traffic and VALU passes and the
               # single-slot run of the final sources copied to profiles/ under the names bench.py reads, then the
               # driver's command and the occupancy build's
-      step traffic && for k in fill_tall fill score; do cp $OUT/traffic_$k.json profiles/r5_traffic_$k.json; done && \
-        step valu && cp $OUT/valu_per_cell.json profiles/r5_valu_per_cell.json && \
-        step bench1 && cp $OUT/bench_streams1.json profiles/r5_streams1_bench.json && step bench && step occ ;;
+      step traffic && for k in fill_tall fill score; do cp $OUT/traffic_$k.json profiles/r6_traffic_$k.json; done && \
+        step valu && cp $OUT/valu_per_cell.json profiles/r6_valu_per_cell.json && \
+        step binding && cp $OUT/binding_summary.json profiles/r6_binding_summary.json && \
+        step occ && cp $OUT/bench_occ.json profiles/r6_occupancy_bench.json && \
+        step bench1 && cp $OUT/bench_streams1.json profiles/r6_streams1_bench.json && step bench ;;
     apiccs)   # HIP API trace of the ccs stage (no counters): calls per API, e.g. no hipDeviceSynchronize in steady state
       timeout -k 10 500 rocprofv3 --hip-trace --stats -f csv -d $OUT/apiccs -o run -- $BENCH --stage ccs --steps 5 \
         --warmup 1 --cpu-sample 0 > $OUT/ccs_api.json 2> $OUT/ccs_api.err && \
