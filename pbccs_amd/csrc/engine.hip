@@ -59,6 +59,7 @@ int env_int(const char* name, int dflt)
 }
 constexpr long long kPhasedMinTasks = 1 << 21;   // (mutation, read) tasks from which a round scores in phases
 constexpr size_t kInitialScratch = 1 << 20;    // doubles for whole-window refills of tiny windows
+constexpr int kMaxCopySegs = 8;                // arrays per k_copy_segs launch
 
 template <class T>
 void upload(DevVec<T>& d, const std::vector<T>& h, hipStream_t s)
@@ -87,6 +88,116 @@ void download(std::vector<T>& h, const DevVec<T>& d, size_t n, hipStream_t s)
 {
     h.resize(n);
     d2h(h.data(), d.ptr, n * sizeof(T), s);
+}
+
+// Several device arrays moved in one host transfer (the runtime's pageable copies are one blit
+// kernel each -- 12,401 of them in a profiled headline run -- and each device-to-host one drains the stream): the
+// arrays are packed into / unpacked from a staging buffer by one k_copy_segs launch beside the single copy.
+struct CopySeg {
+    const unsigned int* src;
+    unsigned int* dst;
+    unsigned long long words;   // 4-byte words
+};
+struct CopySegs {
+    CopySeg s[kMaxCopySegs];
+};
+__global__ void __launch_bounds__(256) k_copy_segs(CopySegs g)
+{
+    const CopySeg q = g.s[blockIdx.y];
+    for (unsigned long long k = (unsigned long long)blockIdx.x * 256 + threadIdx.x; k < q.words;
+         k += (unsigned long long)gridDim.x * 256)
+        q.dst[k] = q.src[k];
+}
+
+// one item of a packed transfer: a device array and its host side (bytes a multiple of 4)
+struct Xfer {
+    void* dev;
+    void* host;
+    size_t bytes;
+};
+
+size_t stage_layout(const std::vector<Xfer>& items, std::vector<size_t>* off)
+{
+    size_t top = 0;
+    off->clear();
+    for (const Xfer& x : items) {
+        if (x.bytes % 4) throw DeviceError("packed transfer of a size not a multiple of 4 bytes");
+        off->push_back(top);
+        top += (x.bytes + 15) & ~(size_t)15;
+    }
+    return top;
+}
+
+void launch_copy_segs(const std::vector<CopySeg>& segs, hipStream_t s)
+{
+    for (size_t b = 0; b < segs.size(); b += kMaxCopySegs) {
+        CopySegs g{};
+        const int n = (int)std::min(segs.size() - b, (size_t)kMaxCopySegs);
+        unsigned long long most = 0;
+        for (int k = 0; k < n; ++k) {
+            g.s[k] = segs[b + k];
+            most = std::max(most, segs[b + k].words);
+        }
+        if (!most) continue;
+        const unsigned gx = (unsigned)std::min<unsigned long long>((most + 255) / 256, 1024);
+        hipLaunchKernelGGL(k_copy_segs, dim3(gx, n), dim3(256), 0, s, g);
+        PBCCS_HIP(hipGetLastError());
+    }
+}
+
+// device arrays -> host: packed on the device, one copy, unpacked on the host (synchronises the stream)
+void download_packed(const std::vector<Xfer>& items, DevVec<unsigned char>& stage, std::vector<unsigned char>& host,
+                     hipStream_t s)
+{
+    std::vector<size_t> off;
+    const size_t top = stage_layout(items, &off);
+    if (!top) return;
+    stage.reserve(top, false);
+    std::vector<CopySeg> segs;
+    for (size_t k = 0; k < items.size(); ++k)
+        if (items[k].bytes)
+            segs.push_back({static_cast<const unsigned int*>(items[k].dev),
+                            reinterpret_cast<unsigned int*>(stage.ptr + off[k]), items[k].bytes / 4});
+    launch_copy_segs(segs, s);
+    host.resize(top);
+    d2h(host.data(), stage.ptr, top, s);
+    PBCCS_HIP(hipStreamSynchronize(s));
+    for (size_t k = 0; k < items.size(); ++k)
+        if (items[k].bytes) std::memcpy(items[k].host, host.data() + off[k], items[k].bytes);
+}
+
+// host arrays -> device arrays (already reserved): packed on the host, one copy, unpacked on the device
+void upload_packed(const std::vector<Xfer>& items, DevVec<unsigned char>& stage, std::vector<unsigned char>& host,
+                   hipStream_t s)
+{
+    std::vector<size_t> off;
+    const size_t top = stage_layout(items, &off);
+    if (!top) return;
+    stage.reserve(top, false);
+    host.resize(top);
+    std::vector<CopySeg> segs;
+    for (size_t k = 0; k < items.size(); ++k) {
+        if (!items[k].bytes) continue;
+        std::memcpy(host.data() + off[k], items[k].host, items[k].bytes);
+        segs.push_back({reinterpret_cast<const unsigned int*>(stage.ptr + off[k]),
+                        static_cast<unsigned int*>(items[k].dev), items[k].bytes / 4});
+    }
+    PBCCS_HIP(hipMemcpyAsync(stage.ptr, host.data(), top, hipMemcpyHostToDevice, s));
+    launch_copy_segs(segs, s);
+}
+
+template <class T>
+Xfer xfer_dl(std::vector<T>& h, const DevVec<T>& d, size_t n)   // n elements of d into h (resized)
+{
+    h.resize(n);
+    return Xfer{d.ptr, h.data(), n * sizeof(T)};
+}
+
+template <class T>
+Xfer xfer_ul(DevVec<T>& d, const std::vector<T>& h)   // h into d (reserved here)
+{
+    d.reserve(std::max<size_t>(h.size(), 1), false);
+    return Xfer{d.ptr, const_cast<T*>(h.data()), h.size() * sizeof(T)};
 }
 
 }  // namespace
@@ -277,7 +388,7 @@ size_t Workspace::TrimRetired()
     t(wMutStart); t(wPosStart); t(wPosBase); t(wQvBase); t(stats); t(aRange); t(bRange); t(aOff); t(bOff); t(aLs);
     t(bLs); t(aPre); t(bSuf); t(fVal); t(fLs); t(fPre); t(fRange); t(fOff); t(codes); t(posOff); t(qv); t(list);
     t(edge); t(edgeCount); t(ckSlots); t(ckCounter); t(delta); t(score); t(fav); t(scratch); t(scratchTop);
-    t(scratchOverflow); t(sel); t(selCount); t(selScore); t(selCode); t(selRank); t(selTmp);
+    t(scratchOverflow); t(xStage); t(sel); t(selCount); t(selScore); t(selCode); t(selRank); t(selTmp);
     b += val.trim_fallback();
     return b;
 }
@@ -1165,16 +1276,14 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         }
         std::vector<int> st, fl, ua, ub, mh;
         std::vector<double> bl, dv;
-        download(mh, dMaxH_, R, stream_);
-        if (anyScan) download(dv, dRDev_, R, stream_);
-        download(st, dRStatus_, R, stream_);
-        download(fl, dRFlips_, R, stream_);
-        download(bl, dRBaseline_, R, stream_);
-        download(ua, dUsedA_, R, stream_);
-        download(ub, dUsedB_, R, stream_);
         unsigned long long bump = (unsigned long long)valTop_;
-        if (grow) d2h(&bump, dBump_.ptr, sizeof(bump), stream_);
-        PBCCS_HIP(hipStreamSynchronize(stream_));
+        {   // the per-read results in one transfer
+            std::vector<Xfer> xs{xfer_dl(mh, dMaxH_, R), xfer_dl(st, dRStatus_, R), xfer_dl(fl, dRFlips_, R),
+                                 xfer_dl(bl, dRBaseline_, R), xfer_dl(ua, dUsedA_, R), xfer_dl(ub, dUsedB_, R)};
+            if (anyScan) xs.push_back(xfer_dl(dv, dRDev_, R));
+            if (grow) xs.push_back(Xfer{dBump_.ptr, &bump, sizeof(bump)});
+            download_packed(xs, ws_->xStage, hXStage_, stream_);
+        }
         if (grow && bump != (unsigned long long)valTop_) {
             // some reads moved to larger regions: adopt the device's descriptors (host mirrors stay exact)
             std::vector<long long> va, vb, vc;
@@ -1338,12 +1447,9 @@ void ArrowBatch::FillReadsSerial(const std::vector<int>& readsIn)
             counters_.fillLaunches += 1;
             std::vector<int> st, fl, ua, ub;
             std::vector<double> bl;
-            download(st, dRStatus_, R, stream_);
-            download(fl, dRFlips_, R, stream_);
-            download(bl, dRBaseline_, R, stream_);
-            download(ua, dUsedA_, R, stream_);
-            download(ub, dUsedB_, R, stream_);
-            PBCCS_HIP(hipStreamSynchronize(stream_));
+            download_packed({xfer_dl(st, dRStatus_, R), xfer_dl(fl, dRFlips_, R), xfer_dl(bl, dRBaseline_, R),
+                             xfer_dl(ua, dUsedA_, R), xfer_dl(ub, dUsedB_, R)},
+                            ws_->xStage, hXStage_, stream_);
             if (trace) TraceSummary(n, H, capSlots);
             for (int r : chunk) {
                 HRead& h = reads_[r];
@@ -1535,14 +1641,10 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
     rTotalPos_ = rPosStart_[n];
     rTotalDelta_ = delta;
     std::vector<long long> mutBase(rMutStart_.begin(), rMutStart_.begin() + n);
-    upload(dWZmw_, zl, stream_);
-    upload(dWNMut_, rNMut_, stream_);
-    upload(dWMutBase_, mutBase, stream_);
-    upload(dWDeltaBase_, rDeltaBase_, stream_);
-    upload(dWWaveStart_, waveStart, stream_);
-    upload(dWMutStart_, rMutStart_, stream_);
-    upload(dWPosStart_, rPosStart_, stream_);
-    upload(dWPosBase_, posBase, stream_);
+    upload_packed({xfer_ul(dWZmw_, zl), xfer_ul(dWNMut_, rNMut_), xfer_ul(dWMutBase_, mutBase),
+                   xfer_ul(dWDeltaBase_, rDeltaBase_), xfer_ul(dWWaveStart_, waveStart), xfer_ul(dWMutStart_, rMutStart_),
+                   xfer_ul(dWPosStart_, rPosStart_), xfer_ul(dWPosBase_, posBase)},
+                  ws_->xStage, hXStage_, stream_);
     dCodes_.reserve(std::max<long long>(rTotalMut_, 1), false);
     dScore_.reserve(std::max<long long>(rTotalMut_, 1), false);
     dFav_.reserve(std::max<long long>(rTotalMut_, 1), false);
@@ -2136,11 +2238,9 @@ void ArrowBatch::Refine(const std::vector<int>& zl, const RefineOptions& ro, std
             std::vector<long long> sel;
             std::vector<double> selScore;
             std::vector<int> selCode, selRank;
-            download(sel, dSel, cnt[0], stream_);
-            download(selScore, dSelScore, cnt[0], stream_);
-            download(selCode, dSelCode, cnt[0], stream_);
-            download(selRank, dSelRank, cnt[0], stream_);
-            PBCCS_HIP(hipStreamSynchronize(stream_));
+            download_packed({xfer_dl(sel, dSel, cnt[0]), xfer_dl(selScore, dSelScore, cnt[0]),
+                             xfer_dl(selCode, dSelCode, cnt[0]), xfer_dl(selRank, dSelRank, cnt[0])},
+                            ws_->xStage, hXStage_, stream_);
 
             favL.assign(actL.size(), {});
             pickedL.assign(actL.size(), {});

@@ -313,6 +313,7 @@ struct Workspace {
     DevVec<unsigned long long> scratchTop;
     DevVec<int> scratchOverflow;
     // favourable-mutation selection (persistent: a per-round hipFree would synchronise the whole device)
+    DevVec<unsigned char> xStage;   // packed transfers (download_packed / upload_packed, engine.hip)
     DevVec<long long> sel, selCount;
     DevVec<double> selScore;
     DevVec<int> selCode, selRank;
@@ -478,6 +479,7 @@ private:
 
     // host mirrors of pools
     std::vector<char> hTpl_, hSeq_;
+    std::vector<unsigned char> hXStage_;   // host side of the packed transfers
     // device state owned by the batch (inputs + descriptors).  The per-ZMW and per-read descriptors and the
     // template pool live in one device arena, filled by one copy from a page-locked staging buffer per
     // UploadDescriptors (UploadDescriptors sets the typed views below).
