@@ -55,12 +55,27 @@ _queue_calls = [0]
 
 
 def dynamic_chunks(zmws, chunk):
-    """The pull queue's work items: ZMW indices in decreasing cost, cut into chunks of `chunk` ZMWs (largest
-    first, so the ranks' last pulls are the cheap chunks).  A lazily generated cell (synth.SmrtCell) gives its
-    costs from the ZMW shapes, without materialising a sequence."""
+    """The pull queue's work items: ZMW indices in decreasing cost (largest first, so the ranks' last pulls are
+    the cheap chunks), cut into chunks of at most `chunk` ZMWs and of at most 1 / ceil(n / chunk) of the total
+    cost each.  The cost cap splits the expensive end finer: equal-count chunks put the cell's 500 costliest
+    ZMWs (20 kb, up to 30 passes) in one chunk, which one rank then polished for 527 s after the other had run
+    out of work (configs[4] at 10,000 ZMWs on two ranks, profiles/r9x_smrtcell_10000_gpus2_rehearsal.json).
+    A lazily generated cell (synth.SmrtCell) gives its costs from the ZMW shapes, without materialising a
+    sequence."""
     costs = zmws.costs() if hasattr(zmws, "costs") else [zmw_cost(z) for z in zmws]
     order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
-    return [order[k:k + chunk] for k in range(0, len(order), chunk)]
+    n_target = max(1, -(-len(order) // max(1, chunk)))
+    cap = sum(costs) / n_target
+    out, cur, cur_cost = [], [], 0
+    for i in order:
+        if cur and (len(cur) >= chunk or cur_cost + costs[i] > cap):
+            out.append(cur)
+            cur, cur_cost = [], 0
+        cur.append(i)
+        cur_cost += costs[i]
+    if cur:
+        out.append(cur)
+    return out
 
 
 STORE_PART = 4 << 20   # bytes per value put on the rank-0 key-value store (whose values are capped at 8 MB)
