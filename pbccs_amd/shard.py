@@ -164,11 +164,15 @@ def polish_dynamic(zmws, settings=None, engine=None, rank=None, world=None, chun
 
     def collector():
         try:
-            last = time.perf_counter()   # the last record collected, or `final` being set
+            last = time.perf_counter()   # the last record collected, `final` being set, or pending filling again
             seen_final = False
+            was_empty = True
             while True:
                 with lock:
                     todo = sorted(pending)
+                if todo and was_empty:   # chunks handed out after an idle spell: their clock starts now
+                    last = time.perf_counter()
+                was_empty = not todo
                 got = [c for c in todo if collect_one(c)]
                 with lock:
                     pending.difference_update(got)

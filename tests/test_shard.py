@@ -157,7 +157,7 @@ def test_gloo_world2_dynamic_queue_balances_and_keeps_order():
     res, st = _run(2, zmws, mode="dynamic")
     assert [r["draft"] for r in res] == [z["draft"][::-1] for z in zmws]
     by_rank = [sum(1 for r in res if r["rank"] == k) for k in (0, 1)]
-    assert by_rank[1] >= 2 and by_rank[0] >= 8, by_rank
+    assert by_rank[1] >= 1 and by_rank[0] >= 8, by_rank   # (rank 1's one chunk may hold one ZMW: cost-capped)
     # records streamed per chunk: rank 0 saw every chunk, the other rank's through the store
     n_ch = len(shard.dynamic_chunks(zmws, 2))   # 2 ZMWs per chunk at most, the costliest end cut finer
     assert st["chunks"] == n_ch and sum(st["chunks_by_rank"]) == n_ch and st["chunks_by_rank"][1] >= 1
