@@ -63,7 +63,24 @@ public:
     {}
     Mutation(MutationType type, int start, int end, const std::string& newBases)
         : type_(type), start_(start), end_(end), newBases_(newBases)
-    {}
+    {
+        if (!CheckInvariants()) throw InvalidInputError();
+    }
+    // Mutation-inl.hpp:66-77: end from the new bases' length (an insertion's is its start), a deletion's bases dropped
+    Mutation(MutationType type, int position, const std::string& newBases)
+        : type_(type), start_(position),
+          end_(type == INSERTION ? position : position + (int)newBases.size()),
+          newBases_(type == DELETION ? std::string() : newBases)
+    {
+        if (!CheckInvariants()) throw InvalidInputError();
+    }
+    // Mutation-inl.hpp:103-115
+    bool CheckInvariants() const
+    {
+        return (type_ == INSERTION && start_ == end_ && !newBases_.empty()) ||
+               (type_ == DELETION && start_ < end_ && newBases_.empty()) ||
+               (type_ == SUBSTITUTION && start_ < end_ && (int)newBases_.size() == end_ - start_);
+    }
     MutationType Type() const { return type_; }
     int Start() const { return start_; }
     int End() const { return end_; }

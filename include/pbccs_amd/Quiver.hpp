@@ -428,12 +428,12 @@ public:
     }
     float Score(MutationType t, int position, const std::string& newBases) const override
     {
-        return Score(Mutation(t, position, t == INSERTION ? position : position + 1, newBases));
+        return Score(Mutation(t, position, newBases));   // Mutation-inl.hpp:66-77
     }
     std::vector<float> Scores(MutationType t, int position, const std::string& newBases,
                               float unscoredValue) const override
     {
-        return Scores(Mutation(t, position, t == INSERTION ? position : position + 1, newBases), unscoredValue);
+        return Scores(Mutation(t, position, newBases), unscoredValue);
     }
     std::vector<float> Scores(MutationType t, int position, const std::string& newBases) const
     {

@@ -1765,6 +1765,8 @@ void ArrowBatch::RunRound(const std::vector<int>& zl, const std::vector<std::vec
             sc.cap = dScratch_.cap;
             sc.overflow = dScratchOverflow_.ptr;
             if (ck.nTasks > 0) {
+                // replay slots: as many as fit kCkptSlotBytes, but at least 64 waves' worth -- a soft bound: for very
+                // tall reads (slots over 16 MB each) the 64-slot floor takes more than 1 GB
                 const long long fit = kCkptSlotBytes / std::max<long long>(1, ckSlotCap_ * (long long)sizeof(double));
                 ck.nSlots = (int)std::max<long long>(
                     1, std::min<long long>(std::min<long long>(ck.nTasks, kCkptSlotsMax), std::max<long long>(64, fit)));
