@@ -264,20 +264,5 @@ __device__ __forceinline__ void scan_chain64(const double (&m)[R], const double 
     }
 }
 
-// The 16-lane fill's chunk (one row per lane, the group one DPP row of the wavefront): four row_shr levels compose
-// the maps of the group's lanes below; lane 0 of each group sees the identity.
-__device__ __forceinline__ double scan_chain16(double m, double k, double d, double carry)
-{
-    const double c = m + d;
-    double A = k, B = c;
-    affine_step<0x111, 0xF>(A, B);   // row_shr:1
-    affine_step<0x112, 0xF>(A, B);   // row_shr:2
-    affine_step<0x114, 0xF>(A, B);   // row_shr:4
-    affine_step<0x118, 0xF>(A, B);   // row_shr:8
-    const double Ae = dpp_d<0x111, 0xF, false>(1.0, A);   // exclusive prefix (row_shr:1, identity at lane 0)
-    const double Be = dpp_d<0x111, 0xF, false>(0.0, B);
-    return k * (Ae * carry + Be) + c;
-}
-
 }  // namespace coop
 }  // namespace pbccs

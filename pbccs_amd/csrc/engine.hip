@@ -1145,12 +1145,12 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
         const int scanPaths = env_int("PBCCS_SCAN_PATHS", 1);
         auto scannable = [&](int r) { return scan_ && !reads_[r].exact; };
         int nScan[kPaths] = {};
-        for (int p = 1; p < kPaths; ++p) {   // bit 2: the 16-lane path
-            if (!((scanPaths >> (p == 1 ? 2 : p - 2)) & 1)) continue;
+        for (int p = 2; p < kPaths; ++p) {
+            if (!((scanPaths >> (p - 2)) & 1)) continue;
             std::stable_partition(todo[p].begin(), todo[p].end(), scannable);
             nScan[p] = (int)std::count_if(todo[p].begin(), todo[p].end(), scannable);
         }
-        const bool anyScan = nScan[1] + nScan[2] + nScan[3] > 0;
+        const bool anyScan = nScan[2] + nScan[3] > 0;
         UploadDescriptors();
         const size_t R = reads_.size();
         dUsedA_.reserve(std::max<size_t>(R, 1), true);

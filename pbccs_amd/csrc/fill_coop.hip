@@ -399,8 +399,7 @@ __device__ PassOut coop_alpha(const Task<G>& T, Band& a, Band& o, bool guided, b
                             x[0] = insertion_chain64_exit(m[0], k[0], d[0], carry, min(reqEnd, I) - 1 - i0, maybe_stop,
                                                           startLane);
                         } else {
-                            if constexpr (SCAN && G == 16) x[0] = scan_chain16(m[0], k[0], d[0], carry);
-                            else x[0] = insertion_chain<G>(m[0], k[0], d[0], carry);
+                            x[0] = insertion_chain<G>(m[0], k[0], d[0], carry);
                         }
                     } else {
                         auto maybe_stop = [&](const double (&xv)[R]) {   // x < pm * invLow implies x < pm / sdn
@@ -756,8 +755,7 @@ __device__ PassOut coop_beta(const Task<G>& T, Band& bm, Band& o, bool guided, b
                             x[0] = insertion_chain64_exit(m[0], k[0], d[0], carry, e - 1 - max(1, reqBegin) - c * G,
                                                           maybe_stop, startLane);
                         } else {
-                            if constexpr (SCAN && G == 16) x[0] = scan_chain16(m[0], k[0], d[0], carry);
-                            else x[0] = insertion_chain<G>(m[0], k[0], d[0], carry);
+                            x[0] = insertion_chain<G>(m[0], k[0], d[0], carry);
                         }
                     } else {
                         auto maybe_stop = [&](const double (&xv)[R]) {   // x < pm * invLow implies x < pm / sdn
@@ -1291,11 +1289,9 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
         K k;
         bool attr;
     };
-    // the certified fast path (scan) exists for the tall paths with two rows per lane and the 16-lane path with one
-    // 
+    // the certified fast path (scan) exists for the tall paths with two rows per lane
     static Entry ks[] = {
         {16, 1, false, false, (K)k_fill_coop<16, PBCCS_NARROW_MINW, false, 1, false>, false},
-        {16, 1, false, true, (K)k_fill_coop<16, PBCCS_NARROW_MINW, false, 1, true>, false},
         {64, 1, false, false, (K)k_fill_coop<64, 2, false, 1, false>, false},
         {64, 2, false, false, (K)k_fill_coop<64, 2, false, 2, false>, false},
         {64, 2, false, true, (K)k_fill_coop<64, 2, false, 2, true>, false},
@@ -1304,7 +1300,7 @@ void launch_fill_coop(int G, const DevBatch& B, const CoopFill& F, const int* re
         {64, 1, true, false, (K)k_fill_coop<64, 1, true, 1, false>, false},
         {64, 2, true, false, (K)k_fill_coop<64, 1, true, 2, false>, false},
         {64, 2, true, true, (K)k_fill_coop<64, 1, true, 2, true>, false}};
-    const bool scan = F.scan && ((G == 64 && R == 2) || (G == 16 && R == 1));
+    const bool scan = F.scan && G == 64 && R == 2;
     Entry* e = nullptr;
     for (Entry& x : ks)
         if (x.g == G && x.r == R && x.gc == gc && x.scan == scan) e = &x;
