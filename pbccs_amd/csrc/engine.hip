@@ -382,6 +382,7 @@ size_t Workspace::TrimRetired()
 {
     size_t b = 0;
     auto t = [&](auto& v) { b += v.trim(); };
+    t(hDesc);
     t(selBase); t(nSel); t(colScratch); t(bump); t(desc); t(seq); t(ckPairs); t(ckStart); t(rBaseline); t(rFlips);
     t(rDev); t(wDev); t(wAmb);
     t(rStatus); t(usedA); t(usedB); t(maxH); t(wZmw); t(wNMut); t(wMutBase); t(wDeltaBase); t(wWaveStart);

@@ -166,17 +166,30 @@ struct PinnedBuf {
             (void)hipGetLastError();
             throw DeviceError("hipHostMalloc failed (" + std::to_string(nc >> 20) + " MB)");
         }
-        if (ptr) (void)hipHostFree(ptr);
+        // the old buffer is retired, not freed: hipHostFree waits for the whole device -- 14 s for one slot behind
+        // the other slots' tall fills at configs[3] (gpurun_out/r9ze/api_gaps.json) -- and a queued copy may still
+        // read it.  trim() frees the retired buffers where the device is idle (Workspace::TrimRetired).
+        if (ptr) retired_.push_back(ptr);
         ptr = p;
         cap = nc;
+    }
+    size_t trim()
+    {
+        for (char* r : retired_) (void)hipHostFree(r);
+        retired_.clear();
+        return 0;   // host memory: not counted with the device bytes TrimRetired returns
     }
     PinnedBuf() = default;
     PinnedBuf(const PinnedBuf&) = delete;
     PinnedBuf& operator=(const PinnedBuf&) = delete;
     ~PinnedBuf()
     {
+        trim();
         if (ptr) (void)hipHostFree(ptr);
     }
+
+private:
+    std::vector<char*> retired_;
 };
 
 // Band value pool: a large virtual-address reservation whose physical backing is mapped in 1 GB
