@@ -926,8 +926,21 @@ int pbccs_plan_batches(const pbccs_zmw_input* in, int n, double budget_bytes, in
         spans.push_back(s);
         k = s.e;
     }
-    // largest first: the queue's tail is then made of short batches (LPT)
-    std::stable_sort(spans.begin(), spans.end(), [](const Span& a, const Span& b) { return a.bytes > b.bytes; });
+    // longest templates first, then largest: a batch's time is its rounds' latency, which grows with the template
+    // (the tall reads' column sweeps), not with its bytes -- most batches of a mixed input are capped at the same
+    // budget, and ordered by bytes the 15-20 kb batches started last and left four of eight slots idle for the last
+    // third of a configs[3] run (profiles/r9ze_mixed_slot_gaps.json); the queue's tail is then made of short batches
+    std::vector<int> spanLen(spans.size());
+    for (size_t k = 0; k < spans.size(); ++k) spanLen[k] = in[idx[spans[k].e - 1]].draft_len;   // ascending inside
+    std::vector<size_t> so(spans.size());
+    for (size_t k = 0; k < so.size(); ++k) so[k] = k;
+    std::stable_sort(so.begin(), so.end(), [&](size_t a, size_t b) {
+        if (spanLen[a] != spanLen[b]) return spanLen[a] > spanLen[b];
+        return spans[a].bytes > spans[b].bytes;
+    });
+    std::vector<Span> sorted;
+    for (size_t k : so) sorted.push_back(spans[k]);
+    spans.swap(sorted);
     int o = 0;
     for (size_t b = 0; b < spans.size(); ++b) {
         batch_start[b] = o;

@@ -28,7 +28,9 @@ def test_plan_is_a_bucketed_partition(budget, cap, ratio):
         bytes_ = sum(est[i] for i in b)
         assert len(b) == 1 or bytes_ <= budget
         sizes.append(bytes_)
-    assert sizes == sorted(sizes, reverse=True)   # largest first
+    # longest templates first (a batch's time follows its rounds' latency), then largest
+    keys = [(max(len(zs[i]["draft"]) for i in b), est_b) for b, est_b in zip(batches, sizes)]
+    assert keys == sorted(keys, reverse=True)
     assert (batches, est) == pbccs_amd.plan_batches(zs, budget, cap, ratio)   # deterministic
 
 
