@@ -1184,7 +1184,9 @@ void ArrowBatch::FillReads(const std::vector<int>& readsIn)
             PBCCS_HIP(hipMemGetInfo(&freeB, &totalB));
             // a quarter of what is free beyond a margin kept for the score buffers and the other slots'
             // hipMalloc growth: speculative headroom must never be what runs the device out of memory
-            const long long spare = std::max<long long>(0, (long long)freeB - (long long)kHeadroomMargin);
+            // PBCCS_HEADROOM_MARGIN_GB (A/B): the free memory the speculative headroom leaves alone
+            static const long long margin = (long long)env_int("PBCCS_HEADROOM_MARGIN_GB", (int)(kHeadroomMargin >> 30)) << 30;
+            const long long spare = std::max<long long>(0, (long long)freeB - margin);
             headroom = std::min<long long>(want, spare / 4 / (long long)sizeof(double));
             // the reads' own regions must be mapped; the growth headroom only as far as device memory
             // allows (several batches grow at once): the kernel's limit is what actually got mapped
