@@ -1963,7 +1963,12 @@ int pbccs_ccs_batch(pbccs_engine* eng, const pbccs_ccs_input* in, int n, long lo
             for (int b0 = 0; b0 < nl; b0 += o.zmws_per_batch) start[nb++] = b0;
             start[nb] = nl;
         } else {
-            rcp = pbccs_plan_batches(est.data(), nl, budget, kQueueMaxZmws, 1.5, perm.data(), start.data(), nullptr, &nb);
+            // about ten chunks per call, 1000-2000 ZMWs each: the POA of chunk k + 1 runs beside the polish of chunk
+            // k, so the first draft and the last polish are the pipeline's fill and drain -- at 10,000 ZMWs 1000-ZMW
+            // chunks ran 1943 / 1917 ZMWs/s against 1717 / 1850 for 2000, at 20,000 2000-ZMW chunks won (1986 / 1987
+            // vs 1874 / 1852; profiles/r9zt_ccs_chunk_ab.txt)
+            const int cap = std::max(std::min(nl / 10, kQueueMaxZmws), std::min(1000, kQueueMaxZmws));
+            rcp = pbccs_plan_batches(est.data(), nl, budget, cap, 1.5, perm.data(), start.data(), nullptr, &nb);
         }
         if (rcp != PBCCS_OK) return rcp;
         std::vector<CcsChunk> chunks(nb);
