@@ -4,6 +4,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <mutex>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -205,6 +206,18 @@ Xfer xfer_ul(DevVec<T>& d, const std::vector<T>& h)   // h into d (reserved here
 // ------------------------------------------------------------------------------------------------
 // VmPool
 // ------------------------------------------------------------------------------------------------
+// Every address range any band pool of the process has reserved for mapping: a range is never mapped twice, by
+// the same pool or another (the same-VA remap, unmap_all).  Returns whether `va` is one; records it if not.
+static bool va_used_before(void* va)
+{
+    static std::mutex mu;
+    static std::vector<void*> used;
+    std::lock_guard<std::mutex> lk(mu);
+    if (std::find(used.begin(), used.end(), va) != used.end()) return true;
+    used.push_back(va);
+    return false;
+}
+
 void VmPool::try_reserve(size_t n)
 {
     if (!vmm_ || n <= cap) return;
@@ -218,24 +231,21 @@ void VmPool::reserve(size_t n, bool keep)
         tried_ = true;
         void* va = nullptr;
         static const bool dbgVa = env_int("PBCCS_DBG_VA", 0) != 0;   // debug: every reservation and unmap
-        // a range this pool mapped before must never be mapped by it again (same-VA remap, unmap_all): the ranges it
-        // unmapped stay reserved (oldVas_), and one the allocator still hands back (past kKeptVas) is parked there too
+        // a range this pool mapped before must never be mapped by it again (same-VA remap, unmap_all): a reservation
+        // that returns one is parked (kept reserved, never mapped: address space only) and the next one taken
         for (int attempt = 0;; ++attempt) {
             vmm_ = hipMemAddressReserve(&va, kVaBytes, 0, nullptr, 0) == hipSuccess && va != nullptr;
             if (!vmm_) {
                 (void)hipGetLastError();
                 break;
             }
-            if (dbgVa) std::fprintf(stderr, "[vmpool %p] reserve va=%p (%zu kept)\n", (void*)this, va, oldVas_.size());
-            if (std::find(usedVas_.begin(), usedVas_.end(), va) == usedVas_.end()) break;
+            if (dbgVa) std::fprintf(stderr, "[vmpool %p] reserve va=%p (%zu parked)\n", (void*)this, va, parkedVas_.size());
+            if (!va_used_before(va)) break;
             reusedVas_ += 1;
-            oldVas_.push_back(va);
-            if (attempt == 3) throw DeviceError("band pool: no address range this pool has not mapped before");
+            parkedVas_.push_back(va);
+            if (attempt == 64) throw DeviceError("band pool: no address range this pool has not mapped before");
         }
-        if (vmm_) {
-            ptr = static_cast<double*>(va);
-            usedVas_.push_back(va);
-        }
+        if (vmm_) ptr = static_cast<double*>(va);   // (recorded as used by va_used_before)
     }
     if (!vmm_) {
         fallback_.reserve(n, keep);
@@ -335,13 +345,10 @@ void VmPool::unmap_all(hipStream_t s)
     // the streams that used the old mapping still alive, gave wrong results -- POA drafts after a pool release,
     // and an out-of-memory rerun on slot-shared streams (its range was the one unmapped two reservations before,
     // PBCCS_DBG_VA=1 logs in profiles/r9s_same_va_oom.txt; with per-batch streams the same reuse was harmless).
-    // So the range stays reserved: the next reservation cannot return it.  Beyond kKeptVas the oldest is freed,
-    // and reserve parks it should the allocator hand it back.
-    oldVas_.push_back(ptr);
-    if (oldVas_.size() > kKeptVas) {
-        (void)hipMemAddressFree(oldVas_.front(), kVaBytes);
-        oldVas_.erase(oldVas_.begin());
-    }
+    // The range is freed now -- the device memory of the unmapped granules comes back only with the range (kept
+    // reserved, 600 MB per repetition stayed taken, tests/test_schedule.py::test_device_memory_does_not_grow_across_calls)
+    // -- and reserve parks a reservation that returns it (va_used_before), so it is never mapped again.
+    (void)hipMemAddressFree(ptr, kVaBytes);
     ptr = nullptr;
     tried_ = false;
     vmm_ = false;
@@ -349,7 +356,7 @@ void VmPool::unmap_all(hipStream_t s)
 
 VmPool::~VmPool()
 {
-    for (void* va : oldVas_) (void)hipMemAddressFree(va, kVaBytes);
+    for (void* va : parkedVas_) (void)hipMemAddressFree(va, kVaBytes);
     if (!vmm_) return;
     (void)hipDeviceSynchronize();
     size_t off = 0;

@@ -219,12 +219,11 @@ private:
     static constexpr size_t kVaBytes = 1ull << 39;      // 512 GB of address space
     static constexpr size_t kChunkBytes = 1ull << 30;   // mapping granule
     bool tried_ = false, vmm_ = false;
-    // The ranges this pool mapped and unmapped, kept reserved so the address allocator cannot hand one back: a
-    // range mapped again while the streams that used it live on reads wrong values ("same-VA remap").
-    // Freed with the pool, or oldest first beyond kKeptVas (reserve then parks it, should it come back).
-    static constexpr size_t kKeptVas = 64;
-    std::vector<void*> oldVas_;
-    std::vector<void*> usedVas_;   // every range this pool has mapped (reserve's check)
+    // A range mapped again while the streams that used it live on reads wrong values ("same-VA
+    // remap"): every range any pool of the process has mapped is recorded (va_used_before, engine.hip), and a
+    // reservation the allocator hands back as one of them is parked -- kept reserved, never mapped (address space
+    // only) -- until the pool is destroyed.
+    std::vector<void*> parkedVas_;
 public:
     long long reusedVas_ = 0;      // reservations that returned such a range (parked, not mapped)
 private:

@@ -208,3 +208,31 @@ def test_out_of_memory_rerun_on_slot_streams_after_same_va_remap(monkeypatch):
     finally:
         for p in blocks:
             hip.hipFree(p)
+
+
+@pytest.mark.gpu
+def test_device_memory_does_not_grow_across_calls(monkeypatch):
+    """ADVICE r5: buffers that stream-ordered growth retires are freed at quiescent points (Workspace::TrimRetired),
+    so repeating the same work on one engine -- growing batches, and an out-of-memory rerun with its pool unmaps --
+    leaves the device's free memory where the previous repetition left it."""
+    import ctypes
+    import pbccs_amd
+    hip = ctypes.CDLL("libamdhip64.so")
+
+    def free_bytes():
+        f, t = ctypes.c_size_t(), ctypes.c_size_t()
+        assert hip.hipDeviceSynchronize() == 0 and hip.hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)) == 0
+        return f.value
+
+    # a 24-ZMW 2 kb batch (its pool runs out under the cap: a rerun, halved) beside a batch of 16 small ZMWs
+    zs = synth.make_zmws(24, 2000, 10, seed=31) + synth.make_zmws(16, 600, 6, seed=41)
+    eng = pbccs_amd.Engine(0)
+    eng.set_concurrency(2)
+    settings = pbccs_amd.ConsensusSettings(zmws_per_batch=24)
+    monkeypatch.setenv("PBCCS_POOL_CAP_MB", "200")
+    frees = []
+    for _ in range(3):   # the first repetition sizes everything; the next two must not take more
+        pbccs_amd.polish_stream(zs, settings, eng)
+        frees.append(free_bytes())
+    assert eng.counters()["oom_retries"] >= 2
+    assert frees[1] - frees[2] < (64 << 20), frees
